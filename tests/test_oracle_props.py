@@ -1,0 +1,89 @@
+"""Randomised agreement of the two independent oracle restatements:
+the emqx_trie walk (both compaction modes) vs brute-force emqx_topic:match/2.
+
+Generators follow the reference's PropEr shapes (apps/emqx/test/
+emqx_proper_types.erl:314-338: '+' with probability 1/3 per level, or a
+trailing '#'), plus '$'-topics, empty levels and deep topics.
+"""
+
+import random
+
+import numpy as np
+import pytest
+
+ALPH = ["a", "b", "c", "", "$x", "$SYS", "dd"]
+
+
+def rand_filter(rng):
+    n = rng.randint(1, 5)
+    ws = [rng.choice(ALPH) for _ in range(n)]
+    kind = rng.random()
+    if kind < 0.2:
+        return "/".join(ws)
+    if kind < 0.6:
+        return "/".join("+" if rng.random() < 1 / 3 else w for w in ws)
+    if kind < 0.8:
+        return "/".join(ws[: rng.randint(0, n)] + ["#"])
+    ws = ["+" if rng.random() < 1 / 3 else w for w in ws]
+    return "/".join(ws + ["#"])
+
+
+def rand_topic(rng):
+    n = rng.randint(1, 6)
+    ws = [rng.choice(ALPH) for _ in range(n)]
+    if rng.random() < 0.05:
+        ws[rng.randrange(n)] = rng.choice(["+", "#"])
+    return "/".join(ws)
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_trie_walk_equals_bruteforce(orc, seed):
+    rng = random.Random(seed)
+    filters = sorted({rand_filter(rng).encode() for _ in range(rng.randint(1, 40))})
+    topics = [rand_topic(rng).encode() for _ in range(40)]
+    wild = np.array([orc.wildcard(f) for f in filters], np.uint8)
+    for compact in (True, False):
+        r = orc.Router(compact)
+        for f in filters:
+            r.add_route(f)
+        # match_routes semantics
+        ro, ids, _ = r.match_batch(topics, filters, mode=1)
+        bro, bids = orc.bruteforce(topics, filters, mode=1)
+        assert np.array_equal(ro, bro) and np.array_equal(ids, bids), (seed, compact)
+        # emqx_trie:match/1 semantics over the wildcard filters in the trie
+        ro, ids, _ = r.match_batch(topics, filters, mode=0)
+        bro, bids = orc.bruteforce(topics, filters, mode=0, in_trie=wild)
+        assert np.array_equal(ro, bro) and np.array_equal(ids, bids), (seed, compact)
+        # no duplicates in any row
+        for i in range(len(topics)):
+            row = ids[ro[i]:ro[i + 1]]
+            assert len(set(row.tolist())) == len(row)
+
+
+def test_dollar_single_word_quirk(orc):
+    """emqx_trie.erl:271-278: a single-word '$X' topic also looks up {'$X',1},
+    so a non-wildcard '$X' inserted into the trie is returned."""
+    for compact in (True, False):
+        t = orc.Trie(compact)
+        t.insert("$SYS")
+        t.insert("$SYS/#")
+        t.insert("plain")
+        assert sorted(t.match("$SYS")) == [b"$SYS", b"$SYS/#"]
+        assert t.match("plain") == []
+
+
+def test_workload_generator_shapes(orc):
+    codes = orc.gen_filter_codes(1, 2000, wildcard_only=False)
+    data, off = orc.render_codes(codes)
+    fs = orc.unpack(data, off)
+    assert len(set(fs)) == len(fs)
+    assert all(f.startswith(b"l0w") or f.startswith(b"+") for f in fs)
+    w = orc.gen_filter_codes(1, 2000, wildcard_only=True)
+    fw = orc.unpack(*orc.render_codes(w))
+    assert all(orc.wildcard(f) for f in fw)
+    tc = orc.gen_topic_codes(7, 0, 1000, codes)
+    ts = orc.unpack(*orc.render_codes(tc))
+    assert all(t.count(b"/") == 4 for t in ts)
+    # counter-based: any window regenerates identically
+    tc2 = orc.gen_topic_codes(7, 500, 10, codes)
+    assert np.array_equal(tc[500:510], tc2)
