@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""Headline benchmark: publish topics matched/sec at 1M wildcard subscriptions.
+
+Workload (BASELINE.json configs[1], SURVEY.md §8d "C2"): 1M wildcard filters
+(seeded generator, exact share 0), a 100M-topic publish batch per GPU generated
+on the device, matched with emqx_router:match_routes/1 semantics into a CSR of
+sorted filter ids.  A step = one emqx_gm_match call over the whole batch (every
+kernel, the overflow check and the CSR assembly).  Inputs are resident in HBM
+before the timed region; the CSR stays in HBM (DEVICE_IO).
+
+Multi-GPU (weak scaling): one process per GPU, replicated index, each rank
+matches its own 100M-topic slice; no collective on the data path.  `value` is
+the topics of all ranks / the max-over-ranks wall time.
+
+Also reported: a roofline object for the dominant kernel (k_match_fast,
+algorithmic bytes per SURVEY.md §8d ÷ its HIP-event time) and a CPU baseline:
+the oracle's faithful emqx_trie restatement (compact mode, ordered key table,
+fresh prefix strings) on the host cores over a bounded sample of the same
+topic stream.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "publish topics matched/sec at 1M wildcard subs (1/2/4/8 GPU); achieved HBM GB/s"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4"])
+    p.add_argument("--filters", type=int, default=None)
+    p.add_argument("--topics", type=int, default=None, help="topics per GPU per step")
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--cpu-threads", type=int, default=None)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return p.parse_args()
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        pg = dist
+    return world, rank, local, pg
+
+
+def barrier_max(pg, local, x: float) -> float:
+    if pg is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def cpu_baseline(codes, filters_packed, seed, target_s, threads):
+    """The oracle's faithful emqx_trie walk (compact) + route lookup on host cores."""
+    from oracle import oracle as orc
+    r = orc.Router(True)
+    fb, fo = filters_packed
+    raw = fb.tobytes()
+    for i in range(len(fo) - 1):
+        r.add_route(raw[int(fo[i]):int(fo[i + 1])])
+    sorted_f = None  # ids not needed for timing
+    # calibrate on a small slice, then time a sample sized for ~target_s
+    probe_n = 20_000 * threads
+    tb, to = orc.render_codes(orc.gen_topic_codes(seed, 0, probe_n, codes))
+    t0 = time.perf_counter()
+    r.match_batch((tb, to), (fb, fo), mode=1, nthreads=threads, want_ids=False)
+    dt = time.perf_counter() - t0
+    rate = probe_n / max(dt, 1e-6)
+    n = int(min(max(rate * target_s, probe_n), 20_000_000))
+    tb, to = orc.render_codes(orc.gen_topic_codes(seed, 0, n, codes))
+    t0 = time.perf_counter()
+    ro, _, lk = r.match_batch((tb, to), (fb, fo), mode=1, nthreads=threads, want_ids=False)
+    dt = time.perf_counter() - t0
+    del sorted_f
+    return {"value": n / dt, "unit": "topics/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} topics of the same seeded C2 stream (seed {seed}), emqx_trie compact walk + "
+                      f"lookup_routes restated in C++ (oracle/emqx_oracle.cpp), {threads} std::threads, "
+                      f"{dt:.1f} s; {float(ro[-1]) / n:.3f} matches/topic; "
+                      f"{float(lk.mean()) if len(lk) else 0:.1f} ordered-set lookups/topic"}
+
+
+def main():
+    a = parse()
+    world, rank, local, pg = dist_setup(a.gpus)
+    import numpy as np
+    from emqx_amd import Context
+    from emqx_amd.engine import gen_filter_codes, render_codes
+
+    cfg = a.config
+    if cfg == "c4":
+        return bench_c4(a, world, rank, local, pg)
+    n_filters = a.filters or {"c1": 10_000, "c2": 1_000_000, "c3": 10_000_000}[cfg]
+    n_topics = a.topics or {"c1": 1_000_000, "c2": 100_000_000, "c3": 100_000_000}[cfg]
+    wildcard_only = cfg == "c2"
+
+    ctx = Context(local)
+    t_build0 = time.perf_counter()
+    codes = gen_filter_codes(a.seed, n_filters, wildcard_only=wildcard_only)
+    fpack = render_codes(codes)
+    idx = ctx.build_index(fpack)
+    t_build = time.perf_counter() - t_build0
+    db, do, tbytes = ctx.gen_topics_device(codes, a.seed, rank * n_topics, n_topics)
+
+    # warmup (also yields the per-batch constants for the roofline)
+    res = None
+    for _ in range(max(a.warmup, 1)):
+        if res is not None:
+            res.free()
+        res = ctx.match_device(idx, db, do, n_topics, exact=True)
+    st = ctx.stats()
+    fbytes_matched = ctx.matched_filter_bytes(idx, res)
+    nnz = res.nnz
+    res.free()
+
+    barrier(pg)
+    ctx.synchronize()
+    kern_ms = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = ctx.match_device(idx, db, do, n_topics, exact=True)
+        kern_ms.append(ctx.stats()["match_kernel_ms"])
+        res.free()
+    ctx.synchronize()
+    barrier(pg)
+    elapsed = time.perf_counter() - t0
+    elapsed = barrier_max(pg, local, elapsed)
+
+    ms_per_step = elapsed * 1000.0 / a.steps
+    value = world * n_topics * a.steps / elapsed
+    # algorithmic bytes of one k_match_fast launch:
+    #   B = Σ len(topic) + 8·n (offsets) + 16·P + Σ_matches (4 + len f) + 8·n (row offsets)
+    algo = tbytes + 8 * n_topics + 16 * st["probes"] + 4 * nnz + fbytes_matched + 8 * n_topics
+    kavg = sum(kern_ms) / len(kern_ms)
+    achieved = algo / (kavg / 1e3) / 1e9
+    traffic = None
+    try:
+        with open(a.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("config") == cfg and tj.get("n_topics") == n_topics:
+            traffic = tj.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "topics/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (seeded §8d generator, topics generated on device)",
+        "config": {"workload": {"c1": "C1: 10k mixed filters, 1M topics", "c2": "C2: 1M wildcard filters, "
+                                "100M-topic publish batch per GPU", "c3": "C3: 10M mixed filters, replicated index, "
+                                "100M topics per GPU"}[cfg] + " (match_routes semantics, CSR of sorted filter ids)",
+                   "filters": int(idx.n_filters), "topics_per_gpu": n_topics,
+                   "parallelism": f"replicated index, batch partitioned over {world} GPU(s)"},
+        "matches_per_sec": world * nnz * a.steps / elapsed,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_match_fast", "kernel_ms": kavg, "algo_bytes_per_launch": algo},
+        "detail": {"nnz_per_step": nnz, "matches_per_topic": nnz / n_topics, "probes_per_topic": st["probes"] /
+                   n_topics, "overflow_rows": st["n_overflow"], "topic_bytes": tbytes,
+                   "index_device_bytes": int(idx.info.device_bytes), "index_nodes": int(idx.info.n_nodes),
+                   "index_build_s": t_build, "device_ms_per_call": st["total_device_ms"]},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu:
+        threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        out["cpu_baseline"] = cpu_baseline(codes, fpack, a.seed, a.cpu_seconds, threads)
+        out["vs_cpu"] = value / out["cpu_baseline"]["value"]
+    ctx.dev_free(db)
+    ctx.dev_free(do)
+    idx.release()
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+def bench_c4(a, world, rank, local, pg):
+    """C4 hot fan-out: 1k topics x 1M subscribers each (10^9 deliveries)."""
+    import numpy as np
+    from emqx_amd import Context
+    K, S = 1000, 1_000_000
+    filters = [b"hot/#", b"hot/+/x/#"] + [b"hot/%d/x/y/z" % k for k in range(K)]
+    # hot/# -> 0..599,999; hot/+/x/# -> 600,000..999,899; each exact topic -> 999,900..999,999
+    lists = [np.arange(0, 600_000), np.arange(600_000, 999_900)] + [np.arange(999_900, S)] * K
+    so = np.zeros(len(lists) + 1, np.uint64)
+    so[1:] = np.cumsum([len(x) for x in lists])
+    si = np.concatenate(lists).astype(np.uint32)
+    ctx = Context(local)
+    idx = ctx.build_index(filters, subs=(so, si))
+    topics = [b"hot/%d/x/y/z" % k for k in range(K)]
+    from emqx_amd.engine import pack
+    tb, to = pack(topics)
+    d_tb = ctx.dev_alloc(len(tb))
+    d_to = ctx.dev_alloc(len(to) * 8)
+    ctx.memcpy_h2d(d_tb, tb, len(tb))
+    ctx.memcpy_h2d(d_to, to, len(to) * 8)
+    m = ctx.match_device(idx, d_tb, d_to, K, exact=True)
+    for _ in range(max(a.warmup, 1)):
+        r = ctx.fanout_device(idx, m)
+        r.free()
+    barrier(pg)
+    ctx.synchronize()
+    kms = []
+    t0 = time.perf_counter()
+    total = 0
+    for _ in range(a.steps):
+        r = ctx.fanout_device(idx, m)
+        total = r.nnz
+        kms.append(ctx.stats()["match_kernel_ms"])
+        r.free()
+    ctx.synchronize()
+    elapsed = barrier_max(pg, local, time.perf_counter() - t0)
+    pairs = total
+    algo = 4 * pairs + 8 * (K + 1) + 4 * S + 16 * K * 3
+    kavg = sum(kms) / len(kms)
+    achieved = algo / (kavg / 1e3) / 1e9
+    out = {"metric": "hot-topic fan-out deliveries/sec (C4: 1k topics x 1M subscribers)",
+           "value": world * pairs * a.steps / elapsed, "unit": "deliveries/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u32", "data": "synthetic (C4 layout, SURVEY.md §8d)",
+           "config": {"workload": "C4: 1k hot topics x 1M subscribers, CSR subscriber lists", "pairs": pairs},
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_fanout_copy",
+                        "kernel_ms": kavg}}
+    m.free()
+    ctx.dev_free(d_tb)
+    ctx.dev_free(d_to)
+    idx.release()
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

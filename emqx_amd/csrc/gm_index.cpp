@@ -1,0 +1,359 @@
+// gm_index.cpp — host compiler: filter set -> flat level trie in HBM.
+//
+// Input is the set of route filters (emqx_route topics; wildcard ones are the
+// emqx_trie entries, apps/emqx/src/emqx_router.erl:112-125) plus, optionally,
+// each filter's subscriber list (the emqx_subscriber bag with the shard
+// indirection of emqx_broker.erl:147-165 / 445-454 already flattened).
+//
+// Filter ids are the lexicographic rank of the filter bytes (Erlang binary
+// order), so a row sorted by id equals lists:sort/1 of the reference result.
+//
+// Layout (gm_common.h): nodes are numbered breadth-first so the hot upper
+// levels of the trie are contiguous in HBM and stay resident in L2/MALL.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+
+#include "gm_internal.h"
+
+namespace gm {
+namespace {
+
+struct ViewHash {
+  size_t operator()(std::string_view s) const {
+    return size_t(hash_word_host(reinterpret_cast<const uint8_t*>(s.data()), s.size()));
+  }
+};
+
+uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 64;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// Open-addressing (u64 key -> u32) map with the same slot function as the
+// device edge table, so the host table IS the device table.
+struct EdgeMap {
+  std::vector<EdgeSlot> slots;
+  uint64_t mask = 0, used = 0;
+  explicit EdgeMap(uint64_t expect) {
+    uint64_t cap = next_pow2(expect * 2 + 2);
+    slots.assign(cap, EdgeSlot{EDGE_EMPTY, NONE, 0});
+    mask = cap - 1;
+  }
+  void grow() {
+    std::vector<EdgeSlot> old;
+    old.swap(slots);
+    uint64_t cap = old.size() * 2;
+    slots.assign(cap, EdgeSlot{EDGE_EMPTY, NONE, 0});
+    mask = cap - 1;
+    used = 0;
+    for (auto& s : old)
+      if (s.key != EDGE_EMPTY) put(s.key, s.child);
+  }
+  uint32_t get(uint64_t key) const {
+    for (uint64_t s = edge_slot(key, mask);; s = (s + 1) & mask) {
+      if (slots[s].key == key) return slots[s].child;
+      if (slots[s].key == EDGE_EMPTY) return NONE;
+    }
+  }
+  void put(uint64_t key, uint32_t child) {
+    if ((used + 1) * 2 > slots.size()) grow();
+    for (uint64_t s = edge_slot(key, mask);; s = (s + 1) & mask) {
+      if (slots[s].key == EDGE_EMPTY) {
+        slots[s] = EdgeSlot{key, child, 0};
+        ++used;
+        return;
+      }
+      if (slots[s].key == key) {
+        slots[s].child = child;
+        return;
+      }
+    }
+  }
+};
+
+struct HNode {
+  uint32_t plus_child = NONE, hash_child = NONE, end_filter = NONE, flags = 0;
+  uint32_t depth = 0;
+};
+
+bool less_bytes(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
+  int c = std::memcmp(a, b, std::min(la, lb));
+  if (c) return c < 0;
+  return la < lb;
+}
+
+// Parallel sort of filter indices by bytes (chunked std::sort + pairwise merges).
+void sort_filters(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t* fo) {
+  auto cmp = [&](uint32_t x, uint32_t y) {
+    return less_bytes(fb + fo[x], fo[x + 1] - fo[x], fb + fo[y], fo[y + 1] - fo[y]);
+  };
+  size_t n = ord.size();
+  unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (n < 200000 || T == 1) {
+    std::sort(ord.begin(), ord.end(), cmp);
+    return;
+  }
+  std::vector<size_t> b(T + 1);
+  for (unsigned k = 0; k <= T; ++k) b[k] = n * k / T;
+  {
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < T; ++k)
+      th.emplace_back([&, k] { std::sort(ord.begin() + b[k], ord.begin() + b[k + 1], cmp); });
+    for (auto& t : th) t.join();
+  }
+  for (size_t width = 1; width < T; width *= 2) {
+    std::vector<std::thread> th;
+    for (size_t k = 0; k + width < T; k += 2 * width) {
+      size_t lo = b[k], mid = b[k + width], hi = b[std::min<size_t>(k + 2 * width, T)];
+      th.emplace_back([&, lo, mid, hi] {
+        std::inplace_merge(ord.begin() + lo, ord.begin() + mid, ord.begin() + hi, cmp);
+      });
+    }
+    for (auto& t : th) t.join();
+  }
+}
+
+}  // namespace
+
+int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_t n, const uint64_t* sub_off,
+                const uint32_t* sub_ids, uint32_t* perm_out, emqx_gm_index** out) {
+  if (!out) return set_err(ctx, EMQX_GM_EINVAL, "index_build: out is NULL");
+  if (n && (!fb || !fo)) return set_err(ctx, EMQX_GM_EINVAL, "index_build: NULL filter buffers");
+  if (n >= 0x7FFFFFFFull) return set_err(ctx, EMQX_GM_EINVAL, "index_build: too many filters");
+  if (sub_off && !sub_ids && n && sub_off[n] > 0)
+    return set_err(ctx, EMQX_GM_EINVAL, "index_build: sub_ids is NULL");
+  for (uint64_t i = 0; i < n; ++i)
+    if (fo[i + 1] < fo[i]) return set_err(ctx, EMQX_GM_EINVAL, "index_build: filter offsets not monotone");
+
+  auto* idx = new emqx_gm_index;
+  idx->device = ctx->device;
+
+  // ---- 1. ids = lexicographic rank of unique filters
+  std::vector<uint32_t> ord(n);
+  std::iota(ord.begin(), ord.end(), 0u);
+  sort_filters(ord, fb, fo);
+  std::vector<uint32_t> id_of(n);
+  uint32_t nf = 0;
+  idx->foff.push_back(0);
+  for (uint64_t k = 0; k < n; ++k) {
+    uint32_t i = ord[k];
+    bool dup = false;
+    if (k) {
+      uint32_t p = ord[k - 1];
+      uint64_t lp = fo[p + 1] - fo[p], li = fo[i + 1] - fo[i];
+      dup = lp == li && std::memcmp(fb + fo[p], fb + fo[i], li) == 0;
+    }
+    if (!dup) {
+      idx->fbytes.insert(idx->fbytes.end(), fb + fo[i], fb + fo[i + 1]);
+      idx->foff.push_back(idx->fbytes.size());
+      ++nf;
+    }
+    id_of[i] = nf - 1;
+  }
+  if (perm_out)
+    for (uint64_t i = 0; i < n; ++i) perm_out[i] = id_of[i];
+
+  // ---- 2. intern words, build the level trie
+  std::unordered_map<std::string_view, uint32_t, ViewHash> wid;  // word -> arena offset
+  std::vector<uint8_t> arena;
+  std::vector<uint64_t> word_hash;  // per distinct word (parallel to insertion order)
+  std::vector<uint32_t> word_ids;
+  std::vector<uint32_t> word_len;
+  uint64_t total_words = 0;
+  for (uint32_t f = 0; f < nf; ++f) {
+    uint64_t a = idx->foff[f], b = idx->foff[f + 1];
+    total_words += 1 + std::count(idx->fbytes.begin() + a, idx->fbytes.begin() + b, uint8_t('/'));
+  }
+  wid.reserve(std::min<uint64_t>(total_words, 1u << 26));
+  EdgeMap edges(std::min<uint64_t>(total_words + 1, 1ull << 30));
+  std::vector<HNode> nodes(1);
+  nodes.reserve(std::min<uint64_t>(total_words + 1, 1ull << 30));
+  uint64_t n_wild = 0;
+  uint32_t max_depth = 0;
+  const uint8_t* FB = idx->fbytes.data();
+
+  auto intern = [&](const uint8_t* p, uint64_t len) -> uint32_t {
+    std::string_view v(reinterpret_cast<const char*>(p), len);
+    auto it = wid.find(v);
+    if (it != wid.end()) return it->second;
+    uint32_t off = uint32_t(arena.size());
+    arena.insert(arena.end(), p, p + len);
+    if (len == 0) arena.push_back(0);  // every word owns >= 1 byte: ids stay unique
+    wid.emplace(v, off);  // view into idx->fbytes (stable for the build)
+    word_hash.push_back(hash_word_host(p, len));
+    word_ids.push_back(off);
+    word_len.push_back(uint32_t(len));
+    if (arena.size() >= 0xFFFFFFF0ull) throw std::length_error("word arena exceeds 4 GiB");
+    return off;
+  };
+
+  for (uint32_t f = 0; f < nf; ++f) {
+    const uint8_t* s = FB + idx->foff[f];
+    uint64_t len = idx->foff[f + 1] - idx->foff[f];
+    uint32_t node = 0, depth = 0;
+    bool wild = false;
+    uint64_t ws = 0;
+    for (uint64_t i = 0; i <= len; ++i) {
+      if (i < len && s[i] != '/') continue;
+      const uint8_t* w = s + ws;
+      uint64_t wl = i - ws;
+      bool plus = wl == 1 && w[0] == '+', hash = wl == 1 && w[0] == '#';
+      wild |= plus || hash;
+      uint32_t id = intern(w, wl);
+      uint64_t key = edge_key(node, id);
+      uint32_t child = edges.get(key);
+      if (child == NONE) {
+        child = uint32_t(nodes.size());
+        if (child == NONE) throw std::length_error("too many trie nodes");
+        nodes.push_back(HNode{});
+        nodes.back().depth = depth + 1;
+        edges.put(key, child);
+        if (plus) { nodes[node].plus_child = child; nodes[node].flags |= NF_HAS_PLUS; }
+        else if (hash) nodes[node].hash_child = child;
+        else nodes[node].flags |= NF_HAS_EXACT;
+      }
+      node = child;
+      ++depth;
+      ws = i + 1;
+    }
+    nodes[node].end_filter = f;
+    if (wild) { nodes[node].flags |= NF_END_WILD; ++n_wild; }
+    max_depth = std::max(max_depth, depth);
+  }
+
+  // ---- 3. breadth-first renumbering (stable by creation order within a level)
+  uint64_t NN = nodes.size();
+  std::vector<uint64_t> per_depth(max_depth + 2, 0);
+  for (auto& nd : nodes) per_depth[nd.depth + 1]++;
+  for (size_t d = 1; d < per_depth.size(); ++d) per_depth[d] += per_depth[d - 1];
+  std::vector<uint32_t> newid(NN);
+  for (uint64_t i = 0; i < NN; ++i) newid[i] = uint32_t(per_depth[nodes[i].depth]++);
+  auto remap = [&](uint32_t x) { return x == NONE ? NONE : newid[x]; };
+
+  std::vector<Node> dnodes(NN);
+  for (uint64_t i = 0; i < NN; ++i) {
+    const HNode& h = nodes[i];
+    Node& d = dnodes[newid[i]];
+    d.plus_child = remap(h.plus_child);
+    d.hash_filter = h.hash_child == NONE ? NONE : nodes[h.hash_child].end_filter;
+    d.end_filter = h.end_filter;
+    d.flags = h.flags;
+  }
+  EdgeMap dedges(edges.used + 1);
+  for (auto& s : edges.slots)
+    if (s.key != EDGE_EMPTY)
+      dedges.put(edge_key(newid[uint32_t(s.key >> 32)], uint32_t(s.key)), newid[s.child]);
+
+  // ---- 4. word dictionary (open addressing by hash, verified by bytes)
+  uint64_t nw = word_ids.size();
+  uint64_t dcap = next_pow2(nw * 2 + 2);
+  std::vector<DictSlot> dict(dcap, DictSlot{0, 0, DICT_EMPTY_LEN});
+  for (uint64_t k = 0; k < nw; ++k) {
+    uint64_t s = dict_slot(word_hash[k], dcap - 1);
+    while (dict[s].len != DICT_EMPTY_LEN) s = (s + 1) & (dcap - 1);
+    dict[s] = DictSlot{word_hash[k], word_ids[k], word_len[k]};
+  }
+  uint32_t plus_word = NONE, hash_word = NONE;
+  {
+    auto it = wid.find(std::string_view("+", 1));
+    if (it != wid.end()) plus_word = it->second;
+    it = wid.find(std::string_view("#", 1));
+    if (it != wid.end()) hash_word = it->second;
+  }
+
+  // ---- 5. subscriber CSR per unique filter id (duplicates concatenated)
+  std::vector<uint64_t> soff(nf + 1, 0);
+  std::vector<uint32_t> sids;
+  if (sub_off) {
+    for (uint64_t i = 0; i < n; ++i) soff[id_of[i] + 1] += sub_off[i + 1] - sub_off[i];
+    for (uint32_t f = 0; f < nf; ++f) soff[f + 1] += soff[f];
+    sids.resize(soff[nf]);
+    std::vector<uint64_t> cur(soff.begin(), soff.end() - 1);
+    for (uint64_t i = 0; i < n; ++i) {
+      uint64_t c = sub_off[i + 1] - sub_off[i];
+      if (c) std::memcpy(&sids[cur[id_of[i]]], sub_ids + sub_off[i], c * 4);
+      cur[id_of[i]] += c;
+    }
+  }
+  std::vector<uint16_t> flen(nf);
+  for (uint32_t f = 0; f < nf; ++f) flen[f] = uint16_t(std::min<uint64_t>(idx->foff[f + 1] - idx->foff[f], 65535));
+
+  // ---- 6. upload: one allocation, 256-B aligned sections
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  size_t o_nodes = 0;
+  size_t o_dict = o_nodes + al(NN * sizeof(Node));
+  size_t o_edges = o_dict + al(dcap * sizeof(DictSlot));
+  size_t o_arena = o_edges + al(dedges.slots.size() * sizeof(EdgeSlot));
+  size_t o_soff = o_arena + al(arena.size() + 16);
+  size_t o_sids = o_soff + al(soff.size() * 8);
+  size_t o_flen = o_sids + al(sids.size() * 4 + 4);
+  size_t total = o_flen + al(flen.size() * 2 + 2);
+
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e == hipSuccess) e = hipMalloc(&idx->dev_base, total);
+  if (e != hipSuccess) {
+    delete idx;
+    return set_err(ctx, EMQX_GM_ENOMEM, std::string("index_build: hipMalloc: ") + hipGetErrorString(e));
+  }
+  idx->dev_bytes = total;
+  uint8_t* B = static_cast<uint8_t*>(idx->dev_base);
+  auto up = [&](size_t off, const void* src, size_t bytes) {
+    if (bytes && e == hipSuccess) e = hipMemcpy(B + off, src, bytes, hipMemcpyHostToDevice);
+  };
+  up(o_nodes, dnodes.data(), NN * sizeof(Node));
+  up(o_dict, dict.data(), dcap * sizeof(DictSlot));
+  up(o_edges, dedges.slots.data(), dedges.slots.size() * sizeof(EdgeSlot));
+  up(o_arena, arena.data(), arena.size());
+  up(o_soff, soff.data(), soff.size() * 8);
+  up(o_sids, sids.data(), sids.size() * 4);
+  up(o_flen, flen.data(), flen.size() * 2);
+  if (e != hipSuccess) {
+    hipFree(idx->dev_base);
+    delete idx;
+    return set_err(ctx, EMQX_GM_EDEVICE, std::string("index_build: upload: ") + hipGetErrorString(e));
+  }
+
+  IndexView& v = idx->view;
+  v.nodes = reinterpret_cast<const Node*>(B + o_nodes);
+  v.dict = reinterpret_cast<const DictSlot*>(B + o_dict);
+  v.edges = reinterpret_cast<const EdgeSlot*>(B + o_edges);
+  v.arena = B + o_arena;
+  v.sub_off = reinterpret_cast<const uint64_t*>(B + o_soff);
+  v.sub_ids = reinterpret_cast<const uint32_t*>(B + o_sids);
+  v.dict_mask = dcap - 1;
+  v.edge_mask = dedges.mask;
+  v.n_nodes = uint32_t(NN);
+  v.n_filters = nf;
+  v.plus_word = plus_word;
+  v.hash_word = hash_word;
+  idx->dev_flen = reinterpret_cast<uint16_t*>(B + o_flen);
+
+  emqx_gm_index_info_t& in = idx->info;
+  in.n_filters = nf;
+  in.n_wildcard = n_wild;
+  in.n_nodes = NN;
+  in.n_edges = dedges.used;
+  in.n_words = nw;
+  in.n_subs = sids.size();
+  in.device_bytes = total;
+  in.max_depth = max_depth;
+  in.trie_empty = n_wild == 0;
+  *out = idx;
+  return EMQX_GM_OK;
+}
+
+void free_index(emqx_gm_index* idx) {
+  if (!idx) return;
+  if (idx->dev_base) {
+    hipSetDevice(idx->device);
+    hipFree(idx->dev_base);
+  }
+  delete idx;
+}
+
+}  // namespace gm

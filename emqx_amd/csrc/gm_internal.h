@@ -1,0 +1,116 @@
+// gm_internal.h — context, index snapshot and device memory pool.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/emqx_gpu_match.h"
+#include "gm_common.h"
+
+namespace gm {
+
+// Caching device allocator: buffers are returned to a size-keyed free list and
+// reused, so steady-state batches do no hipMalloc/hipFree.
+class DevPool {
+ public:
+  explicit DevPool(int device) : device_(device) {}
+  ~DevPool();
+  void* alloc(size_t bytes);           // nullptr on failure
+  void release(void* p);
+  void trim();
+  size_t cached_bytes() const { return cached_; }
+
+ private:
+  int device_;
+  std::multimap<size_t, void*> free_;  // rounded size -> ptr
+  std::map<void*, size_t> live_;       // ptr -> rounded size
+  size_t cached_ = 0;
+};
+
+// RAII handle on a pool buffer.
+struct PoolBuf {
+  DevPool* pool = nullptr;
+  void* p = nullptr;
+  PoolBuf() = default;
+  PoolBuf(DevPool* pl, size_t bytes) : pool(pl), p(pl->alloc(bytes)) {}
+  PoolBuf(const PoolBuf&) = delete;
+  PoolBuf& operator=(const PoolBuf&) = delete;
+  PoolBuf(PoolBuf&& o) noexcept : pool(o.pool), p(o.p) { o.p = nullptr; }
+  PoolBuf& operator=(PoolBuf&& o) noexcept {
+    reset();
+    pool = o.pool;
+    p = o.p;
+    o.p = nullptr;
+    return *this;
+  }
+  ~PoolBuf() { reset(); }
+  void reset() {
+    if (p && pool) pool->release(p);
+    p = nullptr;
+  }
+  void* release_ownership() {
+    void* q = p;
+    p = nullptr;
+    return q;
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// Per-call scratch sizes of the match pipeline.
+constexpr int FAST_FC = 8;    // frontier capacity per lane (LDS)
+constexpr int FAST_MC = 16;   // match capacity per lane (LDS)
+constexpr uint32_t OVF_BIT = 0x80000000u;
+constexpr uint32_t CNT_MASK = 0x7FFFFFFFu;
+
+}  // namespace gm
+
+struct emqx_gm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::recursive_mutex mu;
+  std::string err;
+  gm::DevPool* pool = nullptr;
+  emqx_gm_match_stats stats{};
+  hipEvent_t ev[6]{};
+};
+
+struct emqx_gm_index {
+  std::atomic<int> refs{1};
+  int device = 0;
+  void* dev_base = nullptr;     // one allocation holding every table
+  size_t dev_bytes = 0;
+  gm::IndexView view{};
+  uint16_t* dev_flen = nullptr; // filter lengths (stats only), inside dev_base
+  // host copies
+  std::vector<uint8_t> fbytes;  // sorted unique filters
+  std::vector<uint64_t> foff;
+  emqx_gm_index_info_t info{};
+};
+
+namespace gm {
+// gm_index.cpp
+int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_t n, const uint64_t* sub_off,
+                const uint32_t* sub_ids, uint32_t* perm_out, emqx_gm_index** out);
+void free_index(emqx_gm_index* idx);
+// gm_match.hip
+int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+              uint32_t flags, emqx_gm_csr* out);
+int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
+               emqx_gm_csr* out);
+int set_err(emqx_gm_ctx* ctx, int code, const std::string& msg);
+}  // namespace gm
+
+#define GM_HIP(ctx, expr)                                                                     \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess)                                                                     \
+      return gm::set_err((ctx), EMQX_GM_EDEVICE,                                              \
+                         std::string(#expr) + ": " + hipGetErrorString(_e));                  \
+  } while (0)

@@ -1,0 +1,890 @@
+// gm_match.hip — CDNA4 (gfx950) kernels for batch topic matching and fan-out.
+//
+// Hot path (replaces emqx_trie:match/1 + emqx_router:match_routes/1,
+// apps/emqx/src/emqx_trie.erl:147-333, apps/emqx/src/emqx_router.erl:128-145):
+//
+//   k_match_fast   one lane per publish topic, 64 topics per wave (a tile).
+//                  Streams the topic bytes once, hashes each level word,
+//                  resolves it in the word dictionary (verified byte-for-byte),
+//                  and expands the NFA frontier over exact / '+' / '#' edges.
+//                  Frontier and match lists live in LDS.  Rows are sorted by
+//                  filter id in LDS and compacted per wave with a prefix scan
+//                  into a per-tile staging region.  Topics whose frontier or
+//                  match list exceeds the LDS capacity are queued for
+//                  k_slow_walk (no truncation, no CPU fallback).
+//   k_tile_sums / scan / k_assemble
+//                  count -> scan -> write: builds the CSR (row_off u64, ids u32).
+//   k_slow_walk / k_slow_emit / k_copy_slow
+//                  device slow path: one workgroup per overflowing topic,
+//                  frontier in HBM (bounded by the node count), matches as a
+//                  bitmap over filter ids, emitted in ascending id order.
+//
+// Fan-out (replaces emqx_broker:dispatch/2 + do_dispatch, emqx_broker.erl:
+// 296-322, 506-530): k_fanout_seglen -> scan -> k_fanout_copy, a load-balanced
+// CSR gather in which every workgroup owns a fixed range of OUTPUT elements,
+// so a 1M-subscriber row is split across many workgroups.
+//
+// Everything here is integer/byte work bound by HBM/L2 latency and bandwidth;
+// there is no MFMA.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "gm_internal.h"
+
+namespace gm {
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+
+// Byte reader over a lane's topic with a one-dword cache (aligned 4-B loads).
+struct ByteReader {
+  const uint8_t* base;
+  uint64_t cached_addr;
+  uint32_t cached;
+  __device__ __forceinline__ uint32_t get(uint64_t p) {
+    uint64_t a = p & ~3ull;
+    if (a != cached_addr) {
+      cached_addr = a;
+      cached = *reinterpret_cast<const uint32_t*>(base + a);
+    }
+    return (cached >> ((p & 3) * 8)) & 0xFFu;
+  }
+};
+
+__device__ __forceinline__ uint32_t dict_lookup(const IndexView& ix, uint64_t h, uint32_t len,
+                                                const uint8_t* tb, uint64_t ws) {
+  for (uint64_t s = dict_slot(h, ix.dict_mask);; s = (s + 1) & ix.dict_mask) {
+    const DictSlot d = ix.dict[s];
+    if (d.len == DICT_EMPTY_LEN) return NONE;
+    if (d.h == h && d.len == len) {
+      bool eq = true;
+      for (uint32_t i = 0; i < len; ++i) {
+        if (ix.arena[d.word + i] != tb[ws + i]) {
+          eq = false;
+          break;
+        }
+      }
+      if (eq) return d.word;
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t edge_lookup(const IndexView& ix, uint32_t parent, uint32_t word) {
+  const uint64_t key = edge_key(parent, word);
+  for (uint64_t s = edge_slot(key, ix.edge_mask);; s = (s + 1) & ix.edge_mask) {
+    const EdgeSlot e = ix.edges[s];
+    if (e.key == key) return e.child;
+    if (e.key == EDGE_EMPTY) return NONE;
+  }
+}
+
+// Tokenize the word starting at `pos`; returns its hash, length and first byte;
+// leaves `pos` on the '/' (or end).
+struct WordTok {
+  uint64_t h;
+  uint64_t start;
+  uint32_t len;
+  uint32_t b0;
+};
+__device__ __forceinline__ WordTok next_word(ByteReader& rd, uint64_t& pos, uint64_t end) {
+  WordTok w;
+  w.start = pos;
+  w.b0 = 0;
+  uint64_t h = HASH_SEED, chunk = 0;
+  uint32_t k = 0;
+  while (pos < end) {
+    const uint32_t b = rd.get(pos);
+    if (b == '/') break;
+    if (k == 0) w.b0 = b;
+    chunk |= uint64_t(b) << ((k & 7) * 8);
+    ++k;
+    ++pos;
+    if ((k & 7) == 0) {
+      h = hash_step(h, chunk);
+      chunk = 0;
+    }
+  }
+  if (k & 7) h = hash_step(h, chunk);
+  w.h = hash_final(h, k);
+  w.len = k;
+  return w;
+}
+
+// Literal lookup of a wildcard topic as a filter string: emqx_router:
+// lookup_routes(Topic) for a topic containing '+' / '#' words
+// (emqx_router.erl:128-134 with match_trie = []).
+__device__ uint32_t literal_lookup(const IndexView& ix, const uint8_t* tb, uint64_t pos, uint64_t end) {
+  ByteReader rd{tb, ~0ull, 0};
+  uint32_t node = 0;
+  for (;;) {
+    WordTok w = next_word(rd, pos, end);
+    const uint32_t wid = dict_lookup(ix, w.h, w.len, tb, w.start);
+    if (wid == NONE) return NONE;
+    node = edge_lookup(ix, node, wid);
+    if (node == NONE) return NONE;
+    if (pos >= end) break;
+    ++pos;
+  }
+  return ix.nodes[node].end_filter;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// ---------------------------------------------------------------------------
+// k_match_fast
+// ---------------------------------------------------------------------------
+template <bool EXACT>
+__global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ tb,
+                                                    const uint64_t* __restrict__ toff, uint64_t n,
+                                                    IndexView ix, uint32_t* __restrict__ cnt,
+                                                    uint32_t* __restrict__ stage,
+                                                    uint32_t* __restrict__ ovf_list,
+                                                    uint32_t* __restrict__ ovf_n,
+                                                    unsigned long long* __restrict__ probe_ctr,
+                                                    unsigned long long* __restrict__ wild_ctr) {
+  constexpr int FC = FAST_FC, MC = FAST_MC;
+  __shared__ uint32_t s_fr[2][FC][256];
+  __shared__ uint32_t s_m[MC][256];
+  const int tid = threadIdx.x;
+  const uint64_t t = uint64_t(blockIdx.x) * 256u + tid;
+  const bool valid = t < n;
+
+  uint32_t m_n = 0;
+  bool ovf = false, wild = false;
+  uint32_t probes = 0;
+
+  if (valid) {
+    uint64_t pos = toff[t];
+    const uint64_t end = toff[t + 1];
+    const uint64_t start = pos;
+    ByteReader rd{tb, ~0ull, 0};
+    int cur = 0;
+    uint32_t cur_n = 1;
+    s_fr[0][0][tid] = 0;  // virtual root (the atom `empty`, emqx_trie.erl:264)
+    bool dollar = false;
+    uint32_t level = 0;
+    for (;;) {
+      const WordTok w = next_word(rd, pos, end);
+      const bool last = pos >= end;
+      if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {
+        wild = true;  // emqx_topic:wildcard/1
+        break;
+      }
+      if (level == 0) dollar = w.len > 0 && w.b0 == '$';
+      if (cur_n) {
+        probes += 3 * cur_n;
+        const uint32_t wid = dict_lookup(ix, w.h, w.len, tb, w.start);
+        const int nb = cur ^ 1;
+        uint32_t nn = 0;
+        // '$'-topics skip the root-level '+' and '#' (emqx_trie.erl:271-278).
+        const bool rootskip = dollar && level == 0;
+        for (uint32_t i = 0; i < cur_n; ++i) {
+          const uint32_t nd = s_fr[cur][i][tid];
+          const Node node = ix.nodes[nd];
+          if (!rootskip) {
+            if (node.hash_filter != NONE) {  // 'match_#' at a visited prefix
+              if (m_n < MC) s_m[m_n][tid] = node.hash_filter;
+              ++m_n;
+            }
+            if (node.plus_child != NONE) {
+              if (nn < FC) s_fr[nb][nn][tid] = node.plus_child;
+              ++nn;
+            }
+          }
+          if (wid != NONE && (node.flags & NF_HAS_EXACT)) {
+            const uint32_t c = edge_lookup(ix, nd, wid);
+            if (c != NONE) {
+              if (nn < FC) s_fr[nb][nn][tid] = c;
+              ++nn;
+            }
+          }
+        }
+        if (nn > FC) {
+          ovf = true;
+          break;
+        }
+        cur = nb;
+        cur_n = nn;
+      }
+      if (last) break;
+      ++pos;
+      ++level;
+    }
+    if (wild) {
+      m_n = 0;
+      ovf = false;
+      if (EXACT) {
+        const uint32_t f = literal_lookup(ix, tb, start, end);
+        if (f != NONE) {
+          s_m[0][tid] = f;
+          m_n = 1;
+        }
+      }
+    } else if (!ovf) {
+      probes += 2 * cur_n + 1;
+      for (uint32_t i = 0; i < cur_n; ++i) {
+        const Node node = ix.nodes[s_fr[cur][i][tid]];
+        if (node.hash_filter != NONE) {
+          if (m_n < MC) s_m[m_n][tid] = node.hash_filter;
+          ++m_n;
+        }
+        if (node.end_filter != NONE &&
+            (EXACT || (node.flags & NF_END_WILD) || (dollar && level == 0))) {
+          if (m_n < MC) s_m[m_n][tid] = node.end_filter;
+          ++m_n;
+        }
+      }
+      if (m_n > MC) ovf = true;
+    }
+    if (!ovf) {
+      // insertion sort of the row by filter id (ids are lexicographic ranks)
+      for (uint32_t i = 1; i < m_n; ++i) {
+        const uint32_t x = s_m[i][tid];
+        uint32_t j = i;
+        while (j > 0 && s_m[j - 1][tid] > x) {
+          s_m[j][tid] = s_m[j - 1][tid];
+          --j;
+        }
+        s_m[j][tid] = x;
+      }
+    }
+  }
+
+  const uint32_t keep = (valid && !ovf) ? m_n : 0;
+  uint32_t total;
+  const uint32_t pre = wave_excl_scan(keep, total);
+  const uint64_t tile = t >> 6;
+  uint32_t* dst = stage + tile * (64ull * MC) + pre;
+  for (uint32_t k = 0; k < keep; ++k) dst[k] = s_m[k][tid];
+  if (valid) {
+    cnt[t] = ovf ? OVF_BIT : m_n;
+    if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
+  }
+  // per-wave counters (one atomic per wave)
+  uint32_t ptot;
+  wave_excl_scan(valid ? probes : 0, ptot);
+  const unsigned long long wb = __ballot(valid && wild);
+  if ((tid & 63) == 0) {
+    atomicAdd(probe_ctr, (unsigned long long)ptot);
+    if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// scan (u64, exclusive, n+1 outputs: out[n] = total)
+// ---------------------------------------------------------------------------
+constexpr int SCAN_T = 256, SCAN_V = 4, SCAN_B = SCAN_T * SCAN_V;
+
+template <class LOAD>
+__global__ __launch_bounds__(SCAN_T) void k_scan_local(LOAD load, uint64_t n_in, uint64_t n_out,
+                                                        uint64_t* __restrict__ out,
+                                                        uint64_t* __restrict__ block_sums) {
+  __shared__ uint64_t s_w[SCAN_T / 64];
+  const uint64_t base = uint64_t(blockIdx.x) * SCAN_B + threadIdx.x * SCAN_V;
+  uint64_t v[SCAN_V];
+  uint64_t run = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_V; ++k) {
+    const uint64_t i = base + k;
+    const uint64_t x = i < n_in ? load(i) : 0;
+    v[k] = run;
+    run += x;
+  }
+  // wave inclusive scan of per-thread totals
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t x = run;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  uint64_t wpre = 0;
+  for (int k = 0; k < wv; ++k) wpre += s_w[k];
+  const uint64_t tpre = wpre + x - run;
+#pragma unroll
+  for (int k = 0; k < SCAN_V; ++k) {
+    const uint64_t i = base + k;
+    if (i < n_out) out[i] = tpre + v[k];
+  }
+  if (threadIdx.x == SCAN_T - 1) block_sums[blockIdx.x] = wpre + x;
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_add(uint64_t* __restrict__ out, uint64_t n_out,
+                                                      const uint64_t* __restrict__ block_off) {
+  const uint64_t base = uint64_t(blockIdx.x) * SCAN_B;
+  const uint64_t add = block_off[blockIdx.x];
+  for (int k = threadIdx.x; k < SCAN_B; k += SCAN_T) {
+    const uint64_t i = base + k;
+    if (i < n_out) out[i] += add;
+  }
+}
+
+struct LoadU64 {
+  const uint64_t* p;
+  __device__ uint64_t operator()(uint64_t i) const { return p[i]; }
+};
+struct LoadCnt {  // masked match counts
+  const uint32_t* p;
+  __device__ uint64_t operator()(uint64_t i) const { return p[i] & CNT_MASK; }
+};
+struct LoadSegLen {  // subscriber count of the filter of match entry i
+  const uint32_t* ids;
+  const uint64_t* sub_off;
+  __device__ uint64_t operator()(uint64_t i) const {
+    const uint32_t f = ids[i];
+    return sub_off[f + 1] - sub_off[f];
+  }
+};
+
+// Exclusive scan of n_in loaded values into out[0..n_in] (out[n_in] = total).
+template <class LOAD>
+int scan_excl(emqx_gm_ctx* ctx, LOAD load, uint64_t n_in, uint64_t* out) {
+  const uint64_t n_out = n_in + 1;
+  const uint64_t nb = (n_out + SCAN_B - 1) / SCAN_B;
+  PoolBuf sums(ctx->pool, nb * 8 + 8), offs(ctx->pool, (nb + 1) * 8 + 8);
+  if (!sums.p || !offs.p) return set_err(ctx, EMQX_GM_ENOMEM, "scan: workspace");
+  hipLaunchKernelGGL(k_scan_local<LOAD>, dim3(nb), dim3(SCAN_T), 0, ctx->stream, load, n_in, n_out, out,
+                     sums.as<uint64_t>());
+  if (nb > 1) {
+    int rc = scan_excl(ctx, LoadU64{sums.as<uint64_t>()}, nb, offs.as<uint64_t>());
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(SCAN_T), 0, ctx->stream, out, n_out, offs.as<uint64_t>());
+  }
+  GM_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// assembly
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_tile_sums(const uint32_t* __restrict__ cnt, uint64_t n,
+                                                   uint64_t* __restrict__ tsum) {
+  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  const uint32_t c = t < n ? (cnt[t] & CNT_MASK) : 0;
+  uint32_t tot;
+  wave_excl_scan(c, tot);
+  if ((threadIdx.x & 63) == 0 && (t >> 6) * 64 < n) tsum[t >> 6] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_assemble(const uint32_t* __restrict__ cnt, uint64_t n,
+                                                  const uint64_t* __restrict__ tile_off,
+                                                  const uint32_t* __restrict__ stage,
+                                                  uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  const uint64_t tile = t >> 6;
+  if (tile * 64 >= n) return;  // wave-uniform
+  const uint32_t c = t < n ? cnt[t] : 0;
+  const bool slow = (c & OVF_BIT) != 0;
+  const uint32_t call = c & CNT_MASK, cf = slow ? 0 : call;
+  uint32_t tall, tfast;
+  const uint32_t pa = wave_excl_scan(call, tall);
+  const uint32_t pf = wave_excl_scan(cf, tfast);
+  const uint64_t base = tile_off[tile];
+  if (t < n) row_off[t] = base + pa;
+  if (t == n - 1) row_off[n] = base + pa + call;
+  const uint32_t* src = stage + tile * (64ull * FAST_MC);
+  if (__ballot(slow) == 0) {  // common case: the tile's staging region is its final region
+    for (uint32_t e = lane; e < tfast; e += 64) ids[base + e] = src[e];
+    return;
+  }
+  // Rows completed by the slow path leave gaps: map staged element e to its
+  // row r (largest r with pf[r] <= e) by binary lifting over lane shuffles.
+  for (uint32_t e0 = 0; e0 < tfast; e0 += 64) {
+    const uint32_t e = e0 + lane;
+    int lo = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1) {
+      const uint32_t v = __shfl(pf, lo + step, 64);
+      if (v <= e) lo += step;
+    }
+    const uint32_t pfl = __shfl(pf, lo, 64), pal = __shfl(pa, lo, 64);
+    if (e < tfast) ids[base + pal + (e - pfl)] = src[e];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// slow path
+// ---------------------------------------------------------------------------
+template <bool EXACT>
+__global__ __launch_bounds__(256) void k_slow_walk(const uint8_t* __restrict__ tb,
+                                                   const uint64_t* __restrict__ toff, IndexView ix,
+                                                   const uint32_t* __restrict__ list, uint64_t k0, uint64_t kn,
+                                                   uint32_t* __restrict__ fr_all, uint64_t fr_cap,
+                                                   uint32_t* __restrict__ bm_all, uint64_t bm_words,
+                                                   uint32_t* __restrict__ cnt, uint64_t* __restrict__ slow_cnt) {
+  const uint64_t k = k0 + blockIdx.x;
+  if (k >= kn) return;
+  const uint32_t t = list[k];
+  uint32_t* fr0 = fr_all + uint64_t(blockIdx.x) * 2 * fr_cap;
+  uint32_t* fr1 = fr0 + fr_cap;
+  uint32_t* bm = bm_all + uint64_t(blockIdx.x) * bm_words;
+  __shared__ uint32_t s_cur_n, s_nxt_n, s_wid, s_flags;  // flags: 1 last, 2 wild, 4 dollar
+  __shared__ uint64_t s_pos;
+  __shared__ uint32_t s_level;
+  __shared__ uint32_t s_red[256];
+  const int tid = threadIdx.x;
+  for (uint64_t i = tid; i < bm_words; i += 256) bm[i] = 0;
+  const uint64_t end = toff[t + 1];
+  if (tid == 0) {
+    s_pos = toff[t];
+    s_cur_n = 1;
+    s_nxt_n = 0;
+    s_level = 0;
+    s_flags = 0;
+    fr0[0] = 0;
+  }
+  __syncthreads();
+  uint32_t* cur = fr0;
+  uint32_t* nxt = fr1;
+  for (;;) {
+    if (tid == 0) {
+      ByteReader rd{tb, ~0ull, 0};
+      uint64_t pos = s_pos;
+      const WordTok w = next_word(rd, pos, end);
+      uint32_t fl = s_flags & 4u;
+      if (pos >= end) fl |= 1u;
+      if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) fl |= 2u;
+      if (s_level == 0 && w.len > 0 && w.b0 == '$') fl |= 4u;
+      s_flags = fl;
+      s_wid = (fl & 2u) ? NONE : dict_lookup(ix, w.h, w.len, tb, w.start);
+      s_pos = pos + 1;
+    }
+    __syncthreads();
+    const uint32_t fl = s_flags;
+    if (fl & 2u) break;
+    const uint32_t wid = s_wid, cn = s_cur_n;
+    const bool rootskip = (fl & 4u) && s_level == 0;
+    for (uint32_t i = tid; i < cn; i += 256) {
+      const uint32_t nd = cur[i];
+      const Node node = ix.nodes[nd];
+      if (!rootskip) {
+        if (node.hash_filter != NONE) atomicOr(&bm[node.hash_filter >> 5], 1u << (node.hash_filter & 31));
+        if (node.plus_child != NONE) nxt[atomicAdd(&s_nxt_n, 1u)] = node.plus_child;
+      }
+      if (wid != NONE && (node.flags & NF_HAS_EXACT)) {
+        const uint32_t c = edge_lookup(ix, nd, wid);
+        if (c != NONE) nxt[atomicAdd(&s_nxt_n, 1u)] = c;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      s_cur_n = s_nxt_n;
+      s_nxt_n = 0;
+      if (!(fl & 1u)) s_level = s_level + 1;
+    }
+    uint32_t* tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+    __syncthreads();
+    if (fl & 1u) break;
+  }
+  const uint32_t fl = s_flags;
+  if (fl & 2u) {  // wildcard topic: [] (trie) or the literal filter (routes)
+    __syncthreads();
+    for (uint64_t i = tid; i < bm_words; i += 256) atomicAnd(&bm[i], 0u);
+    __syncthreads();
+    if (EXACT && tid == 0) {
+      const uint32_t f = literal_lookup(ix, tb, toff[t], end);
+      if (f != NONE) atomicOr(&bm[f >> 5], 1u << (f & 31));
+    }
+  } else {
+    const uint32_t cn = s_cur_n;
+    const bool single = s_level == 0 && (fl & 4u);
+    for (uint32_t i = tid; i < cn; i += 256) {
+      const Node node = ix.nodes[cur[i]];
+      if (node.hash_filter != NONE) atomicOr(&bm[node.hash_filter >> 5], 1u << (node.hash_filter & 31));
+      if (node.end_filter != NONE && (EXACT || (node.flags & NF_END_WILD) || single))
+        atomicOr(&bm[node.end_filter >> 5], 1u << (node.end_filter & 31));
+    }
+  }
+  __syncthreads();
+  uint32_t c = 0;
+  for (uint64_t i = tid; i < bm_words; i += 256)
+    c += __popc(__hip_atomic_load(&bm[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  s_red[tid] = c;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) s_red[tid] += s_red[tid + s];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    slow_cnt[k] = s_red[0];
+    cnt[t] = OVF_BIT | s_red[0];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_slow_emit(uint64_t k0, uint64_t kn, const uint32_t* __restrict__ bm_all,
+                                                   uint64_t bm_words, const uint64_t* __restrict__ slow_off,
+                                                   uint32_t* __restrict__ slow_ids) {
+  const uint64_t k = k0 + blockIdx.x;
+  if (k >= kn) return;
+  const uint32_t* bm = bm_all + uint64_t(blockIdx.x) * bm_words;
+  __shared__ uint32_t s_w[4];
+  uint64_t out = slow_off[k];
+  for (uint64_t b = 0; b < bm_words; b += 256) {
+    const uint64_t i = b + threadIdx.x;
+    uint32_t w = i < bm_words ? bm[i] : 0;
+    uint32_t tot;
+    const uint32_t pre = wave_excl_scan(__popc(w), tot);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) s_w[wv] = tot;
+    __syncthreads();
+    uint32_t wpre = 0, all = 0;
+    for (int q = 0; q < 4; ++q) {
+      if (q < wv) wpre += s_w[q];
+      all += s_w[q];
+    }
+    uint64_t o = out + wpre + pre;
+    while (w) {
+      const int bit = __ffs(w) - 1;
+      slow_ids[o++] = uint32_t(i * 32 + bit);
+      w &= w - 1;
+    }
+    out += all;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_copy_slow(const uint32_t* __restrict__ list, uint64_t kn,
+                                                   const uint64_t* __restrict__ row_off,
+                                                   const uint64_t* __restrict__ slow_off,
+                                                   const uint32_t* __restrict__ slow_ids, uint32_t* __restrict__ ids) {
+  const uint64_t k = blockIdx.x;
+  if (k >= kn) return;
+  const uint32_t t = list[k];
+  const uint64_t dst = row_off[t], src = slow_off[k], len = slow_off[k + 1] - src;
+  for (uint64_t i = threadIdx.x; i < len; i += 256) ids[dst + i] = slow_ids[src + i];
+}
+
+// ---------------------------------------------------------------------------
+// fan-out
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fanout_rowoff(const uint64_t* __restrict__ m_off, uint64_t n,
+                                                       const uint64_t* __restrict__ seg_dst,
+                                                       uint64_t* __restrict__ out_off) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (i <= n) out_off[i] = seg_dst[m_off[i]];
+}
+
+constexpr int FAN_PER_BLOCK = 256 * 16;  // output elements per workgroup
+
+__global__ __launch_bounds__(256) void k_fanout_copy(const uint64_t* __restrict__ seg_dst, uint64_t nseg,
+                                                     const uint32_t* __restrict__ m_ids,
+                                                     const uint64_t* __restrict__ sub_off,
+                                                     const uint32_t* __restrict__ sub_ids, uint64_t total,
+                                                     uint32_t* __restrict__ out) {
+  const uint64_t lo = uint64_t(blockIdx.x) * FAN_PER_BLOCK;
+  if (lo >= total) return;
+  const uint64_t hi = min(total, lo + FAN_PER_BLOCK);
+  __shared__ uint64_t s_seg[2];
+  if (threadIdx.x < 2) {
+    // last segment whose start <= x (segments may be empty)
+    const uint64_t x = threadIdx.x == 0 ? lo : hi - 1;
+    uint64_t a = 0, b = nseg;  // seg_dst[a] <= x < seg_dst[b]
+    while (b - a > 1) {
+      const uint64_t m = (a + b) >> 1;
+      if (seg_dst[m] <= x) a = m;
+      else b = m;
+    }
+    s_seg[threadIdx.x] = a;
+  }
+  __syncthreads();
+  const uint64_t s0 = s_seg[0], s1 = s_seg[1];
+  for (uint64_t p = lo + threadIdx.x; p < hi; p += 256) {
+    uint64_t s = s0;
+    if (s1 != s0) {
+      uint64_t a = s0, b = s1 + 1;
+      while (b - a > 1) {
+        const uint64_t m = (a + b) >> 1;
+        if (seg_dst[m] <= p) a = m;
+        else b = m;
+      }
+      s = a;
+    }
+    const uint32_t f = m_ids[s];
+    out[p] = sub_ids[sub_off[f] + (p - seg_dst[s])];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// stats helper: sum of matched filter lengths (for algorithmic bytes)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_sum_flen(const uint32_t* __restrict__ ids, uint64_t nnz,
+                                                  const uint16_t* __restrict__ flen,
+                                                  unsigned long long* __restrict__ acc) {
+  uint64_t s = 0;
+  for (uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x; i < nnz; i += uint64_t(gridDim.x) * 256u)
+    s += flen[ids[i]];
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_down(s, d, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(acc, (unsigned long long)s);
+}
+
+// ---------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------
+namespace {
+
+int finish_csr(emqx_gm_ctx* ctx, uint64_t n, uint64_t nnz, PoolBuf& row_off, PoolBuf& ids, bool device_out,
+               emqx_gm_csr* out) {
+  out->n_rows = n;
+  out->nnz = nnz;
+  out->priv = nullptr;
+  if (device_out) {
+    out->row_off = static_cast<uint64_t*>(row_off.release_ownership());
+    out->ids = static_cast<uint32_t*>(ids.release_ownership());
+    out->on_device = 1;
+    return 0;
+  }
+  uint64_t* h_off = static_cast<uint64_t*>(malloc((n + 1) * 8));
+  uint32_t* h_ids = static_cast<uint32_t*>(malloc(nnz * 4 + 4));
+  if (!h_off || !h_ids) {
+    free(h_off);
+    free(h_ids);
+    return set_err(ctx, EMQX_GM_ENOMEM, "csr: host allocation");
+  }
+  GM_HIP(ctx, hipMemcpyAsync(h_off, row_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  if (nnz) GM_HIP(ctx, hipMemcpyAsync(h_ids, ids.p, nnz * 4, hipMemcpyDeviceToHost, ctx->stream));
+  GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  out->row_off = h_off;
+  out->ids = h_ids;
+  out->on_device = 0;
+  return 0;
+}
+
+float ev_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
+  return ms;
+}
+
+}  // namespace
+
+int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, const uint64_t* to_in, uint64_t n,
+              uint32_t flags, emqx_gm_csr* out) {
+  const bool dev_io = flags & EMQX_GM_DEVICE_IO;
+  const bool exact = flags & EMQX_GM_WITH_EXACT;
+  hipStream_t st = ctx->stream;
+  ctx->stats = emqx_gm_match_stats{};
+  ctx->stats.n_topics = n;
+
+  // ---- inputs on the device
+  PoolBuf d_tb_own, d_to_own;
+  const uint8_t* tb = tb_in;
+  const uint64_t* to = to_in;
+  if (!dev_io) {
+    const uint64_t bytes = n ? to_in[n] : 0;
+    for (uint64_t i = 0; i < n; ++i)
+      if (to_in[i + 1] < to_in[i]) return set_err(ctx, EMQX_GM_EINVAL, "match: topic offsets not monotone");
+    d_tb_own = PoolBuf(ctx->pool, bytes + 64);
+    d_to_own = PoolBuf(ctx->pool, (n + 1) * 8);
+    if (!d_tb_own.p || !d_to_own.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: input workspace");
+    if (bytes) GM_HIP(ctx, hipMemcpyAsync(d_tb_own.p, tb_in, bytes, hipMemcpyHostToDevice, st));
+    GM_HIP(ctx, hipMemsetAsync(static_cast<uint8_t*>(d_tb_own.p) + bytes, 0, 64, st));
+    GM_HIP(ctx, hipMemcpyAsync(d_to_own.p, to_in, (n + 1) * 8, hipMemcpyHostToDevice, st));
+    tb = d_tb_own.as<uint8_t>();
+    to = d_to_own.as<uint64_t>();
+  }
+
+  PoolBuf row_off(ctx->pool, (n + 1) * 8);
+  if (!row_off.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: row_off");
+  if (n == 0) {
+    GM_HIP(ctx, hipMemsetAsync(row_off.p, 0, 8, st));
+    PoolBuf ids(ctx->pool, 16);
+    return finish_csr(ctx, 0, 0, row_off, ids, dev_io, out);
+  }
+
+  const uint64_t n_tiles = (n + 63) / 64;
+  const uint64_t nblk = (n + 255) / 256;
+  PoolBuf cnt(ctx->pool, n * 4 + 16);
+  PoolBuf stage(ctx->pool, n_tiles * 64ull * FAST_MC * 4);
+  PoolBuf ovf_list(ctx->pool, n * 4 + 16);
+  PoolBuf ctrs(ctx->pool, 64);
+  PoolBuf tsum(ctx->pool, n_tiles * 8 + 8);
+  PoolBuf toff(ctx->pool, (n_tiles + 1) * 8);
+  if (!cnt.p || !stage.p || !ovf_list.p || !ctrs.p || !tsum.p || !toff.p)
+    return set_err(ctx, EMQX_GM_ENOMEM, "match: workspace");
+  uint32_t* ovf_n = ctrs.as<uint32_t>();
+  unsigned long long* probe_ctr = reinterpret_cast<unsigned long long*>(ctrs.as<uint8_t>() + 16);
+  unsigned long long* wild_ctr = reinterpret_cast<unsigned long long*>(ctrs.as<uint8_t>() + 24);
+  GM_HIP(ctx, hipMemsetAsync(ctrs.p, 0, 64, st));
+
+  GM_HIP(ctx, hipEventRecord(ctx->ev[0], st));
+  GM_HIP(ctx, hipEventRecord(ctx->ev[1], st));
+  if (exact)
+    hipLaunchKernelGGL(k_match_fast<true>, dim3(nblk), dim3(256), 0, st, tb, to, n, idx->view, cnt.as<uint32_t>(),
+                       stage.as<uint32_t>(), ovf_list.as<uint32_t>(), ovf_n, probe_ctr, wild_ctr);
+  else
+    hipLaunchKernelGGL(k_match_fast<false>, dim3(nblk), dim3(256), 0, st, tb, to, n, idx->view, cnt.as<uint32_t>(),
+                       stage.as<uint32_t>(), ovf_list.as<uint32_t>(), ovf_n, probe_ctr, wild_ctr);
+  GM_HIP(ctx, hipGetLastError());
+  GM_HIP(ctx, hipEventRecord(ctx->ev[2], st));
+
+  uint64_t h_ctr[4] = {0, 0, 0, 0};
+  GM_HIP(ctx, hipMemcpyAsync(h_ctr, ctrs.p, 32, hipMemcpyDeviceToHost, st));
+  GM_HIP(ctx, hipStreamSynchronize(st));
+  const uint64_t n_ovf = uint32_t(h_ctr[0]);
+  ctx->stats.probes = h_ctr[2];
+  ctx->stats.n_wildcard_topics = h_ctr[3];
+  ctx->stats.n_overflow = n_ovf;
+
+  // ---- slow path for overflowing rows
+  PoolBuf slow_off, slow_ids;
+  if (n_ovf) {
+    const uint64_t fr_cap = uint64_t(idx->view.n_nodes) + 1;
+    const uint64_t bm_words = (uint64_t(idx->view.n_filters) + 31) / 32 + 1;
+    const uint64_t per_blk = (2 * fr_cap + bm_words) * 4;
+    uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(256, (2ull << 30) / per_blk));
+    chunk = std::min(chunk, n_ovf);
+    PoolBuf fr(ctx->pool, chunk * 2 * fr_cap * 4);
+    PoolBuf bm(ctx->pool, chunk * bm_words * 4);
+    PoolBuf scnt(ctx->pool, n_ovf * 8 + 8);
+    std::vector<uint64_t> h_off(n_ovf + 1, 0);
+    if (!fr.p || !bm.p || !scnt.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: slow-path workspace");
+    slow_off = PoolBuf(ctx->pool, (n_ovf + 1) * 8);
+    uint64_t cap_ids = std::max<uint64_t>(1024, n_ovf * 64);
+    slow_ids = PoolBuf(ctx->pool, cap_ids * 4);
+    if (!slow_off.p || !slow_ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: slow-path output");
+    for (uint64_t k0 = 0; k0 < n_ovf; k0 += chunk) {
+      const uint64_t kn = std::min(n_ovf, k0 + chunk);
+      if (exact)
+        hipLaunchKernelGGL(k_slow_walk<true>, dim3(kn - k0), dim3(256), 0, st, tb, to, idx->view,
+                           ovf_list.as<uint32_t>(), k0, kn, fr.as<uint32_t>(), fr_cap, bm.as<uint32_t>(), bm_words,
+                           cnt.as<uint32_t>(), scnt.as<uint64_t>());
+      else
+        hipLaunchKernelGGL(k_slow_walk<false>, dim3(kn - k0), dim3(256), 0, st, tb, to, idx->view,
+                           ovf_list.as<uint32_t>(), k0, kn, fr.as<uint32_t>(), fr_cap, bm.as<uint32_t>(), bm_words,
+                           cnt.as<uint32_t>(), scnt.as<uint64_t>());
+      GM_HIP(ctx, hipGetLastError());
+      std::vector<uint64_t> c(kn - k0);
+      GM_HIP(ctx, hipMemcpyAsync(c.data(), scnt.as<uint64_t>() + k0, (kn - k0) * 8, hipMemcpyDeviceToHost, st));
+      GM_HIP(ctx, hipStreamSynchronize(st));
+      for (uint64_t k = k0; k < kn; ++k) h_off[k + 1] = h_off[k] + c[k - k0];
+      if (h_off[kn] > cap_ids) {  // grow the slow output buffer
+        uint64_t ncap = std::max(h_off[kn], cap_ids * 2);
+        PoolBuf nb(ctx->pool, ncap * 4);
+        if (!nb.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: slow-path output grow");
+        if (h_off[k0]) GM_HIP(ctx, hipMemcpyAsync(nb.p, slow_ids.p, h_off[k0] * 4, hipMemcpyDeviceToDevice, st));
+        slow_ids = std::move(nb);
+        cap_ids = ncap;
+      }
+      GM_HIP(ctx, hipMemcpyAsync(slow_off.as<uint64_t>() + k0, h_off.data() + k0, (kn - k0 + 1) * 8,
+                                 hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_slow_emit, dim3(kn - k0), dim3(256), 0, st, k0, kn, bm.as<uint32_t>(), bm_words,
+                         slow_off.as<uint64_t>(), slow_ids.as<uint32_t>());
+      GM_HIP(ctx, hipGetLastError());
+    }
+  }
+
+  // ---- count -> scan -> write
+  hipLaunchKernelGGL(k_tile_sums, dim3(nblk), dim3(256), 0, st, cnt.as<uint32_t>(), n, tsum.as<uint64_t>());
+  GM_HIP(ctx, hipGetLastError());
+  int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff.as<uint64_t>());
+  if (rc) return rc;
+  uint64_t nnz = 0;
+  GM_HIP(ctx, hipMemcpyAsync(&nnz, toff.as<uint64_t>() + n_tiles, 8, hipMemcpyDeviceToHost, st));
+  GM_HIP(ctx, hipStreamSynchronize(st));
+  PoolBuf ids(ctx->pool, nnz * 4 + 16);
+  if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
+  hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt.as<uint32_t>(), n, toff.as<uint64_t>(),
+                     stage.as<uint32_t>(), row_off.as<uint64_t>(), ids.as<uint32_t>());
+  GM_HIP(ctx, hipGetLastError());
+  if (n_ovf) {
+    hipLaunchKernelGGL(k_copy_slow, dim3(n_ovf), dim3(256), 0, st, ovf_list.as<uint32_t>(), n_ovf,
+                       row_off.as<uint64_t>(), slow_off.as<uint64_t>(), slow_ids.as<uint32_t>(), ids.as<uint32_t>());
+    GM_HIP(ctx, hipGetLastError());
+  }
+  GM_HIP(ctx, hipEventRecord(ctx->ev[3], st));
+  GM_HIP(ctx, hipEventSynchronize(ctx->ev[3]));
+  ctx->stats.nnz = nnz;
+  ctx->stats.match_kernel_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
+  ctx->stats.total_device_ms = ev_ms(ctx->ev[0], ctx->ev[3]);
+  return finish_csr(ctx, n, nnz, row_off, ids, dev_io, out);
+}
+
+int scan_lengths(emqx_gm_ctx* ctx, const uint64_t* len, uint64_t n, uint64_t* out) {
+  return scan_excl(ctx, LoadU64{len}, n, out);
+}
+
+int sum_filter_lengths(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint32_t* d_ids, uint64_t nnz,
+                       uint64_t* out) {
+  PoolBuf acc(ctx->pool, 16);
+  if (!acc.p) return set_err(ctx, EMQX_GM_ENOMEM, "sum_flen");
+  GM_HIP(ctx, hipMemsetAsync(acc.p, 0, 8, ctx->stream));
+  if (nnz) {
+    const uint64_t blocks = std::min<uint64_t>(4096, (nnz + 255) / 256);
+    hipLaunchKernelGGL(k_sum_flen, dim3(blocks), dim3(256), 0, ctx->stream, d_ids, nnz, idx->dev_flen,
+                       acc.as<unsigned long long>());
+    GM_HIP(ctx, hipGetLastError());
+  }
+  GM_HIP(ctx, hipMemcpyAsync(out, acc.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+  GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
+               emqx_gm_csr* out) {
+  const bool dev_out = flags & EMQX_GM_DEVICE_IO;
+  hipStream_t st = ctx->stream;
+  const uint64_t n = m->n_rows, nnz = m->nnz;
+  ctx->stats = emqx_gm_match_stats{};
+  ctx->stats.n_topics = n;
+  PoolBuf own_off, own_ids;
+  const uint64_t* m_off = m->row_off;
+  const uint32_t* m_ids = m->ids;
+  if (!m->on_device) {
+    for (uint64_t i = 0; i < nnz; ++i)
+      if (m->ids[i] >= idx->view.n_filters) return set_err(ctx, EMQX_GM_EINVAL, "fanout: filter id out of range");
+    own_off = PoolBuf(ctx->pool, (n + 1) * 8);
+    own_ids = PoolBuf(ctx->pool, nnz * 4 + 16);
+    if (!own_off.p || !own_ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "fanout: input workspace");
+    GM_HIP(ctx, hipMemcpyAsync(own_off.p, m->row_off, (n + 1) * 8, hipMemcpyHostToDevice, st));
+    if (nnz) GM_HIP(ctx, hipMemcpyAsync(own_ids.p, m->ids, nnz * 4, hipMemcpyHostToDevice, st));
+    m_off = own_off.as<uint64_t>();
+    m_ids = own_ids.as<uint32_t>();
+  }
+  PoolBuf seg_dst(ctx->pool, (nnz + 1) * 8);
+  PoolBuf row_off(ctx->pool, (n + 1) * 8);
+  if (!seg_dst.p || !row_off.p) return set_err(ctx, EMQX_GM_ENOMEM, "fanout: workspace");
+  GM_HIP(ctx, hipEventRecord(ctx->ev[0], st));
+  int rc = scan_excl(ctx, LoadSegLen{m_ids, idx->view.sub_off}, nnz, seg_dst.as<uint64_t>());
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_fanout_rowoff, dim3((n + 1 + 255) / 256), dim3(256), 0, st, m_off, n, seg_dst.as<uint64_t>(),
+                     row_off.as<uint64_t>());
+  GM_HIP(ctx, hipGetLastError());
+  uint64_t total = 0;
+  GM_HIP(ctx, hipMemcpyAsync(&total, seg_dst.as<uint64_t>() + nnz, 8, hipMemcpyDeviceToHost, st));
+  GM_HIP(ctx, hipStreamSynchronize(st));
+  PoolBuf ids(ctx->pool, total * 4 + 16);
+  if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "fanout: output");
+  GM_HIP(ctx, hipEventRecord(ctx->ev[1], st));
+  if (total) {
+    const uint64_t blocks = (total + FAN_PER_BLOCK - 1) / FAN_PER_BLOCK;
+    hipLaunchKernelGGL(k_fanout_copy, dim3(blocks), dim3(256), 0, st, seg_dst.as<uint64_t>(), nnz, m_ids,
+                       idx->view.sub_off, idx->view.sub_ids, total, ids.as<uint32_t>());
+    GM_HIP(ctx, hipGetLastError());
+  }
+  GM_HIP(ctx, hipEventRecord(ctx->ev[2], st));
+  GM_HIP(ctx, hipEventSynchronize(ctx->ev[2]));
+  ctx->stats.nnz = total;
+  ctx->stats.match_kernel_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
+  ctx->stats.total_device_ms = ev_ms(ctx->ev[0], ctx->ev[2]);
+  return finish_csr(ctx, n, total, row_off, ids, dev_out, out);
+}
+
+}  // namespace gm

@@ -1,0 +1,276 @@
+"""Host-side engine over the C ABI: contexts, index snapshots, batch match and fan-out.
+
+This is plumbing around the HIP library; every compute call runs the gfx950
+kernels in libemqx_gpu_match.so.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Iterable, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import _lib
+from ._lib import Csr, GpuMatchError, IndexInfo, MatchStats, Opts, check, lib
+
+BytesLike = Union[bytes, bytearray, str]
+
+
+def _b(s: BytesLike) -> bytes:
+    return s.encode() if isinstance(s, str) else bytes(s)
+
+
+def pack(strings: Iterable[BytesLike]) -> Tuple[np.ndarray, np.ndarray]:
+    """Concatenate byte strings -> (uint8 bytes padded by 64, uint64 offsets[n+1])."""
+    bs = [_b(s) for s in strings]
+    off = np.zeros(len(bs) + 1, np.uint64)
+    if bs:
+        np.cumsum([len(b) for b in bs], out=off[1:])
+    data = np.frombuffer(b"".join(bs) + b"\0" * 64, np.uint8).copy()
+    return data, off
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def _csr_to_numpy(csr: Csr) -> Tuple[np.ndarray, np.ndarray]:
+    n, nnz = csr.n_rows, csr.nnz
+    ro = np.ctypeslib.as_array(csr.row_off, shape=(n + 1,)).copy()
+    ids = np.ctypeslib.as_array(csr.ids, shape=(nnz,)).copy() if nnz else np.zeros(0, np.uint32)
+    return ro, ids
+
+
+@dataclass
+class DeviceCsr:
+    """A result CSR resident in HBM (owned by the library until free())."""
+    ctx: "Context"
+    csr: Csr
+
+    @property
+    def n_rows(self) -> int:
+        return int(self.csr.n_rows)
+
+    @property
+    def nnz(self) -> int:
+        return int(self.csr.nnz)
+
+    def to_host(self) -> Tuple[np.ndarray, np.ndarray]:
+        n, nnz = self.n_rows, self.nnz
+        ro = np.zeros(n + 1, np.uint64)
+        ids = np.zeros(max(nnz, 1), np.uint32)
+        self.ctx.memcpy_d2h(ro, C.cast(self.csr.row_off, C.c_void_p).value, (n + 1) * 8)
+        if nnz:
+            self.ctx.memcpy_d2h(ids, C.cast(self.csr.ids, C.c_void_p).value, nnz * 4)
+        return ro, ids[:nnz]
+
+    def free(self):
+        if self.csr.row_off or self.csr.ids:
+            check(lib().emqx_gm_csr_free(self.ctx.h, C.byref(self.csr)), self.ctx.h, "csr_free")
+
+    def __del__(self):
+        try:
+            if self.ctx.h:
+                self.free()
+        except Exception:
+            pass
+
+
+class Index:
+    """An immutable, reference-counted index snapshot resident in HBM."""
+
+    def __init__(self, ctx: "Context", handle, perm: np.ndarray):
+        self.ctx = ctx
+        self.h = handle
+        self.perm = perm
+
+    @property
+    def info(self) -> IndexInfo:
+        inf = IndexInfo()
+        check(lib().emqx_gm_index_info(self.h, C.byref(inf)), None, "index_info")
+        return inf
+
+    @property
+    def n_filters(self) -> int:
+        return int(self.info.n_filters)
+
+    def empty(self) -> bool:
+        """emqx_trie:empty/0: the index holds no wildcard filter."""
+        return bool(self.info.trie_empty)
+
+    def filter(self, fid: int) -> bytes:
+        p, n = C.c_void_p(), C.c_uint64()
+        check(lib().emqx_gm_index_filter(self.h, fid, C.byref(p), C.byref(n)), None, "index_filter")
+        return C.string_at(p, n.value) if n.value else b""
+
+    def filters(self) -> List[bytes]:
+        return [self.filter(i) for i in range(self.n_filters)]
+
+    def release(self):
+        if self.h:
+            lib().emqx_gm_index_release(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+class Context:
+    """One process per GPU: a context binds one HIP device and one stream."""
+
+    def __init__(self, device: int = 0):
+        o = Opts()
+        o.device = device
+        h = C.c_void_p()
+        rc = lib().emqx_gm_open(C.byref(o), C.byref(h))
+        if rc != _lib.OK:
+            raise GpuMatchError(rc, f"emqx_gm_open(device={device}) failed (no MI355X visible?)")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().emqx_gm_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ------------------------------------------------------------------ index
+    def build_index(self, filters, subs=None) -> Index:
+        """filters: sequence of bytes/str, or a packed (bytes, offsets) pair.
+        subs: optional per-filter subscriber lists, or a packed (offsets, ids) pair."""
+        fb, fo = filters if isinstance(filters, tuple) else pack(filters)
+        n = len(fo) - 1
+        so = si = None
+        if subs is not None:
+            if isinstance(subs, tuple):
+                so = np.ascontiguousarray(subs[0], np.uint64)
+                si = np.ascontiguousarray(subs[1], np.uint32)
+            else:
+                so = np.zeros(n + 1, np.uint64)
+                np.cumsum([len(s) for s in subs], out=so[1:])
+                si = np.fromiter((x for s in subs for x in s), np.uint32, count=int(so[-1]))
+            if len(si) == 0:
+                si = np.zeros(1, np.uint32)
+        perm = np.zeros(max(n, 1), np.uint32)
+        h = C.c_void_p()
+        check(lib().emqx_gm_index_build(self.h, _ptr(fb), _ptr(fo), n, _ptr(so), _ptr(si), _ptr(perm),
+                                        C.byref(h)), self.h, "index_build")
+        return Index(self, h, perm[:n])
+
+    # ------------------------------------------------------------------ match
+    def match(self, index: Index, topics, exact: bool = True) -> Tuple[np.ndarray, np.ndarray]:
+        """Batch emqx_router:match_routes/1 (exact=True) or emqx_trie:match/1
+        (exact=False).  Returns CSR (row_off uint64[n+1], filter ids uint32)."""
+        tb, to = topics if isinstance(topics, tuple) else pack(topics)
+        csr = Csr()
+        flags = _lib.WITH_EXACT if exact else 0
+        check(lib().emqx_gm_match(self.h, index.h, _ptr(tb), _ptr(to), len(to) - 1, flags, C.byref(csr)),
+              self.h, "match")
+        try:
+            return _csr_to_numpy(csr)
+        finally:
+            lib().emqx_gm_csr_free(self.h, C.byref(csr))
+
+    def match_device(self, index: Index, d_bytes: int, d_off: int, n: int, exact: bool = True) -> DeviceCsr:
+        """Inputs already in HBM (device pointers); the result stays in HBM."""
+        csr = Csr()
+        flags = _lib.DEVICE_IO | (_lib.WITH_EXACT if exact else 0)
+        check(lib().emqx_gm_match(self.h, index.h, C.c_void_p(d_bytes), C.c_void_p(d_off), n, flags,
+                                  C.byref(csr)), self.h, "match")
+        return DeviceCsr(self, csr)
+
+    def fanout(self, index: Index, row_off: np.ndarray, ids: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """emqx_broker:dispatch/2 over each row's matched filters -> subscriber CSR (multiset rows)."""
+        ro = np.ascontiguousarray(row_off, np.uint64)
+        ii = np.ascontiguousarray(ids, np.uint32)
+        if len(ii) == 0:
+            ii = np.zeros(1, np.uint32)
+        m = Csr()
+        m.n_rows = len(ro) - 1
+        m.nnz = int(ro[-1])
+        m.row_off = ro.ctypes.data_as(C.POINTER(C.c_uint64))
+        m.ids = ii.ctypes.data_as(C.POINTER(C.c_uint32))
+        m.on_device = 0
+        out = Csr()
+        check(lib().emqx_gm_fanout(self.h, index.h, C.byref(m), 0, C.byref(out)), self.h, "fanout")
+        try:
+            return _csr_to_numpy(out)
+        finally:
+            lib().emqx_gm_csr_free(self.h, C.byref(out))
+
+    def fanout_device(self, index: Index, matches: DeviceCsr) -> DeviceCsr:
+        out = Csr()
+        check(lib().emqx_gm_fanout(self.h, index.h, C.byref(matches.csr), _lib.DEVICE_IO, C.byref(out)),
+              self.h, "fanout")
+        return DeviceCsr(self, out)
+
+    # ------------------------------------------------------------------ misc
+    def stats(self) -> dict:
+        s = MatchStats()
+        check(lib().emqx_gm_last_stats(self.h, C.byref(s)), self.h, "last_stats")
+        return {k: getattr(s, k) for k, _ in MatchStats._fields_}
+
+    def synchronize(self):
+        check(lib().emqx_gm_synchronize(self.h), self.h, "synchronize")
+
+    def set_stream(self, hip_stream: int):
+        check(lib().emqx_gm_set_stream(self.h, C.c_void_p(hip_stream or None)), self.h, "set_stream")
+
+    def memcpy_d2h(self, dst: np.ndarray, src_ptr: int, nbytes: int):
+        check(lib().emqx_gm_memcpy(self.h, _ptr(dst), C.c_void_p(src_ptr), nbytes, 1), self.h, "memcpy")
+
+    def memcpy_h2d(self, dst_ptr: int, src: np.ndarray, nbytes: int):
+        check(lib().emqx_gm_memcpy(self.h, C.c_void_p(dst_ptr), _ptr(src), nbytes, 0), self.h, "memcpy")
+
+    def dev_alloc(self, nbytes: int) -> int:
+        p = C.c_void_p()
+        check(lib().emqx_gm_dev_alloc(self.h, nbytes, C.byref(p)), self.h, "dev_alloc")
+        return p.value
+
+    def dev_free(self, ptr: int):
+        lib().emqx_gm_dev_free(self.h, C.c_void_p(ptr))
+
+    def pool_trim(self):
+        lib().emqx_gm_pool_trim(self.h)
+
+    def matched_filter_bytes(self, index: Index, res: DeviceCsr) -> int:
+        out = C.c_uint64()
+        check(lib().emqx_gm_matched_filter_bytes(self.h, index.h, C.byref(res.csr), C.byref(out)), self.h,
+              "matched_filter_bytes")
+        return int(out.value)
+
+    def gen_topics_device(self, filter_codes: np.ndarray, seed: int, start: int, n: int) -> Tuple[int, int, int]:
+        """Generate topics [start, start+n) of the §8d workload on the device.
+        Returns (d_bytes, d_off, total_bytes); free both with dev_free."""
+        fc = np.ascontiguousarray(filter_codes, np.int16)
+        db, do, tot = C.c_void_p(), C.c_void_p(), C.c_uint64()
+        check(lib().emqx_gm_gen_topics(self.h, _ptr(fc) if len(fc) else None, len(fc), seed, start, n,
+                                       C.byref(db), C.byref(do), C.byref(tot)), self.h, "gen_topics")
+        return db.value, do.value, int(tot.value)
+
+
+# ---------------------------------------------------------------------- workload
+def gen_filter_codes(seed: int, n: int, wildcard_only: bool = False) -> np.ndarray:
+    out = np.zeros((n, 5), np.int16)
+    check(lib().emqx_gm_gen_filter_codes(seed, n, int(wildcard_only), _ptr(out)), None, "gen_filter_codes")
+    return out
+
+
+def render_codes(codes: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    codes = np.ascontiguousarray(codes, np.int16)
+    n = len(codes)
+    off = np.zeros(n + 1, np.uint64)
+    total = lib().emqx_gm_render_codes(_ptr(codes), n, None, _ptr(off))
+    data = np.zeros(int(total) + 64, np.uint8)
+    lib().emqx_gm_render_codes(_ptr(codes), n, _ptr(data), _ptr(off))
+    return data, off

@@ -1,0 +1,41 @@
+/*
+ * emqx_gm_ext.h — extensions of libemqx_gpu_match.so that are NOT part of the
+ * reference-facing boundary (emqx_gpu_match.h): the seeded synthetic workload
+ * of SURVEY.md §8d (generated on the device for the bench), device-buffer
+ * helpers for the Python host layer and bench, and roofline accounting.
+ */
+#ifndef EMQX_GM_EXT_H
+#define EMQX_GM_EXT_H
+
+#include "emqx_gpu_match.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Workload generator (spec: DESIGN.md "Workload generator").  codes: n x 5
+ * int16 per filter: word index, -1 '+', -2 '#', -3 absent level. */
+int emqx_gm_gen_filter_codes(uint64_t seed, uint64_t n, int wildcard_only, int16_t *codes);
+/* Render codes to bytes + offsets[n+1]; returns the byte count (pass NULL
+ * buffers to size). */
+uint64_t emqx_gm_render_codes(const int16_t *codes, uint64_t n, uint8_t *bytes, uint64_t *off);
+/* Generate topics [start, start+n) on the device; buffers come from the
+ * context pool (free with emqx_gm_dev_free).  The byte buffer is padded. */
+int emqx_gm_gen_topics(emqx_gm_ctx *ctx, const int16_t *filter_codes, uint64_t n_filters, uint64_t seed,
+                       uint64_t start, uint64_t n, uint8_t **d_bytes, uint64_t **d_off, uint64_t *total_bytes);
+
+/* Device buffers from the context pool. kind: 0 H2D, 1 D2H, 2 D2D. */
+int emqx_gm_dev_alloc(emqx_gm_ctx *ctx, uint64_t bytes, void **out);
+int emqx_gm_dev_free(emqx_gm_ctx *ctx, void *p);
+int emqx_gm_memcpy(emqx_gm_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind);
+int emqx_gm_pool_trim(emqx_gm_ctx *ctx);
+
+/* Sum of the byte lengths of the filters referenced by a device CSR (the
+ * Σ len(f) term of the algorithmic-bytes formula). */
+int emqx_gm_matched_filter_bytes(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const emqx_gm_csr *csr,
+                                 uint64_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EMQX_GM_EXT_H */

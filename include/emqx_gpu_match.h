@@ -1,0 +1,146 @@
+/*
+ * emqx_gpu_match.h — C ABI of libemqx_gpu_match.so, the MI355X batch
+ * topic-matching engine for EMQX's publish routing hot path.
+ *
+ * This is the drop-in boundary that a thin Erlang NIF (`emqx_gpu_match`,
+ * nif/emqx_gpu_match_nif.c) binds.  Each entry point replaces one reference
+ * interface (paths relative to the reference repo root):
+ *
+ *   emqx_gm_index_build   <- the emqx_trie / emqx_route tables as maintained by
+ *                            emqx_router:do_add_route/2 + emqx_trie:insert/1
+ *                            (apps/emqx/src/emqx_router.erl:112-125,
+ *                             apps/emqx/src/emqx_trie.erl:107-119) and the
+ *                            emqx_subscriber bag written by
+ *                            emqx_broker:do_subscribe/4 (emqx_broker.erl:147-165)
+ *   emqx_gm_index_info    <- emqx_trie:empty/0 (emqx_trie.erl:165-170)
+ *   emqx_gm_match         <- emqx_trie:match/1 (emqx_trie.erl:139-161) with
+ *                            flags = 0, or emqx_router:match_routes/1
+ *                            (emqx_router.erl:128-145) with
+ *                            EMQX_GM_WITH_EXACT; batched over many topics
+ *   emqx_gm_fanout        <- emqx_broker:dispatch/2 + do_dispatch/2,3 +
+ *                            subscribers/1 (emqx_broker.erl:296-322, 506-530)
+ *
+ * Result semantics (bit-exact with the reference, compared as sets):
+ *   - filter ids are the lexicographic rank of the filter bytes (Erlang binary
+ *     order = unsigned bytewise, prefix first), so each result row, sorted
+ *     ascending by id, is `lists:sort/1` of the reference's result list;
+ *   - flags = 0: row = emqx_trie:match(Topic) over the indexed filters that the
+ *     trie holds (wildcard filters; a single-word '$X' topic also returns a
+ *     non-wildcard '$X' filter, emqx_trie.erl:271-278); a wildcard topic gives
+ *     an empty row (emqx_trie.erl:149-158);
+ *   - EMQX_GM_WITH_EXACT: row = the distinct filters whose routes
+ *     match_routes(Topic) returns: the literal filter == Topic (also for a
+ *     wildcard Topic) plus the trie matches;
+ *   - fan-out rows are multisets: a subscriber of two matching filters is
+ *     delivered twice (emqx_persistent_session_SUITE.erl:705).
+ *
+ * Ownership: input buffers are borrowed for the duration of a call.  Result
+ * CSR buffers belong to the library until emqx_gm_csr_free().  Indexes are
+ * immutable and reference counted (RCU-style snapshot swap by the caller).
+ * Threading: a context may be used from several threads; calls on one context
+ * are serialised onto its HIP stream.  Errors: every call returns 0 or a
+ * negative EMQX_GM_E* code; nothing aborts the process; the message is in
+ * emqx_gm_last_error().
+ */
+#ifndef EMQX_GPU_MATCH_H
+#define EMQX_GPU_MATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EMQX_GM_ABI_VERSION 1
+
+#define EMQX_GM_OK            0
+#define EMQX_GM_EINVAL       -1 /* bad argument (badarg / function_clause)     */
+#define EMQX_GM_ENOMEM       -2 /* host or device allocation failed            */
+#define EMQX_GM_EDEVICE      -3 /* HIP runtime / device fault                  */
+#define EMQX_GM_EOVERFLOW    -4 /* a row exceeded the device result capacity    */
+#define EMQX_GM_EUNSUPPORTED -5 /* operation not available on this build       */
+
+/* emqx_gm_match / emqx_gm_fanout flags */
+#define EMQX_GM_WITH_EXACT 0x1u /* emqx_router:match_routes/1 semantics        */
+#define EMQX_GM_DEVICE_IO  0x2u /* inputs are device pointers; result stays on
+                                   the device (bench / multi-GPU path)         */
+
+typedef struct emqx_gm_ctx emqx_gm_ctx;
+typedef struct emqx_gm_index emqx_gm_index;
+
+typedef struct {
+  int32_t device;        /* HIP device ordinal; one process per GPU            */
+  uint32_t reserved0;
+  uint64_t reserved[7];
+} emqx_gm_opts;
+
+/* CSR result: row i = ids[row_off[i] .. row_off[i+1]) */
+typedef struct {
+  uint64_t n_rows;
+  uint64_t nnz;
+  uint64_t *row_off;     /* n_rows + 1 entries                                 */
+  uint32_t *ids;         /* nnz entries (filter ids or subscriber ids)          */
+  int32_t on_device;     /* 1: device pointers, 0: host pointers                */
+  int32_t reserved0;
+  void *priv;            /* library bookkeeping; do not touch                   */
+} emqx_gm_csr;
+
+typedef struct {
+  uint64_t n_filters;    /* unique filters; ids 0..n_filters-1                  */
+  uint64_t n_wildcard;   /* filters the trie holds (emqx_topic:wildcard/1)      */
+  uint64_t n_nodes;      /* level-trie nodes                                    */
+  uint64_t n_edges;      /* exact/'+'/'#' edges                                 */
+  uint64_t n_words;      /* distinct words                                      */
+  uint64_t n_subs;       /* subscriber entries (fan-out CSR)                    */
+  uint64_t device_bytes; /* resident index bytes in HBM                         */
+  uint32_t max_depth;    /* deepest filter (levels)                             */
+  int32_t trie_empty;    /* emqx_trie:empty/0 (no wildcard filter)              */
+} emqx_gm_index_info_t;
+
+typedef struct {
+  uint64_t n_topics;
+  uint64_t nnz;
+  uint64_t n_overflow;       /* rows completed by the device slow path        */
+  uint64_t n_wildcard_topics;
+  double match_kernel_ms;    /* device time of the fast match kernel          */
+  double total_device_ms;    /* device time of all kernels of the call         */
+  uint64_t algo_bytes;       /* algorithmic bytes of the fast kernel */
+  uint64_t probes;           /* NFA edge probes counted by the fast kernel     */
+} emqx_gm_match_stats;
+
+/* ---- context ---- */
+int emqx_gm_open(const emqx_gm_opts *opts, emqx_gm_ctx **out);
+int emqx_gm_close(emqx_gm_ctx *ctx);
+const char *emqx_gm_last_error(const emqx_gm_ctx *ctx);
+int emqx_gm_abi_version(void);
+/* Use an external HIP stream (e.g. torch's current stream); NULL = own. */
+int emqx_gm_set_stream(emqx_gm_ctx *ctx, void *hip_stream);
+int emqx_gm_synchronize(emqx_gm_ctx *ctx);
+
+/* ---- index (emqx_trie / emqx_route / emqx_subscriber snapshot) ---- */
+/* filters in any order (duplicates allowed: one id, subscriber lists are
+ * concatenated).  perm_out (optional, n_filters entries) receives the id of
+ * each input filter.  sub_off/sub_ids (optional) give each input filter's
+ * subscriber ids (CSR with n_filters+1 offsets). */
+int emqx_gm_index_build(emqx_gm_ctx *ctx, const uint8_t *filter_bytes, const uint64_t *filter_off,
+                        uint64_t n_filters, const uint64_t *sub_off, const uint32_t *sub_ids,
+                        uint32_t *perm_out, emqx_gm_index **out);
+int emqx_gm_index_retain(emqx_gm_index *idx);
+int emqx_gm_index_release(emqx_gm_index *idx);
+int emqx_gm_index_info(const emqx_gm_index *idx, emqx_gm_index_info_t *info);
+/* bytes of filter `id` (host memory owned by the index) */
+int emqx_gm_index_filter(const emqx_gm_index *idx, uint32_t id, const uint8_t **bytes, uint64_t *len);
+
+/* ---- hot path ---- */
+int emqx_gm_match(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const uint8_t *topic_bytes,
+                  const uint64_t *topic_off, uint64_t n_topics, uint32_t flags, emqx_gm_csr *out);
+int emqx_gm_fanout(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const emqx_gm_csr *matches,
+                   uint32_t flags, emqx_gm_csr *out_subs);
+int emqx_gm_csr_free(emqx_gm_ctx *ctx, emqx_gm_csr *csr);
+int emqx_gm_last_stats(const emqx_gm_ctx *ctx, emqx_gm_match_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EMQX_GPU_MATCH_H */

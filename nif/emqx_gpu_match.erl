@@ -1,0 +1,41 @@
+%% emqx_gpu_match — Erlang side of the GPU topic-matching NIF (spec + wrapper).
+%% Built only where erl_nif.h / erlc exist (not in this container).
+%%
+%% Drop-in points (reference paths under apps/emqx/src):
+%%   match_trie/1 in emqx_router.erl:137-141  -> match_batch/2
+%%   match_routes/1 in emqx_router.erl:128-134 -> match_routes_batch/2 (+ lookup_routes/1 per filter)
+%%   dispatch/2 in emqx_broker.erl:296-306    -> fanout_batch/2
+%% On {error, _} the wrapper falls back to emqx_trie:match/1 (SURVEY.md §8b).
+-module(emqx_gpu_match).
+
+-export([load_index/1, match_batch/2, match_routes_batch/2, fanout_batch/2, empty/1]).
+-export([match/2]).
+
+-on_load(init/0).
+
+init() ->
+    Priv = case code:priv_dir(emqx) of {error, _} -> "priv"; D -> D end,
+    erlang:load_nif(filename:join(Priv, "emqx_gpu_match_nif"), 0).
+
+-spec load_index([binary()]) -> {ok, reference()} | {error, term()}.
+load_index(_Filters) -> erlang:nif_error(nif_not_loaded).
+
+-spec match_batch(reference(), [binary()]) -> [[binary()]] | {error, term()}.
+match_batch(_Index, _Topics) -> erlang:nif_error(nif_not_loaded).
+
+-spec match_routes_batch(reference(), [binary()]) -> [[binary()]] | {error, term()}.
+match_routes_batch(_Index, _Topics) -> erlang:nif_error(nif_not_loaded).
+
+-spec fanout_batch(reference(), [binary()]) -> [[non_neg_integer()]] | {error, term()}.
+fanout_batch(_Index, _Topics) -> erlang:nif_error(nif_not_loaded).
+
+-spec empty(reference()) -> boolean().
+empty(_Index) -> erlang:nif_error(nif_not_loaded).
+
+%% emqx_trie:match/1 drop-in with fallback.
+-spec match(reference(), binary()) -> [binary()].
+match(Index, Topic) when is_binary(Topic) ->
+    case match_batch(Index, [Topic]) of
+        [Row] -> Row;
+        {error, _} -> emqx_trie:match(Topic)
+    end.

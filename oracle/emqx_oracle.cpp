@@ -171,10 +171,12 @@ std::vector<std::string> do_compact(const std::vector<Word>& ws) {
   return acc;
 }
 
+// Per-thread lookup counter (no shared cache line between baseline threads).
+thread_local unsigned long long tl_lookups = 0;
+
 struct Trie {
   bool compact;
   std::map<std::pair<std::string, int>, long long> tab;  // ETS ordered_set
-  std::atomic<unsigned long long> lookups{0};
 
   explicit Trie(bool c) : compact(c) {}
 
@@ -215,13 +217,13 @@ struct Trie {
   bool empty() const { return tab.empty(); }
 
   void lookup_topic(const std::string& t, std::vector<std::string>& acc) {
-    lookups.fetch_add(1, std::memory_order_relaxed);
+    ++tl_lookups;
     auto it = tab.find({t, 1});
     if (it != tab.end() && it->second > 0) acc.push_back(t);
   }
   bool has_prefix(const Prefix& p) {
     if (p.empty_atom) return true;
-    lookups.fetch_add(1, std::memory_order_relaxed);
+    ++tl_lookups;
     auto it = tab.find({p.s, 0});
     return it != tab.end() && it->second > 0;
   }
@@ -545,9 +547,9 @@ void orc_trie_delete(void* t, const char* s, uint64_t n) { static_cast<Trie*>(t)
 int orc_trie_empty(void* t) { return static_cast<Trie*>(t)->empty() ? 1 : 0; }
 StrList* orc_trie_match(void* t, const char* s, uint64_t n, uint64_t* lookups) {
   auto* tr = static_cast<Trie*>(t);
-  uint64_t before = tr->lookups.load();
+  uint64_t before = tl_lookups;
   auto* l = new StrList{tr->match(std::string(s, n))};
-  if (lookups) *lookups = tr->lookups.load() - before;
+  if (lookups) *lookups = tl_lookups - before;
   return l;
 }
 // Table dump (key bytes, kind 0|1, count), in ordered_set order.
@@ -636,10 +638,10 @@ Csr* orc_match_batch(void* router, int mode, const uint8_t* tb, const uint64_t* 
     for (uint64_t i = lo; i < hi; ++i) {
       std::string t(reinterpret_cast<const char*>(tb + toff[i]), toff[i + 1] - toff[i]);
       std::vector<std::string> m;
-      uint64_t before = r->trie.lookups.load(std::memory_order_relaxed);
+      uint64_t before = tl_lookups;
       if (mode == 0) m = r->trie.empty() ? std::vector<std::string>() : r->trie.match(t);
       else m = r->match_route_filters(t);
-      lk[i] = r->trie.lookups.load(std::memory_order_relaxed) - before;  // approximate under threads
+      lk[i] = tl_lookups - before;
       cnt[i] = m.size();
       if (want_ids) {
         auto& row = rows[i];

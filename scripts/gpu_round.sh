@@ -1,0 +1,29 @@
+#!/bin/bash
+# One GPU-box session: parity tests -> smoke -> bench (+ optional rocprof).
+# Stops at the first abort/segfault/timeout (exit >= 124 or signal) per the pool rules.
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "ABORTING after $name"; exit $rc; fi
+  return $rc
+}
+MODE=${1:-all}
+if [ "$MODE" = all ] || [ "$MODE" = test ]; then
+  step pytest_gpu 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+  step smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
+  step bench_small 300 python -u bench.py --topics 10000000 --steps 3 --warmup 1 --cpu-seconds 5
+  step bench 600 python -u bench.py
+fi
+if [ "$MODE" = prof ]; then
+  cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+  step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu
+fi

@@ -1,0 +1,302 @@
+"""GPU parity: the HIP hot path (through the C ABI) vs the CPU oracle.
+
+Bit-exact for every row: filter ids are lexicographic ranks, rows sorted, so
+equality of (row_off, ids) is equality of lists:sort/1 of the reference result.
+"""
+
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from emqx_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _oracle_rows(orc, filters, topics, mode, compact=True):
+    r = orc.Router(compact)
+    for f in filters:
+        if mode == 1:
+            r.add_route(f)
+        else:  # emqx_trie semantics: the index holds exactly what was inserted
+            r.trie.insert(f)
+    ro, ids, _ = r.match_batch(topics, filters, mode=mode)
+    return ro, ids
+
+
+def _check(ctx, orc, filters, topics, exact=True):
+    filters = sorted(set(f if isinstance(f, bytes) else f.encode() for f in filters))
+    topics = [t if isinstance(t, bytes) else t.encode() for t in topics]
+    idx = ctx.build_index(filters)
+    ro, ids = ctx.match(idx, topics, exact=exact)
+    oro, oids = _oracle_rows(orc, filters, topics, 1 if exact else 0)
+    if not (np.array_equal(ro, oro) and np.array_equal(ids, oids)):
+        for i in range(len(topics)):
+            g = ids[ro[i]:ro[i + 1]].tolist()
+            e = oids[oro[i]:oro[i + 1]].tolist()
+            assert g == e, (topics[i], [filters[x] for x in g], [filters[x] for x in e])
+    idx.release()
+    return ro, ids
+
+
+# ------------------------------------------------------------------ reference suite vectors
+def test_trie_suite_vectors(ctx, golden):
+    from emqx_amd import Trie
+    for case in golden["trie_cases"]:
+        t = Trie(ctx)
+        for op, arg in case["ops"]:
+            getattr(t, op)(arg)
+        for q in case["queries"]:
+            got = sorted(t.match(q["topic"]))
+            if "expect_len" in q:
+                assert len(got) == q["expect_len"], case["name"]
+            else:
+                assert got == sorted(x.encode() for x in q["expect"]), (case["name"], q, got)
+
+
+def test_router_match_routes_vector(ctx, golden):
+    from emqx_amd import Router
+    g = golden["router_match_routes"]
+    r = Router(ctx)
+    for f in g["routes"]:
+        r.add_route(f)
+    got = sorted(f for f, _ in r.match_routes(g["topic"]))
+    assert got == sorted(x.encode() for x in g["expect"])
+    for f in g["routes"]:
+        r.delete_route(f)
+    assert r.match_routes(g["topic"]) == []
+
+
+def test_broker_vectors(ctx, golden):
+    from emqx_amd import Broker
+    for case in golden["broker_cases"]:
+        if case.get("force_shard"):
+            continue
+        b = Broker(ctx)
+        for topic, pid in case["subs"]:
+            b.subscribe(topic, pid)
+        if not case["subs"]:
+            b.router.add_route("unrelated/+")
+        assert sorted(b.publish(case["publish"])) == sorted(case["expect_deliveries"]), case["name"]
+
+
+def test_broker_shard_path(ctx):
+    """More than 1,024 subscribers: the shard indirection is flattened and every
+    subscriber is delivered exactly once (t_shard, emqx_broker_SUITE.erl:311-330)."""
+    from emqx_amd import Broker
+    b = Broker(ctx, schedulers=2)
+    for p in range(1, 3001):
+        b.subscribe("topic", p)
+    b.subscribe("top/+", 9)
+    assert sorted(b.publish("topic")) == list(range(1, 3001))
+    assert b.publish("top/x") == [9]
+
+
+# ------------------------------------------------------------------ randomised vs oracle
+ALPH = ["a", "b", "c", "", "$x", "$SYS", "dd", "l0w1"]
+
+
+def _rand_filter(rng):
+    n = rng.randint(1, 5)
+    ws = [rng.choice(ALPH) for _ in range(n)]
+    k = rng.random()
+    if k < 0.2:
+        return "/".join(ws)
+    if k < 0.6:
+        return "/".join("+" if rng.random() < 1 / 3 else w for w in ws)
+    if k < 0.8:
+        return "/".join(ws[: rng.randint(0, n)] + ["#"])
+    return "/".join(["+" if rng.random() < 1 / 3 else w for w in ws] + ["#"])
+
+
+def _rand_topic(rng):
+    n = rng.randint(1, 6)
+    ws = [rng.choice(ALPH) for _ in range(n)]
+    if rng.random() < 0.05:
+        ws[rng.randrange(n)] = rng.choice(["+", "#"])
+    return "/".join(ws)
+
+
+@pytest.mark.parametrize("exact", [True, False], ids=["match_routes", "trie_match"])
+def test_random_small_sets(ctx, orc, exact):
+    rng = random.Random(11)
+    for _ in range(40):
+        filters = [_rand_filter(rng) for _ in range(rng.randint(1, 60))]
+        topics = [_rand_topic(rng) for _ in range(300)]
+        _check(ctx, orc, filters, topics, exact)
+
+
+def test_edge_cases(ctx, orc):
+    filters = ["#", "+", "+/+", "/#", "/+", "$SYS/#", "$SYS/+", "$SYS", "sport/", "sport/+", "sport/#", "a/+/#",
+               "", "+/#", "a//b", "a/+/b", "x/y", "a/+", "a/#/b", "é/+"]
+    topics = ["", "/", "//", "sport", "sport/", "sport/x", "$SYS", "$SYS/", "$SYS/a", "$SYS/a/b", "a", "a/b",
+              "a//b", "a/x/b", "x/y", "+", "#", "a/+", "a/#", "a/#/b", "sport/+", "$x", "é/1", "a/b/c/d/e/f"]
+    for exact in (True, False):
+        _check(ctx, orc, filters, topics, exact)
+
+
+def test_deep_and_long_topics(ctx, orc):
+    deep = "/".join("abcdefghijklmnopqrstuvwxyz")
+    filters = ["#", deep + "/#", deep + "/+", "+/" * 26 + "#", "/".join(["+"] * 1000), "/".join(["x"] * 999) + "/#",
+               "w" * 5000 + "/+", "w" * 5000]
+    topics = [deep, deep + "/1", "/".join(["x"] * 1000), "/".join(["x"] * 5000), "w" * 5000 + "/q", "w" * 5000,
+              "w" * 4999 + "/q", "/".join(["y"] * 1000)]
+    for exact in (True, False):
+        _check(ctx, orc, filters, topics, exact)
+
+
+def test_overflow_slow_path(ctx, orc):
+    """Frontier > LDS capacity and > 16 matches per row go through the device
+    slow path; results stay exact."""
+    lv = ["a", "b", "c", "d", "e", "f"]
+    filters = set()
+    for m in range(1 << 6):  # every '+'/word mix over 6 levels, plus '#' tails
+        ws = ["+" if (m >> i) & 1 else lv[i] for i in range(6)]
+        filters.add("/".join(ws))
+        filters.add("/".join(ws[:3]) + "/#")
+        filters.add("/".join(ws[:5]) + "/#")
+    topics = ["a/b/c/d/e/f", "a/b/c/d/e", "a/b/c", "a/x/c/d/e/f", "q/b/c/d/e/f", "a/b/c/d/e/f/g", "+/b"] * 20
+    ro, ids = _check(ctx, orc, sorted(filters), topics, True)
+    st = ctx.stats()
+    assert int(np.max(np.diff(ro))) > 16
+    _check(ctx, orc, sorted(filters), topics, False)
+
+
+def test_hash_collision_safety(ctx, orc):
+    """Words that share prefixes / lengths / 8-byte chunks never alias."""
+    ws = ["a" * k for k in range(1, 20)] + ["ab" * k for k in range(1, 12)] + ["\x00", "\x00\x00", "a\x00", "\xff"]
+    filters = [w + "/+" for w in ws] + [w + "/#" for w in ws[::2]] + ws
+    topics = [w + "/z" for w in ws] + ws + [w + "b/z" for w in ws]
+    _check(ctx, orc, filters, topics, True)
+
+
+def test_empty_index_and_empty_batch(ctx, orc):
+    idx = ctx.build_index([])
+    ro, ids = ctx.match(idx, ["a/b", "", "#"], exact=True)
+    assert ro.tolist() == [0, 0, 0, 0] and len(ids) == 0
+    assert idx.empty()
+    ro, ids = ctx.match(idx, [], exact=True)
+    assert ro.tolist() == [0]
+    idx.release()
+
+
+# ------------------------------------------------------------------ workload configs
+def test_device_topic_generator_matches_oracle(ctx, orc):
+    from emqx_amd.engine import gen_filter_codes
+    codes = gen_filter_codes(1, 1000)
+    n = 20000
+    db, do, tot = ctx.gen_topics_device(codes, 5, 1234, n)
+    off = np.zeros(n + 1, np.uint64)
+    ctx.memcpy_d2h(off, do, (n + 1) * 8)
+    data = np.zeros(tot, np.uint8)
+    ctx.memcpy_d2h(data, db, tot)
+    ob, oo = orc.render_codes(orc.gen_topic_codes(5, 1234, n, codes))
+    assert np.array_equal(off, oo) and bytes(data) == bytes(ob[:oo[-1]])
+    ctx.dev_free(db)
+    ctx.dev_free(do)
+
+
+@pytest.mark.parametrize("wild_only", [False, True], ids=["C1-mix", "C2-wildcard"])
+def test_config_subsample_vs_oracle(ctx, orc, wild_only):
+    """C1 (10k mixed filters) and C2-shaped (wildcard-only) filter sets, 200k
+    seeded topics generated on the device, every row vs the oracle."""
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    codes = gen_filter_codes(1, 10_000 if not wild_only else 50_000, wildcard_only=wild_only)
+    fb, fo = render_codes(codes)
+    filters = sorted(set(orc.unpack(fb, fo)))
+    idx = ctx.build_index(filters)
+    n = 200_000
+    db, do, tot = ctx.gen_topics_device(codes, 1, 0, n)
+    res = ctx.match_device(idx, db, do, n, exact=True)
+    ro, ids = res.to_host()
+    tb, to = orc.render_codes(orc.gen_topic_codes(1, 0, n, codes))
+    r = orc.Router(True)
+    for f in filters:
+        r.add_route(f)
+    oro, oids, _ = r.match_batch((tb, to), filters, mode=1, nthreads=8)
+    assert np.array_equal(ro, oro) and np.array_equal(ids, oids)
+    res.free()
+    ctx.dev_free(db)
+    ctx.dev_free(do)
+    idx.release()
+
+
+def test_large_batch_properties(ctx, orc):
+    """A 4M-topic batch at C2 shape: sorted unique rows, ids in range, every
+    derived topic matches >= 1 filter, and a strided sample equals the oracle."""
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    codes = gen_filter_codes(2, 200_000, wildcard_only=True)
+    fb, fo = render_codes(codes)
+    filters = sorted(set(orc.unpack(fb, fo)))
+    idx = ctx.build_index(filters)
+    n = 4_000_000
+    db, do, tot = ctx.gen_topics_device(codes, 2, 0, n)
+    res = ctx.match_device(idx, db, do, n, exact=True)
+    ro, ids = res.to_host()
+    d = np.diff(ro.astype(np.int64))
+    assert (d >= 0).all() and int(ro[-1]) == len(ids)
+    assert (ids < len(filters)).all()
+    # rows strictly increasing
+    inner = np.ones(len(ids), bool)
+    inner[ro[:-1][d > 0].astype(np.int64)] = False
+    assert (np.diff(ids.astype(np.int64))[inner[1:]] > 0).all()
+    # sample vs oracle
+    sample = np.arange(0, n, 997)
+    tc = np.concatenate([orc.gen_topic_codes(2, int(i), 1, codes) for i in sample])
+    tb, to = orc.render_codes(tc)
+    r = orc.Router(True)
+    for f in filters:
+        r.add_route(f)
+    oro, oids, _ = r.match_batch((tb, to), filters, mode=1)
+    for k, i in enumerate(sample):
+        assert ids[ro[i]:ro[i + 1]].tolist() == oids[oro[k]:oro[k + 1]].tolist()
+    res.free()
+    ctx.dev_free(db)
+    ctx.dev_free(do)
+    idx.release()
+
+
+# ------------------------------------------------------------------ fan-out
+def test_fanout_vs_oracle(ctx, orc):
+    rng = np.random.default_rng(3)
+    filters = sorted({b"a/#", b"a/+", b"a/b", b"+/b", b"#", b"c/d", b"a/+/c"})
+    subs = [rng.integers(0, 1 << 20, size=int(rng.integers(0, 3000))).astype(np.uint32).tolist() for _ in filters]
+    idx = ctx.build_index(filters, subs=subs)
+    topics = [b"a/b", b"a/x", b"c/d", b"q", b"a/b/c", b"$SYS/a"] * 50
+    ro, ids = ctx.match(idx, topics, exact=True)
+    fro, fids = ctx.fanout(idx, ro, ids)
+    so = np.zeros(len(filters) + 1, np.uint64)
+    so[1:] = np.cumsum([len(s) for s in subs])
+    si = np.array([x for s in subs for x in s], np.uint32)
+    ero, eids = orc.fanout(ro, ids, so, si)
+    assert np.array_equal(fro, ero) and np.array_equal(fids, eids)
+    idx.release()
+
+
+def test_hot_fanout_c4_small(ctx, orc):
+    """C4 shape at 1/10 scale: 100 hot topics x 100k deliveries each."""
+    K, S = 100, 100_000
+    filters = [b"hot/#", b"hot/+/x/#"] + [b"hot/%d/x/y/z" % k for k in range(K)]
+    subs = [list(range(0, 60_000)), list(range(60_000, S - 10 * K))] + \
+           [list(range(S - 10 * K + 10 * k, S - 10 * K + 10 * k + 10)) for k in range(K)]
+    idx = ctx.build_index(filters, subs=subs)
+    topics = [b"hot/%d/x/y/z" % k for k in range(K)]
+    ro, ids = ctx.match(idx, topics, exact=True)
+    fro, fids = ctx.fanout(idx, ro, ids)
+    assert np.all(np.diff(fro) == 60_000 + (S - 10 * K - 60_000) + 10)
+    perm = idx.perm
+    so = np.zeros(len(filters) + 1, np.uint64)
+    order = np.argsort(perm)
+    ssorted = [subs[i] for i in order]
+    so[1:] = np.cumsum([len(s) for s in ssorted])
+    si = np.array([x for s in ssorted for x in s], np.uint32)
+    ero, eids = orc.fanout(ro, ids, so, si)
+    assert np.array_equal(fro, ero) and np.array_equal(fids, eids)
+    idx.release()
