@@ -77,6 +77,7 @@ SIGNATURES = {
     "emqx_gm_dev_free": (_i32, [_vp, _vp]),
     "emqx_gm_memcpy": (_i32, [_vp, _vp, _vp, _u64, _i32]),
     "emqx_gm_pool_trim": (_i32, [_vp]),
+    "emqx_gm_index_compile_host": (_i32, [_vp, _vp, _u64, _vp, _vp, _vp, C.POINTER(IndexInfo)]),
     "emqx_gm_matched_filter_bytes": (_i32, [_vp, _vp, C.POINTER(Csr), C.POINTER(_u64)]),
 }
 

@@ -256,6 +256,14 @@ int emqx_gm_matched_filter_bytes(emqx_gm_ctx* ctx, const emqx_gm_index* idx, con
   GM_GUARD_END(ctx)
 }
 
+int emqx_gm_index_compile_host(const uint8_t* fb, const uint64_t* fo, uint64_t n, const uint64_t* sub_off,
+                               const uint32_t* sub_ids, uint32_t* perm_out, emqx_gm_index_info_t* info) {
+  if (!info) return EMQX_GM_EINVAL;
+  GM_GUARD_BEGIN
+  return gm::build_index(nullptr, fb, fo, n, sub_off, sub_ids, perm_out, nullptr, info);
+  GM_GUARD_END(nullptr)
+}
+
 int emqx_gm_pool_trim(emqx_gm_ctx* ctx) {
   if (!ctx) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);

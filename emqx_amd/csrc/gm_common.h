@@ -31,22 +31,33 @@ constexpr uint32_t NF_END_WILD = 1u;   // end_filter is a wildcard filter (held 
 constexpr uint32_t NF_HAS_EXACT = 2u;  // node has children through non-wildcard words
 constexpr uint32_t NF_HAS_PLUS = 4u;
 
+// A child reference (Node::plus_child, EdgeSlot::child) carries the child's
+// NF_HAS_EXACT flag in bit 31, so a frontier entry knows whether an exact-edge
+// probe can hit before its node record has been read.
+constexpr uint32_t REF_X = 0x80000000u;
+constexpr uint32_t REF_MASK = 0x7FFFFFFFu;
+
+// Edge tables are partitioned by the parent's depth (0..EDGE_DEPTHS-2 each in
+// their own table, deeper parents share the last), so the small upper-level
+// tables stay resident in each XCD's L2.
+constexpr int EDGE_DEPTHS = 16;
+
 struct alignas(16) Node {
-  uint32_t plus_child;   // child through '+', or NONE
+  uint32_t plus_child;   // child ref through '+', or NONE
   uint32_t hash_filter;  // filter id of "<this prefix>/#" (or "#" at the root), or NONE
   uint32_t end_filter;   // filter id ending exactly here, or NONE
   uint32_t flags;
 };
 
 struct alignas(16) DictSlot {
-  uint64_t h;        // word hash
-  uint32_t word;     // word id == byte offset of the word in the arena
+  uint64_t head;     // first 8 bytes of the word, little endian, zero padded
   uint32_t len;      // word length; DICT_EMPTY_LEN marks an empty slot
+  uint32_t word;     // word id == byte offset of the word in the arena
 };
 
 struct alignas(16) EdgeSlot {
   uint64_t key;      // (parent << 32) | word id; EDGE_EMPTY marks an empty slot
-  uint32_t child;
+  uint32_t child;    // child ref (REF_X | node index)
   uint32_t pad;
 };
 
@@ -59,7 +70,8 @@ struct IndexView {
   const uint64_t* sub_off;
   const uint32_t* sub_ids;
   uint64_t dict_mask;
-  uint64_t edge_mask;
+  uint64_t etab_off[EDGE_DEPTHS];   // slot offset of each depth's table
+  uint64_t etab_mask[EDGE_DEPTHS];  // slots - 1
   uint32_t n_nodes;
   uint32_t n_filters;
   uint32_t plus_word;   // word id of "+" (NONE if no filter uses it)
@@ -84,6 +96,12 @@ GM_HD uint64_t hash_step(uint64_t h, uint64_t chunk) {
 GM_HD uint64_t hash_final(uint64_t h, uint64_t len) { return fmix64(h ^ (len * 0x9E3779B97F4A7C15ull)); }
 constexpr uint64_t HASH_SEED = 0x243F6A8885A308D3ull;
 
+inline uint64_t word_head_host(const uint8_t* p, uint64_t len) {
+  uint64_t c = 0;
+  for (uint64_t k = 0; k < 8 && k < len; ++k) c |= uint64_t(p[k]) << (8 * k);
+  return c;
+}
+
 inline uint64_t hash_word_host(const uint8_t* p, uint64_t len) {
   uint64_t h = HASH_SEED;
   uint64_t i = 0;
@@ -101,6 +119,7 @@ inline uint64_t hash_word_host(const uint8_t* p, uint64_t len) {
 }
 
 GM_HD uint64_t dict_slot(uint64_t h, uint64_t mask) { return (h ^ (h >> 29)) & mask; }
+GM_HD int edge_depth(uint32_t depth) { return depth < uint32_t(EDGE_DEPTHS) ? int(depth) : EDGE_DEPTHS - 1; }
 GM_HD uint64_t edge_key(uint32_t parent, uint32_t word) { return (uint64_t(parent) << 32) | word; }
 GM_HD uint64_t edge_slot(uint64_t key, uint64_t mask) { return fmix64(key) & mask; }
 

@@ -121,8 +121,8 @@ void sort_filters(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t*
 }  // namespace
 
 int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_t n, const uint64_t* sub_off,
-                const uint32_t* sub_ids, uint32_t* perm_out, emqx_gm_index** out) {
-  if (!out) return set_err(ctx, EMQX_GM_EINVAL, "index_build: out is NULL");
+                const uint32_t* sub_ids, uint32_t* perm_out, emqx_gm_index** out, emqx_gm_index_info_t* host_only) {
+  if (!out && !host_only) return set_err(ctx, EMQX_GM_EINVAL, "index_build: out is NULL");
   if (n && (!fb || !fo)) return set_err(ctx, EMQX_GM_EINVAL, "index_build: NULL filter buffers");
   if (n >= 0x7FFFFFFFull) return set_err(ctx, EMQX_GM_EINVAL, "index_build: too many filters");
   if (sub_off && !sub_ids && n && sub_off[n] > 0)
@@ -131,7 +131,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     if (fo[i + 1] < fo[i]) return set_err(ctx, EMQX_GM_EINVAL, "index_build: filter offsets not monotone");
 
   auto* idx = new emqx_gm_index;
-  idx->device = ctx->device;
+  idx->device = ctx ? ctx->device : -1;
 
   // ---- 1. ids = lexicographic rank of unique filters
   std::vector<uint32_t> ord(n);
@@ -164,6 +164,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   std::vector<uint64_t> word_hash;  // per distinct word (parallel to insertion order)
   std::vector<uint32_t> word_ids;
   std::vector<uint32_t> word_len;
+  std::vector<uint64_t> word_head;
   uint64_t total_words = 0;
   for (uint32_t f = 0; f < nf; ++f) {
     uint64_t a = idx->foff[f], b = idx->foff[f + 1];
@@ -188,6 +189,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     word_hash.push_back(hash_word_host(p, len));
     word_ids.push_back(off);
     word_len.push_back(uint32_t(len));
+    word_head.push_back(word_head_host(p, len));
     if (arena.size() >= 0xFFFFFFF0ull) throw std::length_error("word arena exceeds 4 GiB");
     return off;
   };
@@ -209,7 +211,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       uint32_t child = edges.get(key);
       if (child == NONE) {
         child = uint32_t(nodes.size());
-        if (child == NONE) throw std::length_error("too many trie nodes");
+        if (child >= REF_X) throw std::length_error("too many trie nodes (>= 2^31)");
         nodes.push_back(HNode{});
         nodes.back().depth = depth + 1;
         edges.put(key, child);
@@ -233,30 +235,50 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (size_t d = 1; d < per_depth.size(); ++d) per_depth[d] += per_depth[d - 1];
   std::vector<uint32_t> newid(NN);
   for (uint64_t i = 0; i < NN; ++i) newid[i] = uint32_t(per_depth[nodes[i].depth]++);
-  auto remap = [&](uint32_t x) { return x == NONE ? NONE : newid[x]; };
 
+  auto ref = [&](uint32_t old) -> uint32_t {  // child reference with the child's HAS_EXACT bit
+    if (old == NONE) return NONE;
+    return newid[old] | ((nodes[old].flags & NF_HAS_EXACT) ? REF_X : 0u);
+  };
   std::vector<Node> dnodes(NN);
   for (uint64_t i = 0; i < NN; ++i) {
     const HNode& h = nodes[i];
     Node& d = dnodes[newid[i]];
-    d.plus_child = remap(h.plus_child);
+    d.plus_child = ref(h.plus_child);
     d.hash_filter = h.hash_child == NONE ? NONE : nodes[h.hash_child].end_filter;
     d.end_filter = h.end_filter;
     d.flags = h.flags;
   }
-  EdgeMap dedges(edges.used + 1);
+  // edge tables partitioned by the parent's depth
+  std::vector<uint64_t> per_tab(EDGE_DEPTHS, 0);
   for (auto& s : edges.slots)
-    if (s.key != EDGE_EMPTY)
-      dedges.put(edge_key(newid[uint32_t(s.key >> 32)], uint32_t(s.key)), newid[s.child]);
+    if (s.key != EDGE_EMPTY) per_tab[edge_depth(nodes[uint32_t(s.key >> 32)].depth)]++;
+  std::vector<EdgeMap> tabs;
+  tabs.reserve(EDGE_DEPTHS);
+  for (int d = 0; d < EDGE_DEPTHS; ++d) tabs.emplace_back(per_tab[d] + 1);
+  for (auto& s : edges.slots)
+    if (s.key != EDGE_EMPTY) {
+      const uint32_t par = uint32_t(s.key >> 32);
+      tabs[edge_depth(nodes[par].depth)].put(edge_key(newid[par], uint32_t(s.key)), ref(s.child));
+    }
+  std::vector<EdgeSlot> dedges;
+  uint64_t etab_off[EDGE_DEPTHS], etab_mask[EDGE_DEPTHS], n_edges = 0;
+  for (int d = 0; d < EDGE_DEPTHS; ++d) {
+    etab_off[d] = dedges.size();
+    etab_mask[d] = tabs[d].mask;
+    n_edges += tabs[d].used;
+    dedges.insert(dedges.end(), tabs[d].slots.begin(), tabs[d].slots.end());
+    std::vector<EdgeSlot>().swap(tabs[d].slots);
+  }
 
   // ---- 4. word dictionary (open addressing by hash, verified by bytes)
   uint64_t nw = word_ids.size();
   uint64_t dcap = next_pow2(nw * 2 + 2);
-  std::vector<DictSlot> dict(dcap, DictSlot{0, 0, DICT_EMPTY_LEN});
+  std::vector<DictSlot> dict(dcap, DictSlot{0, DICT_EMPTY_LEN, 0});
   for (uint64_t k = 0; k < nw; ++k) {
     uint64_t s = dict_slot(word_hash[k], dcap - 1);
     while (dict[s].len != DICT_EMPTY_LEN) s = (s + 1) & (dcap - 1);
-    dict[s] = DictSlot{word_hash[k], word_ids[k], word_len[k]};
+    dict[s] = DictSlot{word_head[k], word_len[k], word_ids[k]};
   }
   uint32_t plus_word = NONE, hash_word = NONE;
   {
@@ -288,12 +310,27 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   size_t o_nodes = 0;
   size_t o_dict = o_nodes + al(NN * sizeof(Node));
   size_t o_edges = o_dict + al(dcap * sizeof(DictSlot));
-  size_t o_arena = o_edges + al(dedges.slots.size() * sizeof(EdgeSlot));
-  size_t o_soff = o_arena + al(arena.size() + 16);
+  size_t o_arena = o_edges + al(dedges.size() * sizeof(EdgeSlot));
+  size_t o_soff = o_arena + al(arena.size() + 64);
   size_t o_sids = o_soff + al(soff.size() * 8);
   size_t o_flen = o_sids + al(sids.size() * 4 + 4);
   size_t total = o_flen + al(flen.size() * 2 + 2);
 
+  if (host_only) {  // compile-only self check (no device): report the table sizes
+    emqx_gm_index_info_t& in = *host_only;
+    in = emqx_gm_index_info_t{};
+    in.n_filters = nf;
+    in.n_wildcard = n_wild;
+    in.n_nodes = NN;
+    in.n_edges = n_edges;
+    in.n_words = nw;
+    in.n_subs = sids.size();
+    in.device_bytes = total;
+    in.max_depth = max_depth;
+    in.trie_empty = n_wild == 0;
+    delete idx;
+    return EMQX_GM_OK;
+  }
   hipError_t e = hipSetDevice(ctx->device);
   if (e == hipSuccess) e = hipMalloc(&idx->dev_base, total);
   if (e != hipSuccess) {
@@ -307,7 +344,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   };
   up(o_nodes, dnodes.data(), NN * sizeof(Node));
   up(o_dict, dict.data(), dcap * sizeof(DictSlot));
-  up(o_edges, dedges.slots.data(), dedges.slots.size() * sizeof(EdgeSlot));
+  up(o_edges, dedges.data(), dedges.size() * sizeof(EdgeSlot));
   up(o_arena, arena.data(), arena.size());
   up(o_soff, soff.data(), soff.size() * 8);
   up(o_sids, sids.data(), sids.size() * 4);
@@ -326,7 +363,10 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.sub_off = reinterpret_cast<const uint64_t*>(B + o_soff);
   v.sub_ids = reinterpret_cast<const uint32_t*>(B + o_sids);
   v.dict_mask = dcap - 1;
-  v.edge_mask = dedges.mask;
+  for (int d = 0; d < EDGE_DEPTHS; ++d) {
+    v.etab_off[d] = etab_off[d];
+    v.etab_mask[d] = etab_mask[d];
+  }
   v.n_nodes = uint32_t(NN);
   v.n_filters = nf;
   v.plus_word = plus_word;
@@ -337,7 +377,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   in.n_filters = nf;
   in.n_wildcard = n_wild;
   in.n_nodes = NN;
-  in.n_edges = dedges.used;
+  in.n_edges = n_edges;
   in.n_words = nw;
   in.n_subs = sids.size();
   in.device_bytes = total;

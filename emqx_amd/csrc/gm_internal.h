@@ -97,7 +97,8 @@ struct emqx_gm_index {
 namespace gm {
 // gm_index.cpp
 int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_t n, const uint64_t* sub_off,
-                const uint32_t* sub_ids, uint32_t* perm_out, emqx_gm_index** out);
+                const uint32_t* sub_ids, uint32_t* perm_out, emqx_gm_index** out,
+                emqx_gm_index_info_t* host_only = nullptr);
 void free_index(emqx_gm_index* idx);
 // gm_match.hip
 int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,

@@ -39,78 +39,96 @@ namespace gm {
 // device helpers
 // ---------------------------------------------------------------------------
 
-// Byte reader over a lane's topic with a one-dword cache (aligned 4-B loads).
+// Byte reader over a lane's topic with an 8-byte cache (aligned 8-B loads;
+// topic buffers are padded, emqx_gpu_match.h).
 struct ByteReader {
   const uint8_t* base;
   uint64_t cached_addr;
-  uint32_t cached;
+  uint64_t cached;
   __device__ __forceinline__ uint32_t get(uint64_t p) {
-    uint64_t a = p & ~3ull;
+    const uint64_t a = p & ~7ull;
     if (a != cached_addr) {
       cached_addr = a;
-      cached = *reinterpret_cast<const uint32_t*>(base + a);
+      cached = *reinterpret_cast<const uint64_t*>(base + a);
     }
-    return (cached >> ((p & 3) * 8)) & 0xFFu;
+    return uint32_t(cached >> ((p & 7) * 8)) & 0xFFu;
   }
 };
 
-__device__ __forceinline__ uint32_t dict_lookup(const IndexView& ix, uint64_t h, uint32_t len,
-                                                const uint8_t* tb, uint64_t ws) {
-  for (uint64_t s = dict_slot(h, ix.dict_mask);; s = (s + 1) & ix.dict_mask) {
-    const DictSlot d = ix.dict[s];
-    if (d.len == DICT_EMPTY_LEN) return NONE;
-    if (d.h == h && d.len == len) {
-      bool eq = true;
-      for (uint32_t i = 0; i < len; ++i) {
-        if (ix.arena[d.word + i] != tb[ws + i]) {
-          eq = false;
-          break;
-        }
-      }
-      if (eq) return d.word;
-    }
-  }
-}
-
-__device__ __forceinline__ uint32_t edge_lookup(const IndexView& ix, uint32_t parent, uint32_t word) {
-  const uint64_t key = edge_key(parent, word);
-  for (uint64_t s = edge_slot(key, ix.edge_mask);; s = (s + 1) & ix.edge_mask) {
-    const EdgeSlot e = ix.edges[s];
-    if (e.key == key) return e.child;
-    if (e.key == EDGE_EMPTY) return NONE;
-  }
-}
-
-// Tokenize the word starting at `pos`; returns its hash, length and first byte;
-// leaves `pos` on the '/' (or end).
+// One tokenized level word: hash, first 8 bytes, length, first byte.
 struct WordTok {
   uint64_t h;
+  uint64_t head;
   uint64_t start;
   uint32_t len;
   uint32_t b0;
 };
+
+// Tokenize the word starting at `pos`; leaves `pos` on the '/' (or end).
 __device__ __forceinline__ WordTok next_word(ByteReader& rd, uint64_t& pos, uint64_t end) {
   WordTok w;
   w.start = pos;
-  w.b0 = 0;
+  w.head = 0;
   uint64_t h = HASH_SEED, chunk = 0;
   uint32_t k = 0;
   while (pos < end) {
     const uint32_t b = rd.get(pos);
     if (b == '/') break;
-    if (k == 0) w.b0 = b;
     chunk |= uint64_t(b) << ((k & 7) * 8);
     ++k;
     ++pos;
     if ((k & 7) == 0) {
+      if (k == 8) w.head = chunk;
       h = hash_step(h, chunk);
       chunk = 0;
     }
   }
-  if (k & 7) h = hash_step(h, chunk);
+  if (k & 7) {
+    if (k < 8) w.head = chunk;
+    h = hash_step(h, chunk);
+  }
   w.h = hash_final(h, k);
   w.len = k;
+  w.b0 = uint32_t(w.head & 0xFF);
   return w;
+}
+
+__device__ __noinline__ bool tail_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+// Resolve a word in the dictionary starting from the (prefetched) first slot.
+// A hit is exact: length + first 8 bytes compared inline, the rest against
+// the arena (only for words longer than 8 bytes).
+__device__ __forceinline__ uint32_t dict_resolve(const IndexView& ix, const WordTok& w, DictSlot d,
+                                                 const uint8_t* tb) {
+  for (uint64_t s = dict_slot(w.h, ix.dict_mask);;) {
+    if (d.len == DICT_EMPTY_LEN) return NONE;
+    if (d.len == w.len && d.head == w.head &&
+        (w.len <= 8 || tail_equal(ix.arena + d.word + 8, tb + w.start + 8, w.len - 8)))
+      return d.word;
+    s = (s + 1) & ix.dict_mask;
+    d = ix.dict[s];
+  }
+}
+
+__device__ __forceinline__ DictSlot dict_first(const IndexView& ix, const WordTok& w) {
+  return ix.dict[dict_slot(w.h, ix.dict_mask)];
+}
+
+__device__ __forceinline__ uint32_t edge_lookup(const IndexView& ix, uint32_t depth, uint32_t parent,
+                                                uint32_t word) {
+  const int d = edge_depth(depth);
+  const EdgeSlot* tab = ix.edges + ix.etab_off[d];
+  const uint64_t mask = ix.etab_mask[d];
+  const uint64_t key = edge_key(parent, word);
+  for (uint64_t s = edge_slot(key, mask);; s = (s + 1) & mask) {
+    const EdgeSlot e = tab[s];
+    if (e.key == key) return e.child;
+    if (e.key == EDGE_EMPTY) return NONE;
+  }
 }
 
 // Literal lookup of a wildcard topic as a filter string: emqx_router:
@@ -119,12 +137,13 @@ __device__ __forceinline__ WordTok next_word(ByteReader& rd, uint64_t& pos, uint
 __device__ uint32_t literal_lookup(const IndexView& ix, const uint8_t* tb, uint64_t pos, uint64_t end) {
   ByteReader rd{tb, ~0ull, 0};
   uint32_t node = 0;
-  for (;;) {
-    WordTok w = next_word(rd, pos, end);
-    const uint32_t wid = dict_lookup(ix, w.h, w.len, tb, w.start);
+  for (uint32_t depth = 0;; ++depth) {
+    const WordTok w = next_word(rd, pos, end);
+    const uint32_t wid = dict_resolve(ix, w, dict_first(ix, w), tb);
     if (wid == NONE) return NONE;
-    node = edge_lookup(ix, node, wid);
-    if (node == NONE) return NONE;
+    const uint32_t c = edge_lookup(ix, depth, node, wid);
+    if (c == NONE) return NONE;
+    node = c & REF_MASK;
     if (pos >= end) break;
     ++pos;
   }
@@ -146,6 +165,12 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) 
 // ---------------------------------------------------------------------------
 // k_match_fast
 // ---------------------------------------------------------------------------
+// Staging layout per 64-topic tile: [slot k][lane], FAST_MC slots, so the k-th
+// match of every lane is one coalesced 256-B row.
+__device__ __forceinline__ uint64_t stage_index(uint64_t tile, uint32_t k, int lane) {
+  return tile * (64ull * FAST_MC) + uint64_t(k) * 64u + uint32_t(lane);
+}
+
 template <bool EXACT>
 __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ tb,
                                                     const uint64_t* __restrict__ toff, uint64_t n,
@@ -157,10 +182,11 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
                                                     unsigned long long* __restrict__ wild_ctr) {
   constexpr int FC = FAST_FC, MC = FAST_MC;
   __shared__ uint32_t s_fr[2][FC][256];
-  __shared__ uint32_t s_m[MC][256];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
   const uint64_t t = uint64_t(blockIdx.x) * 256u + tid;
+  const uint64_t tile = t >> 6;
   const bool valid = t < n;
+  const Node root = ix.nodes[0];  // uniform: one scalar load per wave
 
   uint32_t m_n = 0;
   bool ovf = false, wild = false;
@@ -173,30 +199,50 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
     ByteReader rd{tb, ~0ull, 0};
     int cur = 0;
     uint32_t cur_n = 1;
-    s_fr[0][0][tid] = 0;  // virtual root (the atom `empty`, emqx_trie.erl:264)
+    s_fr[0][0][tid] = (root.flags & NF_HAS_EXACT) ? REF_X : 0u;  // the virtual root (emqx_trie.erl:264)
     bool dollar = false;
     uint32_t level = 0;
+    WordTok w = next_word(rd, pos, end);
+    DictSlot d0 = dict_first(ix, w);
     for (;;) {
-      const WordTok w = next_word(rd, pos, end);
       const bool last = pos >= end;
       if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {
         wild = true;  // emqx_topic:wildcard/1
         break;
       }
       if (level == 0) dollar = w.len > 0 && w.b0 == '$';
+      const uint32_t wid = cur_n ? dict_resolve(ix, w, d0, tb) : NONE;
+      // prefetch the next level's word while this level's frontier expands
+      WordTok wn;
+      DictSlot dn;
+      if (!last) {
+        ++pos;
+        wn = next_word(rd, pos, end);
+        dn = dict_first(ix, wn);
+      }
       if (cur_n) {
         probes += 3 * cur_n;
-        const uint32_t wid = dict_lookup(ix, w.h, w.len, tb, w.start);
         const int nb = cur ^ 1;
         uint32_t nn = 0;
+        const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);  // wave-uniform
+        const int ed = edge_depth(lvl);
+        const EdgeSlot* etab = ix.edges + ix.etab_off[ed];
+        const uint64_t emask = ix.etab_mask[ed];
         // '$'-topics skip the root-level '+' and '#' (emqx_trie.erl:271-278).
         const bool rootskip = dollar && level == 0;
         for (uint32_t i = 0; i < cur_n; ++i) {
-          const uint32_t nd = s_fr[cur][i][tid];
-          const Node node = ix.nodes[nd];
+          const uint32_t ref = s_fr[cur][i][tid];
+          const uint32_t nd = ref & REF_MASK;
+          const bool probe = (ref & REF_X) && wid != NONE;
+          const uint64_t key = edge_key(nd, wid);
+          uint64_t sl = edge_slot(key, emask);
+          EdgeSlot e;
+          e.key = EDGE_EMPTY;
+          if (probe) e = etab[sl];        // issued together with the node read
+          const Node node = level == 0 ? root : ix.nodes[nd];
           if (!rootskip) {
             if (node.hash_filter != NONE) {  // 'match_#' at a visited prefix
-              if (m_n < MC) s_m[m_n][tid] = node.hash_filter;
+              if (m_n < MC) stage[stage_index(tile, m_n, lane)] = node.hash_filter;
               ++m_n;
             }
             if (node.plus_child != NONE) {
@@ -204,10 +250,13 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
               ++nn;
             }
           }
-          if (wid != NONE && (node.flags & NF_HAS_EXACT)) {
-            const uint32_t c = edge_lookup(ix, nd, wid);
-            if (c != NONE) {
-              if (nn < FC) s_fr[nb][nn][tid] = c;
+          if (probe) {
+            while (e.key != key && e.key != EDGE_EMPTY) {
+              sl = (sl + 1) & emask;
+              e = etab[sl];
+            }
+            if (e.key == key) {
+              if (nn < FC) s_fr[nb][nn][tid] = e.child;
               ++nn;
             }
           }
@@ -220,7 +269,8 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
         cur_n = nn;
       }
       if (last) break;
-      ++pos;
+      w = wn;
+      d0 = dn;
       ++level;
     }
     if (wild) {
@@ -229,46 +279,28 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
       if (EXACT) {
         const uint32_t f = literal_lookup(ix, tb, start, end);
         if (f != NONE) {
-          s_m[0][tid] = f;
+          stage[stage_index(tile, 0, lane)] = f;
           m_n = 1;
         }
       }
     } else if (!ovf) {
       probes += 2 * cur_n + 1;
       for (uint32_t i = 0; i < cur_n; ++i) {
-        const Node node = ix.nodes[s_fr[cur][i][tid]];
+        const Node node = ix.nodes[s_fr[cur][i][tid] & REF_MASK];
         if (node.hash_filter != NONE) {
-          if (m_n < MC) s_m[m_n][tid] = node.hash_filter;
+          if (m_n < MC) stage[stage_index(tile, m_n, lane)] = node.hash_filter;
           ++m_n;
         }
         if (node.end_filter != NONE &&
             (EXACT || (node.flags & NF_END_WILD) || (dollar && level == 0))) {
-          if (m_n < MC) s_m[m_n][tid] = node.end_filter;
+          if (m_n < MC) stage[stage_index(tile, m_n, lane)] = node.end_filter;
           ++m_n;
         }
       }
       if (m_n > MC) ovf = true;
     }
-    if (!ovf) {
-      // insertion sort of the row by filter id (ids are lexicographic ranks)
-      for (uint32_t i = 1; i < m_n; ++i) {
-        const uint32_t x = s_m[i][tid];
-        uint32_t j = i;
-        while (j > 0 && s_m[j - 1][tid] > x) {
-          s_m[j][tid] = s_m[j - 1][tid];
-          --j;
-        }
-        s_m[j][tid] = x;
-      }
-    }
   }
 
-  const uint32_t keep = (valid && !ovf) ? m_n : 0;
-  uint32_t total;
-  const uint32_t pre = wave_excl_scan(keep, total);
-  const uint64_t tile = t >> 6;
-  uint32_t* dst = stage + tile * (64ull * MC) + pre;
-  for (uint32_t k = 0; k < keep; ++k) dst[k] = s_m[k][tid];
   if (valid) {
     cnt[t] = ovf ? OVF_BIT : m_n;
     if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
@@ -277,7 +309,7 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
   uint32_t ptot;
   wave_excl_scan(valid ? probes : 0, ptot);
   const unsigned long long wb = __ballot(valid && wild);
-  if ((tid & 63) == 0) {
+  if (lane == 0) {
     atomicAdd(probe_ctr, (unsigned long long)ptot);
     if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
   }
@@ -381,6 +413,26 @@ __global__ __launch_bounds__(256) void k_tile_sums(const uint32_t* __restrict__ 
   if ((threadIdx.x & 63) == 0 && (t >> 6) * 64 < n) tsum[t >> 6] = tot;
 }
 
+// Sort a row held in FAST_MC registers (unused slots = 0xFFFFFFFF) with a
+// bitonic network; every index is static after unrolling.
+__device__ __forceinline__ void sort_row(uint32_t (&m)[FAST_MC]) {
+#pragma unroll
+  for (int k = 2; k <= FAST_MC; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int i = 0; i < FAST_MC; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint32_t a = m[i], b = m[l];
+          const bool up = (i & k) == 0;
+          const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+          m[i] = up ? lo : hi;
+          m[l] = up ? hi : lo;
+        }
+      }
+}
+
 __global__ __launch_bounds__(256) void k_assemble(const uint32_t* __restrict__ cnt, uint64_t n,
                                                   const uint64_t* __restrict__ tile_off,
                                                   const uint32_t* __restrict__ stage,
@@ -392,30 +444,18 @@ __global__ __launch_bounds__(256) void k_assemble(const uint32_t* __restrict__ c
   const uint32_t c = t < n ? cnt[t] : 0;
   const bool slow = (c & OVF_BIT) != 0;
   const uint32_t call = c & CNT_MASK, cf = slow ? 0 : call;
-  uint32_t tall, tfast;
+  uint32_t tall;
   const uint32_t pa = wave_excl_scan(call, tall);
-  const uint32_t pf = wave_excl_scan(cf, tfast);
-  const uint64_t base = tile_off[tile];
-  if (t < n) row_off[t] = base + pa;
-  if (t == n - 1) row_off[n] = base + pa + call;
-  const uint32_t* src = stage + tile * (64ull * FAST_MC);
-  if (__ballot(slow) == 0) {  // common case: the tile's staging region is its final region
-    for (uint32_t e = lane; e < tfast; e += 64) ids[base + e] = src[e];
-    return;
-  }
-  // Rows completed by the slow path leave gaps: map staged element e to its
-  // row r (largest r with pf[r] <= e) by binary lifting over lane shuffles.
-  for (uint32_t e0 = 0; e0 < tfast; e0 += 64) {
-    const uint32_t e = e0 + lane;
-    int lo = 0;
+  const uint64_t base = tile_off[tile] + pa;
+  if (t < n) row_off[t] = base;
+  if (t == n - 1) row_off[n] = base + call;
+  uint32_t m[FAST_MC];
 #pragma unroll
-    for (int step = 32; step > 0; step >>= 1) {
-      const uint32_t v = __shfl(pf, lo + step, 64);
-      if (v <= e) lo += step;
-    }
-    const uint32_t pfl = __shfl(pf, lo, 64), pal = __shfl(pa, lo, 64);
-    if (e < tfast) ids[base + pal + (e - pfl)] = src[e];
-  }
+  for (int k = 0; k < FAST_MC; ++k) m[k] = uint32_t(k) < cf ? stage[stage_index(tile, k, lane)] : 0xFFFFFFFFu;
+  if (cf > 1) sort_row(m);
+#pragma unroll
+  for (int k = 0; k < FAST_MC; ++k)
+    if (uint32_t(k) < cf) ids[base + k] = m[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -462,23 +502,23 @@ __global__ __launch_bounds__(256) void k_slow_walk(const uint8_t* __restrict__ t
       if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) fl |= 2u;
       if (s_level == 0 && w.len > 0 && w.b0 == '$') fl |= 4u;
       s_flags = fl;
-      s_wid = (fl & 2u) ? NONE : dict_lookup(ix, w.h, w.len, tb, w.start);
+      s_wid = (fl & 2u) ? NONE : dict_resolve(ix, w, dict_first(ix, w), tb);
       s_pos = pos + 1;
     }
     __syncthreads();
     const uint32_t fl = s_flags;
     if (fl & 2u) break;
-    const uint32_t wid = s_wid, cn = s_cur_n;
-    const bool rootskip = (fl & 4u) && s_level == 0;
+    const uint32_t wid = s_wid, cn = s_cur_n, lvl = s_level;
+    const bool rootskip = (fl & 4u) && lvl == 0;
     for (uint32_t i = tid; i < cn; i += 256) {
-      const uint32_t nd = cur[i];
+      const uint32_t nd = cur[i] & REF_MASK;
       const Node node = ix.nodes[nd];
       if (!rootskip) {
         if (node.hash_filter != NONE) atomicOr(&bm[node.hash_filter >> 5], 1u << (node.hash_filter & 31));
         if (node.plus_child != NONE) nxt[atomicAdd(&s_nxt_n, 1u)] = node.plus_child;
       }
       if (wid != NONE && (node.flags & NF_HAS_EXACT)) {
-        const uint32_t c = edge_lookup(ix, nd, wid);
+        const uint32_t c = edge_lookup(ix, lvl, nd, wid);
         if (c != NONE) nxt[atomicAdd(&s_nxt_n, 1u)] = c;
       }
     }
@@ -507,7 +547,7 @@ __global__ __launch_bounds__(256) void k_slow_walk(const uint8_t* __restrict__ t
     const uint32_t cn = s_cur_n;
     const bool single = s_level == 0 && (fl & 4u);
     for (uint32_t i = tid; i < cn; i += 256) {
-      const Node node = ix.nodes[cur[i]];
+      const Node node = ix.nodes[cur[i] & REF_MASK];
       if (node.hash_filter != NONE) atomicOr(&bm[node.hash_filter >> 5], 1u << (node.hash_filter & 31));
       if (node.end_filter != NONE && (EXACT || (node.flags & NF_END_WILD) || single))
         atomicOr(&bm[node.end_filter >> 5], 1u << (node.end_filter & 31));

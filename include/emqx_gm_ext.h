@@ -30,6 +30,13 @@ int emqx_gm_dev_free(emqx_gm_ctx *ctx, void *p);
 int emqx_gm_memcpy(emqx_gm_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind);
 int emqx_gm_pool_trim(emqx_gm_ctx *ctx);
 
+/* Host-only self check of the index compiler (no device needed): compiles the
+ * filter set into the flat tables and reports their sizes; perm_out as in
+ * emqx_gm_index_build. */
+int emqx_gm_index_compile_host(const uint8_t *filter_bytes, const uint64_t *filter_off, uint64_t n_filters,
+                               const uint64_t *sub_off, const uint32_t *sub_ids, uint32_t *perm_out,
+                               emqx_gm_index_info_t *info);
+
 /* Sum of the byte lengths of the filters referenced by a device CSR (the
  * Σ len(f) term of the algorithmic-bytes formula). */
 int emqx_gm_matched_filter_bytes(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const emqx_gm_csr *csr,

@@ -121,3 +121,64 @@ def test_broker_bookkeeping_shards():
     for p in range(1, 2501):
         b.unsubscribe("hot/t", p)
     assert not b.router.has_routes("hot/t")
+
+
+def _compile(filters, subs=None):
+    import ctypes as C
+    from emqx_amd import _lib
+    from emqx_amd.engine import pack
+    fb, fo = filters if isinstance(filters, tuple) else pack(filters)
+    n = len(fo) - 1
+    perm = np.zeros(max(n, 1), np.uint32)
+    info = _lib.IndexInfo()
+    so = si = None
+    if subs is not None:
+        so, si = subs
+    rc = _lib.lib().emqx_gm_index_compile_host(
+        C.c_void_p(fb.ctypes.data), C.c_void_p(fo.ctypes.data), n,
+        None if so is None else C.c_void_p(so.ctypes.data), None if si is None else C.c_void_p(si.ctypes.data),
+        C.c_void_p(perm.ctypes.data), C.byref(info))
+    assert rc == 0
+    return info, perm[:n]
+
+
+@pytest.mark.timeout(60)
+def test_index_compiler_host_small(golden):
+    """The host index compiler (the part of emqx_gm_index_build that runs on
+    the CPU) on the reference vectors and edge cases: ids are lexicographic
+    ranks, duplicates collapse, trie_empty follows emqx_trie:empty/0."""
+    fs = [b"sensor/1/metric/2", b"sensor/+/#", b"sensor/#", b"sensor/#", b"", b"#", b"/+", b"a//b", b"$SYS/#"]
+    info, perm = _compile(fs)
+    uniq = sorted(set(fs))
+    assert info.n_filters == len(uniq)
+    assert [uniq[i] for i in perm] == fs
+    assert info.n_wildcard == sum(1 for f in uniq if b"+" in f.split(b"/") or b"#" in f.split(b"/"))
+    assert not info.trie_empty
+    info, _ = _compile([b"a/b", b"c"])
+    assert info.trie_empty and info.n_wildcard == 0
+    info, _ = _compile([])
+    assert info.n_filters == 0 and info.trie_empty and info.n_nodes == 1
+    for case in golden["trie_cases"]:
+        ins = [a.encode() for op, a in case["ops"] if op == "insert"]
+        info, perm = _compile(ins)
+        assert info.n_filters == len(set(ins))
+
+
+@pytest.mark.timeout(120)
+def test_index_compiler_host_c2_scale(orc):
+    """1M wildcard filters (C2) compile in bounded time; node count equals the
+    number of distinct word-list prefixes (the non-compact key count of the
+    reference trie, emqx_trie.erl:223-232, plus the root)."""
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    codes = gen_filter_codes(1, 200_000, wildcard_only=True)
+    fb, fo = render_codes(codes)
+    info, perm = _compile((fb, fo))
+    fs = orc.unpack(fb, fo)
+    prefixes = set()
+    for f in fs:
+        ws = f.split(b"/")
+        for k in range(1, len(ws) + 1):
+            prefixes.add(tuple(ws[:k]))
+    assert info.n_nodes == len(prefixes) + 1
+    assert info.n_edges == len(prefixes)
+    assert info.n_filters == len(set(fs)) == 200_000
