@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-TOPICS=${TOPICS:-20000000}
+TOPICS=${TOPICS:-100000000}
 ARGS="bench.py --topics $TOPICS --steps 2 --warmup 1 --no-cpu"
 run() {  # run <name> <timeout> <rocprof args...>
   local name=$1 t=$2; shift 2
@@ -17,7 +17,7 @@ run() {  # run <name> <timeout> <rocprof args...>
   if [ $rc -ne 0 ]; then echo "ABORT"; exit $rc; fi
 }
 if [ "${1:-}" = "list" ]; then timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "listed rc=$?"; exit 0; fi
-run stats 300 --kernel-trace --stats
+[ -z "${SKIP_STATS:-}" ] && run stats 300 --kernel-trace --stats
 run pmc_fetch 120 --pmc FETCH_SIZE
 run pmc_write 120 --pmc WRITE_SIZE
 run pmc_l2 120 --pmc TCC_HIT_sum TCC_MISS_sum
