@@ -29,7 +29,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <vector>
 
 #include "gm_internal.h"
@@ -172,60 +171,7 @@ __device__ __forceinline__ uint64_t stage_index(uint64_t tile, uint32_t k, int l
   return tile * (64ull * FAST_MC) + uint64_t(k) * 64u + uint32_t(lane);
 }
 
-// A hot slot as the kernel reads it: the 24 used bytes, in two loads
-// (dwordx4 + dwordx2) from one 64-B line.
-struct HotRec {
-  uint4 a;  // key lo, key hi, sig, flags
-  uint2 b;  // hash_filter, end_filter
-};
-__device__ __forceinline__ HotRec hot_load(const HotSlot* tab, uint32_t s) {
-  const uint32_t* p = reinterpret_cast<const uint32_t*>(tab + s);
-  HotRec r;
-  r.a = *reinterpret_cast<const uint4*>(p);
-  r.b = *reinterpret_cast<const uint2*>(p + 4);
-  return r;
-}
-__device__ __forceinline__ bool hot_is(const HotRec& r, uint64_t key) {
-  return r.a.x == uint32_t(key) && r.a.y == uint32_t(key >> 32);
-}
-__device__ __forceinline__ bool hot_empty(const HotRec& r) { return r.a.x == 0xFFFFFFFFu && r.a.y == 0xFFFFFFFFu; }
-// Linear probing from slot s (whose record r is already loaded); returns the
-// slot index of `key` or NONE.
-__device__ __forceinline__ uint32_t hot_resolve(const HotSlot* tab, uint32_t cap, uint64_t key, uint32_t s,
-                                                HotRec& r) {
-  while (!hot_is(r, key)) {
-    if (hot_empty(r)) return NONE;
-    s = s + 1 == cap ? 0 : s + 1;
-    r = hot_load(tab, s);
-  }
-  return s;
-}
-
-// Per-lane match staging: emit one filter id into the lane's row.
-#define GM_EMIT(f)                                                   \
-  do {                                                               \
-    if (m_n < MC) stage[stage_index(tile, m_n, lane)] = (f);         \
-    ++m_n;                                                           \
-  } while (0)
-
-// Visit a node reached at this level (its record r, hot id hs): emit
-// 'match_#' for it; on the topic's last word also its own filter
-// (lookup_topic/3: only wildcard filters in trie mode; the '$X' quirk of
-// emqx_trie.erl:275-276 for single-word '$' topics); otherwise push it.
-#define GM_VISIT(hs, r)                                                                          \
-  do {                                                                                           \
-    if ((r).b.x != NONE) GM_EMIT((r).b.x);                                                       \
-    if (last) {                                                                                  \
-      if ((r).b.y != NONE && (EXACT || ((r).b.y & END_WILD) || (dollar && level == 0)))          \
-        GM_EMIT((r).b.y & ID_MASK);                                                              \
-      ++nfinal;                                                                                  \
-    } else {                                                                                     \
-      if (nn < FC) s_fr[nb][nn][tid] = make_uint2((hs) | (((r).a.w & HOT_PLUS) ? FR_PLUS : 0u), (r).a.z); \
-      ++nn;                                                                                      \
-    }                                                                                            \
-  } while (0)
-
-template <bool EXACT, int FC>
+template <bool EXACT>
 __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ tb,
                                                     const uint64_t* __restrict__ toff, uint64_t n,
                                                     IndexView ix, uint32_t* __restrict__ cnt,
@@ -234,13 +180,13 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ ovf_n,
                                                     unsigned long long* __restrict__ probe_ctr,
                                                     unsigned long long* __restrict__ wild_ctr) {
-  constexpr int MC = FAST_MC;
-  // frontier entry: {hot id | FR_PLUS, exact-child signature}, double buffered
-  __shared__ uint2 s_fr[2][FC][256];
+  constexpr int FC = FAST_FC, MC = FAST_MC;
+  __shared__ uint32_t s_fr[2][FC][256];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint64_t t = uint64_t(blockIdx.x) * 256u + tid;
   const uint64_t tile = t >> 6;
   const bool valid = t < n;
+  const Node root = ix.nodes[0];  // uniform: one scalar load per wave
 
   uint32_t m_n = 0;
   bool ovf = false, wild = false;
@@ -251,23 +197,21 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
     const uint64_t end = toff[t + 1];
     const uint64_t start = pos;
     ByteReader rd{tb, ~0ull, 0};
+    int cur = 0;
+    uint32_t cur_n = 1;
+    s_fr[0][0][tid] = (root.flags & NF_HAS_EXACT) ? REF_X : 0u;  // the virtual root (emqx_trie.erl:264)
+    bool dollar = false;
+    uint32_t level = 0;
     WordTok w = next_word(rd, pos, end);
     DictSlot d0 = dict_first(ix, w);
-    // '$'-topics skip the root-level '+' and '#' (emqx_trie.erl:271-278)
-    const bool dollar = w.len > 0 && w.b0 == '$';
-    if (!dollar && ix.root_hash != NONE) GM_EMIT(ix.root_hash);  // '#' at the virtual root
-    int cur = 0;
-    uint32_t cur_n = 1, nfinal = 0;
-    s_fr[0][0][tid] = make_uint2((!dollar && (ix.root_flags & HOT_PLUS)) ? FR_PLUS : 0u, ix.root_sig);
-    uint32_t level = 0;
     for (;;) {
       const bool last = pos >= end;
       if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {
         wild = true;  // emqx_topic:wildcard/1
         break;
       }
+      if (level == 0) dollar = w.len > 0 && w.b0 == '$';
       const uint32_t wid = cur_n ? dict_resolve(ix, w, d0, tb) : NONE;
-      const uint32_t wbit = sig_bit(w.h);
       // prefetch the next level's word while this level's frontier expands
       WordTok wn;
       DictSlot dn;
@@ -281,33 +225,40 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
         const int nb = cur ^ 1;
         uint32_t nn = 0;
         const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);  // wave-uniform
-        const int ht = hot_table(lvl + 1);
-        const HotSlot* tab = ix.hot + ix.hot_off[ht];
-        const uint64_t cap = ix.hot_cap[ht];
-        const uint32_t capu = uint32_t(cap);
+        const int ed = edge_depth(lvl);
+        const EdgeSlot* etab = ix.edges + ix.etab_off[ed];
+        const uint64_t emask = ix.etab_mask[ed];
+        // '$'-topics skip the root-level '+' and '#' (emqx_trie.erl:271-278).
+        const bool rootskip = dollar && level == 0;
         for (uint32_t i = 0; i < cur_n; ++i) {
-          const uint2 e = s_fr[cur][i][tid];
-          const uint32_t id = e.x & ID_MASK;
-          const bool dx = wid != NONE && (e.y & wbit);
-          const bool dp = (e.x & FR_PLUS) != 0;
-          // issue both probes before consuming either
-          uint32_t sx = 0, sp = 0;
-          HotRec rx, rp;
-          if (dx) {
-            sx = uint32_t(hot_slot(hot_key(id, wid, lvl), cap));
-            rx = hot_load(tab, sx);
+          const uint32_t ref = s_fr[cur][i][tid];
+          const uint32_t nd = ref & REF_MASK;
+          const bool probe = (ref & REF_X) && wid != NONE;
+          const uint64_t key = edge_key(nd, wid);
+          uint64_t sl = edge_slot(key, emask);
+          EdgeSlot e;
+          e.key = EDGE_EMPTY;
+          if (probe) e = etab[sl];        // issued together with the node read
+          const Node node = level == 0 ? root : ix.nodes[nd];
+          if (!rootskip) {
+            if (node.hash_filter != NONE) {  // 'match_#' at a visited prefix
+              if (m_n < MC) stage[stage_index(tile, m_n, lane)] = node.hash_filter;
+              ++m_n;
+            }
+            if (node.plus_child != NONE) {
+              if (nn < FC) s_fr[nb][nn][tid] = node.plus_child;
+              ++nn;
+            }
           }
-          if (dp) {
-            sp = uint32_t(hot_slot(hot_key(id, ix.plus_word, lvl), cap));
-            rp = hot_load(tab, sp);
-          }
-          if (dx) {
-            const uint32_t hs = hot_resolve(tab, capu, hot_key(id, wid, lvl), sx, rx);
-            if (hs != NONE) GM_VISIT(hs, rx);
-          }
-          if (dp) {
-            const uint32_t hs = hot_resolve(tab, capu, hot_key(id, ix.plus_word, lvl), sp, rp);
-            if (hs != NONE) GM_VISIT(hs, rp);
+          if (probe) {
+            while (e.key != key && e.key != EDGE_EMPTY) {
+              sl = (sl + 1) & emask;
+              e = etab[sl];
+            }
+            if (e.key == key) {
+              if (nn < FC) s_fr[nb][nn][tid] = e.child;
+              ++nn;
+            }
           }
         }
         if (nn > FC) {
@@ -333,7 +284,19 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
         }
       }
     } else if (!ovf) {
-      probes += 2 * nfinal + 1;
+      probes += 2 * cur_n + 1;
+      for (uint32_t i = 0; i < cur_n; ++i) {
+        const Node node = ix.nodes[s_fr[cur][i][tid] & REF_MASK];
+        if (node.hash_filter != NONE) {
+          if (m_n < MC) stage[stage_index(tile, m_n, lane)] = node.hash_filter;
+          ++m_n;
+        }
+        if (node.end_filter != NONE &&
+            (EXACT || (node.flags & NF_END_WILD) || (dollar && level == 0))) {
+          if (m_n < MC) stage[stage_index(tile, m_n, lane)] = node.end_filter;
+          ++m_n;
+        }
+      }
       if (m_n > MC) ovf = true;
     }
   }
@@ -351,8 +314,6 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
     if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
   }
 }
-#undef GM_VISIT
-#undef GM_EMIT
 
 // ---------------------------------------------------------------------------
 // scan (u64, exclusive, n+1 outputs: out[n] = total)
@@ -805,20 +766,12 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
 
   GM_HIP(ctx, hipEventRecord(ctx->ev[0], st));
   GM_HIP(ctx, hipEventRecord(ctx->ev[1], st));
-  {
-    // A/B knob: GM_MATCH_FC (4|6|8) frontier capacity per lane (LDS; occupancy)
-    static const int fc = [] {
-      const char* e = getenv("GM_MATCH_FC");
-      const int v = e ? atoi(e) : FAST_FC;
-      return v == 4 || v == 6 || v == 8 ? v : FAST_FC;
-    }();
-    using KernT = decltype(&k_match_fast<true, 8>);
-    static const KernT table[2][3] = {{k_match_fast<false, 4>, k_match_fast<false, 6>, k_match_fast<false, 8>},
-                                      {k_match_fast<true, 4>, k_match_fast<true, 6>, k_match_fast<true, 8>}};
-    KernT kern = table[exact ? 1 : 0][fc == 4 ? 0 : fc == 6 ? 1 : 2];
-    hipLaunchKernelGGL(kern, dim3(nblk), dim3(256), 0, st, tb, to, n, idx->view, cnt.as<uint32_t>(),
+  if (exact)
+    hipLaunchKernelGGL(k_match_fast<true>, dim3(nblk), dim3(256), 0, st, tb, to, n, idx->view, cnt.as<uint32_t>(),
                        stage.as<uint32_t>(), ovf_list.as<uint32_t>(), ovf_n, probe_ctr, wild_ctr);
-  }
+  else
+    hipLaunchKernelGGL(k_match_fast<false>, dim3(nblk), dim3(256), 0, st, tb, to, n, idx->view, cnt.as<uint32_t>(),
+                       stage.as<uint32_t>(), ovf_list.as<uint32_t>(), ovf_n, probe_ctr, wild_ctr);
   GM_HIP(ctx, hipGetLastError());
   GM_HIP(ctx, hipEventRecord(ctx->ev[2], st));
 
