@@ -61,21 +61,50 @@ struct alignas(16) EdgeSlot {
   uint32_t pad;
 };
 
+// ---- hot tables (read by k_match_fast only) --------------------------------
+// One open-addressing table per node depth (1..HOT_TABLES-2 each their own,
+// deeper nodes share the last).  A node reached through an exact or '+' edge
+// owns exactly one 32-B slot, keyed by (parent's slot index, word id), and its
+// id IS that slot index.  The slot carries the node's whole record, so visiting
+// a node costs one line fetch (edge probe and node read in one).  '#' edges
+// have no slot: their filter is the parent's hash_filter ('match_#').
+constexpr int HOT_TABLES = 16;
+constexpr uint32_t ID_MASK = 0x7FFFFFFFu;
+constexpr uint32_t END_WILD = 0x80000000u;  // in end_filter: the filter is a wildcard one
+constexpr uint32_t HOT_PLUS = 1u;           // in flags: the node has a '+' child
+constexpr uint32_t FR_PLUS = 0x80000000u;   // in a frontier entry: the node has a '+' child
+constexpr uint64_t HOT_KEY_MARK = 1ull << 63;  // parent lives in table HOT_TABLES-2, child in the shared last
+
+struct alignas(32) HotSlot {
+  uint64_t key;          // hot_key(parent, word); EDGE_EMPTY marks an empty slot
+  uint32_t sig;          // bit sig_bit(h) set for each exact child word hash h; 0 = no exact child
+  uint32_t flags;        // HOT_PLUS
+  uint32_t hash_filter;  // filter id of "<node>/#", or NONE
+  uint32_t end_filter;   // filter id ending at the node | END_WILD, or NONE
+  uint32_t pad0, pad1;   // 32-B stride: two slots per 64-B line, never straddling one
+};
 // Read-only view of one index resident in HBM (passed by value to kernels).
 struct IndexView {
   const Node* nodes;
   const DictSlot* dict;
   const EdgeSlot* edges;
+  const HotSlot* hot;
   const uint8_t* arena;
   const uint64_t* sub_off;
   const uint32_t* sub_ids;
   uint64_t dict_mask;
   uint64_t etab_off[EDGE_DEPTHS];   // slot offset of each depth's table
   uint64_t etab_mask[EDGE_DEPTHS];  // slots - 1
+  uint64_t hot_off[HOT_TABLES];     // slot offset of each hot table (index = child depth, capped)
+  uint64_t hot_cap[HOT_TABLES];     // slots of each hot table
   uint32_t n_nodes;
   uint32_t n_filters;
   uint32_t plus_word;   // word id of "+" (NONE if no filter uses it)
   uint32_t hash_word;   // word id of "#"
+  uint32_t root_sig;    // the root's exact-child signature
+  uint32_t root_hash;   // filter id of "#", or NONE
+  uint32_t root_flags;  // HOT_PLUS if "+" starts a filter
+  uint32_t pad;
 };
 
 GM_HD uint64_t fmix64(uint64_t k) {
@@ -122,5 +151,28 @@ GM_HD uint64_t dict_slot(uint64_t h, uint64_t mask) { return (h ^ (h >> 29)) & m
 GM_HD int edge_depth(uint32_t depth) { return depth < uint32_t(EDGE_DEPTHS) ? int(depth) : EDGE_DEPTHS - 1; }
 GM_HD uint64_t edge_key(uint32_t parent, uint32_t word) { return (uint64_t(parent) << 32) | word; }
 GM_HD uint64_t edge_slot(uint64_t key, uint64_t mask) { return fmix64(key) & mask; }
+
+// Signature bit of a word (top 5 bits of its 64-bit hash).
+GM_HD uint32_t sig_bit(uint64_t word_hash) { return 1u << (word_hash >> 59); }
+GM_HD int hot_table(uint32_t depth) { return depth < uint32_t(HOT_TABLES) ? int(depth) : HOT_TABLES - 1; }
+// Key of the child of `parent` (a node at depth `pdepth`) through word `word`.
+GM_HD uint64_t hot_key(uint32_t parent, uint32_t word, uint32_t pdepth) {
+  return ((uint64_t(parent) << 32) | word) | (pdepth == uint32_t(HOT_TABLES - 2) ? HOT_KEY_MARK : 0ull);
+}
+GM_HD uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+// Home slot: 32-bit mix of (parent, word) and a multiply-shift range
+// reduction, so a table can hold any number of slots (< 2^32) without a
+// power-of-two blow-up, at a few 32-bit VALU ops per probe.
+GM_HD uint64_t hot_slot(uint64_t key, uint64_t cap) {
+  const uint32_t h = fmix32((uint32_t(key) * 0x9E3779B1u) ^ (uint32_t(key >> 32) * 0x85EBCA77u) ^ 0x27D4EB2Fu);
+  return (uint64_t(h) * cap) >> 32;
+}
 
 }  // namespace gm

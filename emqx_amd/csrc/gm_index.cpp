@@ -79,6 +79,9 @@ struct EdgeMap {
 struct HNode {
   uint32_t plus_child = NONE, hash_child = NONE, end_filter = NONE, flags = 0;
   uint32_t depth = 0;
+  uint32_t parent = NONE, word = NONE;  // incoming edge
+  uint32_t sig = 0;                     // exact-child word signature (HotSlot::sig)
+  uint8_t kind = 0;                     // incoming edge: 0 exact, 1 '+', 2 '#'
 };
 
 bool less_bytes(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
@@ -214,10 +217,13 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
         if (child >= REF_X) throw std::length_error("too many trie nodes (>= 2^31)");
         nodes.push_back(HNode{});
         nodes.back().depth = depth + 1;
+        nodes.back().parent = node;
+        nodes.back().word = id;
+        nodes.back().kind = plus ? 1 : hash ? 2 : 0;
         edges.put(key, child);
         if (plus) { nodes[node].plus_child = child; nodes[node].flags |= NF_HAS_PLUS; }
         else if (hash) nodes[node].hash_child = child;
-        else nodes[node].flags |= NF_HAS_EXACT;
+        else { nodes[node].flags |= NF_HAS_EXACT; nodes[node].sig |= sig_bit(hash_word_host(w, wl)); }
       }
       node = child;
       ++depth;
@@ -271,6 +277,56 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     std::vector<EdgeSlot>().swap(tabs[d].slots);
   }
 
+  // ---- 3b. hot tables: one 32-B slot per node reached through an exact or '+'
+  // edge, slot index = the node's hot id; built depth by depth because a key
+  // holds the parent's hot id.
+  std::vector<uint32_t> by_depth_off(max_depth + 2, 0);  // old nodes bucketed by depth
+  for (uint64_t i = 1; i < NN; ++i) by_depth_off[nodes[i].depth + 1]++;
+  for (size_t d = 1; d < by_depth_off.size(); ++d) by_depth_off[d] += by_depth_off[d - 1];
+  std::vector<uint32_t> by_depth(by_depth_off.back());
+  {
+    std::vector<uint32_t> cur(by_depth_off.begin(), by_depth_off.end() - 1);
+    for (uint64_t i = 1; i < NN; ++i) by_depth[cur[nodes[i].depth]++] = uint32_t(i);
+  }
+  uint64_t hot_n[HOT_TABLES] = {0};
+  for (uint64_t i = 1; i < NN; ++i)
+    if (nodes[i].kind != 2) hot_n[hot_table(nodes[i].depth)]++;
+  uint64_t hot_off[HOT_TABLES], hot_cap[HOT_TABLES], hot_total = 0;
+  for (int t = 0; t < HOT_TABLES; ++t) {
+    // load <= ~0.55; at least 8 slots so the probe loop always finds an empty one
+    hot_cap[t] = hot_n[t] ? std::max<uint64_t>(8, (hot_n[t] * 20 + 10) / 11 + 1) : 0;
+    hot_off[t] = hot_total;
+    hot_total += hot_cap[t];
+  }
+  std::vector<HotSlot> hot(hot_total, HotSlot{EDGE_EMPTY, 0, 0, NONE, NONE, 0, 0});
+  std::vector<uint32_t> hid(NN, NONE);
+  hid[0] = 0;  // the root (depth 0) is not stored; its record goes to IndexView
+  auto end_of = [&](const HNode& h) -> uint32_t {
+    if (h.end_filter == NONE) return NONE;
+    return h.end_filter | ((h.flags & NF_END_WILD) ? END_WILD : 0u);
+  };
+  for (uint32_t d = 1; d <= max_depth; ++d) {
+    const int t = hot_table(d);
+    HotSlot* tab = hot.data() + hot_off[t];
+    const uint64_t cap = hot_cap[t];
+    for (uint32_t k = by_depth_off[d]; k < by_depth_off[d + 1]; ++k) {
+      const uint32_t i = by_depth[k];
+      const HNode& h = nodes[i];
+      if (h.kind == 2 || hid[h.parent] == NONE) continue;  // '#' nodes and their (unmatchable) subtrees
+      const uint64_t key = hot_key(hid[h.parent], h.word, d - 1);
+      uint64_t s = hot_slot(key, cap);
+      while (tab[s].key != EDGE_EMPTY) s = s + 1 == cap ? 0 : s + 1;
+      if (s >= 0x7FFFFFFFull) throw std::length_error("hot table exceeds 2^31 slots");
+      HotSlot& o = tab[s];
+      o.key = key;
+      o.sig = h.sig;
+      o.hash_filter = h.hash_child == NONE ? NONE : nodes[h.hash_child].end_filter;
+      o.end_filter = end_of(h);
+      o.flags = h.plus_child != NONE ? HOT_PLUS : 0u;
+      hid[i] = uint32_t(s);
+    }
+  }
+
   // ---- 4. word dictionary (open addressing by hash, verified by bytes)
   uint64_t nw = word_ids.size();
   uint64_t dcap = next_pow2(nw * 2 + 2);
@@ -310,7 +366,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   size_t o_nodes = 0;
   size_t o_dict = o_nodes + al(NN * sizeof(Node));
   size_t o_edges = o_dict + al(dcap * sizeof(DictSlot));
-  size_t o_arena = o_edges + al(dedges.size() * sizeof(EdgeSlot));
+  size_t o_hot = o_edges + al(dedges.size() * sizeof(EdgeSlot));
+  size_t o_arena = o_hot + al(hot.size() * sizeof(HotSlot));
   size_t o_soff = o_arena + al(arena.size() + 64);
   size_t o_sids = o_soff + al(soff.size() * 8);
   size_t o_flen = o_sids + al(sids.size() * 4 + 4);
@@ -345,6 +402,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   up(o_nodes, dnodes.data(), NN * sizeof(Node));
   up(o_dict, dict.data(), dcap * sizeof(DictSlot));
   up(o_edges, dedges.data(), dedges.size() * sizeof(EdgeSlot));
+  up(o_hot, hot.data(), hot.size() * sizeof(HotSlot));
   up(o_arena, arena.data(), arena.size());
   up(o_soff, soff.data(), soff.size() * 8);
   up(o_sids, sids.data(), sids.size() * 4);
@@ -359,6 +417,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.nodes = reinterpret_cast<const Node*>(B + o_nodes);
   v.dict = reinterpret_cast<const DictSlot*>(B + o_dict);
   v.edges = reinterpret_cast<const EdgeSlot*>(B + o_edges);
+  v.hot = reinterpret_cast<const HotSlot*>(B + o_hot);
   v.arena = B + o_arena;
   v.sub_off = reinterpret_cast<const uint64_t*>(B + o_soff);
   v.sub_ids = reinterpret_cast<const uint32_t*>(B + o_sids);
@@ -367,6 +426,13 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     v.etab_off[d] = etab_off[d];
     v.etab_mask[d] = etab_mask[d];
   }
+  for (int t = 0; t < HOT_TABLES; ++t) {
+    v.hot_off[t] = hot_off[t];
+    v.hot_cap[t] = hot_cap[t];
+  }
+  v.root_sig = nodes[0].sig;
+  v.root_hash = nodes[0].hash_child == NONE ? NONE : nodes[nodes[0].hash_child].end_filter;
+  v.root_flags = nodes[0].plus_child != NONE ? HOT_PLUS : 0u;
   v.n_nodes = uint32_t(NN);
   v.n_filters = nf;
   v.plus_word = plus_word;

@@ -3,21 +3,25 @@
 // Hot path (replaces emqx_trie:match/1 + emqx_router:match_routes/1,
 // apps/emqx/src/emqx_trie.erl:147-333, apps/emqx/src/emqx_router.erl:128-145):
 //
-//   k_match_fast   one lane per publish topic, 64 topics per wave (a tile).
-//                  Streams the topic bytes once, hashes each level word,
-//                  resolves it in the word dictionary (verified byte-for-byte),
-//                  and expands the NFA frontier over exact / '+' / '#' edges.
-//                  Frontier and match lists live in LDS.  Rows are sorted by
-//                  filter id in LDS and compacted per wave with a prefix scan
-//                  into a per-tile staging region.  Topics whose frontier or
-//                  match list exceeds the LDS capacity are queued for
-//                  k_slow_walk (no truncation, no CPU fallback).
+//   k_match_reg    main pass: one lane per publish topic, 64 topics per wave
+//                  (a tile).  Streams the topic bytes once, hashes each level
+//                  word, resolves it in the word dictionary (verified
+//                  byte-for-byte) and expands the NFA frontier over exact /
+//                  '+' / '#' edges.  The frontier lives in registers (no LDS),
+//                  so occupancy is bounded by VGPRs alone; visiting a node is
+//                  one 32-B hot-slot load (edge probe and node record in one).
+//                  Matches are staged per tile as [slot][lane].
+//   k_match_lds    the same walk with the frontier in LDS (capacity FC).  As
+//                  the LISTED pass it re-walks the topics whose frontier or
+//                  row outgrew the main pass (count read on the device, so no
+//                  host round trip between the passes).
 //   k_tile_sums / scan / k_assemble
 //                  count -> scan -> write: builds the CSR (row_off u64, ids u32).
 //   k_slow_walk / k_slow_emit / k_copy_slow
-//                  device slow path: one workgroup per overflowing topic,
-//                  frontier in HBM (bounded by the node count), matches as a
-//                  bitmap over filter ids, emitted in ascending id order.
+//                  device slow path: one workgroup per topic the listed pass
+//                  could not hold, frontier in HBM (bounded by the node
+//                  count), matches as a bitmap over filter ids, emitted in
+//                  ascending id order.  No truncation, no CPU fallback.
 //
 // Fan-out (replaces emqx_broker:dispatch/2 + do_dispatch, emqx_broker.erl:
 // 296-322, 506-530): k_fanout_seglen -> scan -> k_fanout_copy, a load-balanced
@@ -29,6 +33,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "gm_internal.h"
@@ -163,7 +169,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) 
 }
 
 // ---------------------------------------------------------------------------
-// k_match_fast
+// match kernels
 // ---------------------------------------------------------------------------
 // Staging layout per 64-topic tile: [slot k][lane], FAST_MC slots, so the k-th
 // match of every lane is one coalesced 256-B row.
@@ -171,47 +177,157 @@ __device__ __forceinline__ uint64_t stage_index(uint64_t tile, uint32_t k, int l
   return tile * (64ull * FAST_MC) + uint64_t(k) * 64u + uint32_t(lane);
 }
 
-template <bool EXACT>
-__global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ tb,
-                                                    const uint64_t* __restrict__ toff, uint64_t n,
-                                                    IndexView ix, uint32_t* __restrict__ cnt,
-                                                    uint32_t* __restrict__ stage,
-                                                    uint32_t* __restrict__ ovf_list,
-                                                    uint32_t* __restrict__ ovf_n,
-                                                    unsigned long long* __restrict__ probe_ctr,
-                                                    unsigned long long* __restrict__ wild_ctr) {
-  constexpr int FC = FAST_FC, MC = FAST_MC;
-  __shared__ uint32_t s_fr[2][FC][256];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const uint64_t t = uint64_t(blockIdx.x) * 256u + tid;
-  const uint64_t tile = t >> 6;
-  const bool valid = t < n;
-  const Node root = ix.nodes[0];  // uniform: one scalar load per wave
+// A hot slot as the kernel reads it: the 24 used bytes, in two loads
+// (dwordx4 + dwordx2) from one 64-B line.
+struct HotRec {
+  uint4 a;  // key lo, key hi, sig, flags
+  uint2 b;  // hash_filter, end_filter
+};
+__device__ __forceinline__ HotRec hot_load(const HotSlot* tab, uint32_t s) {
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(tab + s);
+  HotRec r;
+  r.a = *reinterpret_cast<const uint4*>(p);
+  r.b = *reinterpret_cast<const uint2*>(p + 4);
+  return r;
+}
+__device__ __forceinline__ bool hot_is(const HotRec& r, uint64_t key) {
+  return r.a.x == uint32_t(key) && r.a.y == uint32_t(key >> 32);
+}
+__device__ __forceinline__ bool hot_empty(const HotRec& r) { return r.a.x == 0xFFFFFFFFu && r.a.y == 0xFFFFFFFFu; }
+// Linear probing from slot s (whose record r is already loaded); returns the
+// slot index of `key` or NONE.
+__device__ __forceinline__ uint32_t hot_resolve(const HotSlot* tab, uint32_t cap, uint64_t key, uint32_t s,
+                                                HotRec& r) {
+  while (!hot_is(r, key)) {
+    if (hot_empty(r)) return NONE;
+    s = s + 1 == cap ? 0 : s + 1;
+    r = hot_load(tab, s);
+  }
+  return s;
+}
 
-  uint32_t m_n = 0;
+// Per-lane match staging: emit one filter id into the topic's row (slot m_n
+// of the topic's lane column `slane` in its tile).
+#define GM_EMIT(f)                                                   \
+  do {                                                               \
+    if (m_n < MC) stage[stage_index(tile, m_n, slane)] = (f);        \
+    ++m_n;                                                           \
+  } while (0)
+
+// Visit a node reached at this level (its record r, hot id hs): emit
+// 'match_#' for it; on the topic's last word also its own filter
+// (lookup_topic/3: only wildcard filters in trie mode; the '$X' quirk of
+// emqx_trie.erl:275-276 for single-word '$' topics); otherwise push it onto
+// the next frontier (GM_PUSH is defined per kernel).
+#define GM_VISIT(hs, r)                                                                 \
+  do {                                                                                  \
+    if ((r).b.x != NONE) GM_EMIT((r).b.x);                                              \
+    if (last) {                                                                         \
+      if ((r).b.y != NONE && (EXACT || ((r).b.y & END_WILD) || (dollar && level == 0))) \
+        GM_EMIT((r).b.y & ID_MASK);                                                     \
+      ++nfinal;                                                                         \
+    } else {                                                                            \
+      GM_PUSH((hs) | (((r).a.w & HOT_PLUS) ? FR_PLUS : 0u), (r).a.z);                   \
+    }                                                                                   \
+  } while (0)
+
+// A wildcard publish topic: [] from the trie (emqx_trie.erl:149-158); with
+// match_routes semantics the literal route lookup_routes(Topic)
+// (emqx_router.erl:128-134).
+#define GM_WILD_ROW()                                        \
+  do {                                                       \
+    m_n = 0;                                                 \
+    ovf = false;                                             \
+    if (EXACT) {                                             \
+      const uint32_t f = literal_lookup(ix, tb, start, end); \
+      if (f != NONE) {                                       \
+        stage[stage_index(tile, 0, slane)] = f;              \
+        m_n = 1;                                             \
+      }                                                      \
+    }                                                        \
+  } while (0)
+
+// ---- k_match_reg ----------------------------------------------------------
+// Frontier: at most RFC entries {hot id | FR_PLUS, exact-child signature} in
+// registers (pushes are select chains over static indices, so nothing spills
+// to scratch).  PAIR: entries are expanded two at a time, so up to four slot
+// loads per lane are in flight before the first is consumed.  A lane whose
+// frontier outgrows RFC, or whose row outgrows FAST_MC, is queued for the
+// listed LDS pass and contributes nothing here.
+constexpr int RFC = 4;
+
+#define GM_PUSH(idv, sigv)                                \
+  do {                                                    \
+    const uint32_t pid_ = (idv), psig_ = (sigv);          \
+    _Pragma("unroll") for (int q_ = 0; q_ < RFC; ++q_) {  \
+      if (nn == uint32_t(q_)) {                           \
+        nid[q_] = pid_;                                   \
+        nsig[q_] = psig_;                                 \
+      }                                                   \
+    }                                                     \
+    ++nn;                                                 \
+  } while (0)
+
+// Issue (load the home slot of) / take (resolve and visit) one probe of a
+// frontier entry: the exact edge (word wid) or the '+' edge.
+#define GM_PROBE_ISSUE(c, e_id, plus, sx, rx)                                           \
+  do {                                                                                  \
+    if (c) {                                                                            \
+      sx = uint32_t(hot_slot(hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), cap));  \
+      rx = hot_load(tab, sx);                                                           \
+    }                                                                                   \
+  } while (0)
+
+#define GM_PROBE_TAKE(c, e_id, plus, sx, rx)                                                              \
+  do {                                                                                                    \
+    if (c) {                                                                                              \
+      const uint32_t hs_ = hot_resolve(tab, capu, hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), sx, rx); \
+      if (hs_ != NONE) GM_VISIT(hs_, rx);                                                                 \
+    }                                                                                                     \
+  } while (0)
+
+// MINW: waves per SIMD the register budget is sized for (__launch_bounds__'s
+// second argument; 1 leaves the allocation to the compiler).
+template <bool EXACT, bool PAIR, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_match_reg(const uint8_t* __restrict__ tb,
+                                                   const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
+                                                   uint32_t* __restrict__ cnt, uint32_t* __restrict__ stage,
+                                                   uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
+                                                   unsigned long long* __restrict__ probe_ctr,
+                                                   unsigned long long* __restrict__ wild_ctr) {
+  constexpr int MC = FAST_MC;
+  const int lane = threadIdx.x & 63;
+  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  const uint64_t tile = t >> 6;
+  const int slane = lane;
+  const bool valid = t < n;
+  uint32_t m_n = 0, probes = 0;
   bool ovf = false, wild = false;
-  uint32_t probes = 0;
 
   if (valid) {
     uint64_t pos = toff[t];
     const uint64_t end = toff[t + 1];
     const uint64_t start = pos;
     ByteReader rd{tb, ~0ull, 0};
-    int cur = 0;
-    uint32_t cur_n = 1;
-    s_fr[0][0][tid] = (root.flags & NF_HAS_EXACT) ? REF_X : 0u;  // the virtual root (emqx_trie.erl:264)
-    bool dollar = false;
-    uint32_t level = 0;
     WordTok w = next_word(rd, pos, end);
     DictSlot d0 = dict_first(ix, w);
+    // '$'-topics skip the root-level '+' and '#' (emqx_trie.erl:271-278)
+    const bool dollar = w.len > 0 && w.b0 == '$';
+    if (!dollar && ix.root_hash != NONE) GM_EMIT(ix.root_hash);  // '#' at the virtual root
+    uint32_t fid[RFC], fsig[RFC];
+#pragma unroll
+    for (int q = 0; q < RFC; ++q) fid[q] = fsig[q] = 0;
+    fid[0] = (!dollar && (ix.root_flags & HOT_PLUS)) ? FR_PLUS : 0u;
+    fsig[0] = ix.root_sig;
+    uint32_t cur_n = 1, nfinal = 0, level = 0;
     for (;;) {
       const bool last = pos >= end;
       if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {
         wild = true;  // emqx_topic:wildcard/1
         break;
       }
-      if (level == 0) dollar = w.len > 0 && w.b0 == '$';
       const uint32_t wid = cur_n ? dict_resolve(ix, w, d0, tb) : NONE;
+      const uint32_t wbit = sig_bit(w.h);
       // prefetch the next level's word while this level's frontier expands
       WordTok wn;
       DictSlot dn;
@@ -222,43 +338,185 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
       }
       if (cur_n) {
         probes += 3 * cur_n;
+        uint32_t nid[RFC], nsig[RFC], nn = 0;
+#pragma unroll
+        for (int q = 0; q < RFC; ++q) nid[q] = nsig[q] = 0;
+        const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);  // wave-uniform
+        const int ht = hot_table(lvl + 1);
+        const HotSlot* tab = ix.hot + ix.hot_off[ht];
+        const uint64_t cap = ix.hot_cap[ht];
+        const uint32_t capu = uint32_t(cap);
+        const bool wok = wid != NONE;
+        if (PAIR) {
+#pragma unroll
+          for (int i = 0; i < RFC; i += 2) {
+            if (uint32_t(i) < cur_n) {
+              const bool hb = uint32_t(i + 1) < cur_n;
+              const uint32_t ia = fid[i] & ID_MASK, ib = fid[i + 1] & ID_MASK;
+              const bool ax = wok && (fsig[i] & wbit), ap = (fid[i] & FR_PLUS) != 0;
+              const bool bx = hb && wok && (fsig[i + 1] & wbit), bp = hb && (fid[i + 1] & FR_PLUS) != 0;
+              uint32_t sax = 0, sap = 0, sbx = 0, sbp = 0;
+              HotRec rax{}, rap{}, rbx{}, rbp{};
+              // issue every load of the pair before consuming any
+              GM_PROBE_ISSUE(ax, ia, false, sax, rax);
+              GM_PROBE_ISSUE(ap, ia, true, sap, rap);
+              GM_PROBE_ISSUE(bx, ib, false, sbx, rbx);
+              GM_PROBE_ISSUE(bp, ib, true, sbp, rbp);
+              GM_PROBE_TAKE(ax, ia, false, sax, rax);
+              GM_PROBE_TAKE(ap, ia, true, sap, rap);
+              GM_PROBE_TAKE(bx, ib, false, sbx, rbx);
+              GM_PROBE_TAKE(bp, ib, true, sbp, rbp);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < RFC; ++i) {
+            if (uint32_t(i) < cur_n) {
+              const uint32_t ia = fid[i] & ID_MASK;
+              const bool ax = wok && (fsig[i] & wbit), ap = (fid[i] & FR_PLUS) != 0;
+              uint32_t sax = 0, sap = 0;
+              HotRec rax{}, rap{};
+              GM_PROBE_ISSUE(ax, ia, false, sax, rax);
+              GM_PROBE_ISSUE(ap, ia, true, sap, rap);
+              GM_PROBE_TAKE(ax, ia, false, sax, rax);
+              GM_PROBE_TAKE(ap, ia, true, sap, rap);
+            }
+          }
+        }
+        if (nn > RFC) {
+          ovf = true;
+          break;
+        }
+#pragma unroll
+        for (int q = 0; q < RFC; ++q) {
+          fid[q] = nid[q];
+          fsig[q] = nsig[q];
+        }
+        cur_n = nn;
+      }
+      if (last) break;
+      w = wn;
+      d0 = dn;
+      ++level;
+    }
+    if (wild) {
+      GM_WILD_ROW();
+    } else if (!ovf) {
+      probes += 2 * nfinal + 1;
+      if (m_n > MC) ovf = true;
+    }
+    if (ovf) probes = 0;  // the listed pass walks this topic again and counts it
+  }
+
+  if (valid) {
+    cnt[t] = ovf ? OVF_BIT : m_n;
+    if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
+  }
+  // per-wave counters (one atomic per wave)
+  uint32_t ptot;
+  wave_excl_scan(probes, ptot);
+  const unsigned long long wb = __ballot(valid && wild);
+  if (lane == 0) {
+    atomicAdd(probe_ctr, (unsigned long long)ptot);
+    if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
+  }
+}
+#undef GM_PUSH
+#undef GM_PROBE_ISSUE
+#undef GM_PROBE_TAKE
+
+// ---- k_match_lds ----------------------------------------------------------
+// Frontier entries double buffered in LDS, FC per lane.  LISTED: grid-stride
+// over the topics list_in[0 .. *list_n) (the main pass's overflow queue; the
+// count is read on the device); otherwise one topic per thread.  Overflow
+// here (frontier > FC or row > FAST_MC) is queued for k_slow_walk.
+#define GM_PUSH(idv, sigv)                                                 \
+  do {                                                                     \
+    if (nn < FC) s_fr[nb][nn][threadIdx.x] = make_uint2((idv), (sigv));    \
+    ++nn;                                                                  \
+  } while (0)
+
+template <bool EXACT, int FC, bool LISTED>
+__global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ tb,
+                                                   const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
+                                                   uint32_t* __restrict__ cnt, uint32_t* __restrict__ stage,
+                                                   const uint32_t* __restrict__ list_in,
+                                                   const uint32_t* __restrict__ list_n,
+                                                   uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
+                                                   unsigned long long* __restrict__ probe_ctr,
+                                                   unsigned long long* __restrict__ wild_ctr) {
+  constexpr int MC = FAST_MC;
+  // frontier entry: {hot id | FR_PLUS, exact-child signature}, double buffered
+  __shared__ uint2 s_fr[2][FC][256];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint64_t n_items = LISTED ? uint64_t(*list_n) : n;
+  uint32_t probes = 0, wilds = 0;
+
+  for (uint64_t item = uint64_t(blockIdx.x) * 256u + tid; item < n_items;
+       item += uint64_t(gridDim.x) * 256u) {
+    const uint64_t t = LISTED ? uint64_t(list_in[item]) : item;
+    const uint64_t tile = t >> 6;
+    const int slane = int(t & 63);
+    uint32_t m_n = 0, tprobes = 0;
+    bool ovf = false, wild = false;
+    uint64_t pos = toff[t];
+    const uint64_t end = toff[t + 1];
+    const uint64_t start = pos;
+    ByteReader rd{tb, ~0ull, 0};
+    WordTok w = next_word(rd, pos, end);
+    DictSlot d0 = dict_first(ix, w);
+    const bool dollar = w.len > 0 && w.b0 == '$';  // emqx_trie.erl:271-278
+    if (!dollar && ix.root_hash != NONE) GM_EMIT(ix.root_hash);
+    int cur = 0;
+    uint32_t cur_n = 1, nfinal = 0;
+    s_fr[0][0][tid] = make_uint2((!dollar && (ix.root_flags & HOT_PLUS)) ? FR_PLUS : 0u, ix.root_sig);
+    uint32_t level = 0;
+    for (;;) {
+      const bool last = pos >= end;
+      if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {
+        wild = true;
+        break;
+      }
+      const uint32_t wid = cur_n ? dict_resolve(ix, w, d0, tb) : NONE;
+      const uint32_t wbit = sig_bit(w.h);
+      WordTok wn;
+      DictSlot dn;
+      if (!last) {
+        ++pos;
+        wn = next_word(rd, pos, end);
+        dn = dict_first(ix, wn);
+      }
+      if (cur_n) {
+        tprobes += 3 * cur_n;
         const int nb = cur ^ 1;
         uint32_t nn = 0;
         const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);  // wave-uniform
-        const int ed = edge_depth(lvl);
-        const EdgeSlot* etab = ix.edges + ix.etab_off[ed];
-        const uint64_t emask = ix.etab_mask[ed];
-        // '$'-topics skip the root-level '+' and '#' (emqx_trie.erl:271-278).
-        const bool rootskip = dollar && level == 0;
+        const int ht = hot_table(lvl + 1);
+        const HotSlot* tab = ix.hot + ix.hot_off[ht];
+        const uint64_t cap = ix.hot_cap[ht];
+        const uint32_t capu = uint32_t(cap);
         for (uint32_t i = 0; i < cur_n; ++i) {
-          const uint32_t ref = s_fr[cur][i][tid];
-          const uint32_t nd = ref & REF_MASK;
-          const bool probe = (ref & REF_X) && wid != NONE;
-          const uint64_t key = edge_key(nd, wid);
-          uint64_t sl = edge_slot(key, emask);
-          EdgeSlot e;
-          e.key = EDGE_EMPTY;
-          if (probe) e = etab[sl];        // issued together with the node read
-          const Node node = level == 0 ? root : ix.nodes[nd];
-          if (!rootskip) {
-            if (node.hash_filter != NONE) {  // 'match_#' at a visited prefix
-              if (m_n < MC) stage[stage_index(tile, m_n, lane)] = node.hash_filter;
-              ++m_n;
-            }
-            if (node.plus_child != NONE) {
-              if (nn < FC) s_fr[nb][nn][tid] = node.plus_child;
-              ++nn;
-            }
+          const uint2 e = s_fr[cur][i][tid];
+          const uint32_t id = e.x & ID_MASK;
+          const bool dx = wid != NONE && (e.y & wbit);
+          const bool dp = (e.x & FR_PLUS) != 0;
+          uint32_t sx = 0, sp = 0;
+          HotRec rx{}, rp{};
+          if (dx) {
+            sx = uint32_t(hot_slot(hot_key(id, wid, lvl), cap));
+            rx = hot_load(tab, sx);
           }
-          if (probe) {
-            while (e.key != key && e.key != EDGE_EMPTY) {
-              sl = (sl + 1) & emask;
-              e = etab[sl];
-            }
-            if (e.key == key) {
-              if (nn < FC) s_fr[nb][nn][tid] = e.child;
-              ++nn;
-            }
+          if (dp) {
+            sp = uint32_t(hot_slot(hot_key(id, ix.plus_word, lvl), cap));
+            rp = hot_load(tab, sp);
+          }
+          if (dx) {
+            const uint32_t hs = hot_resolve(tab, capu, hot_key(id, wid, lvl), sx, rx);
+            if (hs != NONE) GM_VISIT(hs, rx);
+          }
+          if (dp) {
+            const uint32_t hs = hot_resolve(tab, capu, hot_key(id, ix.plus_word, lvl), sp, rp);
+            if (hs != NONE) GM_VISIT(hs, rp);
           }
         }
         if (nn > FC) {
@@ -274,46 +532,30 @@ __global__ __launch_bounds__(256) void k_match_fast(const uint8_t* __restrict__ 
       ++level;
     }
     if (wild) {
-      m_n = 0;
-      ovf = false;
-      if (EXACT) {
-        const uint32_t f = literal_lookup(ix, tb, start, end);
-        if (f != NONE) {
-          stage[stage_index(tile, 0, lane)] = f;
-          m_n = 1;
-        }
-      }
+      GM_WILD_ROW();
     } else if (!ovf) {
-      probes += 2 * cur_n + 1;
-      for (uint32_t i = 0; i < cur_n; ++i) {
-        const Node node = ix.nodes[s_fr[cur][i][tid] & REF_MASK];
-        if (node.hash_filter != NONE) {
-          if (m_n < MC) stage[stage_index(tile, m_n, lane)] = node.hash_filter;
-          ++m_n;
-        }
-        if (node.end_filter != NONE &&
-            (EXACT || (node.flags & NF_END_WILD) || (dollar && level == 0))) {
-          if (m_n < MC) stage[stage_index(tile, m_n, lane)] = node.end_filter;
-          ++m_n;
-        }
-      }
+      tprobes += 2 * nfinal + 1;
       if (m_n > MC) ovf = true;
     }
-  }
-
-  if (valid) {
     cnt[t] = ovf ? OVF_BIT : m_n;
     if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
+    probes += tprobes;
+    wilds += wild ? 1u : 0u;
+    if (!LISTED) break;
   }
   // per-wave counters (one atomic per wave)
-  uint32_t ptot;
-  wave_excl_scan(valid ? probes : 0, ptot);
-  const unsigned long long wb = __ballot(valid && wild);
+  uint32_t ptot, wtot;
+  wave_excl_scan(probes, ptot);
+  wave_excl_scan(wilds, wtot);
   if (lane == 0) {
     atomicAdd(probe_ctr, (unsigned long long)ptot);
-    if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
+    if (wtot) atomicAdd(wild_ctr, (unsigned long long)wtot);
   }
 }
+#undef GM_PUSH
+#undef GM_VISIT
+#undef GM_WILD_ROW
+#undef GM_EMIT
 
 // ---------------------------------------------------------------------------
 // scan (u64, exclusive, n+1 outputs: out[n] = total)
@@ -713,6 +955,59 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+// Main-pass kernel selection.  GM_MATCH_MAIN (A/B knob, read once):
+// reg{1,2}[w6|w8] (register frontier, one entry / pairs per step, register
+// budget for 6 / 8 waves per SIMD), lds4, lds8 (LDS frontier).
+enum MainKind { MAIN_REG1, MAIN_REG1W6, MAIN_REG1W8, MAIN_REG2, MAIN_REG2W6, MAIN_REG2W8, MAIN_LDS4, MAIN_LDS8 };
+MainKind main_kind() {
+  static const MainKind k = [] {
+    const char* e = getenv("GM_MATCH_MAIN");
+    static const struct { const char* name; MainKind kind; } names[] = {
+        {"reg1", MAIN_REG1}, {"reg1w6", MAIN_REG1W6}, {"reg1w8", MAIN_REG1W8}, {"reg2", MAIN_REG2},
+        {"reg2w6", MAIN_REG2W6}, {"reg2w8", MAIN_REG2W8}, {"lds4", MAIN_LDS4}, {"lds8", MAIN_LDS8}};
+    if (e)
+      for (const auto& nk : names)
+        if (!strcmp(e, nk.name)) return nk.kind;
+    return MAIN_REG1W6;
+  }();
+  return k;
+}
+
+constexpr int LISTED_FC = 16;  // frontier capacity of the listed pass
+
+// Main pass, then the listed pass over its overflow queue (count read on the
+// device).  `after_main` is recorded between the two: the roofline times the
+// main pass alone, the same kernel rocprofv3 reports.
+template <bool EXACT>
+void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                  uint32_t* cnt, uint32_t* stage, uint32_t* list1, uint32_t* n1, uint32_t* list2, uint32_t* n2,
+                  unsigned long long* probe_ctr, unsigned long long* wild_ctr, hipEvent_t after_main) {
+  hipStream_t st = ctx->stream;
+  const uint64_t nblk = (n + 255) / 256;
+#define GM_LAUNCH_REG(P, W)                                                                                  \
+  hipLaunchKernelGGL((k_match_reg<EXACT, P, W>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, list1, n1, \
+                     probe_ctr, wild_ctr)
+#define GM_LAUNCH_LDS(F)                                                                                     \
+  hipLaunchKernelGGL((k_match_lds<EXACT, F, false>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, \
+                     nullptr, nullptr, list1, n1, probe_ctr, wild_ctr)
+  switch (main_kind()) {
+    case MAIN_REG1: GM_LAUNCH_REG(false, 1); break;
+    case MAIN_REG1W8: GM_LAUNCH_REG(false, 8); break;
+    case MAIN_REG2: GM_LAUNCH_REG(true, 1); break;
+    case MAIN_REG2W6: GM_LAUNCH_REG(true, 6); break;
+    case MAIN_REG2W8: GM_LAUNCH_REG(true, 8); break;
+    case MAIN_LDS4: GM_LAUNCH_LDS(4); break;
+    case MAIN_LDS8: GM_LAUNCH_LDS(8); break;
+    default: GM_LAUNCH_REG(false, 6);
+  }
+#undef GM_LAUNCH_REG
+#undef GM_LAUNCH_LDS
+  hipEventRecord(after_main, st);
+  const uint64_t lblk = std::min<uint64_t>(nblk, 512);
+  hipLaunchKernelGGL((k_match_lds<EXACT, LISTED_FC, true>), dim3(lblk), dim3(256), 0, st, tb, to, n, v, cnt, stage,
+                     list1, n1, list2, n2, probe_ctr, wild_ctr);
+}
+
 }  // namespace
 
 int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, const uint64_t* to_in, uint64_t n,
@@ -753,13 +1048,16 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   const uint64_t nblk = (n + 255) / 256;
   PoolBuf cnt(ctx->pool, n * 4 + 16);
   PoolBuf stage(ctx->pool, n_tiles * 64ull * FAST_MC * 4);
-  PoolBuf ovf_list(ctx->pool, n * 4 + 16);
+  PoolBuf list1(ctx->pool, n * 4 + 16), list2(ctx->pool, n * 4 + 16);
   PoolBuf ctrs(ctx->pool, 64);
   PoolBuf tsum(ctx->pool, n_tiles * 8 + 8);
   PoolBuf toff(ctx->pool, (n_tiles + 1) * 8);
-  if (!cnt.p || !stage.p || !ovf_list.p || !ctrs.p || !tsum.p || !toff.p)
+  if (!cnt.p || !stage.p || !list1.p || !list2.p || !ctrs.p || !tsum.p || !toff.p)
     return set_err(ctx, EMQX_GM_ENOMEM, "match: workspace");
-  uint32_t* ovf_n = ctrs.as<uint32_t>();
+  // counters: u32 n1 @0 (main-pass overflow), u32 n2 @4 (listed-pass
+  // overflow), u64 probes @16, u64 wildcard topics @24
+  uint32_t* n1 = ctrs.as<uint32_t>();
+  uint32_t* n2 = n1 + 1;
   unsigned long long* probe_ctr = reinterpret_cast<unsigned long long*>(ctrs.as<uint8_t>() + 16);
   unsigned long long* wild_ctr = reinterpret_cast<unsigned long long*>(ctrs.as<uint8_t>() + 24);
   GM_HIP(ctx, hipMemsetAsync(ctrs.p, 0, 64, st));
@@ -767,24 +1065,25 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   GM_HIP(ctx, hipEventRecord(ctx->ev[0], st));
   GM_HIP(ctx, hipEventRecord(ctx->ev[1], st));
   if (exact)
-    hipLaunchKernelGGL(k_match_fast<true>, dim3(nblk), dim3(256), 0, st, tb, to, n, idx->view, cnt.as<uint32_t>(),
-                       stage.as<uint32_t>(), ovf_list.as<uint32_t>(), ovf_n, probe_ctr, wild_ctr);
+    launch_match<true>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
+                       list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, ctx->ev[2]);
   else
-    hipLaunchKernelGGL(k_match_fast<false>, dim3(nblk), dim3(256), 0, st, tb, to, n, idx->view, cnt.as<uint32_t>(),
-                       stage.as<uint32_t>(), ovf_list.as<uint32_t>(), ovf_n, probe_ctr, wild_ctr);
+    launch_match<false>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(),
+                        n1, list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, ctx->ev[2]);
   GM_HIP(ctx, hipGetLastError());
-  GM_HIP(ctx, hipEventRecord(ctx->ev[2], st));
 
   uint64_t h_ctr[4] = {0, 0, 0, 0};
   GM_HIP(ctx, hipMemcpyAsync(h_ctr, ctrs.p, 32, hipMemcpyDeviceToHost, st));
   GM_HIP(ctx, hipStreamSynchronize(st));
-  const uint64_t n_ovf = uint32_t(h_ctr[0]);
+  const uint64_t n_listed = uint32_t(h_ctr[0]);
+  const uint64_t n_ovf = uint32_t(h_ctr[0] >> 32);
   ctx->stats.probes = h_ctr[2];
   ctx->stats.n_wildcard_topics = h_ctr[3];
-  ctx->stats.n_overflow = n_ovf;
+  ctx->stats.n_overflow = n_listed;
 
-  // ---- slow path for overflowing rows
+  // ---- slow path for rows the listed pass could not hold
   PoolBuf slow_off, slow_ids;
+  uint32_t* ovf_list = list2.as<uint32_t>();
   if (n_ovf) {
     const uint64_t fr_cap = uint64_t(idx->view.n_nodes) + 1;
     const uint64_t bm_words = (uint64_t(idx->view.n_filters) + 31) / 32 + 1;
@@ -803,13 +1102,13 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
     for (uint64_t k0 = 0; k0 < n_ovf; k0 += chunk) {
       const uint64_t kn = std::min(n_ovf, k0 + chunk);
       if (exact)
-        hipLaunchKernelGGL(k_slow_walk<true>, dim3(kn - k0), dim3(256), 0, st, tb, to, idx->view,
-                           ovf_list.as<uint32_t>(), k0, kn, fr.as<uint32_t>(), fr_cap, bm.as<uint32_t>(), bm_words,
-                           cnt.as<uint32_t>(), scnt.as<uint64_t>());
+        hipLaunchKernelGGL(k_slow_walk<true>, dim3(kn - k0), dim3(256), 0, st, tb, to, idx->view, ovf_list, k0, kn,
+                           fr.as<uint32_t>(), fr_cap, bm.as<uint32_t>(), bm_words, cnt.as<uint32_t>(),
+                           scnt.as<uint64_t>());
       else
-        hipLaunchKernelGGL(k_slow_walk<false>, dim3(kn - k0), dim3(256), 0, st, tb, to, idx->view,
-                           ovf_list.as<uint32_t>(), k0, kn, fr.as<uint32_t>(), fr_cap, bm.as<uint32_t>(), bm_words,
-                           cnt.as<uint32_t>(), scnt.as<uint64_t>());
+        hipLaunchKernelGGL(k_slow_walk<false>, dim3(kn - k0), dim3(256), 0, st, tb, to, idx->view, ovf_list, k0, kn,
+                           fr.as<uint32_t>(), fr_cap, bm.as<uint32_t>(), bm_words, cnt.as<uint32_t>(),
+                           scnt.as<uint64_t>());
       GM_HIP(ctx, hipGetLastError());
       std::vector<uint64_t> c(kn - k0);
       GM_HIP(ctx, hipMemcpyAsync(c.data(), scnt.as<uint64_t>() + k0, (kn - k0) * 8, hipMemcpyDeviceToHost, st));
@@ -845,8 +1144,8 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
                      stage.as<uint32_t>(), row_off.as<uint64_t>(), ids.as<uint32_t>());
   GM_HIP(ctx, hipGetLastError());
   if (n_ovf) {
-    hipLaunchKernelGGL(k_copy_slow, dim3(n_ovf), dim3(256), 0, st, ovf_list.as<uint32_t>(), n_ovf,
-                       row_off.as<uint64_t>(), slow_off.as<uint64_t>(), slow_ids.as<uint32_t>(), ids.as<uint32_t>());
+    hipLaunchKernelGGL(k_copy_slow, dim3(n_ovf), dim3(256), 0, st, ovf_list, n_ovf, row_off.as<uint64_t>(),
+                       slow_off.as<uint64_t>(), slow_ids.as<uint32_t>(), ids.as<uint32_t>());
     GM_HIP(ctx, hipGetLastError());
   }
   GM_HIP(ctx, hipEventRecord(ctx->ev[3], st));
