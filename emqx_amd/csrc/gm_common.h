@@ -77,7 +77,7 @@ constexpr uint64_t HOT_KEY_MARK = 1ull << 63;  // parent lives in table HOT_TABL
 
 struct alignas(32) HotSlot {
   uint64_t key;          // hot_key(parent, word); EDGE_EMPTY marks an empty slot
-  uint32_t sig;          // bit sig_bit(h) set for each exact child word hash h; 0 = no exact child
+  uint32_t sig;          // bit sig_bit(w) set for each exact child word id w; 0 = no exact child
   uint32_t flags;        // HOT_PLUS
   uint32_t hash_filter;  // filter id of "<node>/#", or NONE
   uint32_t end_filter;   // filter id ending at the node | END_WILD, or NONE
@@ -152,8 +152,6 @@ GM_HD int edge_depth(uint32_t depth) { return depth < uint32_t(EDGE_DEPTHS) ? in
 GM_HD uint64_t edge_key(uint32_t parent, uint32_t word) { return (uint64_t(parent) << 32) | word; }
 GM_HD uint64_t edge_slot(uint64_t key, uint64_t mask) { return fmix64(key) & mask; }
 
-// Signature bit of a word (top 5 bits of its 64-bit hash).
-GM_HD uint32_t sig_bit(uint64_t word_hash) { return 1u << (word_hash >> 59); }
 GM_HD int hot_table(uint32_t depth) { return depth < uint32_t(HOT_TABLES) ? int(depth) : HOT_TABLES - 1; }
 // Key of the child of `parent` (a node at depth `pdepth`) through word `word`.
 GM_HD uint64_t hot_key(uint32_t parent, uint32_t word, uint32_t pdepth) {
@@ -167,6 +165,9 @@ GM_HD uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
+// Signature bit of a word id (the exact-child filter of HotSlot::sig): a
+// function of the id alone, so the walk needs no word hash.
+GM_HD uint32_t sig_bit(uint32_t word_id) { return 1u << (fmix32(word_id * 0x9E3779B1u) >> 27); }
 // Home slot: 32-bit mix of (parent, word) and a multiply-shift range
 // reduction, so a table can hold any number of slots (< 2^32) without a
 // power-of-two blow-up, at a few 32-bit VALU ops per probe.

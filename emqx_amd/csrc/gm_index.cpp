@@ -223,7 +223,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
         edges.put(key, child);
         if (plus) { nodes[node].plus_child = child; nodes[node].flags |= NF_HAS_PLUS; }
         else if (hash) nodes[node].hash_child = child;
-        else { nodes[node].flags |= NF_HAS_EXACT; nodes[node].sig |= sig_bit(hash_word_host(w, wl)); }
+        else { nodes[node].flags |= NF_HAS_EXACT; nodes[node].sig |= sig_bit(id); }
       }
       node = child;
       ++depth;

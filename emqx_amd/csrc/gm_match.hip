@@ -293,7 +293,7 @@ __global__ __launch_bounds__(256, MINW) void k_match_reg(const uint8_t* __restri
                                                    const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
                                                    uint32_t* __restrict__ cnt, uint32_t* __restrict__ stage,
                                                    uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
-                                                   unsigned long long* __restrict__ probe_ctr,
+                                                   unsigned long long* __restrict__ probe_tile,
                                                    unsigned long long* __restrict__ wild_ctr) {
   constexpr int MC = FAST_MC;
   const int lane = threadIdx.x & 63;
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256, MINW) void k_match_reg(const uint8_t* __restri
         break;
       }
       const uint32_t wid = cur_n ? dict_resolve(ix, w, d0, tb) : NONE;
-      const uint32_t wbit = sig_bit(w.h);
+      const uint32_t wbit = sig_bit(wid);
       // prefetch the next level's word while this level's frontier expands
       WordTok wn;
       DictSlot dn;
@@ -412,12 +412,14 @@ __global__ __launch_bounds__(256, MINW) void k_match_reg(const uint8_t* __restri
     cnt[t] = ovf ? OVF_BIT : m_n;
     if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
   }
-  // per-wave counters (one atomic per wave)
+  // per-wave probe count: a plain store into the tile's slot (summed by
+  // k_sum_tiles); one atomic per wave on a single address would serialise
+  // every wave of the launch at the L2.
   uint32_t ptot;
   wave_excl_scan(probes, ptot);
   const unsigned long long wb = __ballot(valid && wild);
   if (lane == 0) {
-    atomicAdd(probe_ctr, (unsigned long long)ptot);
+    if (tile * 64 < n) probe_tile[tile] = ptot;  // waves wholly past n have no slot
     if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
   }
 }
@@ -478,7 +480,7 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
         break;
       }
       const uint32_t wid = cur_n ? dict_resolve(ix, w, d0, tb) : NONE;
-      const uint32_t wbit = sig_bit(w.h);
+      const uint32_t wbit = sig_bit(wid);
       WordTok wn;
       DictSlot dn;
       if (!last) {
@@ -548,8 +550,171 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
   wave_excl_scan(probes, ptot);
   wave_excl_scan(wilds, wtot);
   if (lane == 0) {
-    atomicAdd(probe_ctr, (unsigned long long)ptot);
+    if (LISTED) atomicAdd(probe_ctr, (unsigned long long)ptot);  // few waves
+    else if (((uint64_t(blockIdx.x) * 256u + tid) >> 6) * 64 < n)
+      probe_ctr[(uint64_t(blockIdx.x) * 256u + tid) >> 6] = ptot;  // per-tile slot, see k_match_reg
     if (wtot) atomicAdd(wild_ctr, (unsigned long long)wtot);
+  }
+}
+#undef GM_PUSH
+
+// ---- split form: k_tokenize + k_walk --------------------------------------
+// The per-topic front end (byte scan, word hash, dictionary lookup) and the
+// trie walk have different shapes: the first is streaming ALU work over the
+// topic bytes, the second a chain of dependent gathers.  Split, each kernel
+// keeps only its own state live, so the walk runs at full occupancy.
+//
+// k_tokenize writes, per topic, hdr = levels | TOK_DOLLAR | TOK_WILD | TOK_DEEP
+// and the word id of each level (NONE for a word no filter uses) into
+// wids[level][topic] (level < TOK_LMAX), a layout the walk reads coalesced.
+constexpr int TOK_LMAX = 8;
+constexpr uint32_t TOK_DOLLAR = 1u << 8, TOK_WILD = 1u << 9, TOK_DEEP = 1u << 10;
+
+__global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ toff,
+                                                  uint64_t n, IndexView ix, uint32_t* __restrict__ hdr,
+                                                  uint32_t* __restrict__ wids) {
+  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (t >= n) return;
+  uint64_t pos = toff[t];
+  const uint64_t end = toff[t + 1];
+  ByteReader rd{tb, ~0ull, 0};
+  uint32_t lev = 0, fl = 0;
+  for (;;) {
+    const WordTok w = next_word(rd, pos, end);
+    if (lev == 0 && w.len > 0 && w.b0 == '$') fl |= TOK_DOLLAR;  // emqx_trie.erl:271-278
+    if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {           // emqx_topic:wildcard/1
+      fl |= TOK_WILD;
+      break;
+    }
+    if (lev < TOK_LMAX) wids[uint64_t(lev) * n + t] = dict_resolve(ix, w, dict_first(ix, w), tb);
+    ++lev;
+    if (pos >= end) break;
+    ++pos;
+  }
+  if (lev > TOK_LMAX) fl |= TOK_DEEP;
+  hdr[t] = (lev < 255u ? lev : 255u) | fl;
+}
+
+// k_walk: the NFA walk over pre-resolved word ids, frontier in registers as
+// in k_match_reg.  Deep topics (more than TOK_LMAX levels) are queued for the
+// listed pass, which tokenizes for itself.
+#define GM_PUSH(idv, sigv)                                \
+  do {                                                    \
+    const uint32_t pid_ = (idv), psig_ = (sigv);          \
+    _Pragma("unroll") for (int q_ = 0; q_ < RFC; ++q_) {  \
+      if (nn == uint32_t(q_)) {                           \
+        nid[q_] = pid_;                                   \
+        nsig[q_] = psig_;                                 \
+      }                                                   \
+    }                                                     \
+    ++nn;                                                 \
+  } while (0)
+
+template <bool EXACT, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ toff,
+                                                    uint64_t n, IndexView ix, const uint32_t* __restrict__ hdr,
+                                                    const uint32_t* __restrict__ wids, uint32_t* __restrict__ cnt,
+                                                    uint32_t* __restrict__ stage, uint32_t* __restrict__ ovf_list,
+                                                    uint32_t* __restrict__ ovf_n,
+                                                    unsigned long long* __restrict__ probe_tile,
+                                                    unsigned long long* __restrict__ wild_ctr) {
+  constexpr int MC = FAST_MC;
+  const int lane = threadIdx.x & 63;
+  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  const uint64_t tile = t >> 6;
+  const int slane = lane;
+  const bool valid = t < n;
+  uint32_t m_n = 0, probes = 0;
+  bool ovf = false, wild = false;
+
+  if (valid) {
+    const uint32_t h = hdr[t];
+    const uint32_t nlev = h & 0xFFu;
+    const bool dollar = (h & TOK_DOLLAR) != 0;
+    wild = (h & TOK_WILD) != 0;
+    if (h & TOK_DEEP) {
+      ovf = true;
+    } else if (wild) {
+      const uint64_t start = toff[t], end = toff[t + 1];
+      GM_WILD_ROW();
+    } else {
+      if (!dollar && ix.root_hash != NONE) GM_EMIT(ix.root_hash);  // '#' at the virtual root
+      uint32_t fid[RFC], fsig[RFC];
+#pragma unroll
+      for (int q = 0; q < RFC; ++q) fid[q] = fsig[q] = 0;
+      fid[0] = (!dollar && (ix.root_flags & HOT_PLUS)) ? FR_PLUS : 0u;
+      fsig[0] = ix.root_sig;
+      uint32_t cur_n = 1, nfinal = 0;
+      uint32_t wid_next = wids[t];
+      for (uint32_t level = 0; level < nlev && cur_n; ++level) {
+        const bool last = level + 1 == nlev;
+        const uint32_t wid = wid_next;
+        if (!last) wid_next = wids[uint64_t(level + 1) * n + t];  // prefetch
+        const uint32_t wbit = sig_bit(wid);
+        probes += 3 * cur_n;
+        uint32_t nid[RFC], nsig[RFC], nn = 0;
+#pragma unroll
+        for (int q = 0; q < RFC; ++q) nid[q] = nsig[q] = 0;
+        const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);  // wave-uniform
+        const int ht = hot_table(lvl + 1);
+        const HotSlot* tab = ix.hot + ix.hot_off[ht];
+        const uint64_t cap = ix.hot_cap[ht];
+        const uint32_t capu = uint32_t(cap);
+        const bool wok = wid != NONE;
+#pragma unroll
+        for (int i = 0; i < RFC; ++i) {
+          if (uint32_t(i) < cur_n) {
+            const uint32_t ia = fid[i] & ID_MASK;
+            const bool ax = wok && (fsig[i] & wbit), ap = (fid[i] & FR_PLUS) != 0;
+            uint32_t sax = 0, sap = 0;
+            HotRec rax{}, rap{};
+            if (ax) {
+              sax = uint32_t(hot_slot(hot_key(ia, wid, lvl), cap));
+              rax = hot_load(tab, sax);
+            }
+            if (ap) {
+              sap = uint32_t(hot_slot(hot_key(ia, ix.plus_word, lvl), cap));
+              rap = hot_load(tab, sap);
+            }
+            if (ax) {
+              const uint32_t hs = hot_resolve(tab, capu, hot_key(ia, wid, lvl), sax, rax);
+              if (hs != NONE) GM_VISIT(hs, rax);
+            }
+            if (ap) {
+              const uint32_t hs = hot_resolve(tab, capu, hot_key(ia, ix.plus_word, lvl), sap, rap);
+              if (hs != NONE) GM_VISIT(hs, rap);
+            }
+          }
+        }
+        if (nn > RFC) {
+          ovf = true;
+          break;
+        }
+#pragma unroll
+        for (int q = 0; q < RFC; ++q) {
+          fid[q] = nid[q];
+          fsig[q] = nsig[q];
+        }
+        cur_n = nn;
+      }
+      if (!ovf) {
+        probes += 2 * nfinal + 1;
+        if (m_n > MC) ovf = true;
+      }
+    }
+    if (ovf) probes = 0;  // the listed pass walks this topic again and counts it
+  }
+
+  if (valid) {
+    cnt[t] = ovf ? OVF_BIT : m_n;
+    if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
+  }
+  uint32_t ptot;
+  wave_excl_scan(probes, ptot);
+  const unsigned long long wb = __ballot(valid && wild);
+  if (lane == 0) {
+    if (tile * 64 < n) probe_tile[tile] = ptot;  // waves wholly past n have no slot
+    if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
   }
 }
 #undef GM_PUSH
@@ -917,6 +1082,15 @@ __global__ __launch_bounds__(256) void k_sum_flen(const uint32_t* __restrict__ i
   if ((threadIdx.x & 63) == 0) atomicAdd(acc, (unsigned long long)s);
 }
 
+// Sum of per-tile counters into one (one atomic per wave of a small grid).
+__global__ __launch_bounds__(256) void k_sum_tiles(const unsigned long long* __restrict__ a, uint64_t n,
+                                                   unsigned long long* __restrict__ acc) {
+  unsigned long long s = 0;
+  for (uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256u) s += a[i];
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_down(s, d, 64);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(acc, s);
+}
+
 // ---------------------------------------------------------------------------
 // host orchestration
 // ---------------------------------------------------------------------------
@@ -956,19 +1130,22 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
 }
 
 // Main-pass kernel selection.  GM_MATCH_MAIN (A/B knob, read once):
-// reg{1,2}[w6|w8] (register frontier, one entry / pairs per step, register
+// split[w8] (k_tokenize + k_walk, default), reg{1,2}[w6|w8] (register frontier, one entry / pairs per step, register
 // budget for 6 / 8 waves per SIMD), lds4, lds8 (LDS frontier).
-enum MainKind { MAIN_REG1, MAIN_REG1W6, MAIN_REG1W8, MAIN_REG2, MAIN_REG2W6, MAIN_REG2W8, MAIN_LDS4, MAIN_LDS8 };
+enum MainKind {
+  MAIN_SPLIT, MAIN_SPLITW8, MAIN_REG1, MAIN_REG1W6, MAIN_REG1W8, MAIN_REG2, MAIN_REG2W6, MAIN_REG2W8, MAIN_LDS4,
+  MAIN_LDS8
+};
 MainKind main_kind() {
   static const MainKind k = [] {
     const char* e = getenv("GM_MATCH_MAIN");
     static const struct { const char* name; MainKind kind; } names[] = {
-        {"reg1", MAIN_REG1}, {"reg1w6", MAIN_REG1W6}, {"reg1w8", MAIN_REG1W8}, {"reg2", MAIN_REG2},
+        {"split", MAIN_SPLIT}, {"splitw8", MAIN_SPLITW8}, {"reg1", MAIN_REG1}, {"reg1w6", MAIN_REG1W6}, {"reg1w8", MAIN_REG1W8}, {"reg2", MAIN_REG2},
         {"reg2w6", MAIN_REG2W6}, {"reg2w8", MAIN_REG2W8}, {"lds4", MAIN_LDS4}, {"lds8", MAIN_LDS8}};
     if (e)
       for (const auto& nk : names)
         if (!strcmp(e, nk.name)) return nk.kind;
-    return MAIN_REG1W6;
+    return MAIN_SPLIT;
   }();
   return k;
 }
@@ -981,18 +1158,26 @@ constexpr int LISTED_FC = 16;  // frontier capacity of the listed pass
 template <bool EXACT>
 void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const uint64_t* to, uint64_t n,
                   uint32_t* cnt, uint32_t* stage, uint32_t* list1, uint32_t* n1, uint32_t* list2, uint32_t* n2,
-                  unsigned long long* probe_ctr, unsigned long long* wild_ctr, hipEvent_t after_main) {
+                  unsigned long long* probe_ctr, unsigned long long* wild_ctr, uint32_t* hdr, uint32_t* wids,
+                  unsigned long long* probe_tile, hipEvent_t after_main) {
   hipStream_t st = ctx->stream;
   const uint64_t nblk = (n + 255) / 256;
 #define GM_LAUNCH_REG(P, W)                                                                                  \
   hipLaunchKernelGGL((k_match_reg<EXACT, P, W>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, list1, n1, \
-                     probe_ctr, wild_ctr)
+                     probe_tile, wild_ctr)
 #define GM_LAUNCH_LDS(F)                                                                                     \
   hipLaunchKernelGGL((k_match_lds<EXACT, F, false>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, \
-                     nullptr, nullptr, list1, n1, probe_ctr, wild_ctr)
+                     nullptr, nullptr, list1, n1, probe_tile, wild_ctr)
+#define GM_LAUNCH_SPLIT(W)                                                                                       \
+  hipLaunchKernelGGL(k_tokenize, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids);                         \
+  hipLaunchKernelGGL((k_walk<EXACT, W>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, cnt, stage, list1, \
+                     n1, probe_tile, wild_ctr)
   switch (main_kind()) {
+    case MAIN_SPLIT: GM_LAUNCH_SPLIT(1); break;
+    case MAIN_SPLITW8: GM_LAUNCH_SPLIT(8); break;
     case MAIN_REG1: GM_LAUNCH_REG(false, 1); break;
     case MAIN_REG1W8: GM_LAUNCH_REG(false, 8); break;
+    case MAIN_REG1W6: GM_LAUNCH_REG(false, 6); break;
     case MAIN_REG2: GM_LAUNCH_REG(true, 1); break;
     case MAIN_REG2W6: GM_LAUNCH_REG(true, 6); break;
     case MAIN_REG2W8: GM_LAUNCH_REG(true, 8); break;
@@ -1000,9 +1185,11 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
     case MAIN_LDS8: GM_LAUNCH_LDS(8); break;
     default: GM_LAUNCH_REG(false, 6);
   }
+#undef GM_LAUNCH_SPLIT
 #undef GM_LAUNCH_REG
 #undef GM_LAUNCH_LDS
   hipEventRecord(after_main, st);
+  hipLaunchKernelGGL(k_sum_tiles, dim3(256), dim3(256), 0, st, probe_tile, (n + 63) / 64, probe_ctr);
   const uint64_t lblk = std::min<uint64_t>(nblk, 512);
   hipLaunchKernelGGL((k_match_lds<EXACT, LISTED_FC, true>), dim3(lblk), dim3(256), 0, st, tb, to, n, v, cnt, stage,
                      list1, n1, list2, n2, probe_ctr, wild_ctr);
@@ -1054,6 +1241,14 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   PoolBuf toff(ctx->pool, (n_tiles + 1) * 8);
   if (!cnt.p || !stage.p || !list1.p || !list2.p || !ctrs.p || !tsum.p || !toff.p)
     return set_err(ctx, EMQX_GM_ENOMEM, "match: workspace");
+  PoolBuf probe_tile(ctx->pool, n_tiles * 8 + 8);
+  if (!probe_tile.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: probe workspace");
+  PoolBuf hdr, wids;  // split form: per-topic header and word ids [level][topic]
+  if (main_kind() == MAIN_SPLIT || main_kind() == MAIN_SPLITW8) {
+    hdr = PoolBuf(ctx->pool, n * 4 + 16);
+    wids = PoolBuf(ctx->pool, uint64_t(TOK_LMAX) * n * 4 + 16);
+    if (!hdr.p || !wids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: word-id workspace");
+  }
   // counters: u32 n1 @0 (main-pass overflow), u32 n2 @4 (listed-pass
   // overflow), u64 probes @16, u64 wildcard topics @24
   uint32_t* n1 = ctrs.as<uint32_t>();
@@ -1066,10 +1261,12 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   GM_HIP(ctx, hipEventRecord(ctx->ev[1], st));
   if (exact)
     launch_match<true>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
-                       list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, ctx->ev[2]);
+                       list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
+                       probe_tile.as<unsigned long long>(), ctx->ev[2]);
   else
     launch_match<false>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(),
-                        n1, list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, ctx->ev[2]);
+                        n1, list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
+                        probe_tile.as<unsigned long long>(), ctx->ev[2]);
   GM_HIP(ctx, hipGetLastError());
 
   uint64_t h_ctr[4] = {0, 0, 0, 0};

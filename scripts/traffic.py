@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the dominant kernel from rocprofv3 PMC passes.
+
+Reads the separate FETCH_SIZE and WRITE_SIZE passes that scripts/profile.sh
+writes (gpurun_out/prof/pmc_fetch, pmc_write; one counter group per run) and
+writes profiles/traffic.json, which bench.py reports as roofline.traffic.
+
+Units and corrections (MI355X_MICROARCH.md § HBM): FETCH_SIZE / WRITE_SIZE are
+KB (1024 B).  On gfx950 FETCH_SIZE = TCC_EA0_RDREQ x 64 B while a request moves
+128 B, so the fetch figure is doubled.  The counters sit on the L2's fabric
+side: Infinity-Cache hits are included, so this is L2-miss traffic (an upper
+bound on HBM bytes).  Only launches over the whole batch (Grid_Size >= the
+batch's topics) are averaged.
+
+usage: traffic.py [prof_dir] [--kernel k_match_reg] [--topics N] [--config c2] [--out path]
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_launch(path, kernel, min_grid):
+    vals = []
+    if not os.path.exists(path):
+        return vals
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if kernel in r["Kernel_Name"] and int(r["Grid_Size"]) >= min_grid:
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("prof", nargs="?", default=os.path.join(ROOT, "gpurun_out", "prof"))
+    p.add_argument("--kernel", default="k_match_reg")
+    p.add_argument("--topics", type=int, default=100_000_000)
+    p.add_argument("--config", default="c2")
+    p.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    a = p.parse_args()
+    fetch = per_launch(os.path.join(a.prof, "pmc_fetch", "run_counter_collection.csv"), a.kernel, a.topics)
+    write = per_launch(os.path.join(a.prof, "pmc_write", "run_counter_collection.csv"), a.kernel, a.topics)
+    if not fetch or not write:
+        raise SystemExit(f"no full-batch {a.kernel} launches in {a.prof}")
+    fetch_b = statistics.mean(fetch) * 1024 * 2  # KB -> B, gfx950 x2 correction
+    write_b = statistics.mean(write) * 1024
+    out = {"config": a.config, "n_topics": a.topics, "kernel": a.kernel,
+           "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+           "hbm_bytes_per_launch": fetch_b + write_b, "launches": [len(fetch), len(write)],
+           "note": "FETCH_SIZE x1024 x2 (gfx950 correction) + WRITE_SIZE x1024 per launch; L2 fabric side, "
+                   "Infinity-Cache hits included"}
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
