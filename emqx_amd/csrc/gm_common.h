@@ -71,18 +71,20 @@ struct alignas(16) EdgeSlot {
 constexpr int HOT_TABLES = 16;
 constexpr uint32_t ID_MASK = 0x7FFFFFFFu;
 constexpr uint32_t END_WILD = 0x80000000u;  // in end_filter: the filter is a wildcard one
-constexpr uint32_t HOT_PLUS = 1u;           // in flags: the node has a '+' child
+constexpr uint32_t HOT_PLUS = 0x80000000u;  // in HotSlot::hf: the node has a '+' child
+constexpr uint32_t HF_NONE = 0x7FFFFFFFu;   // HotSlot::hf without a '#' filter
 constexpr uint32_t FR_PLUS = 0x80000000u;   // in a frontier entry: the node has a '+' child
 constexpr uint64_t HOT_KEY_MARK = 1ull << 63;  // parent lives in table HOT_TABLES-2, child in the shared last
 
 struct alignas(32) HotSlot {
   uint64_t key;          // hot_key(parent, word); EDGE_EMPTY marks an empty slot
   uint32_t sig;          // bit sig_bit(w) set for each exact child word id w; 0 = no exact child
-  uint32_t flags;        // HOT_PLUS
-  uint32_t hash_filter;  // filter id of "<node>/#", or NONE
+  uint32_t hf;           // filter id of "<node>/#" (HF_NONE if none) | HOT_PLUS if the node has a '+' child
   uint32_t end_filter;   // filter id ending at the node | END_WILD, or NONE
-  uint32_t pad0, pad1;   // 32-B stride: two slots per 64-B line, never straddling one
+  uint32_t pad[3];       // 32-B stride: slots never straddle a 64-B line
 };
+// The first 16 bytes {key, sig, hf} are all a walk needs below the topic's
+// last level (one dwordx4 per probe); end_filter is read on the last level.
 // Read-only view of one index resident in HBM (passed by value to kernels).
 struct IndexView {
   const Node* nodes;
@@ -168,12 +170,22 @@ GM_HD uint32_t fmix32(uint32_t h) {
 // Signature bit of a word id (the exact-child filter of HotSlot::sig): a
 // function of the id alone, so the walk needs no word hash.
 GM_HD uint32_t sig_bit(uint32_t word_id) { return 1u << (fmix32(word_id * 0x9E3779B1u) >> 27); }
-// Home slot: 32-bit mix of (parent, word) and a multiply-shift range
-// reduction, so a table can hold any number of slots (< 2^32) without a
-// power-of-two blow-up, at a few 32-bit VALU ops per probe.
+// Home slot: a 32-bit multiply-xorshift mix of (parent | mark, word) and a
+// multiply-high range reduction, so a table can hold any number of slots
+// (< 2^32) without a power-of-two blow-up, at a handful of 32-bit VALU ops
+// per probe (one v_mul_hi_u32 for the reduction).
 GM_HD uint64_t hot_slot(uint64_t key, uint64_t cap) {
-  const uint32_t h = fmix32((uint32_t(key) * 0x9E3779B1u) ^ (uint32_t(key >> 32) * 0x85EBCA77u) ^ 0x27D4EB2Fu);
+  uint32_t h = (uint32_t(key >> 32) * 0x9E3779B1u) ^ (uint32_t(key) * 0x85EBCA77u);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umulhi(h, uint32_t(cap));
+#else
   return (uint64_t(h) * cap) >> 32;
+#endif
 }
 
 }  // namespace gm

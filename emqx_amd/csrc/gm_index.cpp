@@ -298,7 +298,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     hot_off[t] = hot_total;
     hot_total += hot_cap[t];
   }
-  std::vector<HotSlot> hot(hot_total, HotSlot{EDGE_EMPTY, 0, 0, NONE, NONE, 0, 0});
+  std::vector<HotSlot> hot(hot_total, HotSlot{EDGE_EMPTY, 0, HF_NONE, NONE, {0, 0, 0}});
   std::vector<uint32_t> hid(NN, NONE);
   hid[0] = 0;  // the root (depth 0) is not stored; its record goes to IndexView
   auto end_of = [&](const HNode& h) -> uint32_t {
@@ -320,9 +320,9 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       HotSlot& o = tab[s];
       o.key = key;
       o.sig = h.sig;
-      o.hash_filter = h.hash_child == NONE ? NONE : nodes[h.hash_child].end_filter;
+      o.hf = (h.hash_child == NONE ? HF_NONE : nodes[h.hash_child].end_filter) |
+             (h.plus_child != NONE ? HOT_PLUS : 0u);
       o.end_filter = end_of(h);
-      o.flags = h.plus_child != NONE ? HOT_PLUS : 0u;
       hid[i] = uint32_t(s);
     }
   }

@@ -71,7 +71,8 @@ struct WordTok {
 };
 
 // Tokenize the word starting at `pos`; leaves `pos` on the '/' (or end).
-__device__ __forceinline__ WordTok next_word(ByteReader& rd, uint64_t& pos, uint64_t end) {
+template <class RD>
+__device__ __forceinline__ WordTok next_word(RD& rd, uint64_t& pos, uint64_t end) {
   WordTok w;
   w.start = pos;
   w.head = 0;
@@ -177,17 +178,17 @@ __device__ __forceinline__ uint64_t stage_index(uint64_t tile, uint32_t k, int l
   return tile * (64ull * FAST_MC) + uint64_t(k) * 64u + uint32_t(lane);
 }
 
-// A hot slot as the kernel reads it: the 24 used bytes, in two loads
-// (dwordx4 + dwordx2) from one 64-B line.
+// A hot slot as the kernel reads it: {key, sig, hf} in one dwordx4; the end
+// filter (a second dword of the same line) only on the topic's last level.
 struct HotRec {
-  uint4 a;  // key lo, key hi, sig, flags
-  uint2 b;  // hash_filter, end_filter
+  uint4 a;      // key lo, key hi, sig, hf (| HOT_PLUS)
+  uint32_t ef;  // end_filter (NONE unless loaded)
 };
-__device__ __forceinline__ HotRec hot_load(const HotSlot* tab, uint32_t s) {
+__device__ __forceinline__ HotRec hot_load(const HotSlot* tab, uint32_t s, bool with_end) {
   const uint32_t* p = reinterpret_cast<const uint32_t*>(tab + s);
   HotRec r;
   r.a = *reinterpret_cast<const uint4*>(p);
-  r.b = *reinterpret_cast<const uint2*>(p + 4);
+  r.ef = with_end ? p[4] : NONE;
   return r;
 }
 __device__ __forceinline__ bool hot_is(const HotRec& r, uint64_t key) {
@@ -197,21 +198,22 @@ __device__ __forceinline__ bool hot_empty(const HotRec& r) { return r.a.x == 0xF
 // Linear probing from slot s (whose record r is already loaded); returns the
 // slot index of `key` or NONE.
 __device__ __forceinline__ uint32_t hot_resolve(const HotSlot* tab, uint32_t cap, uint64_t key, uint32_t s,
-                                                HotRec& r) {
+                                                HotRec& r, bool with_end) {
   while (!hot_is(r, key)) {
     if (hot_empty(r)) return NONE;
     s = s + 1 == cap ? 0 : s + 1;
-    r = hot_load(tab, s);
+    r = hot_load(tab, s, with_end);
   }
   return s;
 }
 
 // Per-lane match staging: emit one filter id into the topic's row (slot m_n
-// of the topic's lane column `slane` in its tile).
-#define GM_EMIT(f)                                                   \
-  do {                                                               \
-    if (m_n < MC) stage[stage_index(tile, m_n, slane)] = (f);        \
-    ++m_n;                                                           \
+// of the topic's lane column in its tile; srow = &stage[stage_index(tile, 0,
+// lane)]).
+#define GM_EMIT(f)                                \
+  do {                                            \
+    if (m_n < MC) srow[m_n * 64u] = (f);          \
+    ++m_n;                                        \
   } while (0)
 
 // Visit a node reached at this level (its record r, hot id hs): emit
@@ -221,13 +223,13 @@ __device__ __forceinline__ uint32_t hot_resolve(const HotSlot* tab, uint32_t cap
 // the next frontier (GM_PUSH is defined per kernel).
 #define GM_VISIT(hs, r)                                                                 \
   do {                                                                                  \
-    if ((r).b.x != NONE) GM_EMIT((r).b.x);                                              \
+    if (((r).a.w & ID_MASK) != HF_NONE) GM_EMIT((r).a.w & ID_MASK);                     \
     if (last) {                                                                         \
-      if ((r).b.y != NONE && (EXACT || ((r).b.y & END_WILD) || (dollar && level == 0))) \
-        GM_EMIT((r).b.y & ID_MASK);                                                     \
+      if ((r).ef != NONE && (EXACT || ((r).ef & END_WILD) || (dollar && level == 0)))   \
+        GM_EMIT((r).ef & ID_MASK);                                                      \
       ++nfinal;                                                                         \
     } else {                                                                            \
-      GM_PUSH((hs) | (((r).a.w & HOT_PLUS) ? FR_PLUS : 0u), (r).a.z);                   \
+      GM_PUSH((hs) | ((r).a.w & FR_PLUS), (r).a.z);                                     \
     }                                                                                   \
   } while (0)
 
@@ -241,7 +243,7 @@ __device__ __forceinline__ uint32_t hot_resolve(const HotSlot* tab, uint32_t cap
     if (EXACT) {                                             \
       const uint32_t f = literal_lookup(ix, tb, start, end); \
       if (f != NONE) {                                       \
-        stage[stage_index(tile, 0, slane)] = f;              \
+        srow[0] = f;                                         \
         m_n = 1;                                             \
       }                                                      \
     }                                                        \
@@ -274,14 +276,14 @@ constexpr int RFC = 4;
   do {                                                                                  \
     if (c) {                                                                            \
       sx = uint32_t(hot_slot(hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), cap));  \
-      rx = hot_load(tab, sx);                                                           \
+      rx = hot_load(tab, sx, last);                                                           \
     }                                                                                   \
   } while (0)
 
 #define GM_PROBE_TAKE(c, e_id, plus, sx, rx)                                                              \
   do {                                                                                                    \
     if (c) {                                                                                              \
-      const uint32_t hs_ = hot_resolve(tab, capu, hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), sx, rx); \
+      const uint32_t hs_ = hot_resolve(tab, capu, hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), sx, rx, last); \
       if (hs_ != NONE) GM_VISIT(hs_, rx);                                                                 \
     }                                                                                                     \
   } while (0)
@@ -299,8 +301,8 @@ __global__ __launch_bounds__(256, MINW) void k_match_reg(const uint8_t* __restri
   const int lane = threadIdx.x & 63;
   const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
   const uint64_t tile = t >> 6;
-  const int slane = lane;
   const bool valid = t < n;
+  uint32_t* const srow = stage + stage_index(tile, 0, lane);
   uint32_t m_n = 0, probes = 0;
   bool ovf = false, wild = false;
 
@@ -424,8 +426,6 @@ __global__ __launch_bounds__(256, MINW) void k_match_reg(const uint8_t* __restri
   }
 }
 #undef GM_PUSH
-#undef GM_PROBE_ISSUE
-#undef GM_PROBE_TAKE
 
 // ---- k_match_lds ----------------------------------------------------------
 // Frontier entries double buffered in LDS, FC per lane.  LISTED: grid-stride
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
        item += uint64_t(gridDim.x) * 256u) {
     const uint64_t t = LISTED ? uint64_t(list_in[item]) : item;
     const uint64_t tile = t >> 6;
-    const int slane = int(t & 63);
+    uint32_t* const srow = stage + stage_index(tile, 0, int(t & 63));
     uint32_t m_n = 0, tprobes = 0;
     bool ovf = false, wild = false;
     uint64_t pos = toff[t];
@@ -506,18 +506,18 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
           HotRec rx{}, rp{};
           if (dx) {
             sx = uint32_t(hot_slot(hot_key(id, wid, lvl), cap));
-            rx = hot_load(tab, sx);
+            rx = hot_load(tab, sx, last);
           }
           if (dp) {
             sp = uint32_t(hot_slot(hot_key(id, ix.plus_word, lvl), cap));
-            rp = hot_load(tab, sp);
+            rp = hot_load(tab, sp, last);
           }
           if (dx) {
-            const uint32_t hs = hot_resolve(tab, capu, hot_key(id, wid, lvl), sx, rx);
+            const uint32_t hs = hot_resolve(tab, capu, hot_key(id, wid, lvl), sx, rx, last);
             if (hs != NONE) GM_VISIT(hs, rx);
           }
           if (dp) {
-            const uint32_t hs = hot_resolve(tab, capu, hot_key(id, ix.plus_word, lvl), sp, rp);
+            const uint32_t hs = hot_resolve(tab, capu, hot_key(id, ix.plus_word, lvl), sp, rp, last);
             if (hs != NONE) GM_VISIT(hs, rp);
           }
         }
@@ -570,29 +570,87 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
 constexpr int TOK_LMAX = 8;
 constexpr uint32_t TOK_DOLLAR = 1u << 8, TOK_WILD = 1u << 9, TOK_DEEP = 1u << 10;
 
-__global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ toff,
-                                                  uint64_t n, IndexView ix, uint32_t* __restrict__ hdr,
-                                                  uint32_t* __restrict__ wids) {
-  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
-  if (t >= n) return;
-  uint64_t pos = toff[t];
-  const uint64_t end = toff[t + 1];
-  ByteReader rd{tb, ~0ull, 0};
+// Reader over topic text staged in LDS (8-byte words; `lo` = the absolute
+// batch offset of lds[0]), with the same one-word cache as ByteReader.
+struct LdsReader {
+  const uint64_t* lds;
+  uint64_t lo;
+  uint64_t cached_addr;
+  uint64_t cached;
+  __device__ __forceinline__ uint32_t get(uint64_t p) {
+    const uint64_t a = p & ~7ull;
+    if (a != cached_addr) {
+      cached_addr = a;
+      cached = lds[(a - lo) >> 3];
+    }
+    return uint32_t(cached >> ((p & 7) * 8)) & 0xFFu;
+  }
+};
+
+// One topic: words -> dictionary ids, the next word's first dictionary slot
+// loaded while this word resolves.
+template <class RD>
+__device__ __forceinline__ uint32_t tokenize_topic(RD& rd, uint64_t pos, uint64_t end, const IndexView& ix,
+                                                   const uint8_t* tb, uint64_t n, uint64_t t,
+                                                   uint32_t* __restrict__ wids) {
   uint32_t lev = 0, fl = 0;
+  WordTok w = next_word(rd, pos, end);
+  DictSlot d = dict_first(ix, w);
+  if (w.len > 0 && w.b0 == '$') fl |= TOK_DOLLAR;  // emqx_trie.erl:271-278
   for (;;) {
-    const WordTok w = next_word(rd, pos, end);
-    if (lev == 0 && w.len > 0 && w.b0 == '$') fl |= TOK_DOLLAR;  // emqx_trie.erl:271-278
-    if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {           // emqx_topic:wildcard/1
+    if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {  // emqx_topic:wildcard/1
       fl |= TOK_WILD;
       break;
     }
-    if (lev < TOK_LMAX) wids[uint64_t(lev) * n + t] = dict_resolve(ix, w, dict_first(ix, w), tb);
+    const bool more = pos < end;
+    WordTok wn;
+    DictSlot dn;
+    if (more) {
+      ++pos;
+      wn = next_word(rd, pos, end);
+      dn = dict_first(ix, wn);
+    }
+    if (lev < TOK_LMAX) wids[uint64_t(lev) * n + t] = dict_resolve(ix, w, d, tb);
     ++lev;
-    if (pos >= end) break;
-    ++pos;
+    if (!more) break;
+    w = wn;
+    d = dn;
   }
   if (lev > TOK_LMAX) fl |= TOK_DEEP;
-  hdr[t] = (lev < 255u ? lev : 255u) | fl;
+  return (lev < 255u ? lev : 255u) | fl;
+}
+
+// The block's topic text [toff[t0], toff[t0+256]) is staged in LDS with
+// coalesced 8-byte loads when it fits TOK_STAGE bytes (a wave's lanes then
+// scan their own topics from LDS instead of issuing dependent global loads
+// at every 8-byte boundary); a longer block reads global memory directly.
+constexpr int TOK_STAGE = 16384;
+
+__global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ toff,
+                                                  uint64_t n, IndexView ix, uint32_t* __restrict__ hdr,
+                                                  uint32_t* __restrict__ wids) {
+  __shared__ uint64_t s_txt[TOK_STAGE / 8];
+  const uint64_t t0 = uint64_t(blockIdx.x) * 256u;
+  const uint64_t t = t0 + threadIdx.x;
+  const uint64_t tl = t0 + 256 < n ? t0 + 256 : n;
+  const uint64_t lo = toff[t0] & ~7ull, hi = toff[tl];
+  const bool staged = hi - lo <= uint64_t(TOK_STAGE) - 8;  // block-uniform
+  if (staged) {
+    const uint64_t nw = (hi - lo + 7) >> 3;
+    for (uint64_t i = threadIdx.x; i < nw; i += 256) s_txt[i] = *reinterpret_cast<const uint64_t*>(tb + lo + 8 * i);
+  }
+  __syncthreads();
+  if (t >= n) return;
+  const uint64_t pos = toff[t], end = toff[t + 1];
+  uint32_t h;
+  if (staged) {
+    LdsReader rd{s_txt, lo, ~0ull, 0};
+    h = tokenize_topic(rd, pos, end, ix, tb, n, t, wids);
+  } else {
+    ByteReader rd{tb, ~0ull, 0};
+    h = tokenize_topic(rd, pos, end, ix, tb, n, t, wids);
+  }
+  hdr[t] = h;
 }
 
 // k_walk: the NFA walk over pre-resolved word ids, frontier in registers as
@@ -610,7 +668,7 @@ __global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb
     ++nn;                                                 \
   } while (0)
 
-template <bool EXACT, int MINW>
+template <bool EXACT, int MINW, bool PAIR>
 __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ toff,
                                                     uint64_t n, IndexView ix, const uint32_t* __restrict__ hdr,
                                                     const uint32_t* __restrict__ wids, uint32_t* __restrict__ cnt,
@@ -622,8 +680,8 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
   const int lane = threadIdx.x & 63;
   const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
   const uint64_t tile = t >> 6;
-  const int slane = lane;
   const bool valid = t < n;
+  uint32_t* const srow = stage + stage_index(tile, 0, lane);
   uint32_t m_n = 0, probes = 0;
   bool ovf = false, wild = false;
 
@@ -661,28 +719,38 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
         const uint64_t cap = ix.hot_cap[ht];
         const uint32_t capu = uint32_t(cap);
         const bool wok = wid != NONE;
+        if (PAIR) {
 #pragma unroll
-        for (int i = 0; i < RFC; ++i) {
-          if (uint32_t(i) < cur_n) {
-            const uint32_t ia = fid[i] & ID_MASK;
-            const bool ax = wok && (fsig[i] & wbit), ap = (fid[i] & FR_PLUS) != 0;
-            uint32_t sax = 0, sap = 0;
-            HotRec rax{}, rap{};
-            if (ax) {
-              sax = uint32_t(hot_slot(hot_key(ia, wid, lvl), cap));
-              rax = hot_load(tab, sax);
+          for (int i = 0; i < RFC; i += 2) {
+            if (uint32_t(i) < cur_n) {
+              const bool hb = uint32_t(i + 1) < cur_n;
+              const uint32_t ia = fid[i] & ID_MASK, ib = fid[i + 1] & ID_MASK;
+              const bool ax = wok && (fsig[i] & wbit), ap = (fid[i] & FR_PLUS) != 0;
+              const bool bx = hb && wok && (fsig[i + 1] & wbit), bp = hb && (fid[i + 1] & FR_PLUS) != 0;
+              uint32_t sax = 0, sap = 0, sbx = 0, sbp = 0;
+              HotRec rax{}, rap{}, rbx{}, rbp{};
+              GM_PROBE_ISSUE(ax, ia, false, sax, rax);
+              GM_PROBE_ISSUE(ap, ia, true, sap, rap);
+              GM_PROBE_ISSUE(bx, ib, false, sbx, rbx);
+              GM_PROBE_ISSUE(bp, ib, true, sbp, rbp);
+              GM_PROBE_TAKE(ax, ia, false, sax, rax);
+              GM_PROBE_TAKE(ap, ia, true, sap, rap);
+              GM_PROBE_TAKE(bx, ib, false, sbx, rbx);
+              GM_PROBE_TAKE(bp, ib, true, sbp, rbp);
             }
-            if (ap) {
-              sap = uint32_t(hot_slot(hot_key(ia, ix.plus_word, lvl), cap));
-              rap = hot_load(tab, sap);
-            }
-            if (ax) {
-              const uint32_t hs = hot_resolve(tab, capu, hot_key(ia, wid, lvl), sax, rax);
-              if (hs != NONE) GM_VISIT(hs, rax);
-            }
-            if (ap) {
-              const uint32_t hs = hot_resolve(tab, capu, hot_key(ia, ix.plus_word, lvl), sap, rap);
-              if (hs != NONE) GM_VISIT(hs, rap);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < RFC; ++i) {
+            if (uint32_t(i) < cur_n) {
+              const uint32_t ia = fid[i] & ID_MASK;
+              const bool ax = wok && (fsig[i] & wbit), ap = (fid[i] & FR_PLUS) != 0;
+              uint32_t sax = 0, sap = 0;
+              HotRec rax{}, rap{};
+              GM_PROBE_ISSUE(ax, ia, false, sax, rax);
+              GM_PROBE_ISSUE(ap, ia, true, sap, rap);
+              GM_PROBE_TAKE(ax, ia, false, sax, rax);
+              GM_PROBE_TAKE(ap, ia, true, sap, rap);
             }
           }
         }
@@ -718,6 +786,8 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
   }
 }
 #undef GM_PUSH
+#undef GM_PROBE_ISSUE
+#undef GM_PROBE_TAKE
 #undef GM_VISIT
 #undef GM_WILD_ROW
 #undef GM_EMIT
@@ -1133,14 +1203,14 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
 // split[w8] (k_tokenize + k_walk, default), reg{1,2}[w6|w8] (register frontier, one entry / pairs per step, register
 // budget for 6 / 8 waves per SIMD), lds4, lds8 (LDS frontier).
 enum MainKind {
-  MAIN_SPLIT, MAIN_SPLITW8, MAIN_REG1, MAIN_REG1W6, MAIN_REG1W8, MAIN_REG2, MAIN_REG2W6, MAIN_REG2W8, MAIN_LDS4,
+  MAIN_SPLIT, MAIN_SPLITW8, MAIN_SPLIT2, MAIN_REG1, MAIN_REG1W6, MAIN_REG1W8, MAIN_REG2, MAIN_REG2W6, MAIN_REG2W8, MAIN_LDS4,
   MAIN_LDS8
 };
 MainKind main_kind() {
   static const MainKind k = [] {
     const char* e = getenv("GM_MATCH_MAIN");
     static const struct { const char* name; MainKind kind; } names[] = {
-        {"split", MAIN_SPLIT}, {"splitw8", MAIN_SPLITW8}, {"reg1", MAIN_REG1}, {"reg1w6", MAIN_REG1W6}, {"reg1w8", MAIN_REG1W8}, {"reg2", MAIN_REG2},
+        {"split", MAIN_SPLIT}, {"splitw8", MAIN_SPLITW8}, {"split2", MAIN_SPLIT2}, {"reg1", MAIN_REG1}, {"reg1w6", MAIN_REG1W6}, {"reg1w8", MAIN_REG1W8}, {"reg2", MAIN_REG2},
         {"reg2w6", MAIN_REG2W6}, {"reg2w8", MAIN_REG2W8}, {"lds4", MAIN_LDS4}, {"lds8", MAIN_LDS8}};
     if (e)
       for (const auto& nk : names)
@@ -1168,13 +1238,14 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
 #define GM_LAUNCH_LDS(F)                                                                                     \
   hipLaunchKernelGGL((k_match_lds<EXACT, F, false>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, \
                      nullptr, nullptr, list1, n1, probe_tile, wild_ctr)
-#define GM_LAUNCH_SPLIT(W)                                                                                       \
+#define GM_LAUNCH_SPLIT(W, P)                                                                                     \
   hipLaunchKernelGGL(k_tokenize, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids);                         \
-  hipLaunchKernelGGL((k_walk<EXACT, W>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, cnt, stage, list1, \
+  hipLaunchKernelGGL((k_walk<EXACT, W, P>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, cnt, stage, list1, \
                      n1, probe_tile, wild_ctr)
   switch (main_kind()) {
-    case MAIN_SPLIT: GM_LAUNCH_SPLIT(1); break;
-    case MAIN_SPLITW8: GM_LAUNCH_SPLIT(8); break;
+    case MAIN_SPLIT: GM_LAUNCH_SPLIT(1, false); break;
+    case MAIN_SPLITW8: GM_LAUNCH_SPLIT(8, false); break;
+    case MAIN_SPLIT2: GM_LAUNCH_SPLIT(1, true); break;
     case MAIN_REG1: GM_LAUNCH_REG(false, 1); break;
     case MAIN_REG1W8: GM_LAUNCH_REG(false, 8); break;
     case MAIN_REG1W6: GM_LAUNCH_REG(false, 6); break;
@@ -1244,7 +1315,7 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   PoolBuf probe_tile(ctx->pool, n_tiles * 8 + 8);
   if (!probe_tile.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: probe workspace");
   PoolBuf hdr, wids;  // split form: per-topic header and word ids [level][topic]
-  if (main_kind() == MAIN_SPLIT || main_kind() == MAIN_SPLITW8) {
+  if (main_kind() == MAIN_SPLIT || main_kind() == MAIN_SPLITW8 || main_kind() == MAIN_SPLIT2) {
     hdr = PoolBuf(ctx->pool, n * 4 + 16);
     wids = PoolBuf(ctx->pool, uint64_t(TOK_LMAX) * n * 4 + 16);
     if (!hdr.p || !wids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: word-id workspace");
