@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--host-io", action="store_true",
+                   help="also time one call with host buffers (PCIe-inclusive rate, reported in detail)")
     return p.parse_args()
 
 
@@ -78,6 +80,17 @@ def barrier(pg):
         pg.barrier()
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(codes, filters_packed, seed, target_s, threads):
     """The oracle's faithful emqx_trie walk (compact) + route lookup on host cores."""
     from oracle import oracle as orc
@@ -99,8 +112,14 @@ def cpu_baseline(codes, filters_packed, seed, target_s, threads):
     t0 = time.perf_counter()
     ro, _, lk = r.match_batch((tb, to), (fb, fo), mode=1, nthreads=threads, want_ids=False)
     dt = time.perf_counter() - t0
+    # single-thread rate on a slice of the same stream (reported beside the all-core one)
+    n1 = max(1000, min(n, int(n / threads / 4)))
+    t1 = time.perf_counter()
+    r.match_batch((tb, to[:n1 + 1]), (fb, fo), mode=1, nthreads=1, want_ids=False)
+    single = n1 / (time.perf_counter() - t1)
     del sorted_f
-    return {"value": n / dt, "unit": "topics/s", "cores": threads, "kind": "port",
+    return {"value": n / dt, "unit": "topics/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "single_thread_value": single,
             "sample": f"first {n} topics of the same seeded C2 stream (seed {seed}), emqx_trie compact walk + "
                       f"lookup_routes restated in C++ (oracle/emqx_oracle.cpp), {threads} std::threads, "
                       f"{dt:.1f} s; {float(ro[-1]) / n:.3f} matches/topic; "
@@ -181,12 +200,22 @@ def main():
         "matches_per_sec": world * nnz * a.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_match_fast", "kernel_ms": kavg, "algo_bytes_per_launch": algo},
+                     "kernel": "k_tokenize+k_walk", "kernel_ms": kavg, "algo_bytes_per_launch": algo},
         "detail": {"nnz_per_step": nnz, "matches_per_topic": nnz / n_topics, "probes_per_topic": st["probes"] /
                    n_topics, "overflow_rows": st["n_overflow"], "topic_bytes": tbytes,
                    "index_device_bytes": int(idx.info.device_bytes), "index_nodes": int(idx.info.n_nodes),
                    "index_build_s": t_build, "device_ms_per_call": st["total_device_ms"]},
     }
+    if a.host_io and rank == 0:
+        # PCIe-inclusive: topics handed over in host memory, CSR returned to host memory
+        hb = np.zeros(tbytes + 64, np.uint8)
+        ho = np.zeros(n_topics + 1, np.uint64)
+        ctx.memcpy_d2h(hb, db, tbytes)
+        ctx.memcpy_d2h(ho, do, (n_topics + 1) * 8)
+        t0 = time.perf_counter()
+        hro, hids = ctx.match(idx, (hb, ho), exact=True)
+        out["detail"]["host_io_topics_per_s"] = n_topics / (time.perf_counter() - t0)
+        del hb, ho, hro, hids
     if rank == 0 and world == 1 and not a.no_cpu:
         threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         out["cpu_baseline"] = cpu_baseline(codes, fpack, a.seed, a.cpu_seconds, threads)

@@ -34,23 +34,36 @@ def per_launch(path, kernel, min_grid):
     return vals
 
 
+def per_launch_sum(path, kernels, min_grid):
+    """Per-launch average of each kernel, summed over the kernels of one match call."""
+    total, counts = 0.0, []
+    for k in kernels:
+        v = per_launch(path, k, min_grid)
+        if not v:
+            return None, counts
+        total += statistics.mean(v)
+        counts.append(len(v))
+    return total, counts
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("prof", nargs="?", default=os.path.join(ROOT, "gpurun_out", "prof"))
-    p.add_argument("--kernel", default="k_match_reg")
+    p.add_argument("--kernel", default="k_tokenize,k_walk", help="comma-separated kernels of one match call")
     p.add_argument("--topics", type=int, default=100_000_000)
     p.add_argument("--config", default="c2")
     p.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic.json"))
     a = p.parse_args()
-    fetch = per_launch(os.path.join(a.prof, "pmc_fetch", "run_counter_collection.csv"), a.kernel, a.topics)
-    write = per_launch(os.path.join(a.prof, "pmc_write", "run_counter_collection.csv"), a.kernel, a.topics)
-    if not fetch or not write:
+    ks = a.kernel.split(",")
+    fetch, nf = per_launch_sum(os.path.join(a.prof, "pmc_fetch", "run_counter_collection.csv"), ks, a.topics)
+    write, nw = per_launch_sum(os.path.join(a.prof, "pmc_write", "run_counter_collection.csv"), ks, a.topics)
+    if fetch is None or write is None:
         raise SystemExit(f"no full-batch {a.kernel} launches in {a.prof}")
-    fetch_b = statistics.mean(fetch) * 1024 * 2  # KB -> B, gfx950 x2 correction
-    write_b = statistics.mean(write) * 1024
+    fetch_b = fetch * 1024 * 2  # KB -> B, gfx950 x2 correction
+    write_b = write * 1024
     out = {"config": a.config, "n_topics": a.topics, "kernel": a.kernel,
            "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
-           "hbm_bytes_per_launch": fetch_b + write_b, "launches": [len(fetch), len(write)],
+           "hbm_bytes_per_launch": fetch_b + write_b, "launches": [nf, nw],
            "note": "FETCH_SIZE x1024 x2 (gfx950 correction) + WRITE_SIZE x1024 per launch; L2 fabric side, "
                    "Infinity-Cache hits included"}
     with open(a.out, "w") as f:
