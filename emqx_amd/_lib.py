@@ -68,6 +68,11 @@ SIGNATURES = {
     "emqx_gm_fanout": (_i32, [_vp, _vp, C.POINTER(Csr), _u32, C.POINTER(Csr)]),
     "emqx_gm_csr_free": (_i32, [_vp, C.POINTER(Csr)]),
     "emqx_gm_last_stats": (_i32, [_vp, C.POINTER(MatchStats)]),
+    "emqx_gm_filter_ranks": (_i32, [_vp, _vp, _u64, _vp, C.POINTER(_u64)]),
+    "emqx_gm_shard_of": (_i32, [_vp, _vp, _u64, _u32, _vp]),
+    "emqx_gm_index_build_shard": (_i32, [_vp, _vp, _vp, _u64, _vp, _vp, _vp, _vp, C.POINTER(_vp)]),
+    "emqx_gm_csr_row_lengths": (_i32, [_vp, C.POINTER(Csr), _vp]),
+    "emqx_gm_merge_rows": (_i32, [_vp, _u64, _u64, _u32, _vp, _vp, _u32, C.POINTER(Csr)]),
     # emqx_gm_ext.h
     "emqx_gm_gen_filter_codes": (_i32, [_u64, _u64, _i32, _vp]),
     "emqx_gm_render_codes": (_u64, [_vp, _u64, _vp, _vp]),
@@ -79,6 +84,7 @@ SIGNATURES = {
     "emqx_gm_pool_trim": (_i32, [_vp]),
     "emqx_gm_index_compile_host": (_i32, [_vp, _vp, _u64, _vp, _vp, _vp, C.POINTER(IndexInfo)]),
     "emqx_gm_matched_filter_bytes": (_i32, [_vp, _vp, C.POINTER(Csr), C.POINTER(_u64)]),
+    "emqx_gm_select_filters": (_i32, [_vp, _vp, _u64, _vp, _u32, _vp, _vp, C.POINTER(_u64), C.POINTER(_u64)]),
 }
 
 _LIB = None

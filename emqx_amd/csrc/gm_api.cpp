@@ -1,6 +1,7 @@
 // gm_api.cpp — extern "C" boundary of libemqx_gpu_match.so (include/emqx_gpu_match.h).
 // No C++ exception crosses the ABI; every failure is an EMQX_GM_E* code with
 // the message in emqx_gm_last_error().
+#include <algorithm>
 #include <cstring>
 #include <new>
 #include <stdexcept>
@@ -188,7 +189,13 @@ int emqx_gm_index_info(const emqx_gm_index* idx, emqx_gm_index_info_t* info) {
 }
 
 int emqx_gm_index_filter(const emqx_gm_index* idx, uint32_t id, const uint8_t** bytes, uint64_t* len) {
-  if (!idx || !bytes || !len || id >= idx->info.n_filters) return EMQX_GM_EINVAL;
+  if (!idx || !bytes || !len) return EMQX_GM_EINVAL;
+  if (!idx->gmap.empty()) {  // shard index: ids are global
+    auto it = std::lower_bound(idx->gmap.begin(), idx->gmap.end(), id);
+    if (it == idx->gmap.end() || *it != id) return EMQX_GM_EINVAL;
+    id = uint32_t(it - idx->gmap.begin());
+  }
+  if (id >= idx->info.n_filters) return EMQX_GM_EINVAL;
   *bytes = idx->fbytes.data() + idx->foff[id];
   *len = idx->foff[id + 1] - idx->foff[id];
   return EMQX_GM_OK;
@@ -216,6 +223,7 @@ int emqx_gm_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr
   if (!idx || !m || !out || (m->nnz && !m->ids) || !m->row_off)
     return gm::set_err(ctx, EMQX_GM_EINVAL, "fanout: NULL argument");
   if (flags & ~(EMQX_GM_WITH_EXACT | EMQX_GM_DEVICE_IO)) return gm::set_err(ctx, EMQX_GM_EINVAL, "fanout: flags");
+  if (idx->view.gmap) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "fanout: shard index (fan out before merging)");
   std::memset(out, 0, sizeof(*out));
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
@@ -262,6 +270,92 @@ int emqx_gm_index_compile_host(const uint8_t* fb, const uint64_t* fo, uint64_t n
   GM_GUARD_BEGIN
   return gm::build_index(nullptr, fb, fo, n, sub_off, sub_ids, perm_out, nullptr, info);
   GM_GUARD_END(nullptr)
+}
+
+// ---- sharded index ----
+int emqx_gm_filter_ranks(const uint8_t* fb, const uint64_t* fo, uint64_t n, uint32_t* rank_out, uint64_t* n_unique) {
+  if (n && (!fb || !fo || !rank_out)) return EMQX_GM_EINVAL;
+  GM_GUARD_BEGIN
+  std::vector<uint32_t> ord(n);
+  for (uint64_t i = 0; i < n; ++i) ord[i] = uint32_t(i);
+  gm::sort_filters(ord, fb, fo);
+  uint32_t r = 0;
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint32_t i = ord[k];
+    if (k) {
+      const uint32_t p = ord[k - 1];
+      const uint64_t lp = fo[p + 1] - fo[p], li = fo[i + 1] - fo[i];
+      if (lp != li || std::memcmp(fb + fo[p], fb + fo[i], li) != 0) ++r;
+    }
+    rank_out[i] = r;
+  }
+  if (n_unique) *n_unique = n ? uint64_t(r) + 1 : 0;
+  return EMQX_GM_OK;
+  GM_GUARD_END(nullptr)
+}
+
+int emqx_gm_shard_of(const uint8_t* fb, const uint64_t* fo, uint64_t n, uint32_t n_shards, uint32_t* out) {
+  if (!n_shards || (n && (!fb || !fo || !out))) return EMQX_GM_EINVAL;
+  for (uint64_t i = 0; i < n; ++i)
+    out[i] = uint32_t(gm::fmix64(gm::hash_word_host(fb + fo[i], fo[i + 1] - fo[i]) ^ 0x5BD1E995ull) % n_shards);
+  return EMQX_GM_OK;
+}
+
+int emqx_gm_select_filters(const uint8_t* fb, const uint64_t* fo, uint64_t n, const uint32_t* shard, uint32_t want,
+                           uint8_t* out_b, uint64_t* out_o, uint64_t* n_out, uint64_t* bytes_out) {
+  if (!n_out || !bytes_out || (n && (!fb || !fo || !shard))) return EMQX_GM_EINVAL;
+  uint64_t k = 0, b = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (shard[i] != want) continue;
+    const uint64_t len = fo[i + 1] - fo[i];
+    if (out_b && out_o) {
+      out_o[k] = b;
+      std::memcpy(out_b + b, fb + fo[i], len);
+    }
+    ++k;
+    b += len;
+  }
+  if (out_o) out_o[k] = b;
+  *n_out = k;
+  *bytes_out = b;
+  return EMQX_GM_OK;
+}
+
+int emqx_gm_index_build_shard(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_t n,
+                              const uint32_t* global_ids, const uint64_t* sub_off, const uint32_t* sub_ids,
+                              uint32_t* perm_out, emqx_gm_index** out) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (n && !global_ids) return gm::set_err(ctx, EMQX_GM_EINVAL, "index_build_shard: global_ids is NULL");
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  return gm::build_index(ctx, fb, fo, n, sub_off, sub_ids, perm_out, out, nullptr, global_ids);
+  GM_GUARD_END(ctx)
+}
+
+int emqx_gm_csr_row_lengths(emqx_gm_ctx* ctx, const emqx_gm_csr* csr, uint32_t* d_lens) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (!csr || !csr->on_device || !d_lens || !csr->row_off)
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "csr_row_lengths: needs a device CSR and a device output");
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  return gm::run_row_lengths(ctx, csr, d_lens);
+  GM_GUARD_END(ctx)
+}
+
+int emqx_gm_merge_rows(emqx_gm_ctx* ctx, uint64_t n_rows, uint64_t stride, uint32_t n_pieces, const uint32_t* d_lens,
+                       const uint32_t* d_ids, uint32_t flags, emqx_gm_csr* out) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (!out || stride < n_rows || !n_pieces || (n_rows && (!d_lens || !d_ids)))
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "merge_rows: bad arguments");
+  if (flags & ~EMQX_GM_DEVICE_IO) return gm::set_err(ctx, EMQX_GM_EINVAL, "merge_rows: flags");
+  std::memset(out, 0, sizeof(*out));
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  return gm::run_merge_rows(ctx, n_rows, stride, n_pieces, d_lens, d_ids, flags, out);
+  GM_GUARD_END(ctx)
 }
 
 int emqx_gm_pool_trim(emqx_gm_ctx* ctx) {

@@ -94,6 +94,7 @@ struct IndexView {
   const uint8_t* arena;
   const uint64_t* sub_off;
   const uint32_t* sub_ids;
+  const uint32_t* gmap;     // shard index: local filter id -> global id (ascending); nullptr otherwise
   uint64_t dict_mask;
   uint64_t etab_off[EDGE_DEPTHS];   // slot offset of each depth's table
   uint64_t etab_mask[EDGE_DEPTHS];  // slots - 1

@@ -91,7 +91,7 @@ bool less_bytes(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
 }
 
 // Parallel sort of filter indices by bytes (chunked std::sort + pairwise merges).
-void sort_filters(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t* fo) {
+void sort_filters_impl(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t* fo) {
   auto cmp = [&](uint32_t x, uint32_t y) {
     return less_bytes(fb + fo[x], fo[x + 1] - fo[x], fb + fo[y], fo[y + 1] - fo[y]);
   };
@@ -123,8 +123,11 @@ void sort_filters(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t*
 
 }  // namespace
 
+void sort_filters(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t* fo) { sort_filters_impl(ord, fb, fo); }
+
 int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_t n, const uint64_t* sub_off,
-                const uint32_t* sub_ids, uint32_t* perm_out, emqx_gm_index** out, emqx_gm_index_info_t* host_only) {
+                const uint32_t* sub_ids, uint32_t* perm_out, emqx_gm_index** out, emqx_gm_index_info_t* host_only,
+                const uint32_t* gids) {
   if (!out && !host_only) return set_err(ctx, EMQX_GM_EINVAL, "index_build: out is NULL");
   if (n && (!fb || !fo)) return set_err(ctx, EMQX_GM_EINVAL, "index_build: NULL filter buffers");
   if (n >= 0x7FFFFFFFull) return set_err(ctx, EMQX_GM_EINVAL, "index_build: too many filters");
@@ -139,7 +142,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // ---- 1. ids = lexicographic rank of unique filters
   std::vector<uint32_t> ord(n);
   std::iota(ord.begin(), ord.end(), 0u);
-  sort_filters(ord, fb, fo);
+  sort_filters_impl(ord, fb, fo);
   std::vector<uint32_t> id_of(n);
   uint32_t nf = 0;
   idx->foff.push_back(0);
@@ -160,6 +163,24 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   }
   if (perm_out)
     for (uint64_t i = 0; i < n; ++i) perm_out[i] = id_of[i];
+  // shard index: rows carry the filters' global ids, which
+  // must follow the byte order (a shard's local order is then the global one)
+  if (gids) {
+    idx->gmap.assign(nf, NONE);
+    for (uint64_t i = 0; i < n; ++i) {
+      uint32_t& g = idx->gmap[id_of[i]];
+      if (g != NONE && g != gids[i]) {
+        delete idx;
+        return set_err(ctx, EMQX_GM_EINVAL, "index_build_shard: equal filters with different global ids");
+      }
+      g = gids[i];
+    }
+    for (uint32_t f = 0; f < nf; ++f)
+      if (idx->gmap[f] >= 0x7FFFFFFFu || (f && idx->gmap[f] <= idx->gmap[f - 1])) {
+        delete idx;
+        return set_err(ctx, EMQX_GM_EINVAL, "index_build_shard: global ids must ascend with the filter bytes");
+      }
+  }
 
   // ---- 2. intern words, build the level trie
   std::unordered_map<std::string_view, uint32_t, ViewHash> wid;  // word -> arena offset
@@ -371,7 +392,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   size_t o_soff = o_arena + al(arena.size() + 64);
   size_t o_sids = o_soff + al(soff.size() * 8);
   size_t o_flen = o_sids + al(sids.size() * 4 + 4);
-  size_t total = o_flen + al(flen.size() * 2 + 2);
+  size_t o_gmap = o_flen + al(flen.size() * 2 + 2);
+  size_t total = o_gmap + al(idx->gmap.size() * 4 + 4);
 
   if (host_only) {  // compile-only self check (no device): report the table sizes
     emqx_gm_index_info_t& in = *host_only;
@@ -407,6 +429,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   up(o_soff, soff.data(), soff.size() * 8);
   up(o_sids, sids.data(), sids.size() * 4);
   up(o_flen, flen.data(), flen.size() * 2);
+  up(o_gmap, idx->gmap.data(), idx->gmap.size() * 4);
   if (e != hipSuccess) {
     hipFree(idx->dev_base);
     delete idx;
@@ -421,6 +444,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.arena = B + o_arena;
   v.sub_off = reinterpret_cast<const uint64_t*>(B + o_soff);
   v.sub_ids = reinterpret_cast<const uint32_t*>(B + o_sids);
+  v.gmap = idx->gmap.empty() ? nullptr : reinterpret_cast<const uint32_t*>(B + o_gmap);
   v.dict_mask = dcap - 1;
   for (int d = 0; d < EDGE_DEPTHS; ++d) {
     v.etab_off[d] = etab_off[d];

@@ -91,6 +91,7 @@ struct emqx_gm_index {
   // host copies
   std::vector<uint8_t> fbytes;  // sorted unique filters
   std::vector<uint64_t> foff;
+  std::vector<uint32_t> gmap;   // shard index: global id of each local filter (ascending); empty otherwise
   emqx_gm_index_info_t info{};
 };
 
@@ -98,13 +99,17 @@ namespace gm {
 // gm_index.cpp
 int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_t n, const uint64_t* sub_off,
                 const uint32_t* sub_ids, uint32_t* perm_out, emqx_gm_index** out,
-                emqx_gm_index_info_t* host_only = nullptr);
+                emqx_gm_index_info_t* host_only = nullptr, const uint32_t* gids = nullptr);
+void sort_filters(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t* fo);
 void free_index(emqx_gm_index* idx);
 // gm_match.hip
 int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
               uint32_t flags, emqx_gm_csr* out);
 int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
                emqx_gm_csr* out);
+int run_merge_rows(emqx_gm_ctx* ctx, uint64_t n_rows, uint64_t stride, uint32_t n_pieces, const uint32_t* d_lens,
+                   const uint32_t* d_ids, uint32_t flags, emqx_gm_csr* out);
+int run_row_lengths(emqx_gm_ctx* ctx, const emqx_gm_csr* csr, uint32_t* d_out);
 int set_err(emqx_gm_ctx* ctx, int code, const std::string& msg);
 }  // namespace gm
 

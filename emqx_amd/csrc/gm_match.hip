@@ -913,7 +913,8 @@ __device__ __forceinline__ void sort_row(uint32_t (&m)[FAST_MC]) {
 __global__ __launch_bounds__(256) void k_assemble(const uint32_t* __restrict__ cnt, uint64_t n,
                                                   const uint64_t* __restrict__ tile_off,
                                                   const uint32_t* __restrict__ stage,
-                                                  uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids) {
+                                                  uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids,
+                                                  const uint32_t* __restrict__ gmap) {
   const int lane = threadIdx.x & 63;
   const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
   const uint64_t tile = t >> 6;
@@ -932,7 +933,7 @@ __global__ __launch_bounds__(256) void k_assemble(const uint32_t* __restrict__ c
   if (cf > 1) sort_row(m);
 #pragma unroll
   for (int k = 0; k < FAST_MC; ++k)
-    if (uint32_t(k) < cf) ids[base + k] = m[k];
+    if (uint32_t(k) < cf) ids[base + k] = gmap ? gmap[m[k]] : m[k];  // shard index: global ids (ascending)
 }
 
 // ---------------------------------------------------------------------------
@@ -1081,12 +1082,16 @@ __global__ __launch_bounds__(256) void k_slow_emit(uint64_t k0, uint64_t kn, con
 __global__ __launch_bounds__(256) void k_copy_slow(const uint32_t* __restrict__ list, uint64_t kn,
                                                    const uint64_t* __restrict__ row_off,
                                                    const uint64_t* __restrict__ slow_off,
-                                                   const uint32_t* __restrict__ slow_ids, uint32_t* __restrict__ ids) {
+                                                   const uint32_t* __restrict__ slow_ids, uint32_t* __restrict__ ids,
+                                                   const uint32_t* __restrict__ gmap) {
   const uint64_t k = blockIdx.x;
   if (k >= kn) return;
   const uint32_t t = list[k];
   const uint64_t dst = row_off[t], src = slow_off[k], len = slow_off[k + 1] - src;
-  for (uint64_t i = threadIdx.x; i < len; i += 256) ids[dst + i] = slow_ids[src + i];
+  for (uint64_t i = threadIdx.x; i < len; i += 256) {
+    const uint32_t f = slow_ids[src + i];
+    ids[dst + i] = gmap ? gmap[f] : f;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1142,14 +1147,76 @@ __global__ __launch_bounds__(256) void k_fanout_copy(const uint64_t* __restrict_
 // ---------------------------------------------------------------------------
 // stats helper: sum of matched filter lengths (for algorithmic bytes)
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (a[m] < x) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+
 __global__ __launch_bounds__(256) void k_sum_flen(const uint32_t* __restrict__ ids, uint64_t nnz,
                                                   const uint16_t* __restrict__ flen,
+                                                  const uint32_t* __restrict__ gmap, uint32_t nf,
                                                   unsigned long long* __restrict__ acc) {
   uint64_t s = 0;
   for (uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x; i < nnz; i += uint64_t(gridDim.x) * 256u)
-    s += flen[ids[i]];
+    s += flen[gmap ? lower_bound_u32(gmap, nf, ids[i]) : ids[i]];
   for (int d = 32; d > 0; d >>= 1) s += __shfl_down(s, d, 64);
   if ((threadIdx.x & 63) == 0) atomicAdd(acc, (unsigned long long)s);
+}
+
+// ---------------------------------------------------------------------------
+// row merge (sharded index)
+// ---------------------------------------------------------------------------
+// Pieces p = 0..P-1 each hold, for the same n rows, a sorted list of filter
+// ids; the lists of one row are disjoint (filters are partitioned over the
+// shards).  lens is [P][stride] (rows >= n have length 0), ids the pieces'
+// rows concatenated piece-major, row-minor (the all-to-all's output), so an
+// exclusive scan of lens gives every (piece, row) list's offset in ids.  Each
+// element's rank in its merged row = its index in its own list + its
+// lower_bound in every other list of the row.
+struct LoadU32 {
+  const uint32_t* p;
+  __device__ uint64_t operator()(uint64_t i) const { return p[i]; }
+};
+struct LoadRowSum {  // merged row length
+  const uint32_t* lens;
+  uint64_t stride;
+  uint32_t pieces;
+  __device__ uint64_t operator()(uint64_t t) const {
+    uint64_t s = 0;
+    for (uint32_t p = 0; p < pieces; ++p) s += lens[p * stride + t];
+    return s;
+  }
+};
+
+__global__ __launch_bounds__(256) void k_merge_rows(const uint32_t* __restrict__ lens, const uint64_t* __restrict__ pos,
+                                                    const uint32_t* __restrict__ ids, uint64_t n, uint64_t stride,
+                                                    uint32_t pieces, const uint64_t* __restrict__ row_off,
+                                                    uint32_t* __restrict__ out) {
+  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t o = row_off[t];
+  for (uint32_t p = 0; p < pieces; ++p) {
+    const uint64_t src = pos[p * stride + t];
+    const uint32_t len = lens[p * stride + t];
+    for (uint32_t j = 0; j < len; ++j) {
+      const uint32_t x = ids[src + j];
+      uint64_t r = j;
+      for (uint32_t q = 0; q < pieces; ++q)
+        if (q != p) r += lower_bound_u32(ids + pos[q * stride + t], lens[q * stride + t], x);
+      out[o + r] = x;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_row_lengths(const uint64_t* __restrict__ row_off, uint64_t n,
+                                                     uint32_t* __restrict__ out) {
+  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (t < n) out[t] = uint32_t(row_off[t + 1] - row_off[t]);
 }
 
 // Sum of per-tile counters into one (one atomic per wave of a small grid).
@@ -1409,11 +1476,11 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   PoolBuf ids(ctx->pool, nnz * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
   hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt.as<uint32_t>(), n, toff.as<uint64_t>(),
-                     stage.as<uint32_t>(), row_off.as<uint64_t>(), ids.as<uint32_t>());
+                     stage.as<uint32_t>(), row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap);
   GM_HIP(ctx, hipGetLastError());
   if (n_ovf) {
     hipLaunchKernelGGL(k_copy_slow, dim3(n_ovf), dim3(256), 0, st, ovf_list, n_ovf, row_off.as<uint64_t>(),
-                       slow_off.as<uint64_t>(), slow_ids.as<uint32_t>(), ids.as<uint32_t>());
+                       slow_off.as<uint64_t>(), slow_ids.as<uint32_t>(), ids.as<uint32_t>(), idx->view.gmap);
     GM_HIP(ctx, hipGetLastError());
   }
   GM_HIP(ctx, hipEventRecord(ctx->ev[3], st));
@@ -1436,7 +1503,7 @@ int sum_filter_lengths(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint32_
   if (nnz) {
     const uint64_t blocks = std::min<uint64_t>(4096, (nnz + 255) / 256);
     hipLaunchKernelGGL(k_sum_flen, dim3(blocks), dim3(256), 0, ctx->stream, d_ids, nnz, idx->dev_flen,
-                       acc.as<unsigned long long>());
+                       idx->view.gmap, idx->view.n_filters, acc.as<unsigned long long>());
     GM_HIP(ctx, hipGetLastError());
   }
   GM_HIP(ctx, hipMemcpyAsync(out, acc.p, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1492,6 +1559,48 @@ int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m,
   ctx->stats.match_kernel_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
   ctx->stats.total_device_ms = ev_ms(ctx->ev[0], ctx->ev[2]);
   return finish_csr(ctx, n, total, row_off, ids, dev_out, out);
+}
+
+int run_merge_rows(emqx_gm_ctx* ctx, uint64_t n, uint64_t stride, uint32_t pieces, const uint32_t* d_lens,
+                   const uint32_t* d_ids, uint32_t flags, emqx_gm_csr* out) {
+  hipStream_t st = ctx->stream;
+  ctx->stats = emqx_gm_match_stats{};
+  ctx->stats.n_topics = n;
+  const uint64_t nl = uint64_t(pieces) * stride;
+  PoolBuf pos(ctx->pool, (nl + 1) * 8), row_off(ctx->pool, (n + 1) * 8);
+  if (!pos.p || !row_off.p) return set_err(ctx, EMQX_GM_ENOMEM, "merge_rows: workspace");
+  GM_HIP(ctx, hipEventRecord(ctx->ev[0], st));
+  int rc = scan_excl(ctx, LoadU32{d_lens}, nl, pos.as<uint64_t>());
+  if (rc) return rc;
+  rc = scan_excl(ctx, LoadRowSum{d_lens, stride, pieces}, n, row_off.as<uint64_t>());
+  if (rc) return rc;
+  uint64_t nnz = 0;
+  GM_HIP(ctx, hipMemcpyAsync(&nnz, row_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+  GM_HIP(ctx, hipStreamSynchronize(st));
+  PoolBuf ids(ctx->pool, nnz * 4 + 16);
+  if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "merge_rows: output");
+  GM_HIP(ctx, hipEventRecord(ctx->ev[1], st));
+  if (n) {
+    hipLaunchKernelGGL(k_merge_rows, dim3((n + 255) / 256), dim3(256), 0, st, d_lens, pos.as<uint64_t>(), d_ids, n,
+                       stride, pieces, row_off.as<uint64_t>(), ids.as<uint32_t>());
+    GM_HIP(ctx, hipGetLastError());
+  }
+  GM_HIP(ctx, hipEventRecord(ctx->ev[2], st));
+  GM_HIP(ctx, hipEventSynchronize(ctx->ev[2]));
+  ctx->stats.nnz = nnz;
+  ctx->stats.match_kernel_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
+  ctx->stats.total_device_ms = ev_ms(ctx->ev[0], ctx->ev[2]);
+  return finish_csr(ctx, n, nnz, row_off, ids, flags & EMQX_GM_DEVICE_IO, out);
+}
+
+int run_row_lengths(emqx_gm_ctx* ctx, const emqx_gm_csr* csr, uint32_t* d_out) {
+  if (csr->n_rows) {
+    hipLaunchKernelGGL(k_row_lengths, dim3((csr->n_rows + 255) / 256), dim3(256), 0, ctx->stream, csr->row_off,
+                       csr->n_rows, d_out);
+    GM_HIP(ctx, hipGetLastError());
+  }
+  GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
 }
 
 }  // namespace gm

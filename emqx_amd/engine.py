@@ -167,6 +167,19 @@ class Context:
                                         C.byref(h)), self.h, "index_build")
         return Index(self, h, perm[:n])
 
+    def build_index_shard(self, filters, global_ids: np.ndarray, subs=None) -> Index:
+        """An index over one shard whose rows carry ``global_ids`` (emqx_gm_index_build_shard)."""
+        fb, fo = filters if isinstance(filters, tuple) else pack(filters)
+        n = len(fo) - 1
+        g = np.ascontiguousarray(global_ids, np.uint32)
+        if len(g) != n:
+            raise ValueError("one global id per filter")
+        perm = np.zeros(max(n, 1), np.uint32)
+        h = C.c_void_p()
+        check(lib().emqx_gm_index_build_shard(self.h, _ptr(fb), _ptr(fo), n, _ptr(g) if n else None, None, None,
+                                              _ptr(perm), C.byref(h)), self.h, "index_build_shard")
+        return Index(self, h, perm[:n])
+
     # ------------------------------------------------------------------ match
     def match(self, index: Index, topics, exact: bool = True) -> Tuple[np.ndarray, np.ndarray]:
         """Batch emqx_router:match_routes/1 (exact=True) or emqx_trie:match/1
@@ -214,6 +227,22 @@ class Context:
               self.h, "fanout")
         return DeviceCsr(self, out)
 
+    # ------------------------------------------------------------------ sharded rows
+    def csr_row_lengths(self, res: DeviceCsr, d_out: int):
+        """Row lengths (u32) of a device CSR into device memory at ``d_out``."""
+        check(lib().emqx_gm_csr_row_lengths(self.h, C.byref(res.csr), C.c_void_p(d_out)), self.h, "csr_row_lengths")
+
+    def merge_rows(self, n_rows: int, stride: int, pieces: int, d_lens: int, d_ids: int) -> DeviceCsr:
+        """Merge per-shard rows by global id (emqx_gm_merge_rows); result stays on the device."""
+        out = Csr()
+        check(lib().emqx_gm_merge_rows(self.h, n_rows, stride, pieces, C.c_void_p(d_lens), C.c_void_p(d_ids),
+                                       _lib.DEVICE_IO, C.byref(out)), self.h, "merge_rows")
+        return DeviceCsr(self, out)
+
+    def memcpy_d2d(self, dst_ptr: int, src_ptr: int, nbytes: int):
+        if nbytes:
+            check(lib().emqx_gm_memcpy(self.h, C.c_void_p(dst_ptr), C.c_void_p(src_ptr), nbytes, 2), self.h, "memcpy")
+
     # ------------------------------------------------------------------ misc
     def stats(self) -> dict:
         s = MatchStats()
@@ -257,6 +286,37 @@ class Context:
         check(lib().emqx_gm_gen_topics(self.h, _ptr(fc) if len(fc) else None, len(fc), seed, start, n,
                                        C.byref(db), C.byref(do), C.byref(tot)), self.h, "gen_topics")
         return db.value, do.value, int(tot.value)
+
+
+# ---------------------------------------------------------------------- sharding helpers (host)
+def filter_ranks(fb: np.ndarray, fo: np.ndarray) -> Tuple[np.ndarray, int]:
+    """Global id of each filter = its rank among the unique filters (emqx_gm_filter_ranks)."""
+    n = len(fo) - 1
+    out = np.zeros(max(n, 1), np.uint32)
+    nu = C.c_uint64()
+    check(lib().emqx_gm_filter_ranks(_ptr(fb), _ptr(fo), n, _ptr(out), C.byref(nu)), None, "filter_ranks")
+    return out[:n], int(nu.value)
+
+
+def shard_of(fb: np.ndarray, fo: np.ndarray, n_shards: int) -> np.ndarray:
+    n = len(fo) - 1
+    out = np.zeros(max(n, 1), np.uint32)
+    check(lib().emqx_gm_shard_of(_ptr(fb), _ptr(fo), n, n_shards, _ptr(out)), None, "shard_of")
+    return out[:n]
+
+
+def select_filters(fb: np.ndarray, fo: np.ndarray, shard: np.ndarray, want: int) -> Tuple[np.ndarray, np.ndarray]:
+    """The filters with shard == want, packed like pack()."""
+    n = len(fo) - 1
+    sh = np.ascontiguousarray(shard, np.uint32)
+    k, nb = C.c_uint64(), C.c_uint64()
+    check(lib().emqx_gm_select_filters(_ptr(fb), _ptr(fo), n, _ptr(sh), want, None, None, C.byref(k), C.byref(nb)),
+          None, "select_filters")
+    ob = np.zeros(nb.value + 64, np.uint8)
+    oo = np.zeros(k.value + 1, np.uint64)
+    check(lib().emqx_gm_select_filters(_ptr(fb), _ptr(fo), n, _ptr(sh), want, _ptr(ob), _ptr(oo), C.byref(k),
+                                       C.byref(nb)), None, "select_filters")
+    return ob, oo
 
 
 # ---------------------------------------------------------------------- workload

@@ -37,6 +37,12 @@ int emqx_gm_index_compile_host(const uint8_t *filter_bytes, const uint64_t *filt
                                const uint64_t *sub_off, const uint32_t *sub_ids, uint32_t *perm_out,
                                emqx_gm_index_info_t *info);
 
+/* The filters with shard[i] == want, packed (two-call sizing: pass NULL
+ * out_bytes/out_off to get *n_out and *bytes_out). */
+int emqx_gm_select_filters(const uint8_t *filter_bytes, const uint64_t *filter_off, uint64_t n_filters,
+                           const uint32_t *shard, uint32_t want, uint8_t *out_bytes, uint64_t *out_off,
+                           uint64_t *n_out, uint64_t *bytes_out);
+
 /* Sum of the byte lengths of the filters referenced by a device CSR (the
  * Σ len(f) term of the algorithmic-bytes formula). */
 int emqx_gm_matched_filter_bytes(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const emqx_gm_csr *csr,

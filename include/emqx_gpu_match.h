@@ -140,6 +140,37 @@ int emqx_gm_fanout(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const emqx_gm_csr
 int emqx_gm_csr_free(emqx_gm_ctx *ctx, emqx_gm_csr *csr);
 int emqx_gm_last_stats(const emqx_gm_ctx *ctx, emqx_gm_match_stats *stats);
 
+/* ---- sharded index (BASELINE configs[4]) ----
+ * For filter sets too large to replicate, filters are hash-partitioned over
+ * devices (emqx_gm_shard_of), every device matches the whole publish batch
+ * against its shard, rows are exchanged (RCCL all-to-all: device q receives
+ * topic slice q from every shard) and merged by global filter id.  The
+ * reference has no sharded trie (every node replicates emqx_route/emqx_trie
+ * through mria, emqx_router.erl:75-84); the merged rows equal the unsharded
+ * match_routes/1 rows. */
+/* Global id of each filter: its lexicographic rank among the unique filters
+ * (the id an unsharded emqx_gm_index_build would assign). */
+int emqx_gm_filter_ranks(const uint8_t *filter_bytes, const uint64_t *filter_off, uint64_t n_filters,
+                         uint32_t *rank_out, uint64_t *n_unique);
+/* Shard of each filter: fmix64(word hash of the filter bytes) mod n_shards. */
+int emqx_gm_shard_of(const uint8_t *filter_bytes, const uint64_t *filter_off, uint64_t n_filters,
+                     uint32_t n_shards, uint32_t *shard_out);
+/* Index over one shard whose result rows carry the given global ids (which
+ * must ascend with the filter bytes).  emqx_gm_fanout is not available on a
+ * shard index (subscribers live with their shard: fan out before merging). */
+int emqx_gm_index_build_shard(emqx_gm_ctx *ctx, const uint8_t *filter_bytes, const uint64_t *filter_off,
+                              uint64_t n_filters, const uint32_t *global_ids, const uint64_t *sub_off,
+                              const uint32_t *sub_ids, uint32_t *perm_out, emqx_gm_index **out);
+/* Row lengths of a device CSR into device memory (u32 per row). */
+int emqx_gm_csr_row_lengths(emqx_gm_ctx *ctx, const emqx_gm_csr *csr, uint32_t *d_lens);
+/* Merge n_pieces per-shard results for the same n_rows rows.  d_lens: device
+ * u32 [n_pieces][stride] (stride >= n_rows, padding rows 0); d_ids: device
+ * u32, the pieces' rows concatenated piece-major.  Rows are disjoint sorted
+ * id lists; the result rows are their sorted unions (flags: DEVICE_IO keeps
+ * the CSR on the device). */
+int emqx_gm_merge_rows(emqx_gm_ctx *ctx, uint64_t n_rows, uint64_t stride, uint32_t n_pieces,
+                       const uint32_t *d_lens, const uint32_t *d_ids, uint32_t flags, emqx_gm_csr *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,146 @@
+"""Sharded index on the GPU: shard indexes that carry
+global filter ids, the device row merge, and the ShardedMatcher pipeline with
+two ranks sharing one device over gloo.  Bar: merged rows bit-exact with the
+unsharded index and the oracle."""
+
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from emqx_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _to_device(ctx, tb, to):
+    d_tb = ctx.dev_alloc(len(tb))
+    d_to = ctx.dev_alloc(len(to) * 8)
+    ctx.memcpy_h2d(d_tb, tb, len(tb))
+    ctx.memcpy_h2d(d_to, to, len(to) * 8)
+    return d_tb, d_to
+
+
+def _sets(kind):
+    from tests.test_gpu_parity import _rand_filter, _rand_topic
+    if kind == "random":
+        rng = random.Random(31)
+        fs = [_rand_filter(rng).encode() for _ in range(400)]
+        ts = [_rand_topic(rng).encode() for _ in range(3000)]
+        return fs, ts
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    from oracle import oracle as orc
+    codes = gen_filter_codes(4, 20_000)
+    fs = orc.unpack(*render_codes(codes))
+    ts = orc.unpack(*orc.render_codes(orc.gen_topic_codes(4, 0, 50_000, codes)))
+    return fs, ts
+
+
+@pytest.mark.parametrize("kind", ["random", "c1"])
+@pytest.mark.parametrize("shards", [2, 3, 5])
+def test_shard_indexes_merge_to_unsharded_rows(ctx, orc, kind, shards):
+    from emqx_amd.engine import pack
+    from emqx_amd.sharded import plan_shard
+    filters, topics = _sets(kind)
+    fb, fo = pack(filters)
+    tb, to = pack(topics)
+    n = len(topics)
+    full = ctx.build_index(filters)
+    fro, fids = ctx.match(full, (tb, to), exact=True)
+    d_tb, d_to = _to_device(ctx, tb, to)
+    d_lens = ctx.dev_alloc(shards * n * 4)
+    parts, idxs, total = [], [], 0
+    for r in range(shards):
+        sfb, sfo, gids, nu = plan_shard(fb, fo, shards, r)
+        idx = ctx.build_index_shard((sfb, sfo), gids)
+        idxs.append(idx)
+        res = ctx.match_device(idx, d_tb, d_to, n, exact=True)
+        ctx.csr_row_lengths(res, d_lens + r * n * 4)
+        parts.append(res)
+        total += res.nnz
+        if len(gids):  # global ids resolve to the shard's own filter bytes
+            g = int(gids[0])
+            assert idx.filter(g) == sorted(set(filters))[g]
+    d_ids = ctx.dev_alloc(max(total, 1) * 4)
+    off = 0
+    for res in parts:
+        import ctypes as C
+        ctx.memcpy_d2d(d_ids + off * 4, C.cast(res.csr.ids, C.c_void_p).value or 0, res.nnz * 4)
+        off += res.nnz
+        res.free()
+    merged = ctx.merge_rows(n, n, shards, d_lens, d_ids)
+    ro, ids = merged.to_host()
+    assert np.array_equal(ro, fro) and np.array_equal(ids, fids)
+    oro, oids = orc.bruteforce((tb, to), sorted(set(filters)), mode=1)
+    assert np.array_equal(ro, oro) and np.array_equal(ids, oids)
+    merged.free()
+    from emqx_amd import GpuMatchError
+    with pytest.raises(GpuMatchError, match="EUNSUPPORTED"):
+        ctx.fanout(idxs[0], ro[:2].copy() * 0, np.zeros(0, np.uint32))
+    for idx in idxs:
+        idx.release()
+    full.release()
+    for p in (d_tb, d_to, d_lens, d_ids):
+        ctx.dev_free(p)
+
+
+def test_shard_global_ids_must_follow_byte_order(ctx):
+    from emqx_amd import GpuMatchError
+    with pytest.raises(GpuMatchError, match="ascend"):
+        ctx.build_index_shard([b"a/#", b"b/+"], np.array([5, 2], np.uint32))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from emqx_amd import Context
+    from emqx_amd.engine import pack
+    from emqx_amd.sharded import ShardedMatcher, plan_shard
+    from oracle import oracle as orc
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = Context(0)
+    try:
+        filters, topics = _sets("c1")
+        fb, fo = pack(filters)
+        tb, to = pack(topics)
+        sfb, sfo, gids, _ = plan_shard(fb, fo, world, rank)
+        idx = ctx.build_index_shard((sfb, sfo), gids)
+        d_tb, d_to = _to_device(ctx, tb, to)
+        m = ShardedMatcher(ctx, idx, world, rank, dist=dist, device_tensors=False)
+        res, first, rows = m.match_device(d_tb, d_to, len(topics))
+        ro, ids = res.to_host()
+        oro, oids = orc.bruteforce((tb, to), sorted(set(filters)), mode=1)
+        for k in range(rows):
+            t = first + k
+            assert ids[ro[k]:ro[k + 1]].tolist() == oids[oro[t]:oro[t + 1]].tolist(), (rank, t)
+        res.free()
+        idx.release()
+        ctx.dev_free(d_tb)
+        ctx.dev_free(d_to)
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write(str(rows))
+    finally:
+        ctx.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_sharded_matcher_two_ranks_gloo(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert sorted(os.listdir(tmp_path)) == ["ok0", "ok1"]
