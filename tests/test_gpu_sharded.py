@@ -21,6 +21,16 @@ def ctx():
     c.close()
 
 
+def _oracle_rows(orc, filters, tb, to):
+    """The oracle's emqx_router:match_routes/1 rows (trie walk + exact routes)."""
+    uniq = sorted(set(filters))
+    r = orc.Router(True)
+    for f in uniq:
+        r.add_route(f)
+    ro, ids, _ = r.match_batch((tb, to), uniq, mode=1, nthreads=8)
+    return ro, ids
+
+
 def _to_device(ctx, tb, to):
     d_tb = ctx.dev_alloc(len(tb))
     d_to = ctx.dev_alloc(len(to) * 8)
@@ -79,7 +89,7 @@ def test_shard_indexes_merge_to_unsharded_rows(ctx, orc, kind, shards):
     merged = ctx.merge_rows(n, n, shards, d_lens, d_ids)
     ro, ids = merged.to_host()
     assert np.array_equal(ro, fro) and np.array_equal(ids, fids)
-    oro, oids = orc.bruteforce((tb, to), sorted(set(filters)), mode=1)
+    oro, oids = _oracle_rows(orc, filters, tb, to)
     assert np.array_equal(ro, oro) and np.array_equal(ids, oids)
     merged.free()
     from emqx_amd import GpuMatchError
@@ -108,13 +118,20 @@ def _free_port():
 
 def _rank(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+
+    def mark(msg):
+        with open(os.path.join(out_dir, f"log{rank}"), "a") as f:
+            f.write(msg + "\n")
     import torch.distributed as dist
     from emqx_amd import Context
     from emqx_amd.engine import pack
     from emqx_amd.sharded import ShardedMatcher, plan_shard
     from oracle import oracle as orc
+    mark("init")
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    mark("pg")
     ctx = Context(0)
+    mark("ctx")
     try:
         filters, topics = _sets("c1")
         fb, fo = pack(filters)
@@ -122,10 +139,12 @@ def _rank(rank, world, port, out_dir):
         sfb, sfo, gids, _ = plan_shard(fb, fo, world, rank)
         idx = ctx.build_index_shard((sfb, sfo), gids)
         d_tb, d_to = _to_device(ctx, tb, to)
+        mark("index")
         m = ShardedMatcher(ctx, idx, world, rank, dist=dist, device_tensors=False)
         res, first, rows = m.match_device(d_tb, d_to, len(topics))
+        mark("matched")
         ro, ids = res.to_host()
-        oro, oids = orc.bruteforce((tb, to), sorted(set(filters)), mode=1)
+        oro, oids = _oracle_rows(orc, filters, tb, to)
         for k in range(rows):
             t = first + k
             assert ids[ro[k]:ro[k + 1]].tolist() == oids[oro[t]:oro[t + 1]].tolist(), (rank, t)
@@ -143,4 +162,4 @@ def _rank(rank, world, port, out_dir):
 def test_sharded_matcher_two_ranks_gloo(tmp_path):
     import torch.multiprocessing as mp
     mp.spawn(_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    assert sorted(os.listdir(tmp_path)) == ["ok0", "ok1"]
+    assert sorted(x for x in os.listdir(tmp_path) if x.startswith("ok")) == ["ok0", "ok1"]
