@@ -7,8 +7,10 @@ reference interfaces (emqx_topic, emqx_trie, emqx_router, emqx_broker dispatch).
 
 from ._lib import GpuMatchError, LIB_PATH  # noqa: F401
 from .engine import Context, DeviceCsr, Index, gen_filter_codes, pack, render_codes  # noqa: F401
-from .routing import Broker, Router, Trie, default_context  # noqa: F401
+from .routing import Broker, Router, SessionRouter, Trie, default_context  # noqa: F401
+from .rules import TopicRuleIndex  # noqa: F401
 from . import topic  # noqa: F401
 
-__all__ = ["Context", "Index", "DeviceCsr", "Trie", "Router", "Broker", "topic", "GpuMatchError",
+__all__ = ["Context", "Index", "DeviceCsr", "Trie", "Router", "SessionRouter", "Broker", "TopicRuleIndex", "topic",
+           "GpuMatchError",
            "pack", "gen_filter_codes", "render_codes", "default_context"]

@@ -170,6 +170,18 @@ int emqx_gm_index_build(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo,
   GM_GUARD_END(ctx)
 }
 
+int emqx_gm_index_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo,
+                         const uint8_t* ops, uint64_t n_ops, emqx_gm_index** out) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (prev && prev->device != ctx->device)
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "index_update: index lives on another device");
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  return gm::update_index(ctx, prev, fb, fo, ops, n_ops, out);
+  GM_GUARD_END(ctx)
+}
+
 int emqx_gm_index_retain(emqx_gm_index* idx) {
   if (!idx) return EMQX_GM_EINVAL;
   idx->refs.fetch_add(1);
@@ -190,6 +202,7 @@ int emqx_gm_index_info(const emqx_gm_index* idx, emqx_gm_index_info_t* info) {
 
 int emqx_gm_index_filter(const emqx_gm_index* idx, uint32_t id, const uint8_t** bytes, uint64_t* len) {
   if (!idx || !bytes || !len) return EMQX_GM_EINVAL;
+  if (idx->ov) return gm::overlay_filter(idx, id, bytes, len);
   if (!idx->gmap.empty()) {  // shard index: ids are global
     auto it = std::lower_bound(idx->gmap.begin(), idx->gmap.end(), id);
     if (it == idx->gmap.end() || *it != id) return EMQX_GM_EINVAL;
@@ -212,6 +225,7 @@ int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb,
   std::memset(out, 0, sizeof(*out));
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
+  if (idx->ov) return gm::run_match_overlay(ctx, idx, tb, to, n, flags, out);
   return gm::run_match(ctx, idx, tb, to, n, flags, out);
   GM_GUARD_END(ctx)
 }
@@ -224,6 +238,7 @@ int emqx_gm_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr
     return gm::set_err(ctx, EMQX_GM_EINVAL, "fanout: NULL argument");
   if (flags & ~(EMQX_GM_WITH_EXACT | EMQX_GM_DEVICE_IO)) return gm::set_err(ctx, EMQX_GM_EINVAL, "fanout: flags");
   if (idx->view.gmap) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "fanout: shard index (fan out before merging)");
+  if (idx->ov) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "fanout: overlay snapshot (subscribers need a rebuild)");
   std::memset(out, 0, sizeof(*out));
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
@@ -258,6 +273,7 @@ int emqx_gm_matched_filter_bytes(emqx_gm_ctx* ctx, const emqx_gm_index* idx, con
                                  uint64_t* out) {
   if (!ctx || !idx || !csr || !out || !csr->on_device) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (idx->ov) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "matched_filter_bytes: overlay snapshot");
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
   return gm::sum_filter_lengths(ctx, idx, csr->ids, csr->nnz, out);

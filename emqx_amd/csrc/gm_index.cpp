@@ -479,6 +479,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
 
 void free_index(emqx_gm_index* idx) {
   if (!idx) return;
+  if (idx->ov) free_overlay(idx);
   if (idx->dev_base) {
     hipSetDevice(idx->device);
     hipFree(idx->dev_base);

@@ -81,6 +81,10 @@ struct emqx_gm_ctx {
   hipEvent_t ev[6]{};
 };
 
+namespace gm {
+struct OverlayState;
+}
+
 struct emqx_gm_index {
   std::atomic<int> refs{1};
   int device = 0;
@@ -92,6 +96,7 @@ struct emqx_gm_index {
   std::vector<uint8_t> fbytes;  // sorted unique filters
   std::vector<uint64_t> foff;
   std::vector<uint32_t> gmap;   // shard index: global id of each local filter (ascending); empty otherwise
+  gm::OverlayState* ov = nullptr;  // overlay snapshot (emqx_gm_index_update); tables above unused then
   emqx_gm_index_info_t info{};
 };
 
@@ -110,6 +115,33 @@ int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m,
 int run_merge_rows(emqx_gm_ctx* ctx, uint64_t n_rows, uint64_t stride, uint32_t n_pieces, const uint32_t* d_lens,
                    const uint32_t* d_ids, uint32_t flags, emqx_gm_csr* out);
 int run_row_lengths(emqx_gm_ctx* ctx, const emqx_gm_csr* csr, uint32_t* d_out);
+
+// gm_overlay.cpp — incremental index maintenance.  An
+// overlay snapshot = an immutable base snapshot (shared, retained) minus
+// tombstoned base filters plus a small delta index over the inserted filters.
+// Final filter ids are ranks in the updated set: a surviving base id b maps to
+// b + (delta filters sorting before b) - (tombstones below b); delta filters
+// carry their final ids directly (shard-style global ids).
+struct OverlayState {
+  emqx_gm_index* base = nullptr;     // retained flat snapshot
+  emqx_gm_index* delta = nullptr;    // flat snapshot over the inserted filters, or nullptr
+  std::vector<uint32_t> tomb;        // deleted base ids, ascending
+  std::vector<uint32_t> ins;         // per delta filter (byte order): base filters sorting before it
+  std::vector<uint32_t> dgid;        // per delta filter: final id
+  std::vector<uint8_t> dbytes;       // delta filters, byte order
+  std::vector<uint64_t> doff;
+  void* dev = nullptr;               // tomb bitmap | its word prefix counts | ins
+  const uint32_t* d_tbm = nullptr;
+  const uint32_t* d_tpre = nullptr;
+  const uint32_t* d_ins = nullptr;
+};
+int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo, const uint8_t* ops,
+                 uint64_t n_ops, emqx_gm_index** out);
+int overlay_filter(const emqx_gm_index* idx, uint32_t id, const uint8_t** bytes, uint64_t* len);
+void free_overlay(emqx_gm_index* idx);
+// gm_match.hip
+int run_match_overlay(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                      uint32_t flags, emqx_gm_csr* out);
 int set_err(emqx_gm_ctx* ctx, int code, const std::string& msg);
 }  // namespace gm
 

@@ -1219,6 +1219,66 @@ __global__ __launch_bounds__(256) void k_row_lengths(const uint64_t* __restrict_
   if (t < n) out[t] = uint32_t(row_off[t + 1] - row_off[t]);
 }
 
+// ---------------------------------------------------------------------------
+// overlay snapshot merge (incremental updates, gm_overlay.cpp)
+// ---------------------------------------------------------------------------
+struct OvView {
+  const uint32_t* tbm;   // tombstone bitmap over base ids
+  const uint32_t* tpre;  // tombstones in the words before each bitmap word
+  const uint32_t* ins;   // insertion point of each delta filter, ascending
+  uint32_t n_ins;
+};
+__device__ __forceinline__ bool ov_dead(const OvView& o, uint32_t b) { return (o.tbm[b >> 5] >> (b & 31)) & 1u; }
+// final id of a surviving base id: + delta filters sorting before it - tombstones below it
+__device__ __forceinline__ uint32_t ov_remap(const OvView& o, uint32_t b) {
+  uint32_t lo = 0, hi = o.n_ins;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (o.ins[m] <= b) lo = m + 1;
+    else hi = m;
+  }
+  const uint32_t w = b >> 5;
+  return b + lo - (o.tpre[w] + __popc(o.tbm[w] & ((1u << (b & 31)) - 1u)));
+}
+struct LoadOvLen {  // merged row length: surviving base ids + delta ids
+  const uint64_t* bo;
+  const uint32_t* bi;
+  const uint64_t* dof;
+  OvView o;
+  __device__ uint64_t operator()(uint64_t t) const {
+    uint64_t c = dof ? dof[t + 1] - dof[t] : 0;
+    for (uint64_t k = bo[t]; k < bo[t + 1]; ++k) c += ov_dead(o, bi[k]) ? 0 : 1;
+    return c;
+  }
+};
+__global__ __launch_bounds__(256) void k_ov_merge(const uint64_t* __restrict__ bo, const uint32_t* __restrict__ bi,
+                                                  const uint64_t* __restrict__ dof, const uint32_t* __restrict__ di,
+                                                  OvView o, uint64_t n, const uint64_t* __restrict__ row_off,
+                                                  uint32_t* __restrict__ out) {
+  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (t >= n) return;
+  uint64_t i = bo[t], w = row_off[t];
+  const uint64_t ie = bo[t + 1];
+  uint64_t j = dof ? dof[t] : 0;
+  const uint64_t je = dof ? dof[t + 1] : 0;
+  auto next_base = [&]() -> uint32_t {
+    while (i < ie && ov_dead(o, bi[i])) ++i;
+    return i < ie ? ov_remap(o, bi[i]) : 0xFFFFFFFFu;
+  };
+  uint32_t b = next_base(), d = j < je ? di[j] : 0xFFFFFFFFu;
+  while (b != 0xFFFFFFFFu || d != 0xFFFFFFFFu) {
+    if (b < d) {
+      out[w++] = b;
+      ++i;
+      b = next_base();
+    } else {
+      out[w++] = d;
+      ++j;
+      d = j < je ? di[j] : 0xFFFFFFFFu;
+    }
+  }
+}
+
 // Sum of per-tile counters into one (one atomic per wave of a small grid).
 __global__ __launch_bounds__(256) void k_sum_tiles(const unsigned long long* __restrict__ a, uint64_t n,
                                                    unsigned long long* __restrict__ acc) {
@@ -1601,6 +1661,73 @@ int run_row_lengths(emqx_gm_ctx* ctx, const emqx_gm_csr* csr, uint32_t* d_out) {
   }
   GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return 0;
+}
+
+// Match on an overlay snapshot: the base and the delta snapshots each match
+// the batch (inputs copied to the device once), then one pass drops
+// tombstoned base ids, remaps the survivors to final ids and merges the delta
+// row in (both rows sorted, disjoint).
+int run_match_overlay(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, const uint64_t* to_in,
+                      uint64_t n, uint32_t flags, emqx_gm_csr* out) {
+  const OverlayState& ov = *idx->ov;
+  const bool dev_io = flags & EMQX_GM_DEVICE_IO;
+  hipStream_t st = ctx->stream;
+  PoolBuf d_tb_own, d_to_own;
+  const uint8_t* tb = tb_in;
+  const uint64_t* to = to_in;
+  if (!dev_io && n) {
+    const uint64_t bytes = to_in[n];
+    for (uint64_t i = 0; i < n; ++i)
+      if (to_in[i + 1] < to_in[i]) return set_err(ctx, EMQX_GM_EINVAL, "match: topic offsets not monotone");
+    d_tb_own = PoolBuf(ctx->pool, bytes + 64);
+    d_to_own = PoolBuf(ctx->pool, (n + 1) * 8);
+    if (!d_tb_own.p || !d_to_own.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: input workspace");
+    if (bytes) GM_HIP(ctx, hipMemcpyAsync(d_tb_own.p, tb_in, bytes, hipMemcpyHostToDevice, st));
+    GM_HIP(ctx, hipMemsetAsync(static_cast<uint8_t*>(d_tb_own.p) + bytes, 0, 64, st));
+    GM_HIP(ctx, hipMemcpyAsync(d_to_own.p, to_in, (n + 1) * 8, hipMemcpyHostToDevice, st));
+    tb = d_tb_own.as<uint8_t>();
+    to = d_to_own.as<uint64_t>();
+  }
+  const uint32_t sub_flags = (flags & EMQX_GM_WITH_EXACT) | EMQX_GM_DEVICE_IO;
+  emqx_gm_csr cb{}, cd{};
+  int rc = run_match(ctx, ov.base, tb, to, n, sub_flags, &cb);
+  if (rc) return rc;
+  PoolBuf b_off, b_ids, d_off, d_ids;  // adopt the sub-results' pool buffers
+  b_off.pool = b_ids.pool = d_off.pool = d_ids.pool = ctx->pool;
+  b_off.p = cb.row_off;
+  b_ids.p = cb.ids;
+  emqx_gm_match_stats st_b = ctx->stats, st_d{};
+  if (ov.delta) {
+    rc = run_match(ctx, ov.delta, tb, to, n, sub_flags, &cd);
+    if (rc) return rc;
+    d_off.p = cd.row_off;
+    d_ids.p = cd.ids;
+    st_d = ctx->stats;
+  }
+  PoolBuf row_off(ctx->pool, (n + 1) * 8);
+  if (!row_off.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: row_off");
+  const OvView o{ov.d_tbm, ov.d_tpre, ov.d_ins, uint32_t(ov.ins.size())};
+  rc = scan_excl(ctx, LoadOvLen{cb.row_off, cb.ids, ov.delta ? cd.row_off : nullptr, o}, n, row_off.as<uint64_t>());
+  if (rc) return rc;
+  uint64_t nnz = 0;
+  GM_HIP(ctx, hipMemcpyAsync(&nnz, row_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+  GM_HIP(ctx, hipStreamSynchronize(st));
+  PoolBuf ids(ctx->pool, nnz * 4 + 16);
+  if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
+  if (n) {
+    hipLaunchKernelGGL(k_ov_merge, dim3((n + 255) / 256), dim3(256), 0, st, cb.row_off, cb.ids,
+                       ov.delta ? cd.row_off : nullptr, ov.delta ? cd.ids : nullptr, o, n, row_off.as<uint64_t>(),
+                       ids.as<uint32_t>());
+    GM_HIP(ctx, hipGetLastError());
+  }
+  GM_HIP(ctx, hipStreamSynchronize(st));
+  ctx->stats = st_b;
+  ctx->stats.nnz = nnz;
+  ctx->stats.probes += st_d.probes;
+  ctx->stats.n_overflow += st_d.n_overflow;
+  ctx->stats.match_kernel_ms += st_d.match_kernel_ms;
+  ctx->stats.total_device_ms += st_d.total_device_ms;
+  return finish_csr(ctx, n, nnz, row_off, ids, dev_io, out);
 }
 
 }  // namespace gm

@@ -180,6 +180,17 @@ class Context:
                                               _ptr(perm), C.byref(h)), self.h, "index_build_shard")
         return Index(self, h, perm[:n])
 
+    def update_index(self, index: Index, ops) -> Index:
+        """A new snapshot = ``index`` with ``ops`` applied in order; ops is a
+        sequence of (filter, insert: bool).  ``index`` stays valid (RCU)."""
+        ops = list(ops)
+        fb, fo = pack([f for f, _ in ops])
+        kinds = np.array([1 if ins else 0 for _, ins in ops] or [0], np.uint8)
+        h = C.c_void_p()
+        check(lib().emqx_gm_index_update(self.h, index.h, _ptr(fb), _ptr(fo), _ptr(kinds), len(ops), C.byref(h)),
+              self.h, "index_update")
+        return Index(self, h, np.zeros(0, np.uint32))
+
     # ------------------------------------------------------------------ match
     def match(self, index: Index, topics, exact: bool = True) -> Tuple[np.ndarray, np.ndarray]:
         """Batch emqx_router:match_routes/1 (exact=True) or emqx_trie:match/1

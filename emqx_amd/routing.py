@@ -9,8 +9,10 @@
 Writes update host tables with the reference's semantics (insert is idempotent
 per topic key, delete only if present, emqx_trie.erl:114-136; a wildcard route
 enters the trie with its first dest, emqx_router_utils.erl:33-38).  Reads go to
-an immutable index snapshot in HBM, rebuilt on the first read after a write
-(RCU-style: a reader holding the old snapshot keeps using it).  The batched
+an immutable index snapshot in HBM; the first read after writes derives a new
+snapshot from the previous one with emqx_gm_index_update (tombstones + a delta
+index, or a flat rebuild once the delta is large) -- RCU: a reader holding the
+old snapshot keeps using it.  The batched
 forms (``match_batch``, ``match_routes_batch``, ``publish_batch``) are the hot
 path; the single-topic forms are the reference API on a batch of one.
 """
@@ -42,11 +44,20 @@ def _b(s) -> bytes:
 
 
 class _Snapshot:
-    """A built index plus the id -> filter table it was built from."""
+    """An index snapshot plus the id -> filter table (sorted filters) it serves."""
 
-    def __init__(self, ctx: Context, filters: List[bytes], subs: Optional[List[List[int]]] = None):
+    def __init__(self, ctx: Context, filters: List[bytes], subs: Optional[List[List[int]]] = None,
+                 index: Optional[Index] = None):
         self.filters = sorted(set(filters))
-        self.index: Index = ctx.build_index(self.filters, subs=None if subs is None else subs)
+        self.index: Index = index if index is not None else ctx.build_index(self.filters, subs=subs)
+
+
+def _refresh(ctx: Context, snap: Optional[_Snapshot], keys, pending: List[Tuple[bytes, bool]]) -> _Snapshot:
+    """The snapshot for the current key set: derived from `snap` by the pending
+    inserts/deletes when there is one, built from scratch otherwise."""
+    if snap is None:
+        return _Snapshot(ctx, list(keys))
+    return _Snapshot(ctx, list(keys), index=ctx.update_index(snap.index, pending))
 
 
 class Trie:
@@ -59,6 +70,7 @@ class Trie:
         self.compact = compact
         self._topics: set = set()
         self._snap: Optional[_Snapshot] = None
+        self._pending: List[Tuple[bytes, bool]] = []
         self._lock = threading.Lock()
 
     def _context(self) -> Context:
@@ -71,14 +83,14 @@ class Trie:
             t = _b(t)
             if t not in self._topics:
                 self._topics.add(t)
-                self._snap = None
+                self._pending.append((t, True))
 
     def delete(self, t) -> None:
         with self._lock:
             t = _b(t)
             if t in self._topics:
                 self._topics.discard(t)
-                self._snap = None
+                self._pending.append((t, False))
 
     def empty(self) -> bool:
         """emqx_trie:empty/0 (ets:first =:= '$end_of_table')."""
@@ -86,8 +98,9 @@ class Trie:
 
     def snapshot(self) -> _Snapshot:
         with self._lock:
-            if self._snap is None:
-                self._snap = _Snapshot(self._context(), list(self._topics))
+            if self._snap is None or self._pending:
+                self._snap = _refresh(self._context(), self._snap, self._topics, self._pending)
+                self._pending = []
             return self._snap
 
     def match_batch(self, topics: Sequence) -> List[List[bytes]]:
@@ -107,6 +120,7 @@ class Router:
         self.node = _b(node)
         self._routes: Dict[bytes, List[object]] = {}
         self._snap: Optional[_Snapshot] = None
+        self._pending: List[Tuple[bytes, bool]] = []
         self._lock = threading.Lock()
 
     def _context(self) -> Context:
@@ -122,7 +136,8 @@ class Router:
             ds = self._routes.setdefault(t, [])
             if dest not in ds:
                 ds.append(dest)
-                self._snap = None
+                if len(ds) == 1:  # the filter enters the index with its first route
+                    self._pending.append((t, True))
 
     def delete_route(self, t, dest=None) -> None:
         """do_delete_route/2 (emqx_router.erl:164-172)."""
@@ -132,9 +147,9 @@ class Router:
             ds = self._routes.get(t)
             if ds and dest in ds:
                 ds.remove(dest)
-                if not ds:
+                if not ds:  # ... and leaves it with its last
                     del self._routes[t]
-                self._snap = None
+                    self._pending.append((t, False))
 
     def lookup_routes(self, t) -> List[Tuple[bytes, object]]:
         t = _b(t)
@@ -151,8 +166,9 @@ class Router:
 
     def snapshot(self) -> _Snapshot:
         with self._lock:
-            if self._snap is None:
-                self._snap = _Snapshot(self._context(), list(self._routes))
+            if self._snap is None or self._pending:
+                self._snap = _refresh(self._context(), self._snap, self._routes, self._pending)
+                self._pending = []
             return self._snap
 
     def match_filters_batch(self, topics: Sequence) -> Tuple[_Snapshot, np.ndarray, np.ndarray]:
@@ -174,6 +190,24 @@ class Router:
 
     def match_routes(self, t) -> List[Tuple[bytes, object]]:
         return self.match_routes_batch([t])[0]
+
+
+class SessionRouter(Router):
+    """emqx_session_router: the persistent-session routing table
+    (apps/emqx/src/emqx_session_router.erl:100-134).  The same algorithm over
+    a second trie (emqx_trie:insert_session/1, match_session/1,
+    emqx_trie.erl:110-112, 143-145), so it is a second index served by the same
+    kernels; a route's dest is a session id instead of a node."""
+
+    def __init__(self, ctx: Optional[Context] = None):
+        super().__init__(ctx, node=b"")
+
+    def add_route(self, t, session_id) -> None:
+        """do_add_route/2 (emqx_session_router.erl:100-118)."""
+        super().add_route(t, session_id)
+
+    def delete_route(self, t, session_id) -> None:
+        super().delete_route(t, session_id)
 
 
 class Broker:

@@ -126,6 +126,19 @@ int emqx_gm_synchronize(emqx_gm_ctx *ctx);
 int emqx_gm_index_build(emqx_gm_ctx *ctx, const uint8_t *filter_bytes, const uint64_t *filter_off,
                         uint64_t n_filters, const uint64_t *sub_off, const uint32_t *sub_ids,
                         uint32_t *perm_out, emqx_gm_index **out);
+/* Incremental maintenance (emqx_router:do_add_route/2 / do_delete_route/2 ->
+ * emqx_trie:insert/1, delete/1, apps/emqx/src/emqx_router.erl:112-125,
+ * 164-172, emqx_trie.erl:107-136).  Applies n_ops filter inserts (ops[i] = 1,
+ * idempotent) and deletes (ops[i] = 0, only if present), in order, to `prev`
+ * and returns a NEW snapshot; `prev` is unchanged (readers holding it keep
+ * it: RCU).  Small deltas share prev's device tables (tombstones + a delta
+ * index); past 1/8 of the base the set is rebuilt flat.  Ids in rows of the
+ * new snapshot are ranks in the updated set, as a full rebuild would give.
+ * Not available for shard indexes or indexes with subscriber lists
+ * (EMQX_GM_EUNSUPPORTED: rebuild those), and emqx_gm_fanout needs a flat
+ * snapshot. */
+int emqx_gm_index_update(emqx_gm_ctx *ctx, emqx_gm_index *prev, const uint8_t *filter_bytes,
+                         const uint64_t *filter_off, const uint8_t *ops, uint64_t n_ops, emqx_gm_index **out);
 int emqx_gm_index_retain(emqx_gm_index *idx);
 int emqx_gm_index_release(emqx_gm_index *idx);
 int emqx_gm_index_info(const emqx_gm_index *idx, emqx_gm_index_info_t *info);
