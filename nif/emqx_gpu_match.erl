@@ -8,7 +8,7 @@
 %% On {error, _} the wrapper falls back to emqx_trie:match/1 (SURVEY.md §8b).
 -module(emqx_gpu_match).
 
--export([load_index/1, match_batch/2, match_routes_batch/2, fanout_batch/2, empty/1]).
+-export([load_index/1, update_index/2, match_batch/2, match_routes_batch/2, fanout_batch/2, empty/1]).
 -export([match/2]).
 
 -on_load(init/0).
@@ -19,6 +19,11 @@ init() ->
 
 -spec load_index([binary()]) -> {ok, reference()} | {error, term()}.
 load_index(_Filters) -> erlang:nif_error(nif_not_loaded).
+
+%% Route changes (do_add_route/do_delete_route) as one batch -> a new snapshot;
+%% the old one stays valid for readers holding it (emqx_gm_index_update).
+-spec update_index(reference(), [{binary(), insert | delete}]) -> {ok, reference()} | {error, term()}.
+update_index(_Index, _Ops) -> erlang:nif_error(nif_not_loaded).
 
 -spec match_batch(reference(), [binary()]) -> [[binary()]] | {error, term()}.
 match_batch(_Index, _Topics) -> erlang:nif_error(nif_not_loaded).

@@ -26,7 +26,7 @@ typedef struct {
 
 static ErlNifResourceType *INDEX_RT;
 static emqx_gm_ctx *CTX;
-static ERL_NIF_TERM A_OK, A_ERROR, A_BADARG;
+static ERL_NIF_TERM A_OK, A_ERROR, A_BADARG, A_INSERT;
 
 static void index_dtor(ErlNifEnv *env, void *obj) {
   gm_index_res *r = (gm_index_res *)obj;
@@ -47,6 +47,7 @@ static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
   A_OK = enif_make_atom(env, "ok");
   A_ERROR = enif_make_atom(env, "error");
   A_BADARG = enif_make_atom(env, "badarg");
+  A_INSERT = enif_make_atom(env, "insert");
   return emqx_gm_open(&o, &CTX) == EMQX_GM_OK && INDEX_RT ? 0 : 1;
 }
 
@@ -88,21 +89,13 @@ static int pack_list(ErlNifEnv *env, ERL_NIF_TERM list, uint8_t **bytes, uint64_
   return 1;
 }
 
-/* load_index([Filter :: binary()]) -> {ok, Index} | {error, Reason} */
-static ERL_NIF_TERM load_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
-  uint8_t *fb;
-  uint64_t *fo, n, i;
-  emqx_gm_index *idx = NULL;
+/* Wrap an index snapshot in a resource that also owns the sorted filter
+ * bytes (result rows are sub-binaries of them). */
+static ERL_NIF_TERM make_index_term(ErlNifEnv *env, emqx_gm_index *idx) {
   emqx_gm_index_info_t info;
   gm_index_res *r;
   ERL_NIF_TERM term;
-  int rc;
-  (void)argc;
-  if (!pack_list(env, argv[0], &fb, &fo, &n)) return enif_make_badarg(env);
-  rc = emqx_gm_index_build(CTX, fb, fo, n, NULL, NULL, NULL, &idx);
-  enif_free(fb);
-  enif_free(fo);
-  if (rc != EMQX_GM_OK) return error_tuple(env, rc);
+  uint64_t i;
   emqx_gm_index_info(idx, &info);
   r = enif_alloc_resource(INDEX_RT, sizeof(*r));
   memset(r, 0, sizeof(*r));
@@ -126,6 +119,58 @@ static ERL_NIF_TERM load_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
   term = enif_make_resource(env, r);
   enif_release_resource(r);
   return enif_make_tuple2(env, A_OK, term);
+}
+
+/* load_index([Filter :: binary()]) -> {ok, Index} | {error, Reason} */
+static ERL_NIF_TERM load_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+  uint8_t *fb;
+  uint64_t *fo, n;
+  emqx_gm_index *idx = NULL;
+  int rc;
+  (void)argc;
+  if (!pack_list(env, argv[0], &fb, &fo, &n)) return enif_make_badarg(env);
+  rc = emqx_gm_index_build(CTX, fb, fo, n, NULL, NULL, NULL, &idx);
+  enif_free(fb);
+  enif_free(fo);
+  if (rc != EMQX_GM_OK) return error_tuple(env, rc);
+  return make_index_term(env, idx);
+}
+
+/* update_index(Index, [{Filter :: binary(), insert | delete}]) -> {ok, NewIndex} | {error, Reason}
+ * emqx_gm_index_update: a new snapshot; Index stays valid for its readers. */
+static ERL_NIF_TERM update_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_index_res *r;
+  unsigned len, i = 0;
+  ERL_NIF_TERM h, t = argv[1], fl = enif_make_list(env, 0);
+  uint8_t *fb, *ops;
+  uint64_t *fo, n;
+  emqx_gm_index *idx = NULL;
+  int rc;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], INDEX_RT, (void **)&r) || !enif_get_list_length(env, argv[1], &len))
+    return enif_make_badarg(env);
+  ops = enif_alloc(len + 1);
+  while (enif_get_list_cell(env, t, &h, &t)) {
+    const ERL_NIF_TERM *tup;
+    int arity;
+    if (!enif_get_tuple(env, h, &arity, &tup) || arity != 2) {
+      enif_free(ops);
+      return enif_make_badarg(env);
+    }
+    fl = enif_make_list_cell(env, tup[0], fl);
+    ops[i++] = enif_is_identical(tup[1], A_INSERT) ? 1 : 0;
+  }
+  /* fl was built by prepending: reverse it back to the ops' order */
+  if (!enif_make_reverse_list(env, fl, &fl) || !pack_list(env, fl, &fb, &fo, &n)) {
+    enif_free(ops);
+    return enif_make_badarg(env);
+  }
+  rc = emqx_gm_index_update(CTX, r->idx, fb, fo, ops, n, &idx);
+  enif_free(fb);
+  enif_free(fo);
+  enif_free(ops);
+  if (rc != EMQX_GM_OK) return error_tuple(env, rc);
+  return make_index_term(env, idx);
 }
 
 static ERL_NIF_TERM do_match(ErlNifEnv *env, const ERL_NIF_TERM argv[], uint32_t flags) {
@@ -213,6 +258,7 @@ static ERL_NIF_TERM empty(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
 
 static ErlNifFunc funcs[] = {
     {"load_index", 1, load_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"update_index", 2, update_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"match_batch", 2, match_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"match_routes_batch", 2, match_routes_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fanout_batch", 2, fanout_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
