@@ -587,6 +587,58 @@ struct LdsReader {
   }
 };
 
+// Word scan over LDS-staged text, 8 bytes per step (SWAR): the next '/' is the
+// lowest zero byte of (word ^ 0x2F..2F) at or after the start (an exact
+// per-byte test: the usual (y - 0x01..) & ~y trick borrows across bytes and
+// can flag a byte just above an earlier '/'); a word's 8-byte
+// chunks (from its own first byte, the last one zero padded -- the same
+// chunking as the byte reader, so the same hash) are funnel shifts of two
+// aligned LDS words.  Needs one staged word of slack past the text.
+__device__ __forceinline__ uint64_t funnel8(const uint64_t* lds, uint64_t wi, uint32_t sh) {
+  const uint64_t a = lds[wi];
+  return sh ? (a >> sh) | (lds[wi + 1] << (64 - sh)) : a;
+}
+
+__device__ __forceinline__ WordTok next_word(LdsReader& rd, uint64_t& pos, uint64_t end) {
+  constexpr uint64_t SL = 0x2F2F2F2F2F2F2F2Full, M7 = 0x7F7F7F7F7F7F7F7Full;
+  // exact per-byte zero test (no borrow between bytes): bit 7 of a byte of
+  // zbytes(y) is set iff that byte of y is 0
+  auto zbytes = [](uint64_t y) { return ~(((y & M7) + M7) | y | M7); };
+  WordTok w;
+  w.start = pos;
+  const uint64_t rel = pos - rd.lo;
+  const uint64_t w0 = rel >> 3;
+  const uint32_t sh = uint32_t(rel & 7) * 8;
+  // find the end of the word
+  uint64_t wi = w0, e = end;
+  uint64_t z = zbytes(rd.lds[wi] ^ SL) & (~0ull << sh);  // bytes before pos do not count
+  for (;;) {
+    if (z) {
+      const uint64_t at = rd.lo + wi * 8 + (__builtin_ctzll(z) >> 3);
+      e = at < end ? at : end;
+      break;
+    }
+    if (rd.lo + (wi + 1) * 8 >= end) break;
+    ++wi;
+    z = zbytes(rd.lds[wi] ^ SL);
+  }
+  const uint32_t len = uint32_t(e - pos);
+  uint64_t h = HASH_SEED;
+  uint64_t head = 0;
+  for (uint32_t k = 0; k < len; k += 8) {
+    uint64_t c = funnel8(rd.lds, w0 + (k >> 3), sh);
+    if (len - k < 8) c &= (1ull << ((len - k) * 8)) - 1;
+    if (k == 0) head = c;
+    h = hash_step(h, c);
+  }
+  w.h = hash_final(h, len);
+  w.head = head;
+  w.len = len;
+  w.b0 = uint32_t(head & 0xFF);
+  pos = e;
+  return w;
+}
+
 // One topic: words -> dictionary ids, the next word's first dictionary slot
 // loaded while this word resolves.
 template <class RD>
@@ -629,14 +681,14 @@ constexpr int TOK_STAGE = 16384;
 __global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ toff,
                                                   uint64_t n, IndexView ix, uint32_t* __restrict__ hdr,
                                                   uint32_t* __restrict__ wids) {
-  __shared__ uint64_t s_txt[TOK_STAGE / 8];
+  __shared__ uint64_t s_txt[TOK_STAGE / 8 + 1];  // + one word of slack for the funnel shifts
   const uint64_t t0 = uint64_t(blockIdx.x) * 256u;
   const uint64_t t = t0 + threadIdx.x;
   const uint64_t tl = t0 + 256 < n ? t0 + 256 : n;
   const uint64_t lo = toff[t0] & ~7ull, hi = toff[tl];
   const bool staged = hi - lo <= uint64_t(TOK_STAGE) - 8;  // block-uniform
   if (staged) {
-    const uint64_t nw = (hi - lo + 7) >> 3;
+    const uint64_t nw = ((hi - lo + 7) >> 3) + 1;  // topic buffers are padded by 64 bytes
     for (uint64_t i = threadIdx.x; i < nw; i += 256) s_txt[i] = *reinterpret_cast<const uint64_t*>(tb + lo + 8 * i);
   }
   __syncthreads();

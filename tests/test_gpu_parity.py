@@ -300,3 +300,27 @@ def test_hot_fanout_c4_small(ctx, orc):
     ero, eids = orc.fanout(ro, ids, so, si)
     assert np.array_equal(fro, ero) and np.array_equal(fids, eids)
     idx.release()
+
+
+def test_tokenizer_alignments_and_bytes(ctx, orc):
+    """Words of every length 0..19 at every byte alignment, with bytes next to
+    '/' in value ('.', '0', 0x2E, 0x30, NUL, 0xFF) right after separators: the
+    staged 8-byte (SWAR) word scan must cut and hash exactly like the oracle."""
+    rng = random.Random(17)
+    alphabet = [b".", b"0", b"a", b"\x00", b"\xff", b"\x2e", b"\x30", b"z"]
+    words = [b"".join(rng.choice(alphabet) for _ in range(k)) for k in range(20) for _ in range(3)]
+    filters = set()
+    for w in words:
+        filters.add(w + b"/+")
+        filters.add(b"+/" + w)
+        filters.add(w + b"/#")
+        filters.add(w)
+    topics = []
+    for pad in range(9):  # shift the topic start through all 8-byte alignments
+        for _ in range(40):
+            a, b = rng.choice(words), rng.choice(words)
+            topics.append(b"p" * pad + b"/" + a + b"/" + b)
+            topics.append(a + b"/" + b)
+            topics.append(a)
+    _check(ctx, orc, sorted(filters), topics, True)
+    _check(ctx, orc, sorted(filters), topics, False)
