@@ -61,15 +61,21 @@ struct alignas(16) EdgeSlot {
   uint32_t pad;
 };
 
-// ---- hot tables (read by k_match_fast only) --------------------------------
+// ---- hot tables (read by the walk kernels) --------------------------------
 // One open-addressing table per node depth (1..HOT_TABLES-2 each their own,
-// deeper nodes share the last).  A node reached through an exact or '+' edge
-// owns exactly one 32-B slot, keyed by (parent's slot index, word id), and its
-// id IS that slot index.  The slot carries the node's whole record, so visiting
-// a node costs one line fetch (edge probe and node read in one).  '#' edges
-// have no slot: their filter is the parent's hash_filter ('match_#').
+// deeper nodes share the last).  A node reached through an exact edge, or
+// through a '+' edge from the root or from an inline node, owns exactly one
+// 32-B slot, keyed by (parent's hot id, word id); its hot id IS that slot
+// index.  The '+' child of a slot-owning node owns no slot: its record sits in
+// the second half of its parent's slot (p_sig, p_hf, p_end) and its hot id is
+// the parent's slot index | HOT_INLINE.  So a frontier entry's '+' expansion
+// re-reads a line the walk fetched one level earlier (an L2 hit) instead of
+// probing a new random line.  '#' edges have no node at all: their filter is
+// the parent's hf ('match_#').
 constexpr int HOT_TABLES = 16;
 constexpr uint32_t ID_MASK = 0x7FFFFFFFu;
+constexpr uint32_t HOT_INLINE = 0x40000000u;  // in a hot id: the '+' child held inline by slot (id & SLOT_MASK)
+constexpr uint32_t SLOT_MASK = 0x3FFFFFFFu;
 constexpr uint32_t END_WILD = 0x80000000u;  // in end_filter: the filter is a wildcard one
 constexpr uint32_t HOT_PLUS = 0x80000000u;  // in HotSlot::hf: the node has a '+' child
 constexpr uint32_t HF_NONE = 0x7FFFFFFFu;   // HotSlot::hf without a '#' filter
@@ -81,10 +87,14 @@ struct alignas(32) HotSlot {
   uint32_t sig;          // bit sig_bit(w) set for each exact child word id w; 0 = no exact child
   uint32_t hf;           // filter id of "<node>/#" (HF_NONE if none) | HOT_PLUS if the node has a '+' child
   uint32_t end_filter;   // filter id ending at the node | END_WILD, or NONE
-  uint32_t pad[3];       // 32-B stride: slots never straddle a 64-B line
+  uint32_t p_sig;        // the inline '+' child's sig, hf and end_filter (same encodings)
+  uint32_t p_hf;
+  uint32_t p_end;
 };
-// The first 16 bytes {key, sig, hf} are all a walk needs below the topic's
-// last level (one dwordx4 per probe); end_filter is read on the last level.
+// The first 16 bytes {key, sig, hf} are all a probe needs below the topic's
+// last level (one dwordx4); end_filter is read on the last level, and the
+// second 16 bytes {end_filter, p_sig, p_hf, p_end} (one dwordx4) are the
+// inline '+' child's record.
 // Read-only view of one index resident in HBM (passed by value to kernels).
 struct IndexView {
   const Node* nodes;

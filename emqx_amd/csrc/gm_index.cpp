@@ -298,9 +298,11 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     std::vector<EdgeSlot>().swap(tabs[d].slots);
   }
 
-  // ---- 3b. hot tables: one 32-B slot per node reached through an exact or '+'
-  // edge, slot index = the node's hot id; built depth by depth because a key
-  // holds the parent's hot id.
+  // ---- 3b. hot tables: one 32-B slot per node reached through an exact edge
+  // (or a '+' edge from the root or from an inline node), slot index = the
+  // node's hot id; the '+' child of a slot-owning node is inline in its
+  // parent's slot (gm_common.h).  Built depth by depth because a key holds the
+  // parent's hot id.
   std::vector<uint32_t> by_depth_off(max_depth + 2, 0);  // old nodes bucketed by depth
   for (uint64_t i = 1; i < NN; ++i) by_depth_off[nodes[i].depth + 1]++;
   for (size_t d = 1; d < by_depth_off.size(); ++d) by_depth_off[d] += by_depth_off[d - 1];
@@ -309,22 +311,32 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     std::vector<uint32_t> cur(by_depth_off.begin(), by_depth_off.end() - 1);
     for (uint64_t i = 1; i < NN; ++i) by_depth[cur[nodes[i].depth]++] = uint32_t(i);
   }
+  // a parent is always created before its child, so one pass in index order
+  std::vector<uint8_t> inl(NN, 0);
+  for (uint64_t i = 1; i < NN; ++i) {
+    const HNode& h = nodes[i];
+    inl[i] = h.kind == 1 && h.parent != 0 && nodes[h.parent].kind != 2 && !inl[h.parent];
+  }
   uint64_t hot_n[HOT_TABLES] = {0};
   for (uint64_t i = 1; i < NN; ++i)
-    if (nodes[i].kind != 2) hot_n[hot_table(nodes[i].depth)]++;
+    if (nodes[i].kind != 2 && !inl[i]) hot_n[hot_table(nodes[i].depth)]++;
   uint64_t hot_off[HOT_TABLES], hot_cap[HOT_TABLES], hot_total = 0;
   for (int t = 0; t < HOT_TABLES; ++t) {
     // load <= ~0.55; at least 8 slots so the probe loop always finds an empty one
     hot_cap[t] = hot_n[t] ? std::max<uint64_t>(8, (hot_n[t] * 20 + 10) / 11 + 1) : 0;
+    if (hot_cap[t] > SLOT_MASK) throw std::length_error("hot table exceeds 2^30 slots");
     hot_off[t] = hot_total;
     hot_total += hot_cap[t];
   }
-  std::vector<HotSlot> hot(hot_total, HotSlot{EDGE_EMPTY, 0, HF_NONE, NONE, {0, 0, 0}});
+  std::vector<HotSlot> hot(hot_total, HotSlot{EDGE_EMPTY, 0, HF_NONE, NONE, 0, HF_NONE, NONE});
   std::vector<uint32_t> hid(NN, NONE);
   hid[0] = 0;  // the root (depth 0) is not stored; its record goes to IndexView
   auto end_of = [&](const HNode& h) -> uint32_t {
     if (h.end_filter == NONE) return NONE;
     return h.end_filter | ((h.flags & NF_END_WILD) ? END_WILD : 0u);
+  };
+  auto hf_of = [&](const HNode& h) -> uint32_t {
+    return (h.hash_child == NONE ? HF_NONE : nodes[h.hash_child].end_filter) | (h.plus_child != NONE ? HOT_PLUS : 0u);
   };
   for (uint32_t d = 1; d <= max_depth; ++d) {
     const int t = hot_table(d);
@@ -334,15 +346,21 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       const uint32_t i = by_depth[k];
       const HNode& h = nodes[i];
       if (h.kind == 2 || hid[h.parent] == NONE) continue;  // '#' nodes and their (unmatchable) subtrees
+      if (inl[i]) {  // into the parent's slot (table of depth d-1)
+        HotSlot& p = hot[hot_off[hot_table(d - 1)] + hid[h.parent]];
+        p.p_sig = h.sig;
+        p.p_hf = hf_of(h);
+        p.p_end = end_of(h);
+        hid[i] = hid[h.parent] | HOT_INLINE;
+        continue;
+      }
       const uint64_t key = hot_key(hid[h.parent], h.word, d - 1);
       uint64_t s = hot_slot(key, cap);
       while (tab[s].key != EDGE_EMPTY) s = s + 1 == cap ? 0 : s + 1;
-      if (s >= 0x7FFFFFFFull) throw std::length_error("hot table exceeds 2^31 slots");
       HotSlot& o = tab[s];
       o.key = key;
       o.sig = h.sig;
-      o.hf = (h.hash_child == NONE ? HF_NONE : nodes[h.hash_child].end_filter) |
-             (h.plus_child != NONE ? HOT_PLUS : 0u);
+      o.hf = hf_of(h);
       o.end_filter = end_of(h);
       hid[i] = uint32_t(s);
     }

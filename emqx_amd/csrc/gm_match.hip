@@ -249,183 +249,54 @@ __device__ __forceinline__ uint32_t hot_resolve(const HotSlot* tab, uint32_t cap
     }                                                        \
   } while (0)
 
-// ---- k_match_reg ----------------------------------------------------------
-// Frontier: at most RFC entries {hot id | FR_PLUS, exact-child signature} in
-// registers (pushes are select chains over static indices, so nothing spills
-// to scratch).  PAIR: entries are expanded two at a time, so up to four slot
-// loads per lane are in flight before the first is consumed.  A lane whose
-// frontier outgrows RFC, or whose row outgrows FAST_MC, is queued for the
-// listed LDS pass and contributes nothing here.
+// ---- probes shared by the walk kernels -------------------------------------
+// Frontier (k_walk): at most RFC entries {hot id | FR_PLUS, exact-child
+// signature} in registers (pushes are select chains over static indices, so
+// nothing spills to scratch).  A lane whose frontier outgrows RFC, or whose row
+// outgrows FAST_MC, is queued for the listed LDS pass and contributes nothing
+// in the main pass.
 constexpr int RFC = 4;
 
-#define GM_PUSH(idv, sigv)                                \
-  do {                                                    \
-    const uint32_t pid_ = (idv), psig_ = (sigv);          \
-    _Pragma("unroll") for (int q_ = 0; q_ < RFC; ++q_) {  \
-      if (nn == uint32_t(q_)) {                           \
-        nid[q_] = pid_;                                   \
-        nsig[q_] = psig_;                                 \
-      }                                                   \
-    }                                                     \
-    ++nn;                                                 \
-  } while (0)
+// The record of the '+' child held inline by slot `id` of its parent's table
+// (gm_common.h): the slot's second 16 bytes, a line this walk read one level
+// earlier when it visited the parent.
+__device__ __forceinline__ HotRec plus_inline_load(const HotSlot* ptab, uint32_t id) {
+  const uint4 q = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(ptab + (id & SLOT_MASK)) + 4);
+  HotRec r;
+  r.a = make_uint4(0u, 0u, q.y, q.z);
+  r.ef = q.w;
+  return r;
+}
+// Whether the '+' child of frontier entry `id` (a node at depth lvl) is inline.
+__device__ __forceinline__ bool plus_is_inline(uint32_t lvl, uint32_t id) { return lvl != 0 && !(id & HOT_INLINE); }
 
 // Issue (load the home slot of) / take (resolve and visit) one probe of a
-// frontier entry: the exact edge (word wid) or the '+' edge.
+// frontier entry: the exact edge (word wid) or the '+' edge.  An inline '+'
+// child is "issued" as the re-read of its parent's slot (sx = NONE).
 #define GM_PROBE_ISSUE(c, e_id, plus, sx, rx)                                           \
   do {                                                                                  \
     if (c) {                                                                            \
-      sx = uint32_t(hot_slot(hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), cap));  \
-      rx = hot_load(tab, sx, last);                                                           \
+      if ((plus) && plus_is_inline(lvl, (e_id))) {                                      \
+        sx = NONE;                                                                      \
+        rx = plus_inline_load(ptab, (e_id));                                            \
+      } else {                                                                          \
+        sx = uint32_t(hot_slot(hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), cap)); \
+        rx = hot_load(tab, sx, last);                                                   \
+      }                                                                                 \
     }                                                                                   \
   } while (0)
 
 #define GM_PROBE_TAKE(c, e_id, plus, sx, rx)                                                              \
   do {                                                                                                    \
     if (c) {                                                                                              \
-      const uint32_t hs_ = hot_resolve(tab, capu, hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), sx, rx, last); \
-      if (hs_ != NONE) GM_VISIT(hs_, rx);                                                                 \
+      if ((plus) && sx == NONE) {                                                                         \
+        GM_VISIT((e_id) | HOT_INLINE, rx);                                                                \
+      } else {                                                                                            \
+        const uint32_t hs_ = hot_resolve(tab, capu, hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), sx, rx, last); \
+        if (hs_ != NONE) GM_VISIT(hs_, rx);                                                               \
+      }                                                                                                   \
     }                                                                                                     \
   } while (0)
-
-// MINW: waves per SIMD the register budget is sized for (__launch_bounds__'s
-// second argument; 1 leaves the allocation to the compiler).
-template <bool EXACT, bool PAIR, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_match_reg(const uint8_t* __restrict__ tb,
-                                                   const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
-                                                   uint32_t* __restrict__ cnt, uint32_t* __restrict__ stage,
-                                                   uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
-                                                   unsigned long long* __restrict__ probe_tile,
-                                                   unsigned long long* __restrict__ wild_ctr) {
-  constexpr int MC = FAST_MC;
-  const int lane = threadIdx.x & 63;
-  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
-  const uint64_t tile = t >> 6;
-  const bool valid = t < n;
-  uint32_t* const srow = stage + stage_index(tile, 0, lane);
-  uint32_t m_n = 0, probes = 0;
-  bool ovf = false, wild = false;
-
-  if (valid) {
-    uint64_t pos = toff[t];
-    const uint64_t end = toff[t + 1];
-    const uint64_t start = pos;
-    ByteReader rd{tb, ~0ull, 0};
-    WordTok w = next_word(rd, pos, end);
-    DictSlot d0 = dict_first(ix, w);
-    // '$'-topics skip the root-level '+' and '#' (emqx_trie.erl:271-278)
-    const bool dollar = w.len > 0 && w.b0 == '$';
-    if (!dollar && ix.root_hash != NONE) GM_EMIT(ix.root_hash);  // '#' at the virtual root
-    uint32_t fid[RFC], fsig[RFC];
-#pragma unroll
-    for (int q = 0; q < RFC; ++q) fid[q] = fsig[q] = 0;
-    fid[0] = (!dollar && (ix.root_flags & HOT_PLUS)) ? FR_PLUS : 0u;
-    fsig[0] = ix.root_sig;
-    uint32_t cur_n = 1, nfinal = 0, level = 0;
-    for (;;) {
-      const bool last = pos >= end;
-      if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {
-        wild = true;  // emqx_topic:wildcard/1
-        break;
-      }
-      const uint32_t wid = cur_n ? dict_resolve(ix, w, d0, tb) : NONE;
-      const uint32_t wbit = sig_bit(wid);
-      // prefetch the next level's word while this level's frontier expands
-      WordTok wn;
-      DictSlot dn;
-      if (!last) {
-        ++pos;
-        wn = next_word(rd, pos, end);
-        dn = dict_first(ix, wn);
-      }
-      if (cur_n) {
-        probes += 3 * cur_n;
-        uint32_t nid[RFC], nsig[RFC], nn = 0;
-#pragma unroll
-        for (int q = 0; q < RFC; ++q) nid[q] = nsig[q] = 0;
-        const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);  // wave-uniform
-        const int ht = hot_table(lvl + 1);
-        const HotSlot* tab = ix.hot + ix.hot_off[ht];
-        const uint64_t cap = ix.hot_cap[ht];
-        const uint32_t capu = uint32_t(cap);
-        const bool wok = wid != NONE;
-        if (PAIR) {
-#pragma unroll
-          for (int i = 0; i < RFC; i += 2) {
-            if (uint32_t(i) < cur_n) {
-              const bool hb = uint32_t(i + 1) < cur_n;
-              const uint32_t ia = fid[i] & ID_MASK, ib = fid[i + 1] & ID_MASK;
-              const bool ax = wok && (fsig[i] & wbit), ap = (fid[i] & FR_PLUS) != 0;
-              const bool bx = hb && wok && (fsig[i + 1] & wbit), bp = hb && (fid[i + 1] & FR_PLUS) != 0;
-              uint32_t sax = 0, sap = 0, sbx = 0, sbp = 0;
-              HotRec rax{}, rap{}, rbx{}, rbp{};
-              // issue every load of the pair before consuming any
-              GM_PROBE_ISSUE(ax, ia, false, sax, rax);
-              GM_PROBE_ISSUE(ap, ia, true, sap, rap);
-              GM_PROBE_ISSUE(bx, ib, false, sbx, rbx);
-              GM_PROBE_ISSUE(bp, ib, true, sbp, rbp);
-              GM_PROBE_TAKE(ax, ia, false, sax, rax);
-              GM_PROBE_TAKE(ap, ia, true, sap, rap);
-              GM_PROBE_TAKE(bx, ib, false, sbx, rbx);
-              GM_PROBE_TAKE(bp, ib, true, sbp, rbp);
-            }
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < RFC; ++i) {
-            if (uint32_t(i) < cur_n) {
-              const uint32_t ia = fid[i] & ID_MASK;
-              const bool ax = wok && (fsig[i] & wbit), ap = (fid[i] & FR_PLUS) != 0;
-              uint32_t sax = 0, sap = 0;
-              HotRec rax{}, rap{};
-              GM_PROBE_ISSUE(ax, ia, false, sax, rax);
-              GM_PROBE_ISSUE(ap, ia, true, sap, rap);
-              GM_PROBE_TAKE(ax, ia, false, sax, rax);
-              GM_PROBE_TAKE(ap, ia, true, sap, rap);
-            }
-          }
-        }
-        if (nn > RFC) {
-          ovf = true;
-          break;
-        }
-#pragma unroll
-        for (int q = 0; q < RFC; ++q) {
-          fid[q] = nid[q];
-          fsig[q] = nsig[q];
-        }
-        cur_n = nn;
-      }
-      if (last) break;
-      w = wn;
-      d0 = dn;
-      ++level;
-    }
-    if (wild) {
-      GM_WILD_ROW();
-    } else if (!ovf) {
-      probes += 2 * nfinal + 1;
-      if (m_n > MC) ovf = true;
-    }
-    if (ovf) probes = 0;  // the listed pass walks this topic again and counts it
-  }
-
-  if (valid) {
-    cnt[t] = ovf ? OVF_BIT : m_n;
-    if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
-  }
-  // per-wave probe count: a plain store into the tile's slot (summed by
-  // k_sum_tiles); one atomic per wave on a single address would serialise
-  // every wave of the launch at the L2.
-  uint32_t ptot;
-  wave_excl_scan(probes, ptot);
-  const unsigned long long wb = __ballot(valid && wild);
-  if (lane == 0) {
-    if (tile * 64 < n) probe_tile[tile] = ptot;  // waves wholly past n have no slot
-    if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
-  }
-}
-#undef GM_PUSH
 
 // ---- k_match_lds ----------------------------------------------------------
 // Frontier entries double buffered in LDS, FC per lane.  LISTED: grid-stride
@@ -495,6 +366,7 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
         const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);  // wave-uniform
         const int ht = hot_table(lvl + 1);
         const HotSlot* tab = ix.hot + ix.hot_off[ht];
+        const HotSlot* ptab = ix.hot + ix.hot_off[hot_table(lvl)];  // the frontier nodes' own table
         const uint64_t cap = ix.hot_cap[ht];
         const uint32_t capu = uint32_t(cap);
         for (uint32_t i = 0; i < cur_n; ++i) {
@@ -504,22 +376,10 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
           const bool dp = (e.x & FR_PLUS) != 0;
           uint32_t sx = 0, sp = 0;
           HotRec rx{}, rp{};
-          if (dx) {
-            sx = uint32_t(hot_slot(hot_key(id, wid, lvl), cap));
-            rx = hot_load(tab, sx, last);
-          }
-          if (dp) {
-            sp = uint32_t(hot_slot(hot_key(id, ix.plus_word, lvl), cap));
-            rp = hot_load(tab, sp, last);
-          }
-          if (dx) {
-            const uint32_t hs = hot_resolve(tab, capu, hot_key(id, wid, lvl), sx, rx, last);
-            if (hs != NONE) GM_VISIT(hs, rx);
-          }
-          if (dp) {
-            const uint32_t hs = hot_resolve(tab, capu, hot_key(id, ix.plus_word, lvl), sp, rp, last);
-            if (hs != NONE) GM_VISIT(hs, rp);
-          }
+          GM_PROBE_ISSUE(dx, id, false, sx, rx);
+          GM_PROBE_ISSUE(dp, id, true, sp, rp);
+          GM_PROBE_TAKE(dx, id, false, sx, rx);
+          GM_PROBE_TAKE(dp, id, true, sp, rp);
         }
         if (nn > FC) {
           ovf = true;
@@ -768,6 +628,7 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
         const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);  // wave-uniform
         const int ht = hot_table(lvl + 1);
         const HotSlot* tab = ix.hot + ix.hot_off[ht];
+        const HotSlot* ptab = ix.hot + ix.hot_off[hot_table(lvl)];  // the frontier nodes' own table
         const uint64_t cap = ix.hot_cap[ht];
         const uint32_t capu = uint32_t(cap);
         const bool wok = wid != NONE;
@@ -1378,19 +1239,15 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
-// Main-pass kernel selection.  GM_MATCH_MAIN (A/B knob, read once):
-// split[w8] (k_tokenize + k_walk, default), reg{1,2}[w6|w8] (register frontier, one entry / pairs per step, register
-// budget for 6 / 8 waves per SIMD), lds4, lds8 (LDS frontier).
-enum MainKind {
-  MAIN_SPLIT, MAIN_SPLITW8, MAIN_SPLIT2, MAIN_REG1, MAIN_REG1W6, MAIN_REG1W8, MAIN_REG2, MAIN_REG2W6, MAIN_REG2W8, MAIN_LDS4,
-  MAIN_LDS8
-};
+// Main-pass kernel selection.  GM_MATCH_MAIN (A/B knob, read once): split
+// (k_tokenize + k_walk, default), splitw8 (register budget for 8 waves per
+// SIMD), split2 (frontier entries expanded in pairs).
+enum MainKind { MAIN_SPLIT, MAIN_SPLITW8, MAIN_SPLIT2 };
 MainKind main_kind() {
   static const MainKind k = [] {
     const char* e = getenv("GM_MATCH_MAIN");
     static const struct { const char* name; MainKind kind; } names[] = {
-        {"split", MAIN_SPLIT}, {"splitw8", MAIN_SPLITW8}, {"split2", MAIN_SPLIT2}, {"reg1", MAIN_REG1}, {"reg1w6", MAIN_REG1W6}, {"reg1w8", MAIN_REG1W8}, {"reg2", MAIN_REG2},
-        {"reg2w6", MAIN_REG2W6}, {"reg2w8", MAIN_REG2W8}, {"lds4", MAIN_LDS4}, {"lds8", MAIN_LDS8}};
+        {"split", MAIN_SPLIT}, {"splitw8", MAIN_SPLITW8}, {"split2", MAIN_SPLIT2}};
     if (e)
       for (const auto& nk : names)
         if (!strcmp(e, nk.name)) return nk.kind;
@@ -1411,33 +1268,16 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
                   unsigned long long* probe_tile, hipEvent_t after_main) {
   hipStream_t st = ctx->stream;
   const uint64_t nblk = (n + 255) / 256;
-#define GM_LAUNCH_REG(P, W)                                                                                  \
-  hipLaunchKernelGGL((k_match_reg<EXACT, P, W>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, list1, n1, \
-                     probe_tile, wild_ctr)
-#define GM_LAUNCH_LDS(F)                                                                                     \
-  hipLaunchKernelGGL((k_match_lds<EXACT, F, false>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, \
-                     nullptr, nullptr, list1, n1, probe_tile, wild_ctr)
 #define GM_LAUNCH_SPLIT(W, P)                                                                                     \
   hipLaunchKernelGGL(k_tokenize, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids);                         \
   hipLaunchKernelGGL((k_walk<EXACT, W, P>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, cnt, stage, list1, \
                      n1, probe_tile, wild_ctr)
   switch (main_kind()) {
-    case MAIN_SPLIT: GM_LAUNCH_SPLIT(1, false); break;
     case MAIN_SPLITW8: GM_LAUNCH_SPLIT(8, false); break;
     case MAIN_SPLIT2: GM_LAUNCH_SPLIT(1, true); break;
-    case MAIN_REG1: GM_LAUNCH_REG(false, 1); break;
-    case MAIN_REG1W8: GM_LAUNCH_REG(false, 8); break;
-    case MAIN_REG1W6: GM_LAUNCH_REG(false, 6); break;
-    case MAIN_REG2: GM_LAUNCH_REG(true, 1); break;
-    case MAIN_REG2W6: GM_LAUNCH_REG(true, 6); break;
-    case MAIN_REG2W8: GM_LAUNCH_REG(true, 8); break;
-    case MAIN_LDS4: GM_LAUNCH_LDS(4); break;
-    case MAIN_LDS8: GM_LAUNCH_LDS(8); break;
-    default: GM_LAUNCH_REG(false, 6);
+    default: GM_LAUNCH_SPLIT(1, false);
   }
 #undef GM_LAUNCH_SPLIT
-#undef GM_LAUNCH_REG
-#undef GM_LAUNCH_LDS
   hipEventRecord(after_main, st);
   hipLaunchKernelGGL(k_sum_tiles, dim3(256), dim3(256), 0, st, probe_tile, (n + 63) / 64, probe_ctr);
   const uint64_t lblk = std::min<uint64_t>(nblk, 512);

@@ -9,7 +9,7 @@ if [ -z "${SKIP_TESTS:-}" ]; then
   timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_pytest.log 2>&1
   rc=$?; tail -n 15 gpurun_out/ab_pytest.log; [ $rc -ne 0 ] && exit $rc
 fi
-for v in ${VARIANTS:-reg1w6 reg1 lds8}; do
+for v in ${VARIANTS:-split splitw8 split2}; do
   GM_MATCH_MAIN=$v timeout -k 10 240 python -u bench.py --steps 5 --warmup 2 --no-cpu > gpurun_out/ab_$v.log 2>&1
   rc=$?; echo "MAIN=$v rc=$rc"; tail -n 1 gpurun_out/ab_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value']/1e9, 'Gtopics/s kernel_ms', d['roofline']['kernel_ms'], 'listed', d['detail']['overflow_rows'])" || tail -n 5 gpurun_out/ab_$v.log
   [ $rc -ne 0 ] && exit $rc
