@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libemqx_gpu_match.so")
+LIB_PATH = os.environ.get("EMQX_GM_LIB") or os.path.join(_HERE, "libemqx_gpu_match.so")
 
 OK, EINVAL, ENOMEM, EDEVICE, EOVERFLOW, EUNSUPPORTED = 0, -1, -2, -3, -4, -5
 WITH_EXACT = 0x1

@@ -96,6 +96,7 @@ struct alignas(32) HotSlot {
 // second 16 bytes {end_filter, p_sig, p_hf, p_end} (one dwordx4) are the
 // inline '+' child's record.
 // Read-only view of one index resident in HBM (passed by value to kernels).
+constexpr uint32_t IX_HOT_FLAT = 1u;  // a hot table reaches 2 GiB: flat loads instead of buffer loads
 struct IndexView {
   const Node* nodes;
   const DictSlot* dict;
@@ -117,7 +118,7 @@ struct IndexView {
   uint32_t root_sig;    // the root's exact-child signature
   uint32_t root_hash;   // filter id of "#", or NONE
   uint32_t root_flags;  // HOT_PLUS if "+" starts a filter
-  uint32_t pad;
+  uint32_t flags;       // IX_* below
 };
 
 GM_HD uint64_t fmix64(uint64_t k) {

@@ -11,6 +11,7 @@
 // Layout (gm_common.h): nodes are numbered breadth-first so the hot upper
 // levels of the trie are contiguous in HBM and stay resident in L2/MALL.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string_view>
@@ -475,6 +476,10 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.root_sig = nodes[0].sig;
   v.root_hash = nodes[0].hash_child == NONE ? NONE : nodes[nodes[0].hash_child].end_filter;
   v.root_flags = nodes[0].plus_child != NONE ? HOT_PLUS : 0u;
+  v.flags = 0;
+  for (int t = 0; t < HOT_TABLES; ++t)
+    if (hot_cap[t] * sizeof(HotSlot) >= (1ull << 31)) v.flags |= IX_HOT_FLAT;
+  if (getenv("GM_HOT_FLAT")) v.flags |= IX_HOT_FLAT;  // test knob: exercise the flat-load path
   v.n_nodes = uint32_t(NN);
   v.n_filters = nf;
   v.plus_word = plus_word;

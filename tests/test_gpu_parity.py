@@ -203,15 +203,21 @@ def test_device_topic_generator_matches_oracle(ctx, orc):
     ctx.dev_free(do)
 
 
-@pytest.mark.parametrize("wild_only", [False, True], ids=["C1-mix", "C2-wildcard"])
-def test_config_subsample_vs_oracle(ctx, orc, wild_only):
+@pytest.mark.parametrize("wild_only,flat", [(False, False), (True, False), (True, True)],
+                         ids=["C1-mix", "C2-wildcard", "C2-wildcard-flat-loads"])
+def test_config_subsample_vs_oracle(ctx, orc, wild_only, flat, monkeypatch):
     """C1 (10k mixed filters) and C2-shaped (wildcard-only) filter sets, 200k
-    seeded topics generated on the device, every row vs the oracle."""
+    seeded topics generated on the device, every row vs the oracle.  flat: the
+    index is built with GM_HOT_FLAT, so the walk uses the flat-load path that
+    an index with a >= 2 GiB hot table takes instead of buffer loads."""
     from emqx_amd.engine import gen_filter_codes, render_codes
     codes = gen_filter_codes(1, 10_000 if not wild_only else 50_000, wildcard_only=wild_only)
     fb, fo = render_codes(codes)
     filters = sorted(set(orc.unpack(fb, fo)))
+    if flat:
+        monkeypatch.setenv("GM_HOT_FLAT", "1")
     idx = ctx.build_index(filters)
+    monkeypatch.delenv("GM_HOT_FLAT", raising=False)
     n = 200_000
     db, do, tot = ctx.gen_topics_device(codes, 1, 0, n)
     res = ctx.match_device(idx, db, do, n, exact=True)
