@@ -111,6 +111,9 @@ struct IndexView {
   uint64_t etab_mask[EDGE_DEPTHS];  // slots - 1
   uint64_t hot_off[HOT_TABLES];     // slot offset of each hot table (index = child depth, capped)
   uint64_t hot_cap[HOT_TABLES];     // slots of each hot table
+  const uint32_t* efilt;            // exact-edge filters (see edge_filter_hash), one bit array per hot table
+  uint64_t efilt_off[HOT_TABLES];   // u32-word offset of each table's filter
+  uint32_t efilt_mask[HOT_TABLES];  // words - 1 of each table's filter; 0 = no filter for that table
   uint32_t n_nodes;
   uint32_t n_filters;
   uint32_t plus_word;   // word id of "+" (NONE if no filter uses it)
@@ -199,5 +202,17 @@ GM_HD uint64_t hot_slot(uint64_t key, uint64_t cap) {
   return (uint64_t(h) * cap) >> 32;
 #endif
 }
+
+// Exact-edge filter: for a hot table whose parents have many exact children
+// (so the 32-bit HotSlot::sig passes most probes that then miss), one bit
+// array over the (parent hot id, word id) keys of its exact children, two
+// bits per key in one 32-bit word (16-32 bits per key, ~1-2 % false
+// positives).  It is small enough to stay in L2, so a probe it rules out
+// costs an L2 hit instead of a random line from HBM / Infinity Cache.
+GM_HD uint32_t edge_filter_hash(uint32_t parent, uint32_t word) {
+  return fmix32((parent * 0x27D4EB2Fu) ^ (word * 0x165667B1u) ^ 0x5BD1E995u);
+}
+GM_HD uint32_t edge_filter_bits(uint32_t h) { return (1u << (h & 31)) | (1u << ((h >> 5) & 31)); }
+GM_HD uint32_t edge_filter_word(uint32_t h, uint32_t mask) { return (h >> 10) & mask; }
 
 }  // namespace gm

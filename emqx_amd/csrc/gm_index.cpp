@@ -367,6 +367,37 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     }
   }
 
+  // ---- 3c. exact-edge filters (gm_common.h), for tables whose parents have
+  // on average >= 4 exact children and whose filter fits 4 MB
+  std::vector<uint64_t> ex_edges(HOT_TABLES, 0), ex_parents(HOT_TABLES, 0);
+  for (uint64_t i = 1; i < NN; ++i) {
+    const HNode& h = nodes[i];
+    if (h.kind != 0 || hid[i] == NONE) continue;
+    ex_edges[hot_table(h.depth)]++;
+  }
+  for (uint64_t i = 0; i < NN; ++i)
+    if ((nodes[i].flags & NF_HAS_EXACT) && hid[i] != NONE) ex_parents[hot_table(nodes[i].depth + 1)]++;
+  uint64_t efilt_off[HOT_TABLES] = {0}, efilt_total = 0;
+  uint32_t efilt_mask[HOT_TABLES] = {0};
+  for (int t = 0; t < HOT_TABLES; ++t) {
+    if (getenv("GM_NO_EDGE_FILTER")) break;  // A/B knob
+    if (!ex_edges[t] || ex_edges[t] < 4 * ex_parents[t]) continue;
+    const uint64_t words = std::max<uint64_t>(32, next_pow2(ex_edges[t] / 2 + 1));  // 16-32 bits per key
+    if (words * 4 > (4ull << 20)) continue;
+    efilt_off[t] = efilt_total;
+    efilt_mask[t] = uint32_t(words - 1);
+    efilt_total += words;
+  }
+  std::vector<uint32_t> efilt(efilt_total, 0u);
+  for (uint64_t i = 1; i < NN; ++i) {
+    const HNode& h = nodes[i];
+    if (h.kind != 0 || hid[i] == NONE) continue;
+    const int t = hot_table(h.depth);
+    if (!efilt_mask[t]) continue;
+    const uint32_t fh = edge_filter_hash(hid[h.parent], h.word);
+    efilt[efilt_off[t] + edge_filter_word(fh, efilt_mask[t])] |= edge_filter_bits(fh);
+  }
+
   // ---- 4. word dictionary (open addressing by hash, verified by bytes)
   uint64_t nw = word_ids.size();
   uint64_t dcap = next_pow2(nw * 2 + 2);
@@ -412,7 +443,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   size_t o_sids = o_soff + al(soff.size() * 8);
   size_t o_flen = o_sids + al(sids.size() * 4 + 4);
   size_t o_gmap = o_flen + al(flen.size() * 2 + 2);
-  size_t total = o_gmap + al(idx->gmap.size() * 4 + 4);
+  size_t o_efilt = o_gmap + al(idx->gmap.size() * 4 + 4);
+  size_t total = o_efilt + al(efilt.size() * 4 + 4);
 
   if (host_only) {  // compile-only self check (no device): report the table sizes
     emqx_gm_index_info_t& in = *host_only;
@@ -449,6 +481,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   up(o_sids, sids.data(), sids.size() * 4);
   up(o_flen, flen.data(), flen.size() * 2);
   up(o_gmap, idx->gmap.data(), idx->gmap.size() * 4);
+  up(o_efilt, efilt.data(), efilt.size() * 4);
   if (e != hipSuccess) {
     hipFree(idx->dev_base);
     delete idx;
@@ -472,7 +505,10 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (int t = 0; t < HOT_TABLES; ++t) {
     v.hot_off[t] = hot_off[t];
     v.hot_cap[t] = hot_cap[t];
+    v.efilt_off[t] = efilt_off[t];
+    v.efilt_mask[t] = efilt_mask[t];
   }
+  v.efilt = reinterpret_cast<const uint32_t*>(B + o_efilt);
   v.root_sig = nodes[0].sig;
   v.root_hash = nodes[0].hash_child == NONE ? NONE : nodes[nodes[0].hash_child].end_filter;
   v.root_flags = nodes[0].plus_child != NONE ? HOT_PLUS : 0u;

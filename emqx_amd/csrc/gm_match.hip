@@ -655,14 +655,38 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
         const uint64_t cap = ix.hot_cap[ht];
         const uint32_t capu = uint32_t(cap);
         const bool wok = wid != NONE;
+        // bit q: the exact probe of entry q can hit (signature, then the
+        // table's exact-edge filter when it has one: an L2 hit that saves a
+        // random line for most of the probes the signature lets through)
+        uint32_t xmask = 0;
+#pragma unroll
+        for (int q = 0; q < RFC; ++q)
+          if (uint32_t(q) < cur_n && wok && (fsig[q] & wbit)) xmask |= 1u << q;
+        const uint32_t fmask = ix.efilt_mask[ht];  // wave-uniform
+        if (fmask && xmask) {
+          const uint32_t* ft = ix.efilt + ix.efilt_off[ht];
+          uint32_t fw[RFC], fb[RFC];
+#pragma unroll
+          for (int q = 0; q < RFC; ++q) {
+            fw[q] = fb[q] = 0;
+            if (xmask & (1u << q)) {
+              const uint32_t fh = edge_filter_hash(fid[q] & ID_MASK, wid);
+              fb[q] = edge_filter_bits(fh);
+              fw[q] = ft[edge_filter_word(fh, fmask)];
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < RFC; ++q)
+            if ((fw[q] & fb[q]) != fb[q]) xmask &= ~(1u << q);
+        }
         if (PAIR) {
 #pragma unroll
           for (int i = 0; i < RFC; i += 2) {
             if (uint32_t(i) < cur_n) {
               const bool hb = uint32_t(i + 1) < cur_n;
               const uint32_t ia = fid[i] & ID_MASK, ib = fid[i + 1] & ID_MASK;
-              const bool ax = wok && (fsig[i] & wbit), ap = (fid[i] & FR_PLUS) != 0;
-              const bool bx = hb && wok && (fsig[i + 1] & wbit), bp = hb && (fid[i + 1] & FR_PLUS) != 0;
+              const bool ax = (xmask >> i) & 1u, ap = (fid[i] & FR_PLUS) != 0;
+              const bool bx = (xmask >> (i + 1)) & 1u, bp = hb && (fid[i + 1] & FR_PLUS) != 0;
               uint32_t sax = 0, sap = 0, sbx = 0, sbp = 0;
               HotRec rax{}, rap{}, rbx{}, rbp{};
               GM_PROBE_ISSUE(ax, ia, false, sax, rax);
@@ -680,7 +704,7 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
           for (int i = 0; i < RFC; ++i) {
             if (uint32_t(i) < cur_n) {
               const uint32_t ia = fid[i] & ID_MASK;
-              const bool ax = wok && (fsig[i] & wbit), ap = (fid[i] & FR_PLUS) != 0;
+              const bool ax = (xmask >> i) & 1u, ap = (fid[i] & FR_PLUS) != 0;
               uint32_t sax = 0, sap = 0;
               HotRec rax{}, rap{};
               GM_PROBE_ISSUE(ax, ia, false, sax, rax);
