@@ -322,9 +322,12 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (uint64_t i = 1; i < NN; ++i)
     if (nodes[i].kind != 2 && !inl[i]) hot_n[hot_table(nodes[i].depth)]++;
   uint64_t hot_off[HOT_TABLES], hot_cap[HOT_TABLES], hot_total = 0;
+  uint64_t hot_load_pct = 40;  // load factor (%); GM_HOT_LOAD_PCT: A/B knob (10..90)
+  if (const char* e = getenv("GM_HOT_LOAD_PCT")) hot_load_pct = std::min<uint64_t>(90, std::max<uint64_t>(10, strtoull(e, nullptr, 10)));
   for (int t = 0; t < HOT_TABLES; ++t) {
-    // load <= ~0.55; at least 8 slots so the probe loop always finds an empty one
-    hot_cap[t] = hot_n[t] ? std::max<uint64_t>(8, (hot_n[t] * 20 + 10) / 11 + 1) : 0;
+    // load <= 0.40 (A/B at C2: 0.55 -> 0.40 cut k_walk by 3 %; lower bought nothing);
+    // at least 8 slots so the probe loop always finds an empty one
+    hot_cap[t] = hot_n[t] ? std::max<uint64_t>(8, hot_n[t] * 100 / hot_load_pct + 1) : 0;
     if (hot_cap[t] > SLOT_MASK) throw std::length_error("hot table exceeds 2^30 slots");
     hot_off[t] = hot_total;
     hot_total += hot_cap[t];
@@ -339,15 +342,29 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   auto hf_of = [&](const HNode& h) -> uint32_t {
     return (h.hash_child == NONE ? HF_NONE : nodes[h.hash_child].end_filter) | (h.plus_child != NONE ? HOT_PLUS : 0u);
   };
+  // Tables of one depth (t < HOT_TABLES-1) are Robin Hood ordered: a key is
+  // placed so that no key between its home slot and its slot is closer to its
+  // own home, which lets a lookup of an absent key stop at the first slot
+  // whose key sits nearer its home than the probe (hot_resolve).  Slots move
+  // while a depth is placed, so its hot ids are assigned once the whole depth
+  // is in (the next depth's keys hold them).  The shared last table keeps
+  // plain linear probing (its earlier depths' ids are already referenced).
+  std::vector<uint32_t> occ;  // old node index per slot of the table being placed
   for (uint32_t d = 1; d <= max_depth; ++d) {
     const int t = hot_table(d);
     HotSlot* tab = hot.data() + hot_off[t];
     const uint64_t cap = hot_cap[t];
+    const bool rh = t < HOT_TABLES - 1;
+    if (rh) occ.assign(cap, NONE);
+    auto home_dist = [&](uint64_t key, uint64_t pos) {
+      const uint64_t h = hot_slot(key, cap);
+      return pos >= h ? pos - h : pos + cap - h;
+    };
     for (uint32_t k = by_depth_off[d]; k < by_depth_off[d + 1]; ++k) {
       const uint32_t i = by_depth[k];
       const HNode& h = nodes[i];
       if (h.kind == 2 || hid[h.parent] == NONE) continue;  // '#' nodes and their (unmatchable) subtrees
-      if (inl[i]) {  // into the parent's slot (table of depth d-1)
+      if (inl[i]) {  // into the parent's slot (table of depth d-1, already final)
         HotSlot& p = hot[hot_off[hot_table(d - 1)] + hid[h.parent]];
         p.p_sig = h.sig;
         p.p_hf = hf_of(h);
@@ -355,16 +372,46 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
         hid[i] = hid[h.parent] | HOT_INLINE;
         continue;
       }
-      const uint64_t key = hot_key(hid[h.parent], h.word, d - 1);
+      uint64_t key = hot_key(hid[h.parent], h.word, d - 1);
       uint64_t s = hot_slot(key, cap);
-      while (tab[s].key != EDGE_EMPTY) s = s + 1 == cap ? 0 : s + 1;
-      HotSlot& o = tab[s];
-      o.key = key;
-      o.sig = h.sig;
-      o.hf = hf_of(h);
-      o.end_filter = end_of(h);
-      hid[i] = uint32_t(s);
+      if (!rh) {
+        while (tab[s].key != EDGE_EMPTY) s = s + 1 == cap ? 0 : s + 1;
+        HotSlot& o = tab[s];
+        o.key = key;
+        o.sig = h.sig;
+        o.hf = hf_of(h);
+        o.end_filter = end_of(h);
+        hid[i] = uint32_t(s);
+        continue;
+      }
+      uint32_t node = i;
+      uint64_t dist = 0;
+      for (;;) {
+        if (tab[s].key == EDGE_EMPTY) {
+          tab[s].key = key;
+          occ[s] = node;
+          break;
+        }
+        const uint64_t d2 = home_dist(tab[s].key, s);
+        if (d2 < dist) {  // the resident is nearer its home: it moves on
+          std::swap(tab[s].key, key);
+          std::swap(occ[s], node);
+          dist = d2;
+        }
+        s = s + 1 == cap ? 0 : s + 1;
+        ++dist;
+      }
     }
+    if (rh)
+      for (uint64_t s = 0; s < cap; ++s)
+        if (occ[s] != NONE) {
+          const HNode& h = nodes[occ[s]];
+          HotSlot& o = tab[s];
+          o.sig = h.sig;
+          o.hf = hf_of(h);
+          o.end_filter = end_of(h);
+          hid[occ[s]] = uint32_t(s);
+        }
   }
 
   // ---- 3c. exact-edge filters (gm_common.h), for tables whose parents have

@@ -210,13 +210,21 @@ __device__ __forceinline__ bool hot_is(const HotRec& r, uint64_t key) {
   return r.a.x == uint32_t(key) && r.a.y == uint32_t(key >> 32);
 }
 __device__ __forceinline__ bool hot_empty(const HotRec& r) { return r.a.x == 0xFFFFFFFFu && r.a.y == 0xFFFFFFFFu; }
-// Linear probing from slot s (whose record r is already loaded); returns the
-// slot index of `key` or NONE.
+// Linear probing from the home slot s of `key` (whose record r is already
+// loaded); returns the slot index of `key` or NONE.  rh: the table is Robin
+// Hood ordered (gm_index.cpp), so an absent key is known at the first slot
+// whose key lies nearer its own home than this probe is from `key`'s.
 __device__ __forceinline__ uint32_t hot_resolve(const HotSlot* tab, uint32_t cap, uint64_t key, uint32_t s,
-                                                HotRec& r, bool with_end, bool flat) {
+                                                HotRec& r, bool with_end, bool flat, bool rh) {
+  uint32_t dist = 0;
   while (!hot_is(r, key)) {
     if (hot_empty(r)) return NONE;
+    if (rh) {
+      const uint32_t h = uint32_t(hot_slot((uint64_t(r.a.y) << 32) | r.a.x, cap));
+      if ((s >= h ? s - h : s + cap - h) < dist) return NONE;
+    }
     s = s + 1 == cap ? 0 : s + 1;
+    ++dist;
     r = hot_load(tab, s, with_end, flat);
   }
   return s;
@@ -313,7 +321,7 @@ __device__ __forceinline__ bool plus_is_inline(uint32_t lvl, uint32_t id) { retu
       if ((plus) && sx == NONE) {                                                                         \
         GM_VISIT((e_id) | HOT_INLINE, rx);                                                                \
       } else {                                                                                            \
-        const uint32_t hs_ = hot_resolve(tab, capu, hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), sx, rx, last, hflat); \
+        const uint32_t hs_ = hot_resolve(tab, capu, hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), sx, rx, last, hflat, hrh); \
         if (hs_ != NONE) GM_VISIT(hs_, rx);                                                               \
       }                                                                                                   \
     }                                                                                                     \
@@ -389,6 +397,7 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
         const HotSlot* tab = ix.hot + ix.hot_off[ht];
         const HotSlot* ptab = ix.hot + ix.hot_off[hot_table(lvl)];  // the frontier nodes' own table
         const bool hflat = (ix.flags & IX_HOT_FLAT) != 0;
+        const bool hrh = ht < HOT_TABLES - 1;  // Robin Hood ordered table
         const uint64_t cap = ix.hot_cap[ht];
         const uint32_t capu = uint32_t(cap);
         for (uint32_t i = 0; i < cur_n; ++i) {
@@ -652,6 +661,7 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
         const HotSlot* tab = ix.hot + ix.hot_off[ht];
         const HotSlot* ptab = ix.hot + ix.hot_off[hot_table(lvl)];  // the frontier nodes' own table
         const bool hflat = (ix.flags & IX_HOT_FLAT) != 0;
+        const bool hrh = ht < HOT_TABLES - 1;  // Robin Hood ordered table
         const uint64_t cap = ix.hot_cap[ht];
         const uint32_t capu = uint32_t(cap);
         const bool wok = wid != NONE;
