@@ -164,7 +164,19 @@ inline uint64_t hash_word_host(const uint8_t* p, uint64_t len) {
   return hash_final(h, len);
 }
 
-GM_HD uint64_t dict_slot(uint64_t h, uint64_t mask) { return (h ^ (h >> 29)) & mask; }
+// Dictionary hash: 32-bit multiply-rotate steps over the same 8-byte chunks
+// (two v_mul_lo_u32 per chunk instead of four 64-bit products: the tokenizer
+// is ALU bound), fmix32 at the end.  A hit is verified by bytes, so the hash
+// only spreads slots.
+GM_HD uint32_t dict_hash_step(uint32_t h, uint64_t chunk) {
+  h ^= uint32_t(chunk);
+  h *= 0x9E3779B1u;
+  h = ((h << 15) | (h >> 17)) ^ uint32_t(chunk >> 32);
+  return h * 0x85EBCA77u;
+}
+GM_HD uint32_t dict_hash_final(uint32_t h, uint32_t len);
+constexpr uint32_t DICT_HASH_SEED = 0x243F6A88u;
+GM_HD uint64_t dict_slot(uint32_t h, uint64_t mask) { return uint64_t(h) & mask; }
 GM_HD int edge_depth(uint32_t depth) { return depth < uint32_t(EDGE_DEPTHS) ? int(depth) : EDGE_DEPTHS - 1; }
 GM_HD uint64_t edge_key(uint32_t parent, uint32_t word) { return (uint64_t(parent) << 32) | word; }
 GM_HD uint64_t edge_slot(uint64_t key, uint64_t mask) { return fmix64(key) & mask; }
@@ -182,6 +194,18 @@ GM_HD uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
+GM_HD uint32_t dict_hash_final(uint32_t h, uint32_t len) { return fmix32(h ^ (len * 0xC2B2AE3Du)); }
+
+inline uint32_t dict_hash_host(const uint8_t* p, uint64_t len) {
+  uint32_t h = DICT_HASH_SEED;
+  for (uint64_t i = 0; i < len; i += 8) {
+    uint64_t c = 0;
+    for (uint64_t k = 0; k < 8 && i + k < len; ++k) c |= uint64_t(p[i + k]) << (8 * k);
+    h = dict_hash_step(h, c);
+  }
+  return dict_hash_final(h, uint32_t(len));
+}
+
 // Signature bit of a word id (the exact-child filter of HotSlot::sig): a
 // function of the id alone, so the walk needs no word hash.
 GM_HD uint32_t sig_bit(uint32_t word_id) { return 1u << (fmix32(word_id * 0x9E3779B1u) >> 27); }

@@ -186,7 +186,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // ---- 2. intern words, build the level trie
   std::unordered_map<std::string_view, uint32_t, ViewHash> wid;  // word -> arena offset
   std::vector<uint8_t> arena;
-  std::vector<uint64_t> word_hash;  // per distinct word (parallel to insertion order)
+  std::vector<uint32_t> word_hash;  // per distinct word (parallel to insertion order)
   std::vector<uint32_t> word_ids;
   std::vector<uint32_t> word_len;
   std::vector<uint64_t> word_head;
@@ -211,7 +211,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     arena.insert(arena.end(), p, p + len);
     if (len == 0) arena.push_back(0);  // every word owns >= 1 byte: ids stay unique
     wid.emplace(v, off);  // view into idx->fbytes (stable for the build)
-    word_hash.push_back(hash_word_host(p, len));
+    word_hash.push_back(dict_hash_host(p, len));
     word_ids.push_back(off);
     word_len.push_back(uint32_t(len));
     word_head.push_back(word_head_host(p, len));

@@ -15,7 +15,7 @@
 //                  the LISTED pass it re-walks the topics whose frontier or
 //                  row outgrew the main pass (count read on the device, so no
 //                  host round trip between the passes).
-//   k_tile_sums / scan / k_assemble
+//   (k_walk tile sums) / scan / k_assemble
 //                  count -> scan -> write: builds the CSR (row_off u64, ids u32).
 //   k_slow_walk / k_slow_emit / k_copy_slow
 //                  device slow path: one workgroup per topic the listed pass
@@ -63,7 +63,7 @@ struct ByteReader {
 
 // One tokenized level word: hash, first 8 bytes, length, first byte.
 struct WordTok {
-  uint64_t h;
+  uint32_t h;  // dict_hash
   uint64_t head;
   uint64_t start;
   uint32_t len;
@@ -76,7 +76,8 @@ __device__ __forceinline__ WordTok next_word(RD& rd, uint64_t& pos, uint64_t end
   WordTok w;
   w.start = pos;
   w.head = 0;
-  uint64_t h = HASH_SEED, chunk = 0;
+  uint32_t h = DICT_HASH_SEED;
+  uint64_t chunk = 0;
   uint32_t k = 0;
   while (pos < end) {
     const uint32_t b = rd.get(pos);
@@ -86,15 +87,15 @@ __device__ __forceinline__ WordTok next_word(RD& rd, uint64_t& pos, uint64_t end
     ++pos;
     if ((k & 7) == 0) {
       if (k == 8) w.head = chunk;
-      h = hash_step(h, chunk);
+      h = dict_hash_step(h, chunk);
       chunk = 0;
     }
   }
   if (k & 7) {
     if (k < 8) w.head = chunk;
-    h = hash_step(h, chunk);
+    h = dict_hash_step(h, chunk);
   }
-  w.h = hash_final(h, k);
+  w.h = dict_hash_final(h, k);
   w.len = k;
   w.b0 = uint32_t(w.head & 0xFF);
   return w;
@@ -346,7 +347,8 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
                                                    const uint32_t* __restrict__ list_n,
                                                    uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
                                                    unsigned long long* __restrict__ probe_ctr,
-                                                   unsigned long long* __restrict__ wild_ctr) {
+                                                   unsigned long long* __restrict__ wild_ctr,
+                                                   uint64_t* __restrict__ tsum) {
   constexpr int MC = FAST_MC;
   // frontier entry: {hot id | FR_PLUS, exact-child signature}, double buffered
   __shared__ uint2 s_fr[2][FC][256];
@@ -432,6 +434,7 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
     }
     cnt[t] = ovf ? OVF_BIT : m_n;
     if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
+    else if (LISTED) atomicAdd(reinterpret_cast<unsigned long long*>(tsum + tile), (unsigned long long)m_n);
     probes += tprobes;
     wilds += wild ? 1u : 0u;
     if (!LISTED) break;
@@ -514,15 +517,15 @@ __device__ __forceinline__ WordTok next_word(LdsReader& rd, uint64_t& pos, uint6
     z = zbytes(rd.lds[wi] ^ SL);
   }
   const uint32_t len = uint32_t(e - pos);
-  uint64_t h = HASH_SEED;
+  uint32_t h = DICT_HASH_SEED;
   uint64_t head = 0;
   for (uint32_t k = 0; k < len; k += 8) {
     uint64_t c = funnel8(rd.lds, w0 + (k >> 3), sh);
     if (len - k < 8) c &= (1ull << ((len - k) * 8)) - 1;
     if (k == 0) head = c;
-    h = hash_step(h, c);
+    h = dict_hash_step(h, c);
   }
-  w.h = hash_final(h, len);
+  w.h = dict_hash_final(h, len);
   w.head = head;
   w.len = len;
   w.b0 = uint32_t(head & 0xFF);
@@ -618,7 +621,8 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ stage, uint32_t* __restrict__ ovf_list,
                                                     uint32_t* __restrict__ ovf_n,
                                                     unsigned long long* __restrict__ probe_tile,
-                                                    unsigned long long* __restrict__ wild_ctr) {
+                                                    unsigned long long* __restrict__ wild_ctr,
+                                                    uint64_t* __restrict__ tsum) {
   constexpr int MC = FAST_MC;
   const int lane = threadIdx.x & 63;
   const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
@@ -747,11 +751,18 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
     cnt[t] = ovf ? OVF_BIT : m_n;
     if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
   }
-  uint32_t ptot;
+  // per-tile probe count and match count (the CSR scan's input; rows the
+  // listed / slow passes finish add theirs there): plain stores into the
+  // tile's slots, not atomics on one address
+  uint32_t ptot, mtot;
   wave_excl_scan(probes, ptot);
+  wave_excl_scan(valid && !ovf ? m_n : 0u, mtot);
   const unsigned long long wb = __ballot(valid && wild);
   if (lane == 0) {
-    if (tile * 64 < n) probe_tile[tile] = ptot;  // waves wholly past n have no slot
+    if (tile * 64 < n) {  // waves wholly past n have no slot
+      probe_tile[tile] = ptot;
+      tsum[tile] = mtot;
+    }
     if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
   }
 }
@@ -851,15 +862,6 @@ int scan_excl(emqx_gm_ctx* ctx, LOAD load, uint64_t n_in, uint64_t* out) {
 // ---------------------------------------------------------------------------
 // assembly
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_tile_sums(const uint32_t* __restrict__ cnt, uint64_t n,
-                                                   uint64_t* __restrict__ tsum) {
-  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
-  const uint32_t c = t < n ? (cnt[t] & CNT_MASK) : 0;
-  uint32_t tot;
-  wave_excl_scan(c, tot);
-  if ((threadIdx.x & 63) == 0 && (t >> 6) * 64 < n) tsum[t >> 6] = tot;
-}
-
 // Sort a row held in FAST_MC registers (unused slots = 0xFFFFFFFF) with a
 // bitonic network; every index is static after unrolling.
 __device__ __forceinline__ void sort_row(uint32_t (&m)[FAST_MC]) {
@@ -880,15 +882,22 @@ __device__ __forceinline__ void sort_row(uint32_t (&m)[FAST_MC]) {
       }
 }
 
+// One wave per 64-topic tile: row offsets from the wave's scan, each lane's
+// row sorted in registers, then the tile's ids (one contiguous range of the
+// output) written through LDS as coalesced 256-B rows.  A tile holding a
+// slow-path row (its ids land later, k_copy_slow) stores lane by lane so
+// that row's range is left alone.
 __global__ __launch_bounds__(256) void k_assemble(const uint32_t* __restrict__ cnt, uint64_t n,
                                                   const uint64_t* __restrict__ tile_off,
                                                   const uint32_t* __restrict__ stage,
                                                   uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids,
                                                   const uint32_t* __restrict__ gmap) {
+  __shared__ uint32_t s_out[4][64 * FAST_MC];
   const int lane = threadIdx.x & 63;
+  uint32_t* const out = s_out[threadIdx.x >> 6];
   const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
   const uint64_t tile = t >> 6;
-  if (tile * 64 >= n) return;  // wave-uniform
+  if (tile * 64 >= n) return;  // wave-uniform; no block barrier below
   const uint32_t c = t < n ? cnt[t] : 0;
   const bool slow = (c & OVF_BIT) != 0;
   const uint32_t call = c & CNT_MASK, cf = slow ? 0 : call;
@@ -901,9 +910,20 @@ __global__ __launch_bounds__(256) void k_assemble(const uint32_t* __restrict__ c
 #pragma unroll
   for (int k = 0; k < FAST_MC; ++k) m[k] = uint32_t(k) < cf ? stage[stage_index(tile, k, lane)] : 0xFFFFFFFFu;
   if (cf > 1) sort_row(m);
+  if (__ballot(slow)) {
+#pragma unroll
+    for (int k = 0; k < FAST_MC; ++k)
+      if (uint32_t(k) < cf) ids[base + k] = gmap ? gmap[m[k]] : m[k];  // shard index: global ids (ascending)
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < FAST_MC; ++k)
-    if (uint32_t(k) < cf) ids[base + k] = gmap ? gmap[m[k]] : m[k];  // shard index: global ids (ascending)
+    if (uint32_t(k) < cf) out[pa + k] = gmap ? gmap[m[k]] : m[k];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  uint32_t* const dst = ids + tile_off[tile];
+  for (uint32_t i = lane; i < tall; i += 64) dst[i] = out[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -915,7 +935,8 @@ __global__ __launch_bounds__(256) void k_slow_walk(const uint8_t* __restrict__ t
                                                    const uint32_t* __restrict__ list, uint64_t k0, uint64_t kn,
                                                    uint32_t* __restrict__ fr_all, uint64_t fr_cap,
                                                    uint32_t* __restrict__ bm_all, uint64_t bm_words,
-                                                   uint32_t* __restrict__ cnt, uint64_t* __restrict__ slow_cnt) {
+                                                   uint32_t* __restrict__ cnt, uint64_t* __restrict__ slow_cnt,
+                                                   uint64_t* __restrict__ tsum) {
   const uint64_t k = k0 + blockIdx.x;
   if (k >= kn) return;
   const uint32_t t = list[k];
@@ -1014,6 +1035,7 @@ __global__ __launch_bounds__(256) void k_slow_walk(const uint8_t* __restrict__ t
   if (tid == 0) {
     slow_cnt[k] = s_red[0];
     cnt[t] = OVF_BIT | s_red[0];
+    atomicAdd(reinterpret_cast<unsigned long long*>(tsum + (t >> 6)), (unsigned long long)s_red[0]);
   }
 }
 
@@ -1323,13 +1345,13 @@ template <bool EXACT>
 void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const uint64_t* to, uint64_t n,
                   uint32_t* cnt, uint32_t* stage, uint32_t* list1, uint32_t* n1, uint32_t* list2, uint32_t* n2,
                   unsigned long long* probe_ctr, unsigned long long* wild_ctr, uint32_t* hdr, uint32_t* wids,
-                  unsigned long long* probe_tile, hipEvent_t after_main) {
+                  unsigned long long* probe_tile, uint64_t* tsum, hipEvent_t after_main) {
   hipStream_t st = ctx->stream;
   const uint64_t nblk = (n + 255) / 256;
 #define GM_LAUNCH_SPLIT(W, P)                                                                                     \
   hipLaunchKernelGGL(k_tokenize, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids);                         \
   hipLaunchKernelGGL((k_walk<EXACT, W, P>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, cnt, stage, list1, \
-                     n1, probe_tile, wild_ctr)
+                     n1, probe_tile, wild_ctr, tsum)
   switch (main_kind()) {
     case MAIN_SPLIT: GM_LAUNCH_SPLIT(1, false); break;
     case MAIN_SPLIT2: GM_LAUNCH_SPLIT(1, true); break;
@@ -1340,7 +1362,7 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
   hipLaunchKernelGGL(k_sum_tiles, dim3(256), dim3(256), 0, st, probe_tile, (n + 63) / 64, probe_ctr);
   const uint64_t lblk = std::min<uint64_t>(nblk, 512);
   hipLaunchKernelGGL((k_match_lds<EXACT, LISTED_FC, true>), dim3(lblk), dim3(256), 0, st, tb, to, n, v, cnt, stage,
-                     list1, n1, list2, n2, probe_ctr, wild_ctr);
+                     list1, n1, list2, n2, probe_ctr, wild_ctr, tsum);
 }
 
 }  // namespace
@@ -1410,11 +1432,11 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   if (exact)
     launch_match<true>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
                        list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
-                       probe_tile.as<unsigned long long>(), ctx->ev[2]);
+                       probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ctx->ev[2]);
   else
     launch_match<false>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(),
                         n1, list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
-                        probe_tile.as<unsigned long long>(), ctx->ev[2]);
+                        probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ctx->ev[2]);
   GM_HIP(ctx, hipGetLastError());
 
   uint64_t h_ctr[4] = {0, 0, 0, 0};
@@ -1449,11 +1471,11 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
       if (exact)
         hipLaunchKernelGGL(k_slow_walk<true>, dim3(kn - k0), dim3(256), 0, st, tb, to, idx->view, ovf_list, k0, kn,
                            fr.as<uint32_t>(), fr_cap, bm.as<uint32_t>(), bm_words, cnt.as<uint32_t>(),
-                           scnt.as<uint64_t>());
+                           scnt.as<uint64_t>(), tsum.as<uint64_t>());
       else
         hipLaunchKernelGGL(k_slow_walk<false>, dim3(kn - k0), dim3(256), 0, st, tb, to, idx->view, ovf_list, k0, kn,
                            fr.as<uint32_t>(), fr_cap, bm.as<uint32_t>(), bm_words, cnt.as<uint32_t>(),
-                           scnt.as<uint64_t>());
+                           scnt.as<uint64_t>(), tsum.as<uint64_t>());
       GM_HIP(ctx, hipGetLastError());
       std::vector<uint64_t> c(kn - k0);
       GM_HIP(ctx, hipMemcpyAsync(c.data(), scnt.as<uint64_t>() + k0, (kn - k0) * 8, hipMemcpyDeviceToHost, st));
@@ -1476,8 +1498,7 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   }
 
   // ---- count -> scan -> write
-  hipLaunchKernelGGL(k_tile_sums, dim3(nblk), dim3(256), 0, st, cnt.as<uint32_t>(), n, tsum.as<uint64_t>());
-  GM_HIP(ctx, hipGetLastError());
+  // (tsum: per-tile match counts, written by k_walk and topped up by the listed and slow passes)
   int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff.as<uint64_t>());
   if (rc) return rc;
   uint64_t nnz = 0;
