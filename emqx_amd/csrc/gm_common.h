@@ -97,6 +97,7 @@ struct alignas(32) HotSlot {
 // inline '+' child's record.
 // Read-only view of one index resident in HBM (passed by value to kernels).
 constexpr uint32_t IX_HOT_FLAT = 1u;  // a hot table reaches 2 GiB: flat loads instead of buffer loads
+constexpr uint32_t IX_RH_EXIT = 2u;   // lookups of absent keys use the Robin Hood early exit
 struct IndexView {
   const Node* nodes;
   const DictSlot* dict;
@@ -209,17 +210,13 @@ inline uint32_t dict_hash_host(const uint8_t* p, uint64_t len) {
 // Signature bit of a word id (the exact-child filter of HotSlot::sig): a
 // function of the id alone, so the walk needs no word hash.
 GM_HD uint32_t sig_bit(uint32_t word_id) { return 1u << (fmix32(word_id * 0x9E3779B1u) >> 27); }
-// Home slot: a 32-bit multiply-xorshift mix of (parent | mark, word) and a
-// multiply-high range reduction, so a table can hold any number of slots
-// (< 2^32) without a power-of-two blow-up, at a handful of 32-bit VALU ops
-// per probe (one v_mul_hi_u32 for the reduction).
+// Hot-key hash: two Fibonacci products (parent hot id, word id) xor-ed --
+// two v_mul_lo_u32 -- and the home slot is its high bits scaled to the table
+// by one v_mul_hi_u32 (any capacity < 2^32, no power-of-two blow-up).  The
+// exact-edge filter takes its word and bits from the same hash folded down.
+GM_HD uint32_t hot_hash(uint64_t key) { return (uint32_t(key >> 32) * 0x9E3779B1u) ^ (uint32_t(key) * 0x85EBCA77u); }
 GM_HD uint64_t hot_slot(uint64_t key, uint64_t cap) {
-  uint32_t h = (uint32_t(key >> 32) * 0x9E3779B1u) ^ (uint32_t(key) * 0x85EBCA77u);
-  h ^= h >> 15;
-  h *= 0x2C1B3C6Du;
-  h ^= h >> 12;
-  h *= 0x297A2D39u;
-  h ^= h >> 15;
+  const uint32_t h = hot_hash(key);
 #if defined(__HIP_DEVICE_COMPILE__)
   return __umulhi(h, uint32_t(cap));
 #else
@@ -229,12 +226,13 @@ GM_HD uint64_t hot_slot(uint64_t key, uint64_t cap) {
 
 // Exact-edge filter: for a hot table whose parents have many exact children
 // (so the 32-bit HotSlot::sig passes most probes that then miss), one bit
-// array over the (parent hot id, word id) keys of its exact children, two
+// array over the hot keys (parent hot id, word id) of its exact children, two
 // bits per key in one 32-bit word (16-32 bits per key, ~1-2 % false
 // positives).  It is small enough to stay in L2, so a probe it rules out
 // costs an L2 hit instead of a random line from HBM / Infinity Cache.
-GM_HD uint32_t edge_filter_hash(uint32_t parent, uint32_t word) {
-  return fmix32((parent * 0x27D4EB2Fu) ^ (word * 0x165667B1u) ^ 0x5BD1E995u);
+GM_HD uint32_t edge_filter_hash(uint64_t key) {
+  const uint32_t h = hot_hash(key);
+  return h ^ (h >> 16);
 }
 GM_HD uint32_t edge_filter_bits(uint32_t h) { return (1u << (h & 31)) | (1u << ((h >> 5) & 31)); }
 GM_HD uint32_t edge_filter_word(uint32_t h, uint32_t mask) { return (h >> 10) & mask; }

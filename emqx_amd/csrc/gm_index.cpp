@@ -441,7 +441,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     if (h.kind != 0 || hid[i] == NONE) continue;
     const int t = hot_table(h.depth);
     if (!efilt_mask[t]) continue;
-    const uint32_t fh = edge_filter_hash(hid[h.parent], h.word);
+    const uint32_t fh = edge_filter_hash(hot_key(hid[h.parent], h.word, h.depth - 1));
     efilt[efilt_off[t] + edge_filter_word(fh, efilt_mask[t])] |= edge_filter_bits(fh);
   }
 
@@ -563,6 +563,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (int t = 0; t < HOT_TABLES; ++t)
     if (hot_cap[t] * sizeof(HotSlot) >= (1ull << 31)) v.flags |= IX_HOT_FLAT;
   if (getenv("GM_HOT_FLAT")) v.flags |= IX_HOT_FLAT;  // test knob: exercise the flat-load path
+  if (!getenv("GM_NO_RH_EXIT")) v.flags |= IX_RH_EXIT;  // A/B knob
   v.n_nodes = uint32_t(NN);
   v.n_filters = nf;
   v.plus_word = plus_word;

@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
         const HotSlot* tab = ix.hot + ix.hot_off[ht];
         const HotSlot* ptab = ix.hot + ix.hot_off[hot_table(lvl)];  // the frontier nodes' own table
         const bool hflat = (ix.flags & IX_HOT_FLAT) != 0;
-        const bool hrh = ht < HOT_TABLES - 1;  // Robin Hood ordered table
+        const bool hrh = ht < HOT_TABLES - 1 && (ix.flags & IX_RH_EXIT);  // Robin Hood ordered table
         const uint64_t cap = ix.hot_cap[ht];
         const uint32_t capu = uint32_t(cap);
         for (uint32_t i = 0; i < cur_n; ++i) {
@@ -665,7 +665,7 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
         const HotSlot* tab = ix.hot + ix.hot_off[ht];
         const HotSlot* ptab = ix.hot + ix.hot_off[hot_table(lvl)];  // the frontier nodes' own table
         const bool hflat = (ix.flags & IX_HOT_FLAT) != 0;
-        const bool hrh = ht < HOT_TABLES - 1;  // Robin Hood ordered table
+        const bool hrh = ht < HOT_TABLES - 1 && (ix.flags & IX_RH_EXIT);  // Robin Hood ordered table
         const uint64_t cap = ix.hot_cap[ht];
         const uint32_t capu = uint32_t(cap);
         const bool wok = wid != NONE;
@@ -684,7 +684,7 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
           for (int q = 0; q < RFC; ++q) {
             fw[q] = fb[q] = 0;
             if (xmask & (1u << q)) {
-              const uint32_t fh = edge_filter_hash(fid[q] & ID_MASK, wid);
+              const uint32_t fh = edge_filter_hash(hot_key(fid[q] & ID_MASK, wid, lvl));
               fb[q] = edge_filter_bits(fh);
               fw[q] = ft[edge_filter_word(fh, fmask)];
             }
