@@ -1096,8 +1096,26 @@ __global__ __launch_bounds__(256) void k_fanout_rowoff(const uint64_t* __restric
   if (i <= n) out_off[i] = seg_dst[m_off[i]];
 }
 
-constexpr int FAN_PER_BLOCK = 256 * 16;  // output elements per workgroup
+constexpr int FAN_PER_BLOCK = 256 * 16;  // output elements per workgroup (4 vectors of 4 per thread)
 
+// Segment of output element p: the last segment whose start <= p, searched in
+// [a, b] (the block's first and last segments).
+__device__ __forceinline__ uint64_t fan_seg(const uint64_t* __restrict__ seg_dst, uint64_t a, uint64_t b, uint64_t p) {
+  if (a == b) return a;
+  ++b;
+  while (b - a > 1) {
+    const uint64_t m = (a + b) >> 1;
+    if (seg_dst[m] <= p) a = m;
+    else b = m;
+  }
+  return a;
+}
+
+// Every workgroup owns FAN_PER_BLOCK consecutive output elements; a thread
+// moves 4 consecutive elements at a time, as one 16-B non-temporal store (the
+// output is streamed out once) when they lie in one segment -- the usual case,
+// a hot row being one long segment -- and element by element across a
+// segment boundary.
 __global__ __launch_bounds__(256) void k_fanout_copy(const uint64_t* __restrict__ seg_dst, uint64_t nseg,
                                                      const uint32_t* __restrict__ m_ids,
                                                      const uint64_t* __restrict__ sub_off,
@@ -1120,19 +1138,22 @@ __global__ __launch_bounds__(256) void k_fanout_copy(const uint64_t* __restrict_
   }
   __syncthreads();
   const uint64_t s0 = s_seg[0], s1 = s_seg[1];
-  for (uint64_t p = lo + threadIdx.x; p < hi; p += 256) {
-    uint64_t s = s0;
-    if (s1 != s0) {
-      uint64_t a = s0, b = s1 + 1;
-      while (b - a > 1) {
-        const uint64_t m = (a + b) >> 1;
-        if (seg_dst[m] <= p) a = m;
-        else b = m;
+  for (uint64_t q = lo + uint64_t(threadIdx.x) * 4; q < hi; q += 256 * 4) {
+    const uint64_t s = fan_seg(seg_dst, s0, s1, q);
+    const uint64_t sd = seg_dst[s];
+    if (q + 4 <= hi && q + 4 <= seg_dst[s + 1]) {
+      const uint32_t* src = sub_ids + sub_off[m_ids[s]] + (q - sd);
+      const uint4 v = make_uint4(src[0], src[1], src[2], src[3]);
+      __builtin_nontemporal_store(v.x, out + q);
+      __builtin_nontemporal_store(v.y, out + q + 1);
+      __builtin_nontemporal_store(v.z, out + q + 2);
+      __builtin_nontemporal_store(v.w, out + q + 3);
+    } else {
+      for (uint64_t p = q; p < q + 4 && p < hi; ++p) {
+        const uint64_t sp = fan_seg(seg_dst, s0, s1, p);
+        out[p] = sub_ids[sub_off[m_ids[sp]] + (p - seg_dst[sp])];
       }
-      s = a;
     }
-    const uint32_t f = m_ids[s];
-    out[p] = sub_ids[sub_off[f] + (p - seg_dst[s])];
   }
 }
 
