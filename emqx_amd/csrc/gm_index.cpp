@@ -327,7 +327,10 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (int t = 0; t < HOT_TABLES; ++t) {
     // load <= 0.40 (A/B at C2: 0.55 -> 0.40 cut k_walk by 3 %; lower bought nothing);
     // at least 8 slots so the probe loop always finds an empty one
-    hot_cap[t] = hot_n[t] ? std::max<uint64_t>(8, hot_n[t] * 100 / hot_load_pct + 1) : 0;
+    uint64_t pct = hot_load_pct;
+    if (const char* e = getenv("GM_HOT_LOAD_PCT_UPPER"))  // A/B knob: load of the depth 1-2 tables
+      if (t <= 2) pct = std::min<uint64_t>(90, std::max<uint64_t>(10, strtoull(e, nullptr, 10)));
+    hot_cap[t] = hot_n[t] ? std::max<uint64_t>(8, hot_n[t] * 100 / pct + 1) : 0;
     if (hot_cap[t] > SLOT_MASK) throw std::length_error("hot table exceeds 2^30 slots");
     hot_off[t] = hot_total;
     hot_total += hot_cap[t];
