@@ -166,9 +166,11 @@ inline uint64_t hash_word_host(const uint8_t* p, uint64_t len) {
 }
 
 // Dictionary hash: 32-bit multiply-rotate steps over the same 8-byte chunks
-// (two v_mul_lo_u32 per chunk instead of four 64-bit products: the tokenizer
-// is ALU bound), fmix32 at the end.  A hit is verified by bytes, so the hash
-// only spreads slots.
+// (two v_mul_lo_u32 per chunk instead of four 64-bit products), then a
+// one-multiply xorshift finish (v_mul_lo_u32 is quarter rate and the
+// tokenizer is VALU bound; a single-multiply chunk step was tried and lets
+// structured words such as "l1w123" collide before the multiply).  A hit is
+// verified by bytes, so the hash only spreads slots.
 GM_HD uint32_t dict_hash_step(uint32_t h, uint64_t chunk) {
   h ^= uint32_t(chunk);
   h *= 0x9E3779B1u;
@@ -195,7 +197,12 @@ GM_HD uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
-GM_HD uint32_t dict_hash_final(uint32_t h, uint32_t len) { return fmix32(h ^ (len * 0xC2B2AE3Du)); }
+GM_HD uint32_t dict_hash_final(uint32_t h, uint32_t len) {
+  h ^= len;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  return h ^ (h >> 13) ^ (h >> 20);
+}
 
 inline uint32_t dict_hash_host(const uint8_t* p, uint64_t len) {
   uint32_t h = DICT_HASH_SEED;

@@ -533,6 +533,147 @@ __device__ __forceinline__ WordTok next_word(LdsReader& rd, uint64_t& pos, uint6
   return w;
 }
 
+// The same scan in 32-bit offsets relative to the block's staged text (at
+// most TOK_STAGE bytes): no 64-bit position arithmetic in the byte scan.
+// `w.start` is relative too, so the word's tail is read from `tb + lo`.
+__device__ __forceinline__ WordTok next_word_s(const uint64_t* lds, uint32_t& pos, uint32_t end) {
+  constexpr uint64_t SL = 0x2F2F2F2F2F2F2F2Full, M7 = 0x7F7F7F7F7F7F7F7Full;
+  auto zbytes = [](uint64_t y) { return ~(((y & M7) + M7) | y | M7); };
+  WordTok w;
+  w.start = pos;
+  const uint32_t w0 = pos >> 3;
+  const uint32_t sh = (pos & 7u) * 8u;
+  uint32_t wi = w0, e = end;
+  uint64_t z = zbytes(lds[wi] ^ SL) & (~0ull << sh);
+  for (;;) {
+    if (z) {
+      const uint32_t at = wi * 8u + (uint32_t(__builtin_ctzll(z)) >> 3);
+      e = at < end ? at : end;
+      break;
+    }
+    if ((wi + 1u) * 8u >= end) break;
+    ++wi;
+    z = zbytes(lds[wi] ^ SL);
+  }
+  const uint32_t len = e - pos;
+  uint32_t h = DICT_HASH_SEED;
+  uint64_t head = 0;
+  for (uint32_t k = 0; k < len; k += 8) {
+    uint64_t c = funnel8(lds, w0 + (k >> 3), sh);
+    if (len - k < 8) c &= (1ull << ((len - k) * 8)) - 1;
+    if (k == 0) head = c;
+    h = dict_hash_step(h, c);
+  }
+  w.h = dict_hash_final(h, len);
+  w.head = head;
+  w.len = len;
+  w.b0 = uint32_t(head & 0xFF);
+  pos = e;
+  return w;
+}
+
+// Staged-text form of tokenize_topic: relative 32-bit positions, and the
+// level's wids[] slot advanced by n (no lev * n product per level).
+__device__ __forceinline__ uint32_t tokenize_staged(const uint64_t* lds, uint32_t pos, uint32_t end,
+                                                    const IndexView& ix, const uint8_t* tb_lo, uint64_t n,
+                                                    uint32_t* __restrict__ wp) {
+  uint32_t lev = 0, fl = 0;
+  WordTok w = next_word_s(lds, pos, end);
+  DictSlot d = dict_first(ix, w);
+  if (w.len > 0 && w.b0 == '$') fl |= TOK_DOLLAR;  // emqx_trie.erl:271-278
+  for (;;) {
+    if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {  // emqx_topic:wildcard/1
+      fl |= TOK_WILD;
+      break;
+    }
+    const bool more = pos < end;
+    WordTok wn;
+    DictSlot dn;
+    if (more) {
+      ++pos;
+      wn = next_word_s(lds, pos, end);
+      dn = dict_first(ix, wn);
+    }
+    if (lev < TOK_LMAX) {
+      *wp = dict_resolve(ix, w, d, tb_lo);
+      wp += n;
+    }
+    ++lev;
+    if (!more) break;
+    w = wn;
+    d = dn;
+  }
+  if (lev > TOK_LMAX) fl |= TOK_DEEP;
+  return (lev < 255u ? lev : 255u) | fl;
+}
+
+// Grouped form: the words of G levels are scanned first and their first
+// dictionary slots loaded together, then resolved -- G L2 round trips in
+// flight per lane instead of the one-ahead prefetch above (the tokenizer
+// waits on the dictionary most of its time).  A word is kept as 4 VGPRs
+// (head, hash, start | len << 16; staged text is < 64 KiB) until it resolves.
+// Same hdr/wids as tokenize_topic: levels past TOK_LMAX are only counted
+// and checked for wildcards.
+template <int G>
+__device__ __forceinline__ uint32_t tokenize_grouped(const uint64_t* lds, uint32_t pos, uint32_t end,
+                                                     const IndexView& ix, const uint8_t* tb_lo, uint64_t n,
+                                                     uint32_t* __restrict__ wp) {
+  uint32_t lev = 0, fl = 0;
+  bool more = true, wild = false;
+  while (more && lev < uint32_t(TOK_LMAX)) {
+    uint64_t hd[G];
+    uint32_t hh[G], sl[G];
+    DictSlot d[G];
+    bool have[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      have[g] = more && lev + g < uint32_t(TOK_LMAX);
+      if (have[g]) {
+        const WordTok w = next_word_s(lds, pos, end);
+        if (g == 0 && lev == 0 && w.len > 0 && w.b0 == '$') fl |= TOK_DOLLAR;  // emqx_trie.erl:271-278
+        if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {  // emqx_topic:wildcard/1
+          wild = true;
+          have[g] = more = false;
+        } else {
+          hd[g] = w.head;
+          hh[g] = w.h;
+          sl[g] = uint32_t(w.start) | (w.len << 16);
+          d[g] = dict_first(ix, w);
+          more = pos < end;
+          pos += more ? 1u : 0u;
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (have[g]) {
+        WordTok w;
+        w.h = hh[g];
+        w.head = hd[g];
+        w.start = sl[g] & 0xFFFFu;
+        w.len = sl[g] >> 16;
+        w.b0 = uint32_t(hd[g] & 0xFF);
+        *wp = dict_resolve(ix, w, d[g], tb_lo);
+        wp += n;
+        ++lev;
+      }
+    }
+  }
+  while (more) {  // deep topic: count the remaining levels
+    const WordTok w = next_word_s(lds, pos, end);
+    if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) {
+      wild = true;
+      break;
+    }
+    ++lev;
+    more = pos < end;
+    pos += more ? 1u : 0u;
+  }
+  if (wild) fl |= TOK_WILD;
+  if (lev > uint32_t(TOK_LMAX)) fl |= TOK_DEEP;
+  return (lev < 255u ? lev : 255u) | fl;
+}
+
 // One topic: words -> dictionary ids, the next word's first dictionary slot
 // loaded while this word resolves.
 template <class RD>
@@ -572,6 +713,7 @@ __device__ __forceinline__ uint32_t tokenize_topic(RD& rd, uint64_t pos, uint64_
 // at every 8-byte boundary); a longer block reads global memory directly.
 constexpr int TOK_STAGE = 16384;
 
+template <int G>
 __global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ toff,
                                                   uint64_t n, IndexView ix, uint32_t* __restrict__ hdr,
                                                   uint32_t* __restrict__ wids) {
@@ -590,8 +732,10 @@ __global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb
   const uint64_t pos = toff[t], end = toff[t + 1];
   uint32_t h;
   if (staged) {
-    LdsReader rd{s_txt, lo, ~0ull, 0};
-    h = tokenize_topic(rd, pos, end, ix, tb, n, t, wids);
+    if constexpr (G == 1)
+      h = tokenize_staged(s_txt, uint32_t(pos - lo), uint32_t(end - lo), ix, tb + lo, n, wids + t);
+    else
+      h = tokenize_grouped<G>(s_txt, uint32_t(pos - lo), uint32_t(end - lo), ix, tb + lo, n, wids + t);
   } else {
     ByteReader rd{tb, ~0ull, 0};
     h = tokenize_topic(rd, pos, end, ix, tb, n, t, wids);
@@ -1366,6 +1510,25 @@ MainKind main_kind() {
 
 constexpr int LISTED_FC = 16;  // frontier capacity of the listed pass
 
+// Tokenizer group size.  GM_TOK_GROUP (A/B knob, read once): 1 = one-ahead
+// dictionary prefetch, 3 (default) / 5 = words scanned and their dictionary
+// slots loaded G at a time.  Measured at C2: 3.54 / 3.42 / 3.90 ms (G = 5
+// needs 80 VGPRs, 6 waves per SIMD).  Read per call, so tests cover all three.
+int tok_group() {
+  const char* e = getenv("GM_TOK_GROUP");
+  const int v = e ? atoi(e) : 3;
+  return (v == 1 || v == 5) ? v : 3;
+}
+
+void launch_tokenize(hipStream_t st, uint64_t nblk, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                     const IndexView& v, uint32_t* hdr, uint32_t* wids) {
+  switch (tok_group()) {
+    case 1: hipLaunchKernelGGL(k_tokenize<1>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids); break;
+    case 5: hipLaunchKernelGGL(k_tokenize<5>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids); break;
+    default: hipLaunchKernelGGL(k_tokenize<3>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids);
+  }
+}
+
 // Main pass, then the listed pass over its overflow queue (count read on the
 // device).  `after_main` is recorded between the two: the roofline times the
 // main pass alone, the same kernel rocprofv3 reports.
@@ -1377,7 +1540,7 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
   hipStream_t st = ctx->stream;
   const uint64_t nblk = (n + 255) / 256;
 #define GM_LAUNCH_SPLIT(W, P)                                                                                     \
-  hipLaunchKernelGGL(k_tokenize, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids);                         \
+  launch_tokenize(st, nblk, tb, to, n, v, hdr, wids);                                                             \
   hipLaunchKernelGGL((k_walk<EXACT, W, P>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, cnt, stage, list1, \
                      n1, probe_tile, wild_ctr, tsum)
   switch (main_kind()) {

@@ -330,3 +330,31 @@ def test_tokenizer_alignments_and_bytes(ctx, orc):
             topics.append(a)
     _check(ctx, orc, sorted(filters), topics, True)
     _check(ctx, orc, sorted(filters), topics, False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group", ["1", "3", "5"])
+def test_tokenizer_groups(ctx, orc, monkeypatch, group):
+    """k_tokenize<G> (GM_TOK_GROUP, words resolved G levels at a time): the
+    group boundary against wildcard words, '$' first words, empty levels,
+    trailing '/', and topics deeper than the 8 tokenized levels must give
+    the same rows as the oracle for every G."""
+    monkeypatch.setenv("GM_TOK_GROUP", group)
+    rng = random.Random(23)
+    words = [b"a", b"b", b"", b"cc", b"longword_over_8_bytes", b"$SYS", b"d"]
+    filters = {b"#", b"+", b"+/+", b"a/#", b"$SYS/#", b"+/b/#", b"a/b/cc", b"/#", b"a//cc", b"a/b/"}
+    for _ in range(200):
+        n = rng.randint(1, 12)
+        lev = [rng.choice(words + [b"+"]) for _ in range(n)]
+        if rng.random() < 0.5:
+            lev[-1] = b"#"
+        filters.add(b"/".join(lev))
+    topics = [b"", b"/", b"a/", b"$SYS/x", b"a/b/cc", b"a//cc", b"a/b/"]
+    for _ in range(1500):
+        n = rng.randint(1, 14)
+        lev = [rng.choice(words) for _ in range(n)]
+        if rng.random() < 0.1:  # a wildcard word at any level, including past the group / 8-level bounds
+            lev[rng.randrange(n)] = rng.choice([b"+", b"#"])
+        topics.append(b"/".join(lev))
+    _check(ctx, orc, sorted(filters), topics, True)
+    _check(ctx, orc, filters, topics, False)
