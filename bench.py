@@ -52,25 +52,41 @@ def parse():
     return p.parse_args()
 
 
+# Rehearsal knobs (tests/test_gpu_bench.py): GM_BENCH_BACKEND=gloo runs the
+# rank plumbing over gloo and GM_BENCH_DEVICE pins every rank to one device, so
+# the N>1 path of this script runs on a one-GPU box.  The driver's runs use
+# neither: one rank per GPU over RCCL ("nccl").
+BACKEND = os.environ.get("GM_BENCH_BACKEND", "nccl")
+
+
 def dist_setup(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "GM_BENCH_DEVICE" in os.environ:
+        local = int(os.environ["GM_BENCH_DEVICE"])
     pg = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if BACKEND == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(BACKEND)
         pg = dist
     return world, rank, local, pg
+
+
+def _reduce_tensor(local, x: float):
+    import torch
+    return torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}" if BACKEND == "nccl" else "cpu")
 
 
 def barrier_max(pg, local, x: float) -> float:
     if pg is None:
         return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    t = _reduce_tensor(local, x)
     pg.all_reduce(t, op=pg.ReduceOp.MAX)
     return float(t.item())
 
@@ -251,7 +267,7 @@ def bench_c5(a, world, rank, local, pg):
     idx = ctx.build_index_shard((sfb, sfo), gids)
     t_build = time.perf_counter() - t0
     db, do, tbytes = ctx.gen_topics_device(codes, a.seed, 0, n_topics)  # same batch on every rank
-    m = ShardedMatcher(ctx, idx, world, rank, dist=pg, device_tensors=True)
+    m = ShardedMatcher(ctx, idx, world, rank, dist=pg, device_tensors=BACKEND == "nccl")
     for _ in range(max(a.warmup, 1)):
         res, first, rows = m.match_device(db, do, n_topics)
         res.free()
@@ -267,8 +283,7 @@ def bench_c5(a, world, rank, local, pg):
     barrier(pg)
     elapsed = barrier_max(pg, local, time.perf_counter() - t0)
     if pg is not None:
-        import torch
-        t = torch.tensor([float(nnz)], dtype=torch.float64, device=f"cuda:{local}")
+        t = _reduce_tensor(local, float(nnz))
         pg.all_reduce(t)
         nnz = int(t.item())
     out = {"metric": "publish topics matched/sec, filters sharded over GPUs (C5)",

@@ -16,7 +16,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-  step pytest_gpu 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
   step smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then

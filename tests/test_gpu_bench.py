@@ -1,0 +1,60 @@
+"""The N>1 path of bench.py, rehearsed on one GPU: two ranks under
+torch.distributed.run with the rank plumbing over gloo and both ranks pinned to
+device 0 (GM_BENCH_BACKEND / GM_BENCH_DEVICE).  The driver's 2/4/8-GPU runs use
+the same code with one rank per GPU over RCCL."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_ranks(args, world=2):
+    env = dict(os.environ, GM_BENCH_BACKEND="gloo", GM_BENCH_DEVICE="0", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-cpu"] + args
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith('{"metric"')]
+    assert len(lines) == 1, p.stdout[-3000:]  # rank 0 prints exactly one line
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_two_ranks_c2():
+    one = _run_ranks(["--filters", "20000", "--topics", "1000000"], world=1)
+    two = _run_ranks(["--filters", "20000", "--topics", "1000000"], world=2)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    # weak scaling: each rank matches its own slice, same per-rank work
+    assert two["config"]["topics_per_gpu"] == one["config"]["topics_per_gpu"] == 1_000_000
+    assert two["value"] > 0 and two["roofline"]["frac"] > 0
+    # the two slices are different windows of the same stream: same matches/topic within noise
+    assert abs(two["detail"]["matches_per_topic"] - one["detail"]["matches_per_topic"]) < 0.1
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_two_ranks_c5_exchange():
+    out = _run_ranks(["--config", "c5", "--filters", "50000", "--topics", "200000"], world=2)
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong"
+    assert out["detail"]["exchange_bytes_per_step_rank0"] > 0
+    assert out["matches_per_sec"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_two_ranks_c4():
+    out = _run_ranks(["--config", "c4"], world=2)
+    assert out["n_gpus"] == 2 and out["config"]["pairs"] == 10**9
