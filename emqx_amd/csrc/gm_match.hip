@@ -1007,14 +1007,17 @@ int scan_excl(emqx_gm_ctx* ctx, LOAD load, uint64_t n_in, uint64_t* out) {
 // assembly
 // ---------------------------------------------------------------------------
 // Sort a row held in FAST_MC registers (unused slots = 0xFFFFFFFF) with a
-// bitonic network; every index is static after unrolling.
+// bitonic network over its first N slots; every index is static after
+// unrolling.  Valid when every slot at or past N holds the sentinel.
+template <int N>
 __device__ __forceinline__ void sort_row(uint32_t (&m)[FAST_MC]) {
+  static_assert(N <= FAST_MC && (N & (N - 1)) == 0, "bitonic width");
 #pragma unroll
-  for (int k = 2; k <= FAST_MC; k <<= 1)
+  for (int k = 2; k <= N; k <<= 1)
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1)
 #pragma unroll
-      for (int i = 0; i < FAST_MC; ++i) {
+      for (int i = 0; i < N; ++i) {
         const int l = i ^ j;
         if (l > i) {
           const uint32_t a = m[i], b = m[l];
@@ -1024,6 +1027,38 @@ __device__ __forceinline__ void sort_row(uint32_t (&m)[FAST_MC]) {
           m[l] = up ? hi : lo;
         }
       }
+}
+
+// One tile's rows once the wave's longest row is known to fit W slots (W is
+// wave-uniform): W stage loads, the W-wide bitonic network and W stores per
+// lane instead of FAST_MC.  At C2 (2.9 matches per topic) most waves take
+// W = 8 (24 compare-exchanges instead of 80); k_assemble was bound by that
+// VALU work (C2: 1.07 ms -> 0.91 ms with the network sized alone, 0.80 ms
+// with loads and stores sized too).
+template <int W>
+__device__ __forceinline__ void assemble_tile(const uint32_t* __restrict__ stage, uint64_t tile, int lane,
+                                              uint32_t cf, bool any_slow, uint64_t base, uint32_t pa,
+                                              uint32_t tall, uint32_t* out, uint32_t* __restrict__ ids,
+                                              uint64_t tile_base, const uint32_t* __restrict__ gmap) {
+  uint32_t m[FAST_MC];
+#pragma unroll
+  for (int k = 0; k < FAST_MC; ++k)
+    m[k] = (k < W && uint32_t(k) < cf) ? stage[stage_index(tile, k, lane)] : 0xFFFFFFFFu;
+  if (W > 1) sort_row<W>(m);
+  if (any_slow) {
+#pragma unroll
+    for (int k = 0; k < W; ++k)
+      if (uint32_t(k) < cf) ids[base + k] = gmap ? gmap[m[k]] : m[k];  // shard index: global ids (ascending)
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < W; ++k)
+    if (uint32_t(k) < cf) out[pa + k] = gmap ? gmap[m[k]] : m[k];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  uint32_t* const dst = ids + tile_base;
+  for (uint32_t i = lane; i < tall; i += 64) dst[i] = out[i];
 }
 
 // One wave per 64-topic tile: row offsets from the wave's scan, each lane's
@@ -1050,24 +1085,20 @@ __global__ __launch_bounds__(256) void k_assemble(const uint32_t* __restrict__ c
   const uint64_t base = tile_off[tile] + pa;
   if (t < n) row_off[t] = base;
   if (t == n - 1) row_off[n] = base + call;
-  uint32_t m[FAST_MC];
-#pragma unroll
-  for (int k = 0; k < FAST_MC; ++k) m[k] = uint32_t(k) < cf ? stage[stage_index(tile, k, lane)] : 0xFFFFFFFFu;
-  if (cf > 1) sort_row(m);
-  if (__ballot(slow)) {
-#pragma unroll
-    for (int k = 0; k < FAST_MC; ++k)
-      if (uint32_t(k) < cf) ids[base + k] = gmap ? gmap[m[k]] : m[k];  // shard index: global ids (ascending)
-    return;
-  }
-#pragma unroll
-  for (int k = 0; k < FAST_MC; ++k)
-    if (uint32_t(k) < cf) out[pa + k] = gmap ? gmap[m[k]] : m[k];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  uint32_t* const dst = ids + tile_off[tile];
-  for (uint32_t i = lane; i < tall; i += 64) dst[i] = out[i];
+  const bool any_slow = __ballot(slow) != 0;
+  const uint64_t tb0 = tile_off[tile];
+#define GM_ASM(W) assemble_tile<W>(stage, tile, lane, cf, any_slow, base, pa, tall, out, ids, tb0, gmap)
+  if (__ballot(cf > 8))
+    GM_ASM(FAST_MC);
+  else if (__ballot(cf > 4))
+    GM_ASM(8);
+  else if (__ballot(cf > 2))
+    GM_ASM(4);
+  else if (__ballot(cf > 1))
+    GM_ASM(2);
+  else
+    GM_ASM(1);
+#undef GM_ASM
 }
 
 // ---------------------------------------------------------------------------
