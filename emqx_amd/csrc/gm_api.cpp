@@ -127,6 +127,12 @@ int emqx_gm_close(emqx_gm_ctx* ctx) {
     for (auto& e : ctx->ev)
       if (e) hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) hipStreamDestroy(ctx->stream);
+    if (ctx->stream2) {
+      hipStreamSynchronize(ctx->stream2);
+      hipStreamDestroy(ctx->stream2);
+    }
+    for (auto& e : ctx->ov_ev)
+      if (e) hipEventDestroy(e);
   }
   delete ctx;
   return EMQX_GM_OK;

@@ -74,6 +74,8 @@ struct emqx_gm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
+  hipStream_t stream2 = nullptr;  // tokenizer stream of the overlapped match (GM_OVERLAP)
+  hipEvent_t ov_ev[9] = {};
   std::recursive_mutex mu;
   std::string err;
   gm::DevPool* pool = nullptr;

@@ -716,9 +716,9 @@ constexpr int TOK_STAGE = 16384;
 template <int G>
 __global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ toff,
                                                   uint64_t n, IndexView ix, uint32_t* __restrict__ hdr,
-                                                  uint32_t* __restrict__ wids) {
+                                                  uint32_t* __restrict__ wids, uint64_t t_base) {
   __shared__ uint64_t s_txt[TOK_STAGE / 8 + 1];  // + one word of slack for the funnel shifts
-  const uint64_t t0 = uint64_t(blockIdx.x) * 256u;
+  const uint64_t t0 = t_base + uint64_t(blockIdx.x) * 256u;
   const uint64_t t = t0 + threadIdx.x;
   const uint64_t tl = t0 + 256 < n ? t0 + 256 : n;
   const uint64_t lo = toff[t0] & ~7ull, hi = toff[tl];
@@ -766,10 +766,10 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ ovf_n,
                                                     unsigned long long* __restrict__ probe_tile,
                                                     unsigned long long* __restrict__ wild_ctr,
-                                                    uint64_t* __restrict__ tsum) {
+                                                    uint64_t* __restrict__ tsum, uint64_t t_base) {
   constexpr int MC = FAST_MC;
   const int lane = threadIdx.x & 63;
-  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  const uint64_t t = t_base + uint64_t(blockIdx.x) * 256u + threadIdx.x;
   const uint64_t tile = t >> 6;
   const bool valid = t < n;
   uint32_t* const srow = stage + stage_index(tile, 0, lane);
@@ -1552,12 +1552,24 @@ int tok_group() {
 }
 
 void launch_tokenize(hipStream_t st, uint64_t nblk, const uint8_t* tb, const uint64_t* to, uint64_t n,
-                     const IndexView& v, uint32_t* hdr, uint32_t* wids) {
+                     const IndexView& v, uint32_t* hdr, uint32_t* wids, uint64_t t_base) {
   switch (tok_group()) {
-    case 1: hipLaunchKernelGGL(k_tokenize<1>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids); break;
-    case 5: hipLaunchKernelGGL(k_tokenize<5>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids); break;
-    default: hipLaunchKernelGGL(k_tokenize<3>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids);
+    case 1: hipLaunchKernelGGL(k_tokenize<1>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, t_base); break;
+    case 5: hipLaunchKernelGGL(k_tokenize<5>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, t_base); break;
+    default: hipLaunchKernelGGL(k_tokenize<3>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, t_base);
   }
+}
+
+// Tokenize / walk overlap.  GM_OVERLAP = K (A/B knob, read per call; 1 = off):
+// the batch is cut into K block ranges; chunk i is tokenized on a second
+// stream while the walk of chunk i-1 runs on the context's stream (the
+// tokenizer is VALU bound, the walk waits on the fabric, so the two can share
+// the CUs).  Kernels index by t_base + their own grid, so the layouts are
+// those of one launch.
+int overlap_chunks() {
+  const char* e = getenv("GM_OVERLAP");
+  const int v = e ? atoi(e) : 1;
+  return v < 1 ? 1 : (v > 8 ? 8 : v);
 }
 
 // Main pass, then the listed pass over its overflow queue (count read on the
@@ -1570,16 +1582,45 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
                   unsigned long long* probe_tile, uint64_t* tsum, hipEvent_t after_main) {
   hipStream_t st = ctx->stream;
   const uint64_t nblk = (n + 255) / 256;
-#define GM_LAUNCH_SPLIT(W, P)                                                                                     \
-  launch_tokenize(st, nblk, tb, to, n, v, hdr, wids);                                                             \
-  hipLaunchKernelGGL((k_walk<EXACT, W, P>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, cnt, stage, list1, \
-                     n1, probe_tile, wild_ctr, tsum)
-  switch (main_kind()) {
-    case MAIN_SPLIT: GM_LAUNCH_SPLIT(1, false); break;
-    case MAIN_SPLIT2: GM_LAUNCH_SPLIT(1, true); break;
-    default: GM_LAUNCH_SPLIT(8, false);
+#define GM_LAUNCH_WALK(W, P, sw, g, base)                                                                        \
+  hipLaunchKernelGGL((k_walk<EXACT, W, P>), dim3(g), dim3(256), 0, sw, tb, to, n, v, hdr, wids, cnt, stage, list1, n1, \
+                     probe_tile, wild_ctr, tsum, base)
+#define GM_WALK(sw, g, base)                                  \
+  do {                                                        \
+    switch (main_kind()) {                                    \
+      case MAIN_SPLIT: GM_LAUNCH_WALK(1, false, sw, g, base); break;  \
+      case MAIN_SPLIT2: GM_LAUNCH_WALK(1, true, sw, g, base); break;  \
+      default: GM_LAUNCH_WALK(8, false, sw, g, base);         \
+    }                                                         \
+  } while (0)
+  int K = overlap_chunks();
+  if (K > 1 && nblk < uint64_t(K) * 1024) K = 1;  // small batches: one launch each
+  if (K > 1 && !ctx->stream2 && hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess) {
+    ctx->stream2 = nullptr;
+    K = 1;
   }
-#undef GM_LAUNCH_SPLIT
+  for (int i = 0; K > 1 && i <= K; ++i)
+    if (!ctx->ov_ev[i] && hipEventCreateWithFlags(&ctx->ov_ev[i], hipEventDisableTiming) != hipSuccess) K = 1;
+  if (K == 1) {
+    launch_tokenize(st, nblk, tb, to, n, v, hdr, wids, 0);
+    GM_WALK(st, nblk, 0ull);
+  } else {
+    hipStream_t st2 = ctx->stream2;
+    hipEventRecord(ctx->ov_ev[0], st);  // the tokenizer stream starts after the work queued so far
+    hipStreamWaitEvent(st2, ctx->ov_ev[0], 0);
+    const uint64_t cb = (nblk + K - 1) / K;
+    for (int i = 0; i < K; ++i) {
+      const uint64_t b0 = uint64_t(i) * cb;
+      if (b0 >= nblk) break;
+      const uint64_t nb = std::min<uint64_t>(cb, nblk - b0);
+      launch_tokenize(st2, nb, tb, to, n, v, hdr, wids, b0 * 256);
+      hipEventRecord(ctx->ov_ev[i + 1], st2);
+      hipStreamWaitEvent(st, ctx->ov_ev[i + 1], 0);
+      GM_WALK(st, nb, b0 * 256);
+    }
+  }
+#undef GM_WALK
+#undef GM_LAUNCH_WALK
   hipEventRecord(after_main, st);
   hipLaunchKernelGGL(k_sum_tiles, dim3(256), dim3(256), 0, st, probe_tile, (n + 63) / 64, probe_ctr);
   const uint64_t lblk = std::min<uint64_t>(nblk, 512);

@@ -358,3 +358,32 @@ def test_tokenizer_groups(ctx, orc, monkeypatch, group):
         topics.append(b"/".join(lev))
     _check(ctx, orc, sorted(filters), topics, True)
     _check(ctx, orc, filters, topics, False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunks", ["2", "3"])
+def test_overlapped_match_equals_single_launch(ctx, orc, monkeypatch, chunks):
+    """GM_OVERLAP=K (tokenizer of chunk i on a second stream while the walk of
+    chunk i-1 runs): the CSR must be bit-identical to the one-launch result
+    (itself checked against the oracle above), and a strided sample of rows
+    must equal the oracle's."""
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    codes = gen_filter_codes(3, 20000, wildcard_only=True)
+    fb, fo = render_codes(codes)
+    filters = orc.unpack(fb, fo)
+    idx = ctx.build_index(sorted(set(filters)))
+    n = 1_300_000  # > K * 1024 blocks of 256 topics, so the chunked path runs
+    tb, to = orc.render_codes(orc.gen_topic_codes(3, 0, n, codes))
+    monkeypatch.setenv("GM_OVERLAP", "1")
+    ro1, ids1 = ctx.match(idx, (tb, to), exact=True)
+    monkeypatch.setenv("GM_OVERLAP", chunks)
+    ro2, ids2 = ctx.match(idx, (tb, to), exact=True)
+    assert np.array_equal(ro1, ro2) and np.array_equal(ids1, ids2)
+    sample = list(range(0, n, 997))
+    topics = orc.unpack(tb, to)
+    sub = [topics[i] for i in sample]
+    fl = sorted(set(filters))
+    oro, oids = _oracle_rows(orc, fl, sub, 1)
+    for j, i in enumerate(sample):
+        assert ids2[ro2[i]:ro2[i + 1]].tolist() == oids[oro[j]:oro[j + 1]].tolist(), topics[i]
+    idx.release()
