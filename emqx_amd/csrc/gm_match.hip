@@ -1320,6 +1320,23 @@ __global__ __launch_bounds__(256) void k_fanout_copy(const uint64_t* __restrict_
   }
   __syncthreads();
   const uint64_t s0 = s_seg[0], s1 = s_seg[1];
+  if (s0 == s1) {
+    // the whole range lies in one segment (a hot row): the source offset is
+    // loop invariant, so each step is an independent load + store with no
+    // dependent segment lookups in between
+    const uint64_t off = sub_off[m_ids[s0]] - seg_dst[s0];  // element q comes from sub_ids[off + q] (mod 2^64)
+    uint64_t q = lo + uint64_t(threadIdx.x) * 4;
+    for (; q + 4 <= hi; q += 256 * 4) {
+      const uint32_t* src = sub_ids + (off + q);
+      const uint4 v = make_uint4(src[0], src[1], src[2], src[3]);
+      __builtin_nontemporal_store(v.x, out + q);
+      __builtin_nontemporal_store(v.y, out + q + 1);
+      __builtin_nontemporal_store(v.z, out + q + 2);
+      __builtin_nontemporal_store(v.w, out + q + 3);
+    }
+    for (uint64_t p = q; p < hi; ++p) out[p] = sub_ids[off + p];  // q + 4 > hi here: at most 3 left
+    return;
+  }
   for (uint64_t q = lo + uint64_t(threadIdx.x) * 4; q < hi; q += 256 * 4) {
     const uint64_t s = fan_seg(seg_dst, s0, s1, q);
     const uint64_t sd = seg_dst[s];

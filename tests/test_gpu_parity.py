@@ -387,3 +387,26 @@ def test_overlapped_match_equals_single_launch(ctx, orc, monkeypatch, chunks):
     for j, i in enumerate(sample):
         assert ids2[ro2[i]:ro2[i + 1]].tolist() == oids[oro[j]:oro[j + 1]].tolist(), topics[i]
     idx.release()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("row", [1, 3, 4097, 65_539, 200_003])
+def test_fanout_long_rows_ragged(ctx, orc, row):
+    """Fan-out rows of ragged lengths (not multiples of 4, shorter and longer
+    than a workgroup's output range): workgroups inside one long row take the
+    hoisted single-segment copy with a 1-3 element tail, the others the
+    per-segment path; the result must equal the oracle's multiset rows."""
+    filters = [b"a/#", b"a/+", b"a/b", b"c"]
+    subs = [list(range(7, 7 + row)), [5, 3, 1], list(range(1000, 1000 + row // 3 + 1)), [9]]
+    idx = ctx.build_index(filters, subs=subs)
+    topics = [b"a/b", b"a/x", b"c", b"a/b", b"a", b"zz"]
+    ro, ids = ctx.match(idx, topics, exact=True)
+    fro, fids = ctx.fanout(idx, ro, ids)
+    order = np.argsort(idx.perm)
+    ssorted = [subs[i] for i in order]
+    so = np.zeros(len(filters) + 1, np.uint64)
+    so[1:] = np.cumsum([len(s) for s in ssorted])
+    si = np.array([x for s in ssorted for x in s], np.uint32)
+    ero, eids = orc.fanout(ro, ids, so, si)
+    assert np.array_equal(fro, ero) and np.array_equal(fids, eids)
+    idx.release()
