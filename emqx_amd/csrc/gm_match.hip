@@ -543,31 +543,43 @@ __device__ __forceinline__ WordTok next_word_s(const uint64_t* lds, uint32_t& po
   w.start = pos;
   const uint32_t w0 = pos >> 3;
   const uint32_t sh = (pos & 7u) * 8u;
-  uint32_t wi = w0, e = end;
-  uint64_t z = zbytes(lds[wi] ^ SL) & (~0ull << sh);
-  for (;;) {
-    if (z) {
-      const uint32_t at = wi * 8u + (uint32_t(__builtin_ctzll(z)) >> 3);
-      e = at < end ? at : end;
-      break;
+  // The two staged words that hold any word of up to 8 bytes, loaded
+  // unconditionally: the common word is cut and hashed with selects, no
+  // divergent loop (the kernels were issue bound on the exec-mask SALU work
+  // of those loops as much as on VALU).  Index w0 + 1 stays inside s_txt
+  // (staged text <= TOK_STAGE - 8 bytes, one word of slack).
+  const uint64_t a0 = lds[w0], a1 = lds[w0 + 1];
+  const uint64_t z0 = zbytes(a0 ^ SL) & (~0ull << sh);  // bytes before pos do not count
+  const uint64_t z1 = zbytes(a1 ^ SL);
+  uint32_t at = z0 ? w0 * 8u + (uint32_t(__builtin_ctzll(z0)) >> 3)
+                   : (z1 ? w0 * 8u + 8u + (uint32_t(__builtin_ctzll(z1)) >> 3) : w0 * 8u + 16u);
+  if (!z0 && !z1 && (w0 + 2u) * 8u < end) {  // a word reaching past the second staged word
+    uint32_t wi = w0 + 2u;
+    at = end;
+    for (;;) {
+      const uint64_t z = zbytes(lds[wi] ^ SL);
+      if (z) {
+        at = wi * 8u + (uint32_t(__builtin_ctzll(z)) >> 3);
+        break;
+      }
+      if ((wi + 1u) * 8u >= end) break;
+      ++wi;
     }
-    if ((wi + 1u) * 8u >= end) break;
-    ++wi;
-    z = zbytes(lds[wi] ^ SL);
   }
+  const uint32_t e = at < end ? at : end;
   const uint32_t len = e - pos;
-  uint32_t h = DICT_HASH_SEED;
-  uint64_t head = 0;
-  for (uint32_t k = 0; k < len; k += 8) {
-    uint64_t c = funnel8(lds, w0 + (k >> 3), sh);
-    if (len - k < 8) c &= (1ull << ((len - k) * 8)) - 1;
-    if (k == 0) head = c;
-    h = dict_hash_step(h, c);
+  uint64_t c = sh ? (a0 >> sh) | (a1 << (64 - sh)) : a0;
+  c &= len >= 8 ? ~0ull : (1ull << ((len & 7u) * 8u)) - 1;
+  uint32_t h = len ? dict_hash_step(DICT_HASH_SEED, c) : DICT_HASH_SEED;
+  for (uint32_t k = 8; k < len; k += 8) {  // words longer than 8 bytes
+    uint64_t ck = funnel8(lds, w0 + (k >> 3), sh);
+    if (len - k < 8) ck &= (1ull << ((len - k) * 8)) - 1;
+    h = dict_hash_step(h, ck);
   }
   w.h = dict_hash_final(h, len);
-  w.head = head;
+  w.head = c;
   w.len = len;
-  w.b0 = uint32_t(head & 0xFF);
+  w.b0 = uint32_t(c & 0xFF);
   pos = e;
   return w;
 }
