@@ -450,7 +450,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
 
   // ---- 4. word dictionary (open addressing by hash, verified by bytes)
   uint64_t nw = word_ids.size();
-  uint64_t dcap = next_pow2(nw * 2 + 2);
+  uint64_t dcap = next_pow2(nw * 4 + 4);  // load <= 0.25: a second (dependent) slot read is rare
   std::vector<DictSlot> dict(dcap, DictSlot{0, DICT_EMPTY_LEN, 0});
   for (uint64_t k = 0; k < nw; ++k) {
     uint64_t s = dict_slot(word_hash[k], dcap - 1);

@@ -112,6 +112,10 @@ __device__ __noinline__ bool tail_equal(const uint8_t* a, const uint8_t* b, uint
 // the arena (only for words longer than 8 bytes).
 __device__ __forceinline__ uint32_t dict_resolve(const IndexView& ix, const WordTok& w, DictSlot d,
                                                  const uint8_t* tb) {
+  // the common outcomes decided from the prefetched slot with selects
+  const bool empty0 = d.len == DICT_EMPTY_LEN;
+  const bool hit0 = d.len == w.len && d.head == w.head && w.len <= 8;
+  if (empty0 || hit0) return hit0 ? d.word : NONE;
   for (uint64_t s = dict_slot(w.h, ix.dict_mask);;) {
     if (d.len == DICT_EMPTY_LEN) return NONE;
     if (d.len == w.len && d.head == w.head &&
