@@ -12,11 +12,13 @@ Multi-GPU (weak scaling): one process per GPU, replicated index, each rank
 matches its own 100M-topic slice; no collective on the data path.  `value` is
 the topics of all ranks / the max-over-ranks wall time.
 
-Also reported: a roofline object for the dominant kernel (k_match_fast,
-algorithmic bytes per SURVEY.md §8d ÷ its HIP-event time) and a CPU baseline:
-the oracle's faithful emqx_trie restatement (compact mode, ordered key table,
-fresh prefix strings) on the host cores over a bounded sample of the same
-topic stream.
+Also reported: a roofline object for the dominant kernels (k_tokenize +
+k_walk, algorithmic bytes per SURVEY.md §8d ÷ their HIP-event time), a CPU
+baseline (the oracle's faithful emqx_trie restatement -- compact mode, ordered
+key table, fresh prefix strings -- on every core of the process's affinity
+mask over a bounded sample of the same topic stream) and `parity_sample`: the
+last timed step's CSR, still in HBM, compared row for row with the oracle on
+strided windows of the batch (outside the timed region).
 """
 
 from __future__ import annotations
@@ -46,6 +48,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-parity", action="store_true", help="skip the oracle check of the last step's sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--host-io", action="store_true",
                    help="also time one call with host buffers (PCIe-inclusive rate, reported in detail)")
@@ -107,39 +110,105 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(codes, filters_packed, seed, target_s, threads):
-    """The oracle's faithful emqx_trie walk (compact) + route lookup on host cores."""
+def cpu_quota():
+    """The cgroup v2 CPU quota of this process (cores), or None when unlimited."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            rel = f.read().strip().split("::", 1)[-1]
+        with open(os.path.join("/sys/fs/cgroup", rel.lstrip("/"), "cpu.max")) as f:
+            q, per = f.read().split()
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
+def oracle_router(filters_packed):
+    """The oracle's emqx_router over the index's filters (cpu_baseline leg only)."""
     from oracle import oracle as orc
     r = orc.Router(True)
-    fb, fo = filters_packed
-    raw = fb.tobytes()
-    for i in range(len(fo) - 1):
-        r.add_route(raw[int(fo[i]):int(fo[i + 1])])
-    sorted_f = None  # ids not needed for timing
+    r.add_routes(filters_packed)
+    return r
+
+
+def sorted_unique(fb, fo):
+    """(bytes, offsets) of the unique filters in Erlang binary order, computed
+    independently of the product (fixed-width byte rows: no NUL in generated filters)."""
+    import numpy as np
+    n = len(fo) - 1
+    lens = np.diff(fo.astype(np.int64))
+    width = max(1, int(lens.max()) if n else 1)
+    rows = np.zeros((n, width), np.uint8)
+    rid = np.repeat(np.arange(n), lens)
+    col = np.arange(int(fo[-1])) - np.repeat(fo[:-1].astype(np.int64), lens)
+    rows[rid, col] = fb[:int(fo[-1])]
+    u = np.unique(rows.view(f"S{width}").ravel())
+    ul = np.char.str_len(u).astype(np.uint64)
+    off = np.zeros(len(u) + 1, np.uint64)
+    off[1:] = np.cumsum(ul)
+    return np.frombuffer(b"".join(u.tolist()) + b"\0" * 64, np.uint8).copy(), off
+
+
+def cpu_baseline(r, codes, seed, target_s, threads):
+    """The oracle's faithful emqx_trie walk (compact) + route lookup on all host cores."""
+    from oracle import oracle as orc
     # calibrate on a small slice, then time a sample sized for ~target_s
     probe_n = 20_000 * threads
     tb, to = orc.render_codes(orc.gen_topic_codes(seed, 0, probe_n, codes))
     t0 = time.perf_counter()
-    r.match_batch((tb, to), (fb, fo), mode=1, nthreads=threads, want_ids=False)
+    r.match_batch((tb, to), None, mode=1, nthreads=threads, want_ids=False)
     dt = time.perf_counter() - t0
     rate = probe_n / max(dt, 1e-6)
-    n = int(min(max(rate * target_s, probe_n), 20_000_000))
+    n = int(min(max(rate * target_s, probe_n), 40_000_000))
     tb, to = orc.render_codes(orc.gen_topic_codes(seed, 0, n, codes))
     t0 = time.perf_counter()
-    ro, _, lk = r.match_batch((tb, to), (fb, fo), mode=1, nthreads=threads, want_ids=False)
+    ro, _, lk = r.match_batch((tb, to), None, mode=1, nthreads=threads, want_ids=False)
     dt = time.perf_counter() - t0
     # single-thread rate on a slice of the same stream (BASELINE.md: reported beside the all-core one)
-    n1 = max(1000, min(n, int(n / threads / 4)))
+    n1 = max(1000, min(n, int(rate / threads * 3)))
     t1 = time.perf_counter()
-    r.match_batch((tb, to[:n1 + 1]), (fb, fo), mode=1, nthreads=1, want_ids=False)
+    r.match_batch((tb, to[:n1 + 1]), None, mode=1, nthreads=1, want_ids=False)
     single = n1 / (time.perf_counter() - t1)
-    del sorted_f
+    quota = cpu_quota()
     return {"value": n / dt, "unit": "topics/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
-            "single_thread_value": single,
-            "sample": f"first {n} topics of the same seeded C2 stream (seed {seed}), emqx_trie compact walk + "
-                      f"lookup_routes restated in C++ (oracle/emqx_oracle.cpp), {threads} std::threads, "
-                      f"{dt:.1f} s; {float(ro[-1]) / n:.3f} matches/topic; "
+            "cpu_quota_cores": quota, "single_thread_value": single,
+            "sample": f"first {n} topics of the same seeded stream (seed {seed}), emqx_trie compact walk + "
+                      f"lookup_routes restated in C++ (oracle/emqx_oracle.cpp), {threads} std::threads = every "
+                      f"core in this process's affinity mask, {dt:.1f} s; {float(ro[-1]) / n:.3f} matches/topic; "
                       f"{float(lk.mean()) if len(lk) else 0:.1f} ordered-set lookups/topic"}
+
+
+def parity_sample(ctx, r, res, codes, fpack_sorted, seed, first_topic, n_topics, threads, windows=20, width=50_000):
+    """A strided sample of one step's CSR (still in HBM) against the oracle: `windows`
+    windows of `width` topics spread over the batch, the last window included."""
+    import numpy as np
+    from oracle import oracle as orc
+    ranker = orc.Ranker(fpack_sorted)
+    width = min(width, n_topics)
+    starts = sorted({int(x) for x in np.linspace(0, n_topics - width, windows)})
+    ro_ptr = ctypes_ptr(res.csr.row_off)
+    ids_ptr = ctypes_ptr(res.csr.ids)
+    checked, ok, bad = 0, True, []
+    for s in starts:
+        ro = np.zeros(width + 1, np.uint64)
+        ctx.memcpy_d2h(ro, ro_ptr + 8 * s, (width + 1) * 8)
+        nnz = int(ro[-1] - ro[0])
+        ids = np.zeros(max(nnz, 1), np.uint32)
+        if nnz:
+            ctx.memcpy_d2h(ids, ids_ptr + 4 * int(ro[0]), nnz * 4)
+        tb, to = orc.render_codes(orc.gen_topic_codes(seed, first_topic + s, width, codes))
+        oro, oids, _ = r.match_batch((tb, to), ranker, mode=1, nthreads=threads)
+        good = np.array_equal(ro - ro[0], oro) and np.array_equal(ids[:nnz], oids)
+        checked += width
+        if not good:
+            ok = False
+            bad.append(s)
+    return {"topics": checked, "windows": len(starts), "window_topics": width, "ok": ok,
+            "mismatched_windows": bad[:8]}
+
+
+def ctypes_ptr(p) -> int:
+    import ctypes
+    return ctypes.cast(p, ctypes.c_void_p).value or 0
 
 
 def main():
@@ -180,11 +249,13 @@ def main():
     barrier(pg)
     ctx.synchronize()
     kern_ms = []
+    last = None
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        res = ctx.match_device(idx, db, do, n_topics, exact=True)
+        if last is not None:
+            last.free()
+        last = ctx.match_device(idx, db, do, n_topics, exact=True)
         kern_ms.append(ctx.stats()["match_kernel_ms"])
-        res.free()
     ctx.synchronize()
     barrier(pg)
     elapsed = time.perf_counter() - t0
@@ -192,7 +263,7 @@ def main():
 
     ms_per_step = elapsed * 1000.0 / a.steps
     value = world * n_topics * a.steps / elapsed
-    # algorithmic bytes of one k_match_fast launch:
+    # algorithmic bytes of one match call's k_tokenize + k_walk:
     #   B = Σ len(topic) + 8·n (offsets) + 16·P + Σ_matches (4 + len f) + 8·n (row offsets)
     algo = tbytes + 8 * n_topics + 16 * st["probes"] + 4 * nnz + fbytes_matched + 8 * n_topics
     kavg = sum(kern_ms) / len(kern_ms)
@@ -234,10 +305,21 @@ def main():
         hro, hids = ctx.match(idx, (hb, ho), exact=True)
         out["detail"]["host_io_topics_per_s"] = n_topics / (time.perf_counter() - t0)
         del hb, ho, hro, hids
-    if rank == 0 and world == 1 and not a.no_cpu:
-        threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        out["cpu_baseline"] = cpu_baseline(codes, fpack, a.seed, a.cpu_seconds, threads)
-        out["vs_cpu"] = value / out["cpu_baseline"]["value"]
+    # the cpu_baseline leg (oracle): timed on all host cores at N=1, and, outside the
+    # timed region, the last step's CSR checked against it on a strided sample
+    want_cpu = rank == 0 and world == 1 and not a.no_cpu
+    want_parity = rank == 0 and not a.no_parity and n_filters <= 2_000_000
+    if want_cpu or want_parity:
+        threads = a.cpu_threads or len(os.sched_getaffinity(0))
+        r = oracle_router(fpack)
+        if want_parity:
+            out["parity_sample"] = parity_sample(ctx, r, last, codes, sorted_unique(*fpack), a.seed,
+                                                 rank * n_topics, n_topics, threads)
+        if want_cpu:
+            out["cpu_baseline"] = cpu_baseline(r, codes, a.seed, a.cpu_seconds, threads)
+            out["vs_cpu"] = value / out["cpu_baseline"]["value"]
+        del r
+    last.free()
     ctx.dev_free(db)
     ctx.dev_free(do)
     idx.release()
@@ -306,7 +388,12 @@ def bench_c5(a, world, rank, local, pg):
 
 
 def bench_c4(a, world, rank, local, pg):
-    """C4 hot fan-out: 1k topics x 1M subscribers each (10^9 deliveries)."""
+    """C4 hot fan-out: 1k topics x 1M subscribers each (10^9 deliveries),
+    split across the ranks: the deliveries are numbered in
+    emqx_gm_fanout order and rank r produces the contiguous range
+    [T*r/N, T*(r+1)/N) (emqx_gm_fanout_part), so rows and 1M-wide rows alike
+    are cut across GPUs; the parts are disjoint and sum to T ("strong"
+    scaling: the job is fixed, N GPUs share it)."""
     import numpy as np
     from emqx_amd import Context
     K, S = 1000, 1_000_000
@@ -327,32 +414,43 @@ def bench_c4(a, world, rank, local, pg):
     ctx.memcpy_h2d(d_to, to, len(to) * 8)
     m = ctx.match_device(idx, d_tb, d_to, K, exact=True)
     for _ in range(max(a.warmup, 1)):
-        r = ctx.fanout_device(idx, m)
+        r, first = ctx.fanout_part(idx, m, rank, world)
         r.free()
     barrier(pg)
     ctx.synchronize()
     kms = []
     t0 = time.perf_counter()
-    total = 0
+    part = 0
     for _ in range(a.steps):
-        r = ctx.fanout_device(idx, m)
-        total = r.nnz
+        r, first = ctx.fanout_part(idx, m, rank, world)
+        part = r.nnz
         kms.append(ctx.stats()["match_kernel_ms"])
         r.free()
     ctx.synchronize()
+    barrier(pg)
     elapsed = barrier_max(pg, local, time.perf_counter() - t0)
-    pairs = total
-    algo = 4 * pairs + 8 * (K + 1) + 4 * S + 16 * K * 3
+    parts = [part]
+    if pg is not None:
+        import torch
+        t = torch.zeros(world, dtype=torch.float64, device=f"cuda:{local}" if BACKEND == "nccl" else "cpu")
+        t[rank] = float(part)
+        pg.all_reduce(t)
+        parts = [int(x) for x in t.tolist()]
+    pairs = sum(parts)
+    # algorithmic bytes of this rank's k_fanout_copy launch: its deliveries
+    # written (4 B each), the row offsets, and the distinct subscriber lists read once
+    algo = 4 * part + 8 * (K + 1) + 4 * S
     kavg = sum(kms) / len(kms)
     achieved = algo / (kavg / 1e3) / 1e9
     out = {"metric": "hot-topic fan-out deliveries/sec (C4: 1k topics x 1M subscribers)",
-           "value": world * pairs * a.steps / elapsed, "unit": "deliveries/s", "n_gpus": world, "steps": a.steps,
-           "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": None, "dtype": "u32", "data": "synthetic (C4 layout, SURVEY.md §8d)",
-           "config": {"workload": "C4: 1k hot topics x 1M subscribers, CSR subscriber lists", "pairs": pairs},
+           "value": pairs * a.steps / elapsed, "unit": "deliveries/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps, "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "u32", "data": "synthetic (C4 layout, SURVEY.md §8d)",
+           "config": {"workload": "C4: 1k hot topics x 1M subscribers, CSR subscriber lists, delivery range "
+                                  f"split over {world} GPU(s)", "pairs": pairs, "pairs_per_rank": parts},
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_fanout_copy",
-                        "kernel_ms": kavg}}
+                        "kernel_ms": kavg, "algo_bytes_per_launch": algo}}
     m.free()
     ctx.dev_free(d_tb)
     ctx.dev_free(d_to)

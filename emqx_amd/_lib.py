@@ -65,6 +65,7 @@ SIGNATURES = {
     "emqx_gm_index_release": (_i32, [_vp]),
     "emqx_gm_index_info": (_i32, [_vp, C.POINTER(IndexInfo)]),
     "emqx_gm_index_filter": (_i32, [_vp, _u32, C.POINTER(_vp), C.POINTER(_u64)]),
+    "emqx_gm_index_subscriber_count": (_i32, [_vp, _u32, C.POINTER(_u64)]),
     "emqx_gm_match": (_i32, [_vp, _vp, _vp, _vp, _u64, _u32, C.POINTER(Csr)]),
     "emqx_gm_fanout": (_i32, [_vp, _vp, C.POINTER(Csr), _u32, C.POINTER(Csr)]),
     "emqx_gm_csr_free": (_i32, [_vp, C.POINTER(Csr)]),
@@ -85,6 +86,7 @@ SIGNATURES = {
     "emqx_gm_pool_trim": (_i32, [_vp]),
     "emqx_gm_index_compile_host": (_i32, [_vp, _vp, _u64, _vp, _vp, _vp, C.POINTER(IndexInfo)]),
     "emqx_gm_matched_filter_bytes": (_i32, [_vp, _vp, C.POINTER(Csr), C.POINTER(_u64)]),
+    "emqx_gm_fanout_part": (_i32, [_vp, _vp, C.POINTER(Csr), _u32, _u32, _u32, C.POINTER(Csr), C.POINTER(_u64)]),
     "emqx_gm_select_filters": (_i32, [_vp, _vp, _u64, _vp, _u32, _vp, _vp, C.POINTER(_u64), C.POINTER(_u64)]),
 }
 

@@ -7,11 +7,20 @@
 #include <stdexcept>
 
 #include "gm_internal.h"
+#include "../../include/emqx_gm_ext.h"
 
 namespace gm {
 
+// The message of the calling thread's last failing call.  Per thread, not per
+// context: a context is shared by concurrent callers (e.g. NIF calls on
+// several dirty schedulers), and a call runs start to end on one thread, so a
+// caller reading emqx_gm_last_error() right after its own failure always gets
+// its own message and the pointer stays valid until that thread's next call.
+thread_local std::string tl_err;
+
 int set_err(emqx_gm_ctx* ctx, int code, const std::string& msg) {
-  if (ctx) ctx->err = msg;
+  (void)ctx;
+  tl_err = msg;
   return code;
 }
 
@@ -138,7 +147,10 @@ int emqx_gm_close(emqx_gm_ctx* ctx) {
   return EMQX_GM_OK;
 }
 
-const char* emqx_gm_last_error(const emqx_gm_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+const char* emqx_gm_last_error(const emqx_gm_ctx* ctx) {
+  (void)ctx;
+  return gm::tl_err.c_str();
+}
 
 int emqx_gm_set_stream(emqx_gm_ctx* ctx, void* s) {
   if (!ctx) return EMQX_GM_EINVAL;
@@ -220,6 +232,13 @@ int emqx_gm_index_filter(const emqx_gm_index* idx, uint32_t id, const uint8_t** 
   return EMQX_GM_OK;
 }
 
+int emqx_gm_index_subscriber_count(const emqx_gm_index* idx, uint32_t id, uint64_t* n) {
+  if (!idx || !n || idx->ov || !idx->gmap.empty()) return EMQX_GM_EINVAL;
+  if (id >= idx->info.n_filters) return EMQX_GM_EINVAL;
+  *n = idx->soff.empty() ? 0 : idx->soff[id + 1] - idx->soff[id];
+  return EMQX_GM_OK;
+}
+
 int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to,
                   uint64_t n, uint32_t flags, emqx_gm_csr* out) {
   if (!ctx) return EMQX_GM_EINVAL;
@@ -249,6 +268,24 @@ int emqx_gm_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
   return gm::run_fanout(ctx, idx, m, flags, out);
+  GM_GUARD_END(ctx)
+}
+
+int emqx_gm_fanout_part(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t part,
+                        uint32_t n_parts, uint32_t flags, emqx_gm_csr* out, uint64_t* first) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (!idx || !m || !out || (m->nnz && !m->ids) || !m->row_off)
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "fanout_part: NULL argument");
+  if (!n_parts || part >= n_parts) return gm::set_err(ctx, EMQX_GM_EINVAL, "fanout_part: part out of range");
+  if (flags & ~(EMQX_GM_WITH_EXACT | EMQX_GM_DEVICE_IO))
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "fanout_part: flags");
+  if (idx->view.gmap) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "fanout_part: shard index");
+  if (idx->ov) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "fanout_part: overlay snapshot");
+  std::memset(out, 0, sizeof(*out));
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  return gm::run_fanout(ctx, idx, m, flags, out, part, n_parts, first);
   GM_GUARD_END(ctx)
 }
 

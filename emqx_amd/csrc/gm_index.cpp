@@ -573,6 +573,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.hash_word = hash_word;
   idx->dev_flen = reinterpret_cast<uint16_t*>(B + o_flen);
 
+  if (sub_off) idx->soff = std::move(soff);
   emqx_gm_index_info_t& in = idx->info;
   in.n_filters = nf;
   in.n_wildcard = n_wild;

@@ -77,7 +77,6 @@ struct emqx_gm_ctx {
   hipStream_t stream2 = nullptr;  // tokenizer stream of the overlapped match (GM_OVERLAP)
   hipEvent_t ov_ev[9] = {};
   std::recursive_mutex mu;
-  std::string err;
   gm::DevPool* pool = nullptr;
   emqx_gm_match_stats stats{};
   hipEvent_t ev[6]{};
@@ -98,6 +97,7 @@ struct emqx_gm_index {
   std::vector<uint8_t> fbytes;  // sorted unique filters
   std::vector<uint64_t> foff;
   std::vector<uint32_t> gmap;   // shard index: global id of each local filter (ascending); empty otherwise
+  std::vector<uint64_t> soff;   // subscriber CSR offsets per filter id (host copy; empty without subscribers)
   gm::OverlayState* ov = nullptr;  // overlay snapshot (emqx_gm_index_update); tables above unused then
   emqx_gm_index_info_t info{};
 };
@@ -113,7 +113,7 @@ void free_index(emqx_gm_index* idx);
 int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
               uint32_t flags, emqx_gm_csr* out);
 int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
-               emqx_gm_csr* out);
+               emqx_gm_csr* out, uint32_t part = 0, uint32_t n_parts = 1, uint64_t* first_out = nullptr);
 int run_merge_rows(emqx_gm_ctx* ctx, uint64_t n_rows, uint64_t stride, uint32_t n_pieces, const uint32_t* d_lens,
                    const uint32_t* d_ids, uint32_t flags, emqx_gm_csr* out);
 int run_row_lengths(emqx_gm_ctx* ctx, const emqx_gm_csr* csr, uint32_t* d_out);

@@ -1317,11 +1317,13 @@ __device__ __forceinline__ uint64_t fan_seg(const uint64_t* __restrict__ seg_dst
 __global__ __launch_bounds__(256) void k_fanout_copy(const uint64_t* __restrict__ seg_dst, uint64_t nseg,
                                                      const uint32_t* __restrict__ m_ids,
                                                      const uint64_t* __restrict__ sub_off,
-                                                     const uint32_t* __restrict__ sub_ids, uint64_t total,
-                                                     uint64_t per_block, uint32_t* __restrict__ out) {
-  const uint64_t lo = uint64_t(blockIdx.x) * per_block;
+                                                     const uint32_t* __restrict__ sub_ids, uint64_t glo,
+                                                     uint64_t total, uint64_t per_block, uint32_t* __restrict__ out0) {
+  // this launch produces the global delivery range [glo, total); out0[0] is delivery glo
+  const uint64_t lo = glo + uint64_t(blockIdx.x) * per_block;
   if (lo >= total) return;
   const uint64_t hi = min(total, lo + per_block);
+  uint32_t* const out = out0 - glo;  // indexed by global delivery number
   __shared__ uint64_t s_seg[2];
   if (threadIdx.x < 2) {
     // last segment whose start <= x (segments may be empty)
@@ -1839,7 +1841,7 @@ int sum_filter_lengths(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint32_
 }
 
 int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
-               emqx_gm_csr* out) {
+               emqx_gm_csr* out, uint32_t part, uint32_t n_parts, uint64_t* first_out) {
   const bool dev_out = flags & EMQX_GM_DEVICE_IO;
   hipStream_t st = ctx->stream;
   const uint64_t n = m->n_rows, nnz = m->nnz;
@@ -1871,22 +1873,28 @@ int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m,
   uint64_t total = 0;
   GM_HIP(ctx, hipMemcpyAsync(&total, seg_dst.as<uint64_t>() + nnz, 8, hipMemcpyDeviceToHost, st));
   GM_HIP(ctx, hipStreamSynchronize(st));
-  PoolBuf ids(ctx->pool, total * 4 + 16);
+  // part `part` of n_parts: the contiguous delivery range [glo, ghi) of the
+  // whole fan-out (rows and wide rows alike are cut wherever the range ends)
+  const uint64_t glo = uint64_t((unsigned __int128)total * part / n_parts);
+  const uint64_t ghi = uint64_t((unsigned __int128)total * (part + 1) / n_parts);
+  const uint64_t cnt = ghi - glo;
+  if (first_out) *first_out = glo;
+  PoolBuf ids(ctx->pool, cnt * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "fanout: output");
   GM_HIP(ctx, hipEventRecord(ctx->ev[1], st));
-  if (total) {
-    const uint64_t per = fan_per_block(total);
-    const uint64_t blocks = (total + per - 1) / per;
+  if (cnt) {
+    const uint64_t per = fan_per_block(cnt);
+    const uint64_t blocks = (cnt + per - 1) / per;
     hipLaunchKernelGGL(k_fanout_copy, dim3(blocks), dim3(256), 0, st, seg_dst.as<uint64_t>(), nnz, m_ids,
-                       idx->view.sub_off, idx->view.sub_ids, total, per, ids.as<uint32_t>());
+                       idx->view.sub_off, idx->view.sub_ids, glo, ghi, per, ids.as<uint32_t>());
     GM_HIP(ctx, hipGetLastError());
   }
   GM_HIP(ctx, hipEventRecord(ctx->ev[2], st));
   GM_HIP(ctx, hipEventSynchronize(ctx->ev[2]));
-  ctx->stats.nnz = total;
+  ctx->stats.nnz = cnt;
   ctx->stats.match_kernel_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
   ctx->stats.total_device_ms = ev_ms(ctx->ev[0], ctx->ev[2]);
-  return finish_csr(ctx, n, total, row_off, ids, dev_out, out);
+  return finish_csr(ctx, n, cnt, row_off, ids, dev_out, out);
 }
 
 int run_merge_rows(emqx_gm_ctx* ctx, uint64_t n, uint64_t stride, uint32_t pieces, const uint32_t* d_lens,

@@ -66,6 +66,16 @@ class DeviceCsr:
             self.ctx.memcpy_d2h(ids, C.cast(self.csr.ids, C.c_void_p).value, nnz * 4)
         return ro, ids[:nnz]
 
+    def rows(self, start: int, count: int) -> Tuple[np.ndarray, np.ndarray]:
+        """Rows [start, start+count) copied to the host: (row offsets rebased to 0, ids)."""
+        ro = np.zeros(count + 1, np.uint64)
+        self.ctx.memcpy_d2h(ro, C.cast(self.csr.row_off, C.c_void_p).value + 8 * start, (count + 1) * 8)
+        nnz = int(ro[-1] - ro[0])
+        ids = np.zeros(max(nnz, 1), np.uint32)
+        if nnz:
+            self.ctx.memcpy_d2h(ids, C.cast(self.csr.ids, C.c_void_p).value + 4 * int(ro[0]), nnz * 4)
+        return ro - ro[0], ids[:nnz]
+
     def free(self):
         if self.csr.row_off or self.csr.ids:
             check(lib().emqx_gm_csr_free(self.ctx.h, C.byref(self.csr)), self.ctx.h, "csr_free")
@@ -104,6 +114,12 @@ class Index:
         p, n = C.c_void_p(), C.c_uint64()
         check(lib().emqx_gm_index_filter(self.h, fid, C.byref(p), C.byref(n)), None, "index_filter")
         return C.string_at(p, n.value) if n.value else b""
+
+    def subscriber_count(self, fid: int) -> int:
+        """Length of filter ``fid``'s segment in a fan-out row (emqx_gm_index_subscriber_count)."""
+        n = C.c_uint64()
+        check(lib().emqx_gm_index_subscriber_count(self.h, fid, C.byref(n)), None, "index_subscriber_count")
+        return int(n.value)
 
     def filters(self) -> List[bytes]:
         return [self.filter(i) for i in range(self.n_filters)]
@@ -231,6 +247,16 @@ class Context:
             return _csr_to_numpy(out)
         finally:
             lib().emqx_gm_csr_free(self.h, C.byref(out))
+
+    def fanout_part(self, index: Index, matches: DeviceCsr, part: int, n_parts: int) -> Tuple[DeviceCsr, int]:
+        """Part ``part`` of ``n_parts`` of the fan-out of ``matches`` (emqx_gm_fanout_part):
+        a device CSR whose row_off are the global delivery offsets and whose ids are the
+        contiguous delivery range starting at the returned global number."""
+        out = Csr()
+        first = C.c_uint64()
+        check(lib().emqx_gm_fanout_part(self.h, index.h, C.byref(matches.csr), part, n_parts, _lib.DEVICE_IO,
+                                        C.byref(out), C.byref(first)), self.h, "fanout_part")
+        return DeviceCsr(self, out), int(first.value)
 
     def fanout_device(self, index: Index, matches: DeviceCsr) -> DeviceCsr:
         out = Csr()

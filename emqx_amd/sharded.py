@@ -74,7 +74,10 @@ class ShardedMatcher:
 
     ``device_tensors`` True exchanges device buffers (RCCL, backend "nccl");
     False stages them through host memory (backend "gloo", e.g. several ranks
-    sharing one device in tests).
+    sharing one device in tests).  On the device path the library runs on
+    torch's current stream (emqx_gm_set_stream), so its kernels, torch's
+    tensor ops and the collectives are ordered by one stream: no cross-stream
+    race, no device-wide synchronisation between the steps.
     """
 
     def __init__(self, ctx: Context, index: Index, world: int, rank: int, dist=None, group=None,
@@ -82,6 +85,9 @@ class ShardedMatcher:
         self.ctx, self.index, self.world, self.rank = ctx, index, world, rank
         self.dist, self.group, self.device_tensors = dist, group, device_tensors
         self.last_exchange_bytes = 0
+        if device_tensors and world > 1:
+            import torch
+            ctx.set_stream(torch.cuda.current_stream(torch.device("cuda", ctx.device)).cuda_stream)
 
     def match_device(self, d_tb: int, d_to: int, n: int, exact: bool = True) -> Tuple[DeviceCsr, int, int]:
         """Rows of this rank's topic slice; returns (csr, first_row, n_rows)."""
@@ -93,27 +99,26 @@ class ShardedMatcher:
         W, r = self.world, self.rank
         S, b = slice_bounds(n, W)
         nnz = res.nnz
-        ro_ptr, ids_ptr = _ptr(res.csr.row_off), _ptr(res.csr.ids)
-        bounds = np.zeros(W + 1, np.uint64)
-        for q in range(W + 1):
-            ctx.memcpy_d2h(bounds[q:q + 1], ro_ptr + 8 * b[q], 8)
+        ids_ptr = _ptr(res.csr.ids)
         if self.device_tensors:
             dev = torch.device("cuda", ctx.device)
-            lens = torch.zeros(W * S, dtype=torch.int32, device=dev)
+            lens = torch.zeros(W * S, dtype=torch.int32, device=dev)  # same stream as the kernel below
             ctx.csr_row_lengths(res, lens.data_ptr())
-            ids = torch.empty(nnz, dtype=torch.int32, device=dev)
+            ids = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
             ctx.memcpy_d2d(ids.data_ptr(), ids_ptr, nnz * 4)
+            # where each peer's slice starts in ids: one device reduction, one D2H of W values
+            per = lens.view(W, S).to(torch.int64).sum(1).cumsum(0).cpu().tolist()
+            bounds = [0] + [int(x) for x in per]
         else:
             ro_h, ids_h = res.to_host()
             lens = torch.zeros(W * S, dtype=torch.int32)
             lens[:n] = torch.from_numpy(np.diff(ro_h.astype(np.int64)).astype(np.int32))
             ids = torch.from_numpy(ids_h.view(np.int32).copy())
+            bounds = [int(ro_h[x]) for x in b]
         res.free()
-        ctx.synchronize()
-        rl, ri = exchange_rows(self.dist, lens, ids, bounds.tolist(), W, self.group)
+        rl, ri = exchange_rows(self.dist, lens, ids, bounds, W, self.group)
         self.last_exchange_bytes = 4 * (W * S + int(nnz))
         if self.device_tensors:
-            torch.cuda.synchronize(rl.device)
             out = ctx.merge_rows(b[r + 1] - b[r], S, W, rl.data_ptr(), ri.data_ptr())
         else:
             nl, ni = rl.numel() * 4, max(ri.numel(), 1) * 4

@@ -48,6 +48,19 @@ int emqx_gm_select_filters(const uint8_t *filter_bytes, const uint64_t *filter_o
 int emqx_gm_matched_filter_bytes(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const emqx_gm_csr *csr,
                                  uint64_t *out);
 
+/* One part of a fan-out split over n_parts devices ("split
+ * rows and split wide rows across GPUs").  The deliveries emqx_gm_fanout would
+ * return are numbered 0..T-1 in its order; part p produces the contiguous range
+ * [T*p/n_parts, T*(p+1)/n_parts), so every row -- a 1M-subscriber row too -- is
+ * cut wherever a range ends and the parts are disjoint and cover all T.  out:
+ * row_off = the n_rows+1 GLOBAL delivery offsets (as emqx_gm_fanout's), nnz =
+ * the part's length, ids = its deliveries; *first = its first global number.
+ * This mirrors the reference's own split of a hot topic's subscribers into
+ * shards dispatched independently (emqx_broker_helper.erl:82-91,
+ * emqx_broker.erl:526-530). */
+int emqx_gm_fanout_part(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const emqx_gm_csr *matches, uint32_t part,
+                        uint32_t n_parts, uint32_t flags, emqx_gm_csr *out, uint64_t *first);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,7 +40,12 @@
  * Threading: a context may be used from several threads; calls on one context
  * are serialised onto its HIP stream.  Errors: every call returns 0 or a
  * negative EMQX_GM_E* code; nothing aborts the process; the message is in
- * emqx_gm_last_error().
+ * emqx_gm_last_error(), which is kept per calling thread (a failing call's
+ * message cannot be replaced by a concurrent call on another thread).
+ *
+ * Device topic buffers (EMQX_GM_DEVICE_IO): the tokenizer reads whole aligned
+ * 8-byte words, so at least 64 readable bytes must follow topic_bytes[toff[n]]
+ * (the library pads its own copies of host buffers the same way).
  */
 #ifndef EMQX_GPU_MATCH_H
 #define EMQX_GPU_MATCH_H
@@ -112,6 +117,8 @@ typedef struct {
 /* ---- context ---- */
 int emqx_gm_open(const emqx_gm_opts *opts, emqx_gm_ctx **out);
 int emqx_gm_close(emqx_gm_ctx *ctx);
+/* Message of the calling thread's last failing call (valid until that
+ * thread's next call into the library). */
 const char *emqx_gm_last_error(const emqx_gm_ctx *ctx);
 int emqx_gm_abi_version(void);
 /* Use an external HIP stream (e.g. torch's current stream); NULL = own. */
@@ -144,6 +151,12 @@ int emqx_gm_index_release(emqx_gm_index *idx);
 int emqx_gm_index_info(const emqx_gm_index *idx, emqx_gm_index_info_t *info);
 /* bytes of filter `id` (host memory owned by the index) */
 int emqx_gm_index_filter(const emqx_gm_index *idx, uint32_t id, const uint8_t **bytes, uint64_t *len);
+/* Number of subscribers of filter `id` (0 for an index built without
+ * subscriber lists): the length of that filter's segment in a fan-out row,
+ * which lets a caller split a row back into (filter, subscribers) groups --
+ * do_dispatch/2 sends {deliver, Filter, Msg} per filter (emqx_broker.erl:
+ * 506-525). */
+int emqx_gm_index_subscriber_count(const emqx_gm_index *idx, uint32_t id, uint64_t *n);
 
 /* ---- hot path ---- */
 int emqx_gm_match(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const uint8_t *topic_bytes,

@@ -4,11 +4,14 @@
 %% Drop-in points (reference paths under apps/emqx/src):
 %%   match_trie/1 in emqx_router.erl:137-141  -> match_batch/2
 %%   match_routes/1 in emqx_router.erl:128-134 -> match_routes_batch/2 (+ lookup_routes/1 per filter)
-%%   dispatch/2 in emqx_broker.erl:296-306    -> fanout_batch/2
+%%   dispatch/2 in emqx_broker.erl:296-306    -> fanout_batch/2 (index from load_index/2)
+%% The publish batching aggregator in front of these is
+%% emqx_gpu_match_batcher (publish_batch/1).
 %% On {error, _} the wrapper falls back to emqx_trie:match/1 (SURVEY.md §8b).
 -module(emqx_gpu_match).
 
--export([load_index/1, update_index/2, match_batch/2, match_routes_batch/2, fanout_batch/2, empty/1]).
+-export([load_index/1, load_index/2, update_index/2, match_batch/2, match_routes_batch/2, fanout_batch/2,
+         empty/1]).
 -export([match/2]).
 
 -on_load(init/0).
@@ -17,11 +20,20 @@ init() ->
     Priv = case code:priv_dir(emqx) of {error, _} -> "priv"; D -> D end,
     erlang:load_nif(filename:join(Priv, "emqx_gpu_match_nif"), 0).
 
+%% The route filters (emqx_route topics; wildcard ones are the emqx_trie
+%% entries) -> an immutable index snapshot in HBM.
 -spec load_index([binary()]) -> {ok, reference()} | {error, term()}.
 load_index(_Filters) -> erlang:nif_error(nif_not_loaded).
 
+%% Filters with their subscriber ids, one list per filter (the emqx_subscriber
+%% bag, emqx_broker.erl:147-165, with its {shard, I} buckets flattened): the
+%% index fanout_batch/2 needs.
+-spec load_index([binary()], [[non_neg_integer()]]) -> {ok, reference()} | {error, term()}.
+load_index(_Filters, _SubIds) -> erlang:nif_error(nif_not_loaded).
+
 %% Route changes (do_add_route/do_delete_route) as one batch -> a new snapshot;
 %% the old one stays valid for readers holding it (emqx_gm_index_update).
+%% Any op other than insert | delete is badarg.
 -spec update_index(reference(), [{binary(), insert | delete}]) -> {ok, reference()} | {error, term()}.
 update_index(_Index, _Ops) -> erlang:nif_error(nif_not_loaded).
 
@@ -31,7 +43,10 @@ match_batch(_Index, _Topics) -> erlang:nif_error(nif_not_loaded).
 -spec match_routes_batch(reference(), [binary()]) -> [[binary()]] | {error, term()}.
 match_routes_batch(_Index, _Topics) -> erlang:nif_error(nif_not_loaded).
 
--spec fanout_batch(reference(), [binary()]) -> [[non_neg_integer()]] | {error, term()}.
+%% Per topic: its matched filters, ascending, each with the subscriber ids
+%% do_dispatch/2 folds over (a subscriber of two matching filters appears
+%% under both: deliveries are a multiset).
+-spec fanout_batch(reference(), [binary()]) -> [[{binary(), [non_neg_integer()]}]] | {error, term()}.
 fanout_batch(_Index, _Topics) -> erlang:nif_error(nif_not_loaded).
 
 -spec empty(reference()) -> boolean().

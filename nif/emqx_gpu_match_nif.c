@@ -17,23 +17,23 @@
 
 #include "emqx_gpu_match.h"
 
+/* An index snapshot.  Result rows are binaries that point straight into the
+ * snapshot's host copy of the filter bytes (emqx_gm_index_filter) and keep
+ * this resource -- hence the snapshot -- alive: no per-snapshot copy of the
+ * filter set is made, so an incremental update_index costs O(delta), not
+ * O(filters). */
 typedef struct {
   emqx_gm_index *idx;
-  ErlNifBinary filters; /* concatenated sorted filters (sub-binaries are returned) */
-  uint64_t *foff;
-  uint64_t n;
 } gm_index_res;
 
 static ErlNifResourceType *INDEX_RT;
 static emqx_gm_ctx *CTX;
-static ERL_NIF_TERM A_OK, A_ERROR, A_BADARG, A_INSERT;
+static ERL_NIF_TERM A_OK, A_ERROR, A_BADARG, A_INSERT, A_DELETE;
 
 static void index_dtor(ErlNifEnv *env, void *obj) {
   gm_index_res *r = (gm_index_res *)obj;
   (void)env;
   if (r->idx) emqx_gm_index_release(r->idx);
-  if (r->foff) enif_free(r->foff);
-  enif_release_binary(&r->filters);
 }
 
 static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
@@ -48,6 +48,7 @@ static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
   A_ERROR = enif_make_atom(env, "error");
   A_BADARG = enif_make_atom(env, "badarg");
   A_INSERT = enif_make_atom(env, "insert");
+  A_DELETE = enif_make_atom(env, "delete");
   return emqx_gm_open(&o, &CTX) == EMQX_GM_OK && INDEX_RT ? 0 : 1;
 }
 
@@ -57,10 +58,12 @@ static void unload(ErlNifEnv *env, void *priv) {
   if (CTX) emqx_gm_close(CTX);
 }
 
+/* The failing call's own message: emqx_gm_last_error() is per calling thread,
+ * and this NIF call runs start to end on one dirty scheduler thread. */
 static ERL_NIF_TERM error_tuple(ErlNifEnv *env, int rc) {
   const char *m = emqx_gm_last_error(CTX);
   (void)rc;
-  return enif_make_tuple2(env, A_ERROR, enif_make_string(env, m ? m : "device", ERL_NIF_LATIN1));
+  return enif_make_tuple2(env, A_ERROR, enif_make_string(env, m && *m ? m : "device", ERL_NIF_LATIN1));
 }
 
 /* Pack a list of binaries into (bytes, offsets). */
@@ -89,49 +92,69 @@ static int pack_list(ErlNifEnv *env, ERL_NIF_TERM list, uint8_t **bytes, uint64_
   return 1;
 }
 
-/* Wrap an index snapshot in a resource that also owns the sorted filter
- * bytes (result rows are sub-binaries of them). */
 static ERL_NIF_TERM make_index_term(ErlNifEnv *env, emqx_gm_index *idx) {
-  emqx_gm_index_info_t info;
-  gm_index_res *r;
+  gm_index_res *r = enif_alloc_resource(INDEX_RT, sizeof(*r));
   ERL_NIF_TERM term;
-  uint64_t i;
-  emqx_gm_index_info(idx, &info);
-  r = enif_alloc_resource(INDEX_RT, sizeof(*r));
-  memset(r, 0, sizeof(*r));
   r->idx = idx;
-  r->n = info.n_filters;
-  r->foff = enif_alloc((r->n + 1) * sizeof(uint64_t));
-  r->foff[0] = 0;
-  for (i = 0; i < r->n; ++i) {
-    const uint8_t *p;
-    uint64_t l;
-    emqx_gm_index_filter(idx, (uint32_t)i, &p, &l);
-    r->foff[i + 1] = r->foff[i] + l;
-  }
-  enif_alloc_binary(r->foff[r->n], &r->filters);
-  for (i = 0; i < r->n; ++i) {
-    const uint8_t *p;
-    uint64_t l;
-    emqx_gm_index_filter(idx, (uint32_t)i, &p, &l);
-    memcpy(r->filters.data + r->foff[i], p, l);
-  }
   term = enif_make_resource(env, r);
   enif_release_resource(r);
   return enif_make_tuple2(env, A_OK, term);
 }
 
-/* load_index([Filter :: binary()]) -> {ok, Index} | {error, Reason} */
+/* Subscriber lists [[SubId :: non_neg_integer()]] -> CSR (n+1 offsets); one
+ * list per filter. */
+static int pack_subs(ErlNifEnv *env, ERL_NIF_TERM lists, uint64_t n, uint64_t **off, uint32_t **ids) {
+  unsigned len, k;
+  ERL_NIF_TERM h, t = lists, e, u;
+  uint64_t total = 0, i = 0;
+  if (!enif_get_list_length(env, lists, &len) || len != n) return 0;
+  while (enif_get_list_cell(env, t, &h, &t)) {
+    if (!enif_get_list_length(env, h, &k)) return 0;
+    total += k;
+  }
+  *off = enif_alloc((n + 1) * sizeof(uint64_t));
+  *ids = enif_alloc((total ? total : 1) * sizeof(uint32_t));
+  (*off)[0] = 0;
+  t = lists;
+  while (enif_get_list_cell(env, t, &h, &t)) {
+    uint64_t o = (*off)[i];
+    u = h;
+    while (enif_get_list_cell(env, u, &e, &u)) {
+      unsigned v;
+      if (!enif_get_uint(env, e, &v)) {
+        enif_free(*off);
+        enif_free(*ids);
+        return 0;
+      }
+      (*ids)[o++] = v;
+    }
+    (*off)[++i] = o;
+  }
+  return 1;
+}
+
+/* load_index([Filter :: binary()]) -> {ok, Index} | {error, Reason}
+ * load_index([Filter :: binary()], [[SubId :: non_neg_integer()]]) -> idem,
+ *   with each filter's subscriber ids (the emqx_subscriber bag of
+ *   emqx_broker.erl:147-165 with its {shard, I} buckets flattened), which
+ *   fanout_batch/2 returns per topic. */
 static ERL_NIF_TERM load_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
   uint8_t *fb;
-  uint64_t *fo, n;
+  uint64_t *fo, n, *so = NULL;
+  uint32_t *si = NULL;
   emqx_gm_index *idx = NULL;
   int rc;
-  (void)argc;
   if (!pack_list(env, argv[0], &fb, &fo, &n)) return enif_make_badarg(env);
-  rc = emqx_gm_index_build(CTX, fb, fo, n, NULL, NULL, NULL, &idx);
+  if (argc == 2 && !pack_subs(env, argv[1], n, &so, &si)) {
+    enif_free(fb);
+    enif_free(fo);
+    return enif_make_badarg(env);
+  }
+  rc = emqx_gm_index_build(CTX, fb, fo, n, so, si, NULL, &idx);
   enif_free(fb);
   enif_free(fo);
+  if (so) enif_free(so);
+  if (si) enif_free(si);
   if (rc != EMQX_GM_OK) return error_tuple(env, rc);
   return make_index_term(env, idx);
 }
@@ -156,6 +179,10 @@ static ERL_NIF_TERM update_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM ar
     if (!enif_get_tuple(env, h, &arity, &tup) || arity != 2) {
       enif_free(ops);
       return enif_make_badarg(env);
+    }
+    if (!enif_is_identical(tup[1], A_INSERT) && !enif_is_identical(tup[1], A_DELETE)) {
+      enif_free(ops);
+      return enif_make_badarg(env);  /* only insert | delete */
     }
     fl = enif_make_list_cell(env, tup[0], fl);
     ops[i++] = enif_is_identical(tup[1], A_INSERT) ? 1 : 0;
@@ -186,14 +213,16 @@ static ERL_NIF_TERM do_match(ErlNifEnv *env, const ERL_NIF_TERM argv[], uint32_t
   enif_free(tb);
   enif_free(to);
   if (rc != EMQX_GM_OK) return error_tuple(env, rc);
-  /* one binary term backed by the resource; rows are sub-binaries of it */
-  bin = enif_make_resource_binary(env, r, r->filters.data, r->filters.size);
+  /* each filter is a binary over the snapshot's own host bytes, kept alive by the resource */
   rows = enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1));
   for (i = 0; i < n; ++i) {
     ERL_NIF_TERM row = enif_make_list(env, 0);
     for (k = out.row_off[i + 1]; k > out.row_off[i]; --k) {
-      uint32_t f = out.ids[k - 1];
-      row = enif_make_list_cell(env, enif_make_sub_binary(env, bin, r->foff[f], r->foff[f + 1] - r->foff[f]), row);
+      const uint8_t *p;
+      uint64_t l;
+      emqx_gm_index_filter(r->idx, out.ids[k - 1], &p, &l);
+      bin = enif_make_resource_binary(env, r, p, l);
+      row = enif_make_list_cell(env, bin, row);
     }
     rows[i] = row;
   }
@@ -215,11 +244,16 @@ static ERL_NIF_TERM match_routes_batch(ErlNifEnv *env, int argc, const ERL_NIF_T
   return do_match(env, argv, EMQX_GM_WITH_EXACT);
 }
 
-/* fanout_batch(Index, [Topic]) -> [[SubscriberId]]  (emqx_broker:dispatch/2 multiset) */
+/* fanout_batch(Index, [Topic]) -> [[{Filter, [SubId]}]]
+ * emqx_broker:publish/1's route + dispatch for each topic: its matched filters
+ * (match_routes/1) in ascending order, each with the subscribers do_dispatch/2
+ * folds over (emqx_broker.erl:296-322, 506-530) -- the order of the GPU
+ * fan-out row, cut back into one segment per filter so the caller can send
+ * {deliver, Filter, Msg}.  The index must come from load_index/2. */
 static ERL_NIF_TERM fanout_batch(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
   gm_index_res *r;
   uint8_t *tb;
-  uint64_t *to, n, i, k;
+  uint64_t *to, n, i, k, d_pos;
   emqx_gm_csr m, d;
   ERL_NIF_TERM result, *rows;
   int rc;
@@ -231,17 +265,31 @@ static ERL_NIF_TERM fanout_batch(ErlNifEnv *env, int argc, const ERL_NIF_TERM ar
   enif_free(to);
   if (rc != EMQX_GM_OK) return error_tuple(env, rc);
   rc = emqx_gm_fanout(CTX, r->idx, &m, 0, &d);
-  emqx_gm_csr_free(CTX, &m);
-  if (rc != EMQX_GM_OK) return error_tuple(env, rc);
+  if (rc != EMQX_GM_OK) {
+    ERL_NIF_TERM e = error_tuple(env, rc);
+    emqx_gm_csr_free(CTX, &m);
+    return e;
+  }
   rows = enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1));
   for (i = 0; i < n; ++i) {
     ERL_NIF_TERM row = enif_make_list(env, 0);
-    for (k = d.row_off[i + 1]; k > d.row_off[i]; --k)
-      row = enif_make_list_cell(env, enif_make_uint(env, d.ids[k - 1]), row);
+    d_pos = d.row_off[i + 1];
+    for (k = m.row_off[i + 1]; k > m.row_off[i]; --k) {  /* filters back to front */
+      const uint8_t *p;
+      uint64_t l, c, j;
+      ERL_NIF_TERM subs = enif_make_list(env, 0);
+      const uint32_t f = m.ids[k - 1];
+      emqx_gm_index_filter(r->idx, f, &p, &l);
+      emqx_gm_index_subscriber_count(r->idx, f, &c);
+      for (j = 0; j < c; ++j) subs = enif_make_list_cell(env, enif_make_uint(env, d.ids[d_pos - 1 - j]), subs);
+      d_pos -= c;
+      row = enif_make_list_cell(env, enif_make_tuple2(env, enif_make_resource_binary(env, r, p, l), subs), row);
+    }
     rows[i] = row;
   }
   result = enif_make_list_from_array(env, rows, (unsigned)n);
   enif_free(rows);
+  emqx_gm_csr_free(CTX, &m);
   emqx_gm_csr_free(CTX, &d);
   return result;
 }
@@ -258,6 +306,7 @@ static ERL_NIF_TERM empty(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
 
 static ErlNifFunc funcs[] = {
     {"load_index", 1, load_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"load_index", 2, load_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"update_index", 2, update_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"match_batch", 2, match_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"match_routes_batch", 2, match_routes_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},

@@ -576,6 +576,14 @@ void orc_router_free(void* r) { delete static_cast<Router*>(r); }
 void orc_router_add_route(void* r, const char* t, uint64_t tl, const char* d, uint64_t dl) {
   static_cast<Router*>(r)->add_route(std::string(t, tl), std::string(d, dl));
 }
+// add_route/1 for each of n packed filters (dest "node"): the same
+// do_add_route/2 as above, without a foreign call per filter (large configs).
+void orc_router_add_routes(void* r, const uint8_t* fb, const uint64_t* fo, uint64_t n) {
+  auto* rt = static_cast<Router*>(r);
+  const std::string node("node");
+  for (uint64_t i = 0; i < n; ++i)
+    rt->add_route(std::string(reinterpret_cast<const char*>(fb + fo[i]), fo[i + 1] - fo[i]), node);
+}
 void orc_router_delete_route(void* r, const char* t, uint64_t tl, const char* d, uint64_t dl) {
   static_cast<Router*>(r)->delete_route(std::string(t, tl), std::string(d, dl));
 }
@@ -622,15 +630,38 @@ U64List* orc_broker_publish(void* b, const char* t, uint64_t tl) {
 // ---- batch matching (trie walk; multi-threaded CPU baseline) ----
 // mode 0 = emqx_trie:match/1 result set; mode 1 = match_routes/1 filter set.
 // Filters are ranked by `ranked` (sorted unique filter strings = the id space).
+// Filter string -> id (its rank among the sorted unique filters), built once
+// and reused by many batches (orc_match_batch_ranked).
+struct Ranker {
+  std::unordered_map<std::string, uint32_t> rank;
+};
+void* orc_ranker_new(const uint8_t* fb, const uint64_t* foff, uint64_t nf) {
+  auto* k = new Ranker;
+  k->rank.reserve(nf * 2);
+  for (uint64_t i = 0; i < nf; ++i)
+    k->rank.emplace(std::string(reinterpret_cast<const char*>(fb + foff[i]), foff[i + 1] - foff[i]), uint32_t(i));
+  return k;
+}
+void orc_ranker_free(void* k) { delete static_cast<Ranker*>(k); }
+
+Csr* orc_match_batch_ranked(void* router, int mode, const uint8_t* tb, const uint64_t* toff, uint64_t n,
+                            const void* ranker, int nthreads);
+
 Csr* orc_match_batch(void* router, int mode, const uint8_t* tb, const uint64_t* toff, uint64_t n,
                      const uint8_t* fb, const uint64_t* foff, uint64_t nf, int nthreads, int want_ids) {
+  Ranker* k = want_ids ? static_cast<Ranker*>(orc_ranker_new(fb, foff, nf)) : nullptr;
+  Csr* c = orc_match_batch_ranked(router, mode, tb, toff, n, k, nthreads);
+  delete k;
+  return c;
+}
+
+// ranker == nullptr: counts (and lookup counts) only, no ids (the CPU baseline).
+Csr* orc_match_batch_ranked(void* router, int mode, const uint8_t* tb, const uint64_t* toff, uint64_t n,
+                            const void* ranker, int nthreads) {
   auto* r = static_cast<Router*>(router);
-  std::unordered_map<std::string, uint32_t> rank;
-  if (want_ids) {
-    rank.reserve(nf * 2);
-    for (uint64_t i = 0; i < nf; ++i)
-      rank.emplace(std::string(reinterpret_cast<const char*>(fb + foff[i]), foff[i + 1] - foff[i]), uint32_t(i));
-  }
+  const bool want_ids = ranker != nullptr;
+  static const std::unordered_map<std::string, uint32_t> no_rank;
+  const auto& rank = want_ids ? static_cast<const Ranker*>(ranker)->rank : no_rank;
   if (nthreads < 1) nthreads = 1;
   std::vector<std::vector<uint32_t>> rows(n);
   std::vector<uint64_t> cnt(n), lk(n);

@@ -62,6 +62,7 @@ def lib():
             "orc_router_free": (None, [vp]),
             "orc_router_add_route": (None, [vp, cp, u64, cp, u64]),
             "orc_router_delete_route": (None, [vp, cp, u64, cp, u64]),
+            "orc_router_add_routes": (None, [vp, vp, vp, u64]),
             "orc_router_trie": (vp, [vp]),
             "orc_router_match_routes": (vp, [vp, cp, u64]),
             "orc_router_topics": (vp, [vp]),
@@ -73,6 +74,9 @@ def lib():
             "orc_broker_shard_entries": (i64, [vp, cp, u64]),
             "orc_broker_publish": (vp, [vp, cp, u64]),
             "orc_match_batch": (vp, [vp, C.c_int, vp, vp, u64, vp, vp, u64, C.c_int, C.c_int]),
+            "orc_ranker_new": (vp, [vp, vp, u64]),
+            "orc_ranker_free": (None, [vp]),
+            "orc_match_batch_ranked": (vp, [vp, C.c_int, vp, vp, u64, vp, C.c_int]),
             "orc_bruteforce_batch": (vp, [C.c_int, vp, vp, u64, vp, vp, u64, vp]),
             "orc_fanout": (vp, [vp, vp, u64, vp, vp]),
             "orc_gen_filter_codes": (None, [u64, u64, C.c_int, vp]),
@@ -234,6 +238,13 @@ class Router:
         t, d = _b(t), _b(dest)
         lib().orc_router_add_route(self.h, t, len(t), d, len(d))
 
+    def add_routes(self, packed):
+        """add_route/1 for every filter of a packed (bytes, offsets) pair, in one call."""
+        fb, fo = packed
+        fb = np.ascontiguousarray(fb, np.uint8)
+        fo = np.ascontiguousarray(fo, np.uint64)
+        lib().orc_router_add_routes(self.h, _ptr(fb), _ptr(fo), len(fo) - 1)
+
     def delete_route(self, t, dest=b"node"):
         t, d = _b(t), _b(dest)
         lib().orc_router_delete_route(self.h, t, len(t), d, len(d))
@@ -247,13 +258,33 @@ class Router:
         return _strlist(lib().orc_router_topics(self.h))
 
     def match_batch(self, topics, sorted_filters, mode: int = 1, nthreads: int = 1, want_ids: bool = True):
-        """Returns (row_off, ids, lookups) with ids = rank in ``sorted_filters``."""
+        """Returns (row_off, ids, lookups) with ids = rank in ``sorted_filters``
+        (a list, a packed (bytes, offsets) pair, or a :class:`Ranker` built once
+        for many batches; None with want_ids=False: counts only)."""
         tb, to = topics if isinstance(topics, tuple) else pack(topics)
-        fb, fo = sorted_filters if isinstance(sorted_filters, tuple) else pack(sorted_filters)
         n = len(to) - 1
+        if isinstance(sorted_filters, Ranker) or not want_ids:
+            k = sorted_filters.h if (want_ids and sorted_filters is not None) else None
+            return _csr(lib().orc_match_batch_ranked(self.h, mode, _ptr(tb), _ptr(to), n, k, nthreads))
+        fb, fo = sorted_filters if isinstance(sorted_filters, tuple) else pack(sorted_filters)
         nf = len(fo) - 1
         return _csr(lib().orc_match_batch(self.h, mode, _ptr(tb), _ptr(to), n, _ptr(fb), _ptr(fo), nf,
                                           nthreads, int(want_ids)))
+
+
+class Ranker:
+    """Filter -> id map (rank among the sorted unique filters), built once."""
+
+    def __init__(self, sorted_filters):
+        fb, fo = sorted_filters if isinstance(sorted_filters, tuple) else pack(sorted_filters)
+        fb = np.ascontiguousarray(fb, np.uint8)
+        fo = np.ascontiguousarray(fo, np.uint64)
+        self.h = lib().orc_ranker_new(_ptr(fb), _ptr(fo), len(fo) - 1)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_ranker_free(self.h)
+            self.h = None
 
 
 # ---------------------------------------------------------------- emqx_broker

@@ -5,6 +5,7 @@ predicate it restates)."""
 
 import random
 
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -84,3 +85,41 @@ def test_topic_rule_index_vs_predicate(ctx, orc):
     with pytest.raises(ValueError):
         idx.rules_for_topics(["a/+"])
     idx.release()
+
+
+@pytest.mark.gpu
+def test_publish_batcher_c_abi_sequence_vs_oracle(orc):
+    """The NIF's fanout_batch/2 sequence (index built with subscriber lists ->
+    emqx_gm_match WITH_EXACT -> emqx_gm_fanout -> rows cut into per-filter
+    groups by emqx_gm_index_subscriber_count) behind the aggregator: every
+    publish's deliveries equal the oracle's dispatch fold, group by group."""
+    from emqx_amd import Context
+    from emqx_amd.batcher import FanoutGroups, PublishBatcher
+    rng = np.random.default_rng(5)
+    filters = sorted({b"a/#", b"a/+", b"a/b", b"+/b", b"#", b"c/d", b"a/+/c", b"$SYS/#", b"c/+"})
+    subs = [sorted(set(rng.integers(0, 500, size=int(rng.integers(0, 40))).tolist())) for _ in filters]
+    topics = [b"a/b", b"a/x", b"c/d", b"q", b"a/b/c", b"$SYS/a", b"c/e", b"a/+"] * 40
+    with Context(0) as ctx:
+        idx = ctx.build_index(filters, subs=subs)
+        inbox = {i: [] for i in range(500)}
+        b = PublishBatcher(FanoutGroups(ctx, idx, filters), max_batch=64, window_s=0.002, subscribers=inbox)
+        futs = [b.publish(t, k) for k, t in enumerate(topics)]
+        results = [f.result(timeout=60) for f in futs]
+        b.close()
+        assert b.batches >= len(topics) // 64
+        r = orc.Router(True)
+        for f in filters:
+            r.add_route(f)
+        oro, oids, _ = r.match_batch(topics, filters, mode=1)
+        so = np.zeros(len(filters) + 1, np.uint64)
+        so[1:] = np.cumsum([len(s) for s in subs])
+        si = np.array([x for s in subs for x in s] or [0], np.uint32)
+        ero, eids = orc.fanout(oro, oids, so, si)
+        for k, t in enumerate(topics):
+            want = [(filters[f], ("ok", len(subs[f])) if subs[f] else ("error", "no_subscribers"))
+                    for f in oids[oro[k]:oro[k + 1]]]
+            assert results[k] == want, t
+        got = sorted((sid, k) for sid, box in inbox.items() for _, k in box)
+        exp = sorted((int(s), k) for k in range(len(topics)) for s in eids[ero[k]:ero[k + 1]])
+        assert got == exp
+        idx.release()

@@ -4,6 +4,7 @@ Bit-exact for every row: filter ids are lexicographic ranks, rows sorted, so
 equality of (row_off, ids) is equality of lists:sort/1 of the reference result.
 """
 
+import ctypes
 import random
 
 import numpy as np
@@ -410,3 +411,73 @@ def test_fanout_long_rows_ragged(ctx, orc, row):
     ero, eids = orc.fanout(ro, ids, so, si)
     assert np.array_equal(fro, ero) and np.array_equal(fids, eids)
     idx.release()
+
+
+# ------------------------------------------------------------------ fan-out split over devices (C4)
+@pytest.mark.parametrize("n_parts", [1, 2, 3, 8])
+def test_fanout_parts_cover_disjointly(ctx, orc, n_parts):
+    """emqx_gm_fanout_part: the parts are contiguous, disjoint, carry the
+    global row offsets, and concatenated equal the whole fan-out (1/10-scale C4:
+    every part cuts through 100k-wide rows)."""
+    from tests._fanout_part_worker import c4_small
+    from emqx_amd.engine import pack
+    filters, subs, topics = c4_small()
+    idx = ctx.build_index(filters, subs=subs)
+    tb, to = pack(topics)
+    d_tb, d_to = ctx.dev_alloc(len(tb)), ctx.dev_alloc(len(to) * 8)
+    ctx.memcpy_h2d(d_tb, tb, len(tb))
+    ctx.memcpy_h2d(d_to, to, len(to) * 8)
+    m = ctx.match_device(idx, d_tb, d_to, len(topics), exact=True)
+    whole = ctx.fanout_device(idx, m)
+    w_ro, w_ids = whole.rows(0, len(topics))
+    pos, got = 0, []
+    for p in range(n_parts):
+        part, first = ctx.fanout_part(idx, m, p, n_parts)
+        assert first == pos
+        g_ro = np.zeros(len(topics) + 1, np.uint64)
+        ctx.memcpy_d2h(g_ro, ctypes.cast(part.csr.row_off, ctypes.c_void_p).value,
+                       g_ro.nbytes)
+        assert np.array_equal(g_ro, w_ro)
+        if part.nnz:
+            ids = np.zeros(part.nnz, np.uint32)
+            ctx.memcpy_d2h(ids, ctypes.cast(part.csr.ids, ctypes.c_void_p).value,
+                           part.nnz * 4)
+            got.append(ids)
+        pos += part.nnz
+        part.free()
+    assert pos == len(w_ids) == 100 * 100_000
+    assert np.array_equal(np.concatenate(got), w_ids)
+    mro, mids = m.to_host()
+    order = np.argsort(idx.perm)
+    ssorted = [subs[i] for i in order]
+    so = np.zeros(len(filters) + 1, np.uint64)
+    so[1:] = np.cumsum([len(s) for s in ssorted])
+    si = np.array([x for s in ssorted for x in s], np.uint32)
+    ero, eids = orc.fanout(mro, mids, so, si)
+    assert np.array_equal(w_ro, ero) and np.array_equal(w_ids, eids)
+    for x in (whole, m):
+        x.free()
+    ctx.dev_free(d_tb)
+    ctx.dev_free(d_to)
+    idx.release()
+
+
+@pytest.mark.timeout(300)
+def test_fanout_split_two_ranks():
+    """The C4 split as two processes (gloo rank plumbing, both on device 0):
+    rank 0 gathers both parts and checks disjoint, complete coverage against
+    the oracle (tests/_fanout_part_worker.py)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "tests", "_fanout_part_worker.py")]
+    p = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=280,
+                       env=dict(os.environ, PYTHONUNBUFFERED="1"))
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "FANOUT_SPLIT_OK world=2 deliveries=10000000" in p.stdout

@@ -182,3 +182,26 @@ def test_index_compiler_host_c2_scale(orc):
     assert info.n_nodes == len(prefixes) + 1
     assert info.n_edges == len(prefixes)
     assert info.n_filters == len(set(fs)) == 200_000
+
+
+def test_nif_shim_type_checks():
+    """The NIF shim compiles cleanly (-Wall -Wextra -Werror) against the OTP NIF
+    API declarations it uses (tests/nif_stub/erl_nif.h: no Erlang on this
+    image) and the library's public header."""
+    import subprocess
+    p = subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-fsyntax-only",
+                        "-I", os.path.join(ROOT, "tests", "nif_stub"), "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "nif", "emqx_gpu_match_nif.c")], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+
+
+def test_nif_exports_match_erlang_module():
+    """Every NIF function/arity the shim registers is declared by the Erlang
+    module (nif/emqx_gpu_match.erl) and vice versa for the nif_error stubs."""
+    src = open(os.path.join(ROOT, "nif", "emqx_gpu_match_nif.c")).read()
+    nif = set(re.findall(r'\{"([a-z_]+)", (\d), [a-z_]+, ', src))
+    erl = open(os.path.join(ROOT, "nif", "emqx_gpu_match.erl")).read()
+    stubs = set()
+    for name, args in re.findall(r"^([a-z_]+)\(([^)]*)\) -> erlang:nif_error", erl, re.M):
+        stubs.add((name, str(len([a for a in args.split(",") if a.strip()]))))
+    assert nif == stubs, (nif ^ stubs)
