@@ -99,6 +99,23 @@ def barrier(pg):
         pg.barrier()
 
 
+def physical_cores() -> int:
+    """Distinct (physical id, core id) pairs in /proc/cpuinfo."""
+    seen, phys, core = set(), None, None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":", 1)[1].strip()
+                elif not line.strip() and phys is not None:
+                    seen.add((phys, core))
+    except OSError:
+        pass
+    return len(seen) or (os.cpu_count() or 1)
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -111,15 +128,24 @@ def cpu_model() -> str:
 
 
 def cpu_quota():
-    """The cgroup v2 CPU quota of this process (cores), or None when unlimited."""
+    """The cgroup v2 CPU quota of this process (cores), or None when unlimited:
+    the file of its own cgroup, else the namespace root's (a container sees its
+    own cgroup as /sys/fs/cgroup)."""
+    paths = ["/sys/fs/cgroup/cpu.max"]
     try:
         with open("/proc/self/cgroup") as f:
             rel = f.read().strip().split("::", 1)[-1]
-        with open(os.path.join("/sys/fs/cgroup", rel.lstrip("/"), "cpu.max")) as f:
-            q, per = f.read().split()
-        return None if q == "max" else float(q) / float(per)
-    except (OSError, ValueError):
-        return None
+        paths.insert(0, os.path.join("/sys/fs/cgroup", rel.lstrip("/"), "cpu.max"))
+    except OSError:
+        pass
+    for p in paths:
+        try:
+            with open(p) as f:
+                q, per = f.read().split()
+            return None if q == "max" else float(q) / float(per)
+        except (OSError, ValueError):
+            continue
+    return None
 
 
 def oracle_router(filters_packed):
@@ -169,11 +195,16 @@ def cpu_baseline(r, codes, seed, target_s, threads):
     r.match_batch((tb, to[:n1 + 1]), None, mode=1, nthreads=1, want_ids=False)
     single = n1 / (time.perf_counter() - t1)
     quota = cpu_quota()
+    phys = physical_cores()
     return {"value": n / dt, "unit": "topics/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
             "cpu_quota_cores": quota, "single_thread_value": single,
+            # measured value is capped by the cgroup quota when one is set; this is the
+            # single-thread rate scaled to every physical core (an estimate, not a measurement)
+            "linear_estimate_all_physical_cores": {"value": single * phys, "physical_cores": phys},
             "sample": f"first {n} topics of the same seeded stream (seed {seed}), emqx_trie compact walk + "
                       f"lookup_routes restated in C++ (oracle/emqx_oracle.cpp), {threads} std::threads = every "
-                      f"core in this process's affinity mask, {dt:.1f} s; {float(ro[-1]) / n:.3f} matches/topic; "
+                      f"core in this process's affinity mask (cgroup CPU quota: {quota} cores), {dt:.1f} s; "
+                      f"{float(ro[-1]) / n:.3f} matches/topic; "
                       f"{float(lk.mean()) if len(lk) else 0:.1f} ordered-set lookups/topic"}
 
 
