@@ -933,6 +933,202 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
 #undef GM_WILD_ROW
 #undef GM_EMIT
 
+// ---- k_walk_coop: the wave's frontier as one compacted work list ---------
+// k_walk gives every lane its own topic's frontier, so at each level a wave
+// runs as many probe rounds as its LONGEST frontier (C2: ~1.6 entries per
+// topic on average, but the longest of 64 lanes is 3-4) and pays the exec-mask
+// bookkeeping of those divergent rounds.  Here the frontier entries of all 64
+// topics of the tile form one list in LDS, {node | FR_PLUS, signature, topic
+// lane}; every round each lane takes the next entry of the list, so a level
+// costs ceil(entries / 64) rounds with every lane busy.  Children are
+// appended to the next level's list with ballot + mbcnt compaction; matches go
+// to the topic's staging column through an LDS counter per topic (one
+// ds_add_rtn per match).  A topic whose entries do not fit the list, or whose
+// row outgrows FAST_MC, is marked (CW_OVF) and queued for the listed pass
+// like k_walk's overflow.  Same hdr / wids input, same stage / cnt / tile-sum
+// output as k_walk, so the listed pass, the scan and k_assemble are shared.
+constexpr int CW_CAP = 192;                // frontier entries per wave and level
+constexpr uint32_t CW_OVF = 0x40000000u;   // in a topic's LDS match counter: queued for the listed pass
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint32_t lane_prefix(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi(uint32_t(mask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mask), 0u));
+}
+
+template <bool EXACT>
+__global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict__ tb,
+                                                      const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
+                                                      const uint32_t* __restrict__ hdr,
+                                                      const uint32_t* __restrict__ wids, uint32_t* __restrict__ cnt,
+                                                      uint32_t* __restrict__ stage, uint32_t* __restrict__ ovf_list,
+                                                      uint32_t* __restrict__ ovf_n,
+                                                      unsigned long long* __restrict__ probe_tile,
+                                                      unsigned long long* __restrict__ wild_ctr,
+                                                      uint64_t* __restrict__ tsum, uint64_t t_base) {
+  constexpr uint32_t MC = FAST_MC;
+  __shared__ uint2 s_e[4][2][CW_CAP];      // {hot id | FR_PLUS, exact-child signature}
+  __shared__ uint8_t s_ln[4][2][CW_CAP];   // the entry's topic (lane of the tile)
+  __shared__ uint2 s_lw[4][64];            // per topic: {this level's word id, levels | TOK_DOLLAR}
+  __shared__ uint32_t s_mc[4][64];         // per topic: matches emitted | CW_OVF
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t t = t_base + uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  const uint64_t tile = t >> 6;
+  if (tile * 64 >= n) return;  // wave-uniform: no workgroup barrier below
+  const bool valid = t < n;
+  uint32_t* const MCNT = s_mc[wv];
+  uint2* const LW = s_lw[wv];
+  uint32_t* const stile = stage + tile * (64ull * MC);
+
+  const uint32_t h = valid ? hdr[t] : 0u;
+  const uint32_t nlev = h & 0xFFu;
+  const bool dollar = (h & TOK_DOLLAR) != 0, wild = valid && (h & TOK_WILD), deep = valid && (h & TOK_DEEP);
+  const bool walk = valid && !wild && !deep;
+  uint32_t m0 = deep ? CW_OVF : 0u;  // deep topics: the listed pass tokenizes them itself
+  if (wild && EXACT) {  // a wildcard publish topic: the literal route only (emqx_router.erl:128-134)
+    const uint32_t f = literal_lookup(ix, tb, toff[t], toff[t + 1]);
+    if (f != NONE) {
+      stile[lane] = f;
+      m0 = 1;
+    }
+  }
+  if (walk && !dollar && ix.root_hash != NONE) {  // '#' at the virtual root ('$' rule: emqx_trie.erl:271-278)
+    stile[lane] = ix.root_hash;
+    m0 = 1;
+  }
+  MCNT[lane] = m0;
+  uint32_t probes = walk ? 1u : 0u;  // + the exact-route probe
+  // level 0: one root entry per walking topic
+  const unsigned long long bw = __ballot(walk);
+  if (walk) {
+    const uint32_t p = lane_prefix(bw);
+    s_e[wv][0][p] = make_uint2((!dollar && (ix.root_flags & HOT_PLUS)) ? FR_PLUS : 0u, ix.root_sig);
+    s_ln[wv][0][p] = uint8_t(lane);
+  }
+  uint32_t cur_total = uint32_t(__popcll(bw));
+  uint32_t wnext = walk ? wids[t] : NONE;
+  const bool hflat = (ix.flags & IX_HOT_FLAT) != 0;
+  int cur = 0;
+  for (uint32_t level = 0; cur_total; ++level) {
+    LW[lane] = make_uint2(wnext, nlev | (dollar ? TOK_DOLLAR : 0u));
+    if (walk && level + 1 < nlev) wnext = wids[uint64_t(level + 1) * n + t];  // next level's word, in flight
+    wave_lds_sync();
+    const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);
+    const int ht = hot_table(lvl + 1);
+    const HotSlot* tab = ix.hot + ix.hot_off[ht];
+    const HotSlot* ptab = ix.hot + ix.hot_off[hot_table(lvl)];  // the frontier nodes' own table
+    const bool hrh = ht < HOT_TABLES - 1 && (ix.flags & IX_RH_EXIT);
+    const uint64_t cap = ix.hot_cap[ht];
+    const uint32_t capu = uint32_t(cap);
+    const uint32_t fmask = ix.efilt_mask[ht];
+    const uint32_t* ft = ix.efilt + ix.efilt_off[ht];
+    const uint2* E = s_e[wv][cur];
+    const uint8_t* LNc = s_ln[wv][cur];
+    uint2* EN = s_e[wv][cur ^ 1];
+    uint8_t* LNn = s_ln[wv][cur ^ 1];
+    uint32_t nxt_total = 0;
+    for (uint32_t base = 0; base < cur_total; base += 64) {
+      const uint32_t e = base + uint32_t(lane);
+      const bool act = e < cur_total;
+      const uint2 en = act ? E[e] : make_uint2(0u, 0u);
+      const uint32_t tl = act ? LNc[e] : 0u;
+      const uint2 lw = LW[tl];
+      const uint32_t wid = lw.x, id = en.x & ID_MASK;
+      const bool last = act && level + 1 == (lw.y & 0xFFu);
+      const bool ldollar = (lw.y & TOK_DOLLAR) != 0;
+      bool dx = act && wid != NONE && (en.y & sig_bit(wid));
+      if (fmask && dx) {  // the table's exact-edge filter (an L2 hit) before a random line
+        const uint32_t fh = edge_filter_hash(hot_key(id, wid, lvl));
+        const uint32_t fb = edge_filter_bits(fh);
+        dx = (ft[edge_filter_word(fh, fmask)] & fb) == fb;
+      }
+      const bool dp = act && (en.x & FR_PLUS);
+      probes += act ? 3u : 0u;
+      // issue both probes, then resolve
+      uint32_t sx = 0, sp = 0;
+      HotRec rx{}, rp{};
+      const bool pin = dp && plus_is_inline(lvl, id);
+      if (dx) {
+        sx = uint32_t(hot_slot(hot_key(id, wid, lvl), cap));
+        rx = hot_load(tab, sx, last, hflat);
+      }
+      if (pin) {
+        rp = plus_inline_load(ptab, id, hflat);
+      } else if (dp) {
+        sp = uint32_t(hot_slot(hot_key(id, ix.plus_word, lvl), cap));
+        rp = hot_load(tab, sp, last, hflat);
+      }
+      const uint32_t hx = dx ? hot_resolve(tab, capu, hot_key(id, wid, lvl), sx, rx, last, hflat, hrh) : NONE;
+      const uint32_t hp = pin ? (id | HOT_INLINE)
+                              : dp ? hot_resolve(tab, capu, hot_key(id, ix.plus_word, lvl), sp, rp, last, hflat, hrh)
+                                   : NONE;
+      // visits: 'match_#', the end filter on the last level, else the next frontier
+#define GM_CW_EMIT(f)                                   \
+  do {                                                  \
+    const uint32_t k_ = atomicAdd(&MCNT[tl], 1u);       \
+    if (k_ < MC) stile[k_ * 64u + tl] = (f);            \
+  } while (0)
+#define GM_CW_VISIT(r)                                                                          \
+  do {                                                                                          \
+    if (((r).a.w & ID_MASK) != HF_NONE) GM_CW_EMIT((r).a.w & ID_MASK);                          \
+    if (last) {                                                                                 \
+      if ((r).ef != NONE && (EXACT || ((r).ef & END_WILD) || (ldollar && level == 0)))          \
+        GM_CW_EMIT((r).ef & ID_MASK);                                                           \
+      probes += 2u;                                                                             \
+    }                                                                                           \
+  } while (0)
+      if (hx != NONE) GM_CW_VISIT(rx);
+      if (hp != NONE) GM_CW_VISIT(rp);
+#undef GM_CW_VISIT
+#undef GM_CW_EMIT
+      const bool cx = hx != NONE && !last, cp = hp != NONE && !last;
+      const unsigned long long bx = __ballot(cx), bp = __ballot(cp);
+      const uint32_t nx = uint32_t(__popcll(bx));
+      if (cx) {
+        const uint32_t q = nxt_total + lane_prefix(bx);
+        if (q < uint32_t(CW_CAP)) {
+          EN[q] = make_uint2(hx | (rx.a.w & FR_PLUS), rx.a.z);
+          LNn[q] = uint8_t(tl);
+        } else {
+          atomicOr(&MCNT[tl], CW_OVF);
+        }
+      }
+      if (cp) {
+        const uint32_t q = nxt_total + nx + lane_prefix(bp);
+        if (q < uint32_t(CW_CAP)) {
+          EN[q] = make_uint2(hp | (rp.a.w & FR_PLUS), rp.a.z);
+          LNn[q] = uint8_t(tl);
+        } else {
+          atomicOr(&MCNT[tl], CW_OVF);
+        }
+      }
+      nxt_total += nx + uint32_t(__popcll(bp));
+    }
+    cur ^= 1;
+    cur_total = nxt_total < uint32_t(CW_CAP) ? nxt_total : uint32_t(CW_CAP);
+    wave_lds_sync();
+  }
+  wave_lds_sync();
+  const uint32_t m_n = MCNT[lane];
+  const bool ovf = valid && m_n > MC;  // CW_OVF or a row past the staging capacity
+  if (valid) {
+    cnt[t] = ovf ? OVF_BIT : m_n;
+    if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
+  }
+  uint32_t ptot, mtot;
+  wave_excl_scan(probes, ptot);
+  wave_excl_scan(valid && !ovf ? m_n : 0u, mtot);
+  const unsigned long long wb = __ballot(wild);
+  if (lane == 0) {
+    probe_tile[tile] = ptot;
+    tsum[tile] = mtot;
+    if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
+  }
+}
+
 // ---------------------------------------------------------------------------
 // scan (u64, exclusive, n+1 outputs: out[n] = total)
 // ---------------------------------------------------------------------------
@@ -1556,22 +1752,20 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
-// Main-pass kernel selection.  GM_MATCH_MAIN (A/B knob, read once): splitw8
-// (k_tokenize + k_walk with a register budget for 8 waves per SIMD, default),
-// split (budget left to the compiler), split2 (frontier entries expanded in
-// pairs).
-enum MainKind { MAIN_SPLIT, MAIN_SPLITW8, MAIN_SPLIT2 };
+// Main-pass kernel selection.  GM_MATCH_MAIN (A/B knob, read per call so tests
+// cover every kind): coop (k_tokenize + k_walk_coop, the wave's frontier as one
+// compacted list, default), splitw8 (k_tokenize + k_walk, lane-private
+// register frontier, 8-wave register budget), split (budget left to the
+// compiler), split2 (k_walk expanding frontier entries in pairs).
+enum MainKind { MAIN_SPLIT, MAIN_SPLITW8, MAIN_SPLIT2, MAIN_COOP };
 MainKind main_kind() {
-  static const MainKind k = [] {
-    const char* e = getenv("GM_MATCH_MAIN");
-    static const struct { const char* name; MainKind kind; } names[] = {
-        {"split", MAIN_SPLIT}, {"splitw8", MAIN_SPLITW8}, {"split2", MAIN_SPLIT2}};
-    if (e)
-      for (const auto& nk : names)
-        if (!strcmp(e, nk.name)) return nk.kind;
-    return MAIN_SPLITW8;
-  }();
-  return k;
+  const char* e = getenv("GM_MATCH_MAIN");
+  static const struct { const char* name; MainKind kind; } names[] = {
+      {"split", MAIN_SPLIT}, {"splitw8", MAIN_SPLITW8}, {"split2", MAIN_SPLIT2}, {"coop", MAIN_COOP}};
+  if (e)
+    for (const auto& nk : names)
+      if (!strcmp(e, nk.name)) return nk.kind;
+  return MAIN_COOP;
 }
 
 constexpr int LISTED_FC = 16;  // frontier capacity of the listed pass
@@ -1625,6 +1819,10 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
     switch (main_kind()) {                                    \
       case MAIN_SPLIT: GM_LAUNCH_WALK(1, false, sw, g, base); break;  \
       case MAIN_SPLIT2: GM_LAUNCH_WALK(1, true, sw, g, base); break;  \
+      case MAIN_COOP:                                         \
+        hipLaunchKernelGGL((k_walk_coop<EXACT>), dim3(g), dim3(256), 0, sw, tb, to, n, v, hdr, wids, cnt, stage, \
+                           list1, n1, probe_tile, wild_ctr, tsum, base);                                        \
+        break;                                                \
       default: GM_LAUNCH_WALK(8, false, sw, g, base);         \
     }                                                         \
   } while (0)
@@ -1712,7 +1910,7 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   PoolBuf probe_tile(ctx->pool, n_tiles * 8 + 8);
   if (!probe_tile.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: probe workspace");
   PoolBuf hdr, wids;  // split form: per-topic header and word ids [level][topic]
-  if (main_kind() == MAIN_SPLIT || main_kind() == MAIN_SPLITW8 || main_kind() == MAIN_SPLIT2) {
+  {
     hdr = PoolBuf(ctx->pool, n * 4 + 16);
     wids = PoolBuf(ctx->pool, uint64_t(TOK_LMAX) * n * 4 + 16);
     if (!hdr.p || !wids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: word-id workspace");

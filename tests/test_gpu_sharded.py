@@ -165,78 +165,19 @@ def test_sharded_matcher_two_ranks_gloo(tmp_path):
     assert sorted(x for x in os.listdir(tmp_path) if x.startswith("ok")) == ["ok0", "ok1"]
 
 
-class _RecordExchange:
-    """A `dist` stand-in that records what one rank sends in each all_to_all_single."""
-
-    def __init__(self):
-        self.sends = []
-
-    def all_to_all_single(self, out, inp, output_split_sizes=None, input_split_sizes=None, group=None):
-        self.sends.append((inp.clone(), input_split_sizes))
-        out.zero_()
-
-
-class _ReplayExchange:
-    """Rank `rank`'s receive side of the exchange, assembled from every rank's
-    recorded sends: piece p = the part of rank p's send buffer addressed to `rank`."""
-
-    def __init__(self, recorders, rank):
-        self.recorders, self.rank, self.k = recorders, rank, 0
-
-    def all_to_all_single(self, out, inp, output_split_sizes=None, input_split_sizes=None, group=None):
-        import torch
-        chunks = []
-        for rec in self.recorders:
-            t, splits = rec.sends[self.k]
-            if splits is None:
-                size = t.numel() // len(self.recorders)
-                chunks.append(t[self.rank * size:(self.rank + 1) * size])
-            else:
-                off = sum(splits[:self.rank])
-                chunks.append(t[off:off + splits[self.rank]])
-        self.k += 1
-        out.copy_(torch.cat(chunks).to(out.device))
-
-
-def test_device_tensor_path_with_replayed_exchange(ctx, orc):
+def test_device_tensor_path_with_replayed_exchange():
     """ShardedMatcher(device_tensors=True) -- the RCCL code path: the library on
     torch's stream, row lengths and ids in device tensors, bounds from one
     device reduction, the device merge -- run for both ranks of a 2-way shard
     on one device, with the collective itself replayed from the other rank's
     recorded send buffers (two ranks cannot share one GPU under RCCL).  Rank
-    0's merged slice must equal the unsharded index and the oracle."""
-    import torch
-    from emqx_amd.engine import pack
-    from emqx_amd.sharded import ShardedMatcher, plan_shard, slice_bounds
-    fs, ts = _sets("c1")
-    fb, fo = pack(fs)
-    tb, to = pack(ts)
-    d_tb, d_to = _to_device(ctx, tb, to)
-    n, W = len(ts), 2
-    idxs = []
-    for q in range(W):
-        sfb, sfo, gids, _ = plan_shard(fb, fo, W, q)
-        idxs.append(ctx.build_index_shard((sfb, sfo), gids))
-    recs = [_RecordExchange() for _ in range(W)]
-    for q in range(W):
-        res, _, _ = ShardedMatcher(ctx, idxs[q], W, q, dist=recs[q], device_tensors=True).match_device(d_tb, d_to, n)
-        res.free()
-    out, first, rows = ShardedMatcher(ctx, idxs[0], W, 0, dist=_ReplayExchange(recs, 0),
-                                      device_tensors=True).match_device(d_tb, d_to, n)
-    torch.cuda.synchronize()
-    S, b = slice_bounds(n, W)
-    assert (first, rows) == (0, S)
-    mro, mids = out.rows(0, rows)
-    full = ctx.build_index((fb, fo))
-    r = ctx.match_device(full, d_tb, d_to, n, exact=True)
-    fro, fids = r.rows(0, rows)
-    assert np.array_equal(mro, fro) and np.array_equal(mids, fids)
-    oro, oids = _oracle_rows(orc, fs, *pack(ts[:rows]))
-    assert np.array_equal(mro, oro) and np.array_equal(mids, oids)
-    ctx.set_stream(0)
-    for x in (out, r):
-        x.free()
-    for i in idxs + [full]:
-        i.release()
-    ctx.dev_free(d_tb)
-    ctx.dev_free(d_to)
+    0's merged slice must equal the unsharded index and the oracle.  Runs in
+    its own process with torch's device runtime initialised first, the order
+    bench.py uses (tests/_sharded_device_worker.py)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "tests", "_sharded_device_worker.py")], cwd=root,
+                       capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "SHARDED_DEVICE_PATH_OK" in p.stdout
