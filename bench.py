@@ -50,8 +50,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-parity", action="store_true", help="skip the oracle check of the last step's sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    p.add_argument("--host-io", action="store_true",
-                   help="also time one call with host buffers (PCIe-inclusive rate, reported in detail)")
+    p.add_argument("--no-host-io", action="store_true",
+                   help="skip the host-buffer call (PCIe-inclusive rate, reported in detail, never `value`)")
     return p.parse_args()
 
 
@@ -326,16 +326,26 @@ def main():
                    "index_device_bytes": int(idx.info.device_bytes), "index_nodes": int(idx.info.n_nodes),
                    "index_build_s": t_build, "device_ms_per_call": st["total_device_ms"]},
     }
-    if a.host_io and rank == 0:
-        # PCIe-inclusive: topics handed over in host memory, CSR returned to host memory
+    if not a.no_host_io and rank == 0:
+        # PCIe-inclusive, outside the timed region: the same batch handed over in host
+        # memory and its CSR returned in host memory (the NIF's call, gm_host.cpp)
         hb = np.zeros(tbytes + 64, np.uint8)
         ho = np.zeros(n_topics + 1, np.uint64)
         ctx.memcpy_d2h(hb, db, tbytes)
         ctx.memcpy_d2h(ho, do, (n_topics + 1) * 8)
-        t0 = time.perf_counter()
-        hro, hids = ctx.match(idx, (hb, ho), exact=True)
-        out["detail"]["host_io_topics_per_s"] = n_topics / (time.perf_counter() - t0)
-        del hb, ho, hro, hids
+        ctx.match_host(idx, (hb, ho), exact=True).free()  # pinned staging and workers warm
+        best = None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            h = ctx.match_host(idx, (hb, ho), exact=True)
+            dt = time.perf_counter() - t0
+            ok = h.nnz == nnz
+            h.free()
+            best = dt if best is None else min(best, dt)
+        out["detail"]["host_io_topics_per_s"] = n_topics / best
+        out["detail"]["host_io_ms"] = best * 1e3
+        out["detail"]["host_io_nnz_matches_device"] = ok
+        del hb, ho
     # the cpu_baseline leg (oracle): timed on all host cores at N=1, and, outside the
     # timed region, the last step's CSR checked against it on a strided sample
     want_cpu = rank == 0 and world == 1 and not a.no_cpu

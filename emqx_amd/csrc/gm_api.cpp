@@ -2,6 +2,7 @@
 // No C++ exception crosses the ABI; every failure is an EMQX_GM_E* code with
 // the message in emqx_gm_last_error().
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <stdexcept>
@@ -132,6 +133,7 @@ int emqx_gm_close(emqx_gm_ctx* ctx) {
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    gm::free_host_pipe(ctx);
     delete ctx->pool;
     for (auto& e : ctx->ev)
       if (e) hipEventDestroy(e);
@@ -251,6 +253,8 @@ int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb,
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
   if (idx->ov) return gm::run_match_overlay(ctx, idx, tb, to, n, flags, out);
+  if (!(flags & EMQX_GM_DEVICE_IO) && !getenv("GM_HOST_SIMPLE"))  // host buffers: chunked, pipelined
+    return gm::run_match_host(ctx, idx, tb, to, n, flags, out);
   return gm::run_match(ctx, idx, tb, to, n, flags, out);
   GM_GUARD_END(ctx)
 }

@@ -1,0 +1,408 @@
+// gm_host.cpp — emqx_gm_match on HOST buffers: the drop-in path a NIF takes.
+//
+// The reference matches in the publisher's own process on host data
+// (emqx_router:match_routes/1, apps/emqx/src/emqx_router.erl:128-145), so the
+// boundary hands over host topics and expects host rows back.  The batch is
+// cut into chunks (GM_HOST_CHUNK topics, <= 512 MiB of text each) that flow
+// through three slots so that PCIe in, the match kernels and PCIe out of
+// consecutive chunks overlap:
+//
+//   worker threads   stage chunk i+1: validate offsets, copy text, offsets as
+//                    u32 chunk-relative (4 B/topic over PCIe instead of 8)
+//                    into pinned memory
+//   h2d stream       pinned -> device                       (chunk i+1)
+//   ctx stream       u32 -> u64 offsets, the device match (run_match), row
+//                    offsets back to u32                     (chunk i)
+//   d2h stream       rows -> pinned                          (chunk i)
+//   worker threads   unpack rows into the caller-visible CSR: u64 offsets
+//                    rebased by the rows of earlier chunks, ids copied
+//                                                            (chunk i-1)
+//
+// Nothing pageable crosses PCIe and no host thread copies more than its share.
+// The result is the same CSR run_match returns (malloc'd, freed by
+// emqx_gm_csr_free), so the rows are bit-identical to the device-buffer path.
+#include <algorithm>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <future>
+#include <memory>
+#include <queue>
+#include <thread>
+
+#include "gm_internal.h"
+
+namespace gm {
+
+namespace {
+
+class Workers {
+ public:
+  explicit Workers(unsigned n) {
+    for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~Workers() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  unsigned size() const { return unsigned(th_.size()); }
+  std::future<void> submit(std::function<void()> f) {
+    auto task = std::make_shared<std::packaged_task<void()>>(std::move(f));
+    std::future<void> fut = task->get_future();
+    {
+      std::lock_guard<std::mutex> l(m_);
+      q_.push([task] { (*task)(); });
+    }
+    cv_.notify_one();
+    return fut;
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return stop_ || !q_.empty(); });
+        if (stop_ && q_.empty()) return;
+        f = std::move(q_.front());
+        q_.pop();
+      }
+      f();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::queue<std::function<void()>> q_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+};
+
+struct Pinned {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool reserve(size_t b) {
+    if (b <= cap) return true;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t nb = std::max(b, size_t(1) << 20);
+    if (hipHostMalloc(&p, nb, hipHostMallocDefault) != hipSuccess) return false;
+    cap = nb;
+    return true;
+  }
+  ~Pinned() {
+    if (p) hipHostFree(p);
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct Device {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool reserve(size_t b) {
+    if (b <= cap) return true;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t nb = std::max(b, size_t(1) << 20);
+    if (hipMalloc(&p, nb) != hipSuccess) return false;
+    cap = nb;
+    return true;
+  }
+  ~Device() {
+    if (p) hipFree(p);
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+constexpr int SLOTS = 3;
+
+struct Slot {
+  Pinned in_b, in_o, out_o, out_i;  // text, u32 offsets in; u32 row offsets, ids out
+  Device d_b, d_o32, d_o64;
+  hipEvent_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+  std::vector<std::future<void>> out_f;  // this slot's last unpack
+  emqx_gm_csr csr{};                     // device rows of the chunk in flight
+  uint64_t c0 = 0, nc = 0, nbytes = 0, nnz = 0;
+};
+
+uint64_t env_u64(const char* name, uint64_t dflt) {
+  const char* e = getenv(name);
+  return e ? strtoull(e, nullptr, 10) : dflt;
+}
+
+void join(std::vector<std::future<void>>& fs) {
+  for (auto& f : fs)
+    if (f.valid()) f.get();
+  fs.clear();
+}
+
+}  // namespace
+
+struct HostPipe {
+  int device = 0;
+  hipStream_t h2d = nullptr, d2h = nullptr;
+  Slot slot[SLOTS];
+  std::unique_ptr<Workers> w;
+};
+
+void free_host_pipe(emqx_gm_ctx* ctx) {
+  HostPipe* hp = ctx->host;
+  if (!hp) return;
+  hipSetDevice(hp->device);
+  for (auto& s : hp->slot) {
+    join(s.out_f);
+    for (hipEvent_t e : {s.h2d, s.comp, s.d2h})
+      if (e) hipEventDestroy(e);
+  }
+  if (hp->h2d) hipStreamDestroy(hp->h2d);
+  if (hp->d2h) hipStreamDestroy(hp->d2h);
+  delete hp;
+  ctx->host = nullptr;
+}
+
+static int host_pipe(emqx_gm_ctx* ctx, HostPipe** out) {
+  if (!ctx->host) {
+    auto* hp = new HostPipe;
+    hp->device = ctx->device;
+    ctx->host = hp;
+    if (hipStreamCreateWithFlags(&hp->h2d, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&hp->d2h, hipStreamNonBlocking) != hipSuccess)
+      return set_err(ctx, EMQX_GM_EDEVICE, "match: host pipe streams");
+    for (auto& s : hp->slot)
+      for (hipEvent_t* e : {&s.h2d, &s.comp, &s.d2h})
+        if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
+          return set_err(ctx, EMQX_GM_EDEVICE, "match: host pipe events");
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    hp->w.reset(new Workers(unsigned(std::max<uint64_t>(1, env_u64("GM_HOST_THREADS", std::min(16u, hw))))));
+  }
+  *out = ctx->host;
+  return 0;
+}
+
+int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                   uint32_t flags, emqx_gm_csr* out) {
+  HostPipe* hp = nullptr;
+  int rc = host_pipe(ctx, &hp);
+  if (rc) return rc;
+  Workers& W = *hp->w;
+  const uint64_t CH = std::max<uint64_t>(1024, env_u64("GM_HOST_CHUNK", 4u << 20));
+  const uint64_t CB = 512ull << 20;
+  const unsigned T = W.size();
+
+  // the caller-visible result (malloc'd: emqx_gm_csr_free frees it)
+  uint64_t* r_off = static_cast<uint64_t*>(malloc((n + 1) * 8));
+  uint64_t ids_cap = std::max<uint64_t>(1024, n * 4);
+  uint32_t* r_ids = static_cast<uint32_t*>(malloc(ids_cap * 4));
+  if (!r_off || !r_ids) {
+    free(r_off);
+    free(r_ids);
+    return set_err(ctx, EMQX_GM_ENOMEM, "match: host result");
+  }
+  emqx_gm_match_stats tot{};
+  tot.n_topics = n;
+  std::vector<std::future<void>> stage_f;
+  std::atomic<int> bad{0};
+  uint64_t base = 0;  // rows of the chunks before the current one
+  int prev = -1;      // slot of the previous chunk (its device rows are released once copied out)
+
+  auto fail = [&](int code, const char* msg) {
+    join(stage_f);
+    for (auto& s : hp->slot) join(s.out_f);
+    hipStreamSynchronize(hp->h2d);
+    hipStreamSynchronize(ctx->stream);
+    hipStreamSynchronize(hp->d2h);
+    for (auto& s : hp->slot)
+      if (s.csr.row_off || s.csr.ids) {
+        ctx->pool->release(s.csr.row_off);
+        ctx->pool->release(s.csr.ids);
+        s.csr = emqx_gm_csr{};
+      }
+    free(r_off);
+    free(r_ids);
+    return msg ? set_err(ctx, code, msg) : code;  // nullptr: keep the message of the failing step
+  };
+
+  // chunk i = topics [c0, c1): at most CH topics and CB bytes (at least one topic)
+  auto plan = [&](uint64_t c0, uint64_t* c1) -> bool {
+    uint64_t lo = c0 + 1, hi = std::min(n, c0 + CH);
+    if (to[hi] < to[c0] || to[lo] < to[c0]) return false;
+    if (to[hi] - to[c0] > CB) {
+      while (lo < hi) {  // largest c1 with the chunk's text <= CB
+        const uint64_t m = (lo + hi + 1) / 2;
+        if (to[m] >= to[c0] && to[m] - to[c0] <= CB) lo = m;
+        else hi = m - 1;
+      }
+      hi = lo;
+    }
+    *c1 = hi;
+    return to[hi] >= to[c0] && to[hi] - to[c0] < (1ull << 32);
+  };
+
+  // worker-side staging of chunk [c0, c1) into slot s: offsets checked and
+  // rebased to u32, text copied, 64 zero bytes of padding (the tokenizer's slack)
+  auto stage = [&](Slot& s) {
+    const uint64_t c0 = s.c0, nc = s.nc, b0 = to[c0];
+    uint32_t* o = s.in_o.as<uint32_t>();
+    uint8_t* b = s.in_b.as<uint8_t>();
+    const uint64_t parts = nc < 65536 ? 1 : T;
+    for (uint64_t p = 0; p < parts; ++p) {
+      const uint64_t a = c0 + nc * p / parts, e = c0 + nc * (p + 1) / parts;
+      const uint64_t b1 = to[c0 + nc];
+      auto job = [=, &bad] {
+        for (uint64_t j = a; j < e; ++j) {
+          if (to[j + 1] < to[j]) {
+            bad.store(1);
+            return;
+          }
+          o[j - c0] = uint32_t(to[j] - b0);
+        }
+        if (to[a] < b0 || to[e] > b1) {  // inside the chunk's text (plan() checked b0 <= b1)
+          bad.store(1);
+          return;
+        }
+        if (e > a) std::memcpy(b + (to[a] - b0), tb + to[a], to[e] - to[a]);
+        if (e == c0 + nc) {
+          o[nc] = uint32_t(to[e] - b0);
+          std::memset(b + (to[e] - b0), 0, 64);
+        }
+      };
+      if (parts == 1) job();
+      else stage_f.push_back(W.submit(job));
+    }
+  };
+
+  uint64_t c0 = 0, c1 = 0;
+  int i = 0;
+  if (n && !plan(0, &c1)) return fail(EMQX_GM_EINVAL, "match: topic offsets not monotone");
+  // chunk 0: stage and send
+  auto begin_chunk = [&](int k, uint64_t a, uint64_t b) -> int {
+    Slot& s = hp->slot[k];
+    join(s.out_f);  // the slot's last unpack has read its pinned output
+    hipEventSynchronize(s.h2d);  // and its last send has read its pinned input
+    s.c0 = a;
+    s.nc = b - a;
+    s.nbytes = to[b] - to[a];
+    if (!s.in_b.reserve(s.nbytes + 64) || !s.in_o.reserve((s.nc + 1) * 4) || !s.d_b.reserve(s.nbytes + 64) ||
+        !s.d_o32.reserve((s.nc + 1) * 4) || !s.d_o64.reserve((s.nc + 1) * 8) || !s.out_o.reserve((s.nc + 1) * 4))
+      return EMQX_GM_ENOMEM;
+    stage(s);
+    return 0;
+  };
+  auto send_chunk = [&](int k) -> int {
+    Slot& s = hp->slot[k];
+    join(stage_f);
+    if (bad.load()) return EMQX_GM_EINVAL;
+    if (hipMemcpyAsync(s.d_b.p, s.in_b.p, s.nbytes + 64, hipMemcpyHostToDevice, hp->h2d) != hipSuccess ||
+        hipMemcpyAsync(s.d_o32.p, s.in_o.p, (s.nc + 1) * 4, hipMemcpyHostToDevice, hp->h2d) != hipSuccess ||
+        hipEventRecord(s.h2d, hp->h2d) != hipSuccess)
+      return EMQX_GM_EDEVICE;
+    return 0;
+  };
+  if (n) {
+    if ((rc = begin_chunk(0, 0, c1)) || (rc = send_chunk(0)))
+      return fail(rc, rc == EMQX_GM_EINVAL ? "match: topic offsets not monotone" : "match: host pipe chunk 0");
+  }
+  for (c0 = 0; c0 < n; ++i) {
+    const int k = i % SLOTS;
+    Slot& s = hp->slot[k];
+    // stage the next chunk [c1, n1) on the workers while this one [c0, c1) is matched
+    uint64_t n1 = c1;
+    const int kn = (i + 1) % SLOTS;
+    if (c1 < n) {
+      if (!plan(c1, &n1)) return fail(EMQX_GM_EINVAL, "match: topic offsets not monotone");
+      if ((rc = begin_chunk(kn, c1, n1))) return fail(rc, "match: host pipe staging");
+    }
+    // match chunk i on the context's stream once its text is on the device
+    if (hipStreamWaitEvent(ctx->stream, s.h2d, 0) != hipSuccess ||
+        launch_off32_to_64(ctx->stream, s.d_o32.as<uint32_t>(), s.nc + 1, s.d_o64.as<uint64_t>()))
+      return fail(EMQX_GM_EDEVICE, "match: offsets to device");
+    s.csr = emqx_gm_csr{};
+    rc = run_match(ctx, idx, s.d_b.as<uint8_t>(), s.d_o64.as<uint64_t>(), s.nc, flags | EMQX_GM_DEVICE_IO, &s.csr);
+    if (rc) return fail(rc, nullptr);
+    const emqx_gm_match_stats& cs = ctx->stats;
+    tot.nnz += cs.nnz;
+    tot.n_overflow += cs.n_overflow;
+    tot.n_wildcard_topics += cs.n_wildcard_topics;
+    tot.probes += cs.probes;
+    tot.match_kernel_ms += cs.match_kernel_ms;
+    tot.total_device_ms += cs.total_device_ms;
+    s.nnz = s.csr.nnz;
+    if (launch_off64_to_32(ctx->stream, s.csr.row_off, s.nc + 1, s.d_o32.as<uint32_t>()) ||
+        hipEventRecord(s.comp, ctx->stream) != hipSuccess)
+      return fail(EMQX_GM_EDEVICE, "match: row offsets");
+    // rows back to pinned memory on the d2h stream
+    if (!s.out_i.reserve(s.nnz * 4 + 4)) return fail(EMQX_GM_ENOMEM, "match: pinned rows");
+    if (hipStreamWaitEvent(hp->d2h, s.comp, 0) != hipSuccess ||
+        hipMemcpyAsync(s.out_o.p, s.d_o32.p, (s.nc + 1) * 4, hipMemcpyDeviceToHost, hp->d2h) != hipSuccess ||
+        (s.nnz && hipMemcpyAsync(s.out_i.p, s.csr.ids, s.nnz * 4, hipMemcpyDeviceToHost, hp->d2h) != hipSuccess) ||
+        hipEventRecord(s.d2h, hp->d2h) != hipSuccess)
+      return fail(EMQX_GM_EDEVICE, "match: rows to host");
+    // send the next chunk (its staging ran while this one was matched)
+    if (c1 < n && (rc = send_chunk(kn)))
+      return fail(rc, rc == EMQX_GM_EINVAL ? "match: topic offsets not monotone" : "match: host pipe send");
+    // the previous chunk's device rows are in pinned memory once its d2h event fires
+    if (prev >= 0) {
+      Slot& p = hp->slot[prev];
+      hipEventSynchronize(p.d2h);
+      ctx->pool->release(p.csr.row_off);
+      ctx->pool->release(p.csr.ids);
+      p.csr = emqx_gm_csr{};
+    }
+    // unpack chunk i into the result on the workers
+    if (base + s.nnz > ids_cap) {
+      for (auto& q : hp->slot) join(q.out_f);  // nobody writes r_ids while it moves
+      while (ids_cap < base + s.nnz) ids_cap *= 2;
+      uint32_t* g = static_cast<uint32_t*>(realloc(r_ids, ids_cap * 4));
+      if (!g) return fail(EMQX_GM_ENOMEM, "match: host result grow");
+      r_ids = g;
+    }
+    {
+      const uint64_t parts = s.nc < 65536 ? 1 : T;
+      const uint32_t* ro = s.out_o.as<uint32_t>();
+      const uint32_t* ri = s.out_i.as<uint32_t>();
+      const hipEvent_t ev = s.d2h;
+      const uint64_t sc0 = s.c0, snc = s.nc, sbase = base;
+      uint32_t* dst_ids = r_ids;
+      for (uint64_t p = 0; p < parts; ++p) {
+        const uint64_t a = snc * p / parts, e = snc * (p + 1) / parts;
+        s.out_f.push_back(W.submit([=] {
+          hipEventSynchronize(ev);
+          for (uint64_t j = a; j < e; ++j) r_off[sc0 + j] = sbase + ro[j];
+          if (e > a) std::memcpy(dst_ids + sbase + ro[a], ri + ro[a], uint64_t(ro[e] - ro[a]) * 4);
+        }));
+      }
+    }
+    base += s.nnz;
+    prev = k;
+    c0 = c1;
+    c1 = n1;
+  }
+  for (auto& q : hp->slot) join(q.out_f);
+  if (prev >= 0) {
+    Slot& p = hp->slot[prev];
+    hipEventSynchronize(p.d2h);
+    ctx->pool->release(p.csr.row_off);
+    ctx->pool->release(p.csr.ids);
+    p.csr = emqx_gm_csr{};
+  }
+  r_off[n] = base;
+  if (n == 0) r_off[0] = 0;
+  tot.nnz = base;
+  ctx->stats = tot;
+  out->n_rows = n;
+  out->nnz = base;
+  out->row_off = r_off;
+  out->ids = r_ids;
+  out->on_device = 0;
+  out->priv = nullptr;
+  return 0;
+}
+
+}  // namespace gm

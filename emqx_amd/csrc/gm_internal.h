@@ -70,8 +70,13 @@ constexpr uint32_t CNT_MASK = 0x7FFFFFFFu;
 
 }  // namespace gm
 
+namespace gm {
+struct HostPipe;  // gm_host.cpp: pinned staging + copy streams + worker threads of the host-buffer path
+}
+
 struct emqx_gm_ctx {
   int device = 0;
+  gm::HostPipe* host = nullptr;
   hipStream_t stream = nullptr;
   bool own_stream = false;
   hipStream_t stream2 = nullptr;  // tokenizer stream of the overlapped match (GM_OVERLAP)
@@ -145,6 +150,13 @@ void free_overlay(emqx_gm_index* idx);
 int run_match_overlay(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                       uint32_t flags, emqx_gm_csr* out);
 int set_err(emqx_gm_ctx* ctx, int code, const std::string& msg);
+// gm_match.hip: offset conversions of the host-buffer path (n1 = entries)
+int launch_off32_to_64(hipStream_t st, const uint32_t* in, uint64_t n1, uint64_t* out);
+int launch_off64_to_32(hipStream_t st, const uint64_t* in, uint64_t n1, uint32_t* out);
+// gm_host.cpp: emqx_gm_match on host buffers, chunked and pipelined (H2D / match / D2H overlap)
+int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                   uint32_t flags, emqx_gm_csr* out);
+void free_host_pipe(emqx_gm_ctx* ctx);
 }  // namespace gm
 
 #define GM_HIP(ctx, expr)                                                                     \

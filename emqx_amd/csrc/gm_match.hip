@@ -45,6 +45,20 @@ namespace gm {
 // device helpers
 // ---------------------------------------------------------------------------
 
+// Stream accesses (topic text, word ids, headers, staging, counts, the CSR)
+// touch each byte once; NT = non-temporal, so they do not evict the index
+// tables from L2 / the Infinity Cache (GM_NT knob, A/B).
+template <bool NT, class T>
+__device__ __forceinline__ T ld_s(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, class T>
+__device__ __forceinline__ void st_s(T* p, T v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 // Byte reader over a lane's topic with an 8-byte cache (aligned 8-B loads;
 // topic buffers are padded, emqx_gpu_match.h).
 struct ByteReader {
@@ -630,7 +644,7 @@ __device__ __forceinline__ uint32_t tokenize_staged(const uint64_t* lds, uint32_
 // (head, hash, start | len << 16; staged text is < 64 KiB) until it resolves.
 // Same hdr/wids as tokenize_topic: levels past TOK_LMAX are only counted
 // and checked for wildcards.
-template <int G>
+template <int G, bool NT>
 __device__ __forceinline__ uint32_t tokenize_grouped(const uint64_t* lds, uint32_t pos, uint32_t end,
                                                      const IndexView& ix, const uint8_t* tb_lo, uint64_t n,
                                                      uint32_t* __restrict__ wp) {
@@ -669,7 +683,7 @@ __device__ __forceinline__ uint32_t tokenize_grouped(const uint64_t* lds, uint32
         w.start = sl[g] & 0xFFFFu;
         w.len = sl[g] >> 16;
         w.b0 = uint32_t(hd[g] & 0xFF);
-        *wp = dict_resolve(ix, w, d[g], tb_lo);
+        st_s<NT>(wp, dict_resolve(ix, w, d[g], tb_lo));
         wp += n;
         ++lev;
       }
@@ -729,7 +743,7 @@ __device__ __forceinline__ uint32_t tokenize_topic(RD& rd, uint64_t pos, uint64_
 // at every 8-byte boundary); a longer block reads global memory directly.
 constexpr int TOK_STAGE = 16384;
 
-template <int G>
+template <int G, bool NT>
 __global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ toff,
                                                   uint64_t n, IndexView ix, uint32_t* __restrict__ hdr,
                                                   uint32_t* __restrict__ wids, uint64_t t_base) {
@@ -741,7 +755,7 @@ __global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb
   const bool staged = hi - lo <= uint64_t(TOK_STAGE) - 8;  // block-uniform
   if (staged) {
     const uint64_t nw = ((hi - lo + 7) >> 3) + 1;  // topic buffers are padded by 64 bytes
-    for (uint64_t i = threadIdx.x; i < nw; i += 256) s_txt[i] = *reinterpret_cast<const uint64_t*>(tb + lo + 8 * i);
+    for (uint64_t i = threadIdx.x; i < nw; i += 256) s_txt[i] = ld_s<NT>(reinterpret_cast<const uint64_t*>(tb + lo + 8 * i));
   }
   __syncthreads();
   if (t >= n) return;
@@ -751,12 +765,12 @@ __global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb
     if constexpr (G == 1)
       h = tokenize_staged(s_txt, uint32_t(pos - lo), uint32_t(end - lo), ix, tb + lo, n, wids + t);
     else
-      h = tokenize_grouped<G>(s_txt, uint32_t(pos - lo), uint32_t(end - lo), ix, tb + lo, n, wids + t);
+      h = tokenize_grouped<G, NT>(s_txt, uint32_t(pos - lo), uint32_t(end - lo), ix, tb + lo, n, wids + t);
   } else {
     ByteReader rd{tb, ~0ull, 0};
     h = tokenize_topic(rd, pos, end, ix, tb, n, t, wids);
   }
-  hdr[t] = h;
+  st_s<NT>(hdr + t, h);
 }
 
 // k_walk: the NFA walk over pre-resolved word ids, frontier in registers as
@@ -959,7 +973,7 @@ __device__ __forceinline__ uint32_t lane_prefix(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(uint32_t(mask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mask), 0u));
 }
 
-template <bool EXACT>
+template <bool EXACT, bool NT>
 __global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict__ tb,
                                                       const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
                                                       const uint32_t* __restrict__ hdr,
@@ -983,7 +997,7 @@ __global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict_
   uint2* const LW = s_lw[wv];
   uint32_t* const stile = stage + tile * (64ull * MC);
 
-  const uint32_t h = valid ? hdr[t] : 0u;
+  const uint32_t h = valid ? ld_s<NT>(hdr + t) : 0u;
   const uint32_t nlev = h & 0xFFu;
   const bool dollar = (h & TOK_DOLLAR) != 0, wild = valid && (h & TOK_WILD), deep = valid && (h & TOK_DEEP);
   const bool walk = valid && !wild && !deep;
@@ -1009,12 +1023,12 @@ __global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict_
     s_ln[wv][0][p] = uint8_t(lane);
   }
   uint32_t cur_total = uint32_t(__popcll(bw));
-  uint32_t wnext = walk ? wids[t] : NONE;
+  uint32_t wnext = walk ? ld_s<NT>(wids + t) : NONE;
   const bool hflat = (ix.flags & IX_HOT_FLAT) != 0;
   int cur = 0;
   for (uint32_t level = 0; cur_total; ++level) {
     LW[lane] = make_uint2(wnext, nlev | (dollar ? TOK_DOLLAR : 0u));
-    if (walk && level + 1 < nlev) wnext = wids[uint64_t(level + 1) * n + t];  // next level's word, in flight
+    if (walk && level + 1 < nlev) wnext = ld_s<NT>(wids + uint64_t(level + 1) * n + t);  // next level's word, in flight
     wave_lds_sync();
     const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);
     const int ht = hot_table(lvl + 1);
@@ -1069,7 +1083,7 @@ __global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict_
 #define GM_CW_EMIT(f)                                   \
   do {                                                  \
     const uint32_t k_ = atomicAdd(&MCNT[tl], 1u);       \
-    if (k_ < MC) stile[k_ * 64u + tl] = (f);            \
+    if (k_ < MC) st_s<NT>(stile + k_ * 64u + tl, (f));  \
   } while (0)
 #define GM_CW_VISIT(r)                                                                          \
   do {                                                                                          \
@@ -1115,7 +1129,7 @@ __global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict_
   const uint32_t m_n = MCNT[lane];
   const bool ovf = valid && m_n > MC;  // CW_OVF or a row past the staging capacity
   if (valid) {
-    cnt[t] = ovf ? OVF_BIT : m_n;
+    st_s<NT>(cnt + t, ovf ? OVF_BIT : m_n);
     if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
   }
   uint32_t ptot, mtot;
@@ -1705,6 +1719,28 @@ __global__ __launch_bounds__(256) void k_ov_merge(const uint64_t* __restrict__ b
   }
 }
 
+// Offsets of the host-buffer path: topics cross PCIe with u32 chunk-relative
+// offsets (4 B per topic instead of 8) and rows come back the same way.
+__global__ __launch_bounds__(256) void k_off32_to_64(const uint32_t* __restrict__ in, uint64_t n1,
+                                                     uint64_t* __restrict__ out) {
+  for (uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x; i < n1; i += uint64_t(gridDim.x) * 256u) out[i] = in[i];
+}
+__global__ __launch_bounds__(256) void k_off64_to_32(const uint64_t* __restrict__ in, uint64_t n1,
+                                                     uint32_t* __restrict__ out) {
+  for (uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x; i < n1; i += uint64_t(gridDim.x) * 256u)
+    out[i] = uint32_t(in[i]);
+}
+int launch_off32_to_64(hipStream_t st, const uint32_t* in, uint64_t n1, uint64_t* out) {
+  const uint64_t g = std::min<uint64_t>(2048, (n1 + 255) / 256);
+  hipLaunchKernelGGL(k_off32_to_64, dim3(g ? g : 1), dim3(256), 0, st, in, n1, out);
+  return hipGetLastError() == hipSuccess ? 0 : EMQX_GM_EDEVICE;
+}
+int launch_off64_to_32(hipStream_t st, const uint64_t* in, uint64_t n1, uint32_t* out) {
+  const uint64_t g = std::min<uint64_t>(2048, (n1 + 255) / 256);
+  hipLaunchKernelGGL(k_off64_to_32, dim3(g ? g : 1), dim3(256), 0, st, in, n1, out);
+  return hipGetLastError() == hipSuccess ? 0 : EMQX_GM_EDEVICE;
+}
+
 // Sum of per-tile counters into one (one atomic per wave of a small grid).
 __global__ __launch_bounds__(256) void k_sum_tiles(const unsigned long long* __restrict__ a, uint64_t n,
                                                    unsigned long long* __restrict__ acc) {
@@ -1780,13 +1816,27 @@ int tok_group() {
   return (v == 1 || v == 5) ? v : 3;
 }
 
+// Non-temporal stream accesses.  GM_NT (A/B knob, read per call): 1 = the
+// topic text, word ids, headers, staging and counts as nt loads / stores.
+bool nt_streams() {
+  const char* e = getenv("GM_NT");
+  return e && atoi(e) != 0;
+}
+
 void launch_tokenize(hipStream_t st, uint64_t nblk, const uint8_t* tb, const uint64_t* to, uint64_t n,
                      const IndexView& v, uint32_t* hdr, uint32_t* wids, uint64_t t_base) {
+  const bool nt = nt_streams();
+#define GM_TOK(G)                                                                                          \
+  do {                                                                                                     \
+    if (nt) hipLaunchKernelGGL((k_tokenize<G, true>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, t_base); \
+    else hipLaunchKernelGGL((k_tokenize<G, false>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, t_base); \
+  } while (0)
   switch (tok_group()) {
-    case 1: hipLaunchKernelGGL(k_tokenize<1>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, t_base); break;
-    case 5: hipLaunchKernelGGL(k_tokenize<5>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, t_base); break;
-    default: hipLaunchKernelGGL(k_tokenize<3>, dim3(nblk), dim3(256), 0, st, tb, to, n, v, hdr, wids, t_base);
+    case 1: GM_TOK(1); break;
+    case 5: GM_TOK(5); break;
+    default: GM_TOK(3);
   }
+#undef GM_TOK
 }
 
 // Tokenize / walk overlap.  GM_OVERLAP = K (A/B knob, read per call; 1 = off):
@@ -1820,8 +1870,12 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
       case MAIN_SPLIT: GM_LAUNCH_WALK(1, false, sw, g, base); break;  \
       case MAIN_SPLIT2: GM_LAUNCH_WALK(1, true, sw, g, base); break;  \
       case MAIN_COOP:                                         \
-        hipLaunchKernelGGL((k_walk_coop<EXACT>), dim3(g), dim3(256), 0, sw, tb, to, n, v, hdr, wids, cnt, stage, \
-                           list1, n1, probe_tile, wild_ctr, tsum, base);                                        \
+        if (nt_streams())                                     \
+          hipLaunchKernelGGL((k_walk_coop<EXACT, true>), dim3(g), dim3(256), 0, sw, tb, to, n, v, hdr, wids, cnt, \
+                             stage, list1, n1, probe_tile, wild_ctr, tsum, base);                                 \
+        else                                                  \
+          hipLaunchKernelGGL((k_walk_coop<EXACT, false>), dim3(g), dim3(256), 0, sw, tb, to, n, v, hdr, wids, cnt, \
+                             stage, list1, n1, probe_tile, wild_ctr, tsum, base);                                  \
         break;                                                \
       default: GM_LAUNCH_WALK(8, false, sw, g, base);         \
     }                                                         \

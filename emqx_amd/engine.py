@@ -88,6 +88,26 @@ class DeviceCsr:
             pass
 
 
+class HostCsr:
+    """A result CSR in host memory owned by the library (emqx_gm_match without
+    DEVICE_IO); ``row_off`` / ``ids`` are views valid until ``free()``."""
+
+    def __init__(self, ctx: "Context", csr: Csr):
+        self.ctx, self.csr = ctx, csr
+        n, nnz = int(csr.n_rows), int(csr.nnz)
+        self.row_off = np.ctypeslib.as_array(csr.row_off, shape=(n + 1,))
+        self.ids = np.ctypeslib.as_array(csr.ids, shape=(nnz,)) if nnz else np.zeros(0, np.uint32)
+
+    @property
+    def nnz(self) -> int:
+        return int(self.csr.nnz)
+
+    def free(self):
+        if self.csr.row_off or self.csr.ids:
+            self.row_off = self.ids = None
+            lib().emqx_gm_csr_free(self.ctx.h, C.byref(self.csr))
+
+
 class Index:
     """An immutable, reference-counted index snapshot resident in HBM."""
 
@@ -220,6 +240,16 @@ class Context:
             return _csr_to_numpy(csr)
         finally:
             lib().emqx_gm_csr_free(self.h, C.byref(csr))
+
+    def match_host(self, index: Index, topics, exact: bool = True) -> "HostCsr":
+        """Host buffers in, host rows out (the NIF's call), without copying the
+        result: numpy views of the library's buffers, valid until ``free()``."""
+        tb, to = topics if isinstance(topics, tuple) else pack(topics)
+        csr = Csr()
+        flags = _lib.WITH_EXACT if exact else 0
+        check(lib().emqx_gm_match(self.h, index.h, _ptr(tb), _ptr(to), len(to) - 1, flags, C.byref(csr)),
+              self.h, "match")
+        return HostCsr(self, csr)
 
     def match_device(self, index: Index, d_bytes: int, d_off: int, n: int, exact: bool = True) -> DeviceCsr:
         """Inputs already in HBM (device pointers); the result stays in HBM."""

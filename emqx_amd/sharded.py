@@ -57,7 +57,8 @@ def exchange_rows(dist, lens, ids, id_bounds: Sequence[int], world: int, group=N
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc, group=group)
     recv_counts = [int(x) for x in rc.tolist()]
-    recv_ids = torch.empty(sum(recv_counts), dtype=torch.int32, device=dev)
+    # never a NULL buffer, also when nothing is received (the merge takes a device pointer)
+    recv_ids = torch.empty(max(sum(recv_counts), 1), dtype=torch.int32, device=dev)[:sum(recv_counts)]
     dist.all_to_all_single(recv_ids, ids, output_split_sizes=recv_counts, input_split_sizes=send_counts,
                            group=group)
     recv_lens = torch.empty_like(lens)

@@ -481,3 +481,53 @@ def test_fanout_split_two_ranks():
                        env=dict(os.environ, PYTHONUNBUFFERED="1"))
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     assert "FANOUT_SPLIT_OK world=2 deliveries=9901000" in p.stdout
+
+
+# ------------------------------------------------------------------ host-buffer path (gm_host.cpp)
+@pytest.mark.parametrize("chunk", ["1024", "5000", "4194304"])
+def test_host_path_chunks_equal_device_path(ctx, orc, monkeypatch, chunk):
+    """emqx_gm_match on host buffers -- chunked (GM_HOST_CHUNK topics), staged
+    through pinned memory with u32 chunk-relative offsets, three chunks in
+    flight -- gives the rows of one DEVICE_IO call over the same batch, which
+    a strided sample ties to the oracle.  Small chunks put many chunk
+    boundaries (and partial last chunks) in one call."""
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    codes = gen_filter_codes(7, 20_000)
+    fb, fo = render_codes(codes)
+    filters = sorted(set(orc.unpack(fb, fo)))
+    idx = ctx.build_index(filters)
+    n = 300_007
+    tb, to = orc.render_codes(orc.gen_topic_codes(7, 0, n, codes))
+    tb = np.concatenate([tb, np.zeros(64, np.uint8)])
+    monkeypatch.setenv("GM_HOST_CHUNK", chunk)
+    ro, ids = ctx.match(idx, (tb, to), exact=True)
+    d_tb, d_to = ctx.dev_alloc(len(tb)), ctx.dev_alloc(len(to) * 8)
+    ctx.memcpy_h2d(d_tb, tb, len(tb))
+    ctx.memcpy_h2d(d_to, to, len(to) * 8)
+    res = ctx.match_device(idx, d_tb, d_to, n, exact=True)
+    dro, dids = res.to_host()
+    assert np.array_equal(ro, dro) and np.array_equal(ids, dids)
+    sample = list(range(0, n, 1009)) + [n - 1]
+    topics = orc.unpack(tb, to)
+    oro, oids = _oracle_rows(orc, filters, [topics[i] for i in sample], 1)
+    for j, i in enumerate(sample):
+        assert ids[ro[i]:ro[i + 1]].tolist() == oids[oro[j]:oro[j + 1]].tolist()
+    res.free()
+    ctx.dev_free(d_tb)
+    ctx.dev_free(d_to)
+    idx.release()
+
+
+def test_host_path_rejects_bad_offsets_and_survives(ctx):
+    """Non-monotone host offsets -> EINVAL with a message (no GPU fault, no
+    partial result), and the context keeps working afterwards."""
+    from emqx_amd._lib import GpuMatchError
+    idx = ctx.build_index([b"a/+", b"b/#"])
+    tb = np.frombuffer(b"a/xb/yb" + b"\0" * 64, np.uint8).copy()
+    bad = np.array([0, 3, 2, 7], np.uint64)
+    with pytest.raises(GpuMatchError) as e:
+        ctx.match(idx, (tb, bad), exact=True)
+    assert "monotone" in str(e.value)
+    ro, ids = ctx.match(idx, (tb, np.array([0, 3, 6, 7], np.uint64)), exact=True)
+    assert ro.tolist() == [0, 1, 2, 3] and ids.tolist() == [0, 1, 1]  # a/x; b/y, b via b/#
+    idx.release()
