@@ -3,11 +3,11 @@
 // The reference matches in the publisher's own process on host data
 // (emqx_router:match_routes/1, apps/emqx/src/emqx_router.erl:128-145), so the
 // boundary hands over host topics and expects host rows back.  The batch is
-// cut into chunks (GM_HOST_CHUNK topics, <= 512 MiB of text each) that flow
-// through three slots so that PCIe in, the match kernels and PCIe out of
+// cut into chunks (256K..4M topics, <= 512 MiB of text each) that flow
+// through four slots so that PCIe in, the match kernels and PCIe out of
 // consecutive chunks overlap:
 //
-//   worker threads   stage chunk i+1: validate offsets, copy text, offsets as
+//   worker threads   stage chunk i+2: validate offsets, copy text, offsets as
 //                    u32 chunk-relative (4 B/topic over PCIe instead of 8)
 //                    into pinned memory
 //   h2d stream       pinned -> device                       (chunk i+1)
@@ -121,11 +121,11 @@ struct Device {
   template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
-constexpr int SLOTS = 3;
+constexpr int SLOTS = 4;
 
 struct Slot {
   Pinned in_b, in_o, out_o, out_i;  // text, u32 offsets in; u32 row offsets, ids out
-  Device d_b, d_o32, d_o64;
+  Device d_b, d_o32, d_o64, d_r32;  // text, offsets u32 -> u64 in; row offsets u32 out
   hipEvent_t h2d = nullptr, comp = nullptr, d2h = nullptr;
   std::vector<std::future<void>> out_f;  // this slot's last unpack
   emqx_gm_csr csr{};                     // device rows of the chunk in flight
@@ -192,7 +192,10 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
   int rc = host_pipe(ctx, &hp);
   if (rc) return rc;
   Workers& W = *hp->w;
-  const uint64_t CH = std::max<uint64_t>(1024, env_u64("GM_HOST_CHUNK", 4u << 20));
+  // chunks: ~6 per call (so PCIe in, the kernels and PCIe out overlap) of
+  // 256K..4M topics; GM_HOST_CHUNK pins the size (tests)
+  const uint64_t CH = std::max<uint64_t>(
+      1024, env_u64("GM_HOST_CHUNK", std::min<uint64_t>(4u << 20, std::max<uint64_t>(256u << 10, n / 6))));
   const uint64_t CB = 512ull << 20;
   const unsigned T = W.size();
 
@@ -278,25 +281,34 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
     }
   };
 
-  uint64_t c0 = 0, c1 = 0;
-  int i = 0;
-  if (n && !plan(0, &c1)) return fail(EMQX_GM_EINVAL, "match: topic offsets not monotone");
-  // chunk 0: stage and send
-  auto begin_chunk = [&](int k, uint64_t a, uint64_t b) -> int {
-    Slot& s = hp->slot[k];
-    join(s.out_f);  // the slot's last unpack has read its pinned output
+  // chunk boundaries (plan() validates the offsets it relies on)
+  std::vector<uint64_t> cb{0};
+  while (cb.back() < n) {
+    uint64_t c1 = 0;
+    if (!plan(cb.back(), &c1)) return fail(EMQX_GM_EINVAL, "match: topic offsets not monotone");
+    cb.push_back(c1);
+  }
+  const int m = int(cb.size()) - 1;
+  // input side of a slot: pinned text/offsets -> device text/offsets (busy from
+  // staging until its chunk is matched); output side: device row offsets ->
+  // pinned rows (busy until its unpack ran).  Chunk i+2 is staged while i+1
+  // crosses PCIe and i is matched, so the h2d stream never waits for the CPU.
+  auto begin_chunk = [&](int i) -> int {
+    Slot& s = hp->slot[i % SLOTS];
+    join(s.out_f);               // the slot's last unpack has read its pinned rows
     hipEventSynchronize(s.h2d);  // and its last send has read its pinned input
-    s.c0 = a;
-    s.nc = b - a;
-    s.nbytes = to[b] - to[a];
+    s.c0 = cb[i];
+    s.nc = cb[i + 1] - cb[i];
+    s.nbytes = to[cb[i + 1]] - to[cb[i]];
     if (!s.in_b.reserve(s.nbytes + 64) || !s.in_o.reserve((s.nc + 1) * 4) || !s.d_b.reserve(s.nbytes + 64) ||
-        !s.d_o32.reserve((s.nc + 1) * 4) || !s.d_o64.reserve((s.nc + 1) * 8) || !s.out_o.reserve((s.nc + 1) * 4))
+        !s.d_o32.reserve((s.nc + 1) * 4) || !s.d_o64.reserve((s.nc + 1) * 8) || !s.d_r32.reserve((s.nc + 1) * 4) ||
+        !s.out_o.reserve((s.nc + 1) * 4))
       return EMQX_GM_ENOMEM;
     stage(s);
     return 0;
   };
-  auto send_chunk = [&](int k) -> int {
-    Slot& s = hp->slot[k];
+  auto send_chunk = [&](int i) -> int {
+    Slot& s = hp->slot[i % SLOTS];
     join(stage_f);
     if (bad.load()) return EMQX_GM_EINVAL;
     if (hipMemcpyAsync(s.d_b.p, s.in_b.p, s.nbytes + 64, hipMemcpyHostToDevice, hp->h2d) != hipSuccess ||
@@ -305,20 +317,16 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
       return EMQX_GM_EDEVICE;
     return 0;
   };
-  if (n) {
-    if ((rc = begin_chunk(0, 0, c1)) || (rc = send_chunk(0)))
-      return fail(rc, rc == EMQX_GM_EINVAL ? "match: topic offsets not monotone" : "match: host pipe chunk 0");
-  }
-  for (c0 = 0; c0 < n; ++i) {
-    const int k = i % SLOTS;
-    Slot& s = hp->slot[k];
-    // stage the next chunk [c1, n1) on the workers while this one [c0, c1) is matched
-    uint64_t n1 = c1;
-    const int kn = (i + 1) % SLOTS;
-    if (c1 < n) {
-      if (!plan(c1, &n1)) return fail(EMQX_GM_EINVAL, "match: topic offsets not monotone");
-      if ((rc = begin_chunk(kn, c1, n1))) return fail(rc, "match: host pipe staging");
-    }
+  auto pipe_err = [](int code) {
+    return code == EMQX_GM_EINVAL ? "match: topic offsets not monotone"
+                                  : code == EMQX_GM_ENOMEM ? "match: pinned staging" : "match: host pipe copy";
+  };
+  if (m > 0 && ((rc = begin_chunk(0)) || (rc = send_chunk(0)))) return fail(rc, pipe_err(rc));
+  if (m > 1 && (rc = begin_chunk(1))) return fail(rc, pipe_err(rc));
+  for (int i = 0; i < m; ++i) {
+    Slot& s = hp->slot[i % SLOTS];
+    if (i + 1 < m && (rc = send_chunk(i + 1))) return fail(rc, pipe_err(rc));  // queued behind chunk i's send
+    if (i + 2 < m && (rc = begin_chunk(i + 2))) return fail(rc, pipe_err(rc));  // staged on the workers meanwhile
     // match chunk i on the context's stream once its text is on the device
     if (hipStreamWaitEvent(ctx->stream, s.h2d, 0) != hipSuccess ||
         launch_off32_to_64(ctx->stream, s.d_o32.as<uint32_t>(), s.nc + 1, s.d_o64.as<uint64_t>()))
@@ -334,19 +342,16 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
     tot.match_kernel_ms += cs.match_kernel_ms;
     tot.total_device_ms += cs.total_device_ms;
     s.nnz = s.csr.nnz;
-    if (launch_off64_to_32(ctx->stream, s.csr.row_off, s.nc + 1, s.d_o32.as<uint32_t>()) ||
+    if (launch_off64_to_32(ctx->stream, s.csr.row_off, s.nc + 1, s.d_r32.as<uint32_t>()) ||
         hipEventRecord(s.comp, ctx->stream) != hipSuccess)
       return fail(EMQX_GM_EDEVICE, "match: row offsets");
     // rows back to pinned memory on the d2h stream
     if (!s.out_i.reserve(s.nnz * 4 + 4)) return fail(EMQX_GM_ENOMEM, "match: pinned rows");
     if (hipStreamWaitEvent(hp->d2h, s.comp, 0) != hipSuccess ||
-        hipMemcpyAsync(s.out_o.p, s.d_o32.p, (s.nc + 1) * 4, hipMemcpyDeviceToHost, hp->d2h) != hipSuccess ||
+        hipMemcpyAsync(s.out_o.p, s.d_r32.p, (s.nc + 1) * 4, hipMemcpyDeviceToHost, hp->d2h) != hipSuccess ||
         (s.nnz && hipMemcpyAsync(s.out_i.p, s.csr.ids, s.nnz * 4, hipMemcpyDeviceToHost, hp->d2h) != hipSuccess) ||
         hipEventRecord(s.d2h, hp->d2h) != hipSuccess)
       return fail(EMQX_GM_EDEVICE, "match: rows to host");
-    // send the next chunk (its staging ran while this one was matched)
-    if (c1 < n && (rc = send_chunk(kn)))
-      return fail(rc, rc == EMQX_GM_EINVAL ? "match: topic offsets not monotone" : "match: host pipe send");
     // the previous chunk's device rows are in pinned memory once its d2h event fires
     if (prev >= 0) {
       Slot& p = hp->slot[prev];
@@ -380,9 +385,7 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
       }
     }
     base += s.nnz;
-    prev = k;
-    c0 = c1;
-    c1 = n1;
+    prev = i % SLOTS;
   }
   for (auto& q : hp->slot) join(q.out_f);
   if (prev >= 0) {

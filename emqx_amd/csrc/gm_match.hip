@@ -644,10 +644,29 @@ __device__ __forceinline__ uint32_t tokenize_staged(const uint64_t* lds, uint32_
 // (head, hash, start | len << 16; staged text is < 64 KiB) until it resolves.
 // Same hdr/wids as tokenize_topic: levels past TOK_LMAX are only counted
 // and checked for wildcards.
-template <int G, bool NT>
+// Where the word ids of one topic go: level-major HBM for k_walk / k_walk_coop,
+// registers for the fused kernel.  Called for levels 0, 1, 2, ... in order.
+template <bool NT>
+struct WidsToHbm {
+  uint32_t* wp;  // wids + t
+  uint64_t n;
+  __device__ __forceinline__ void operator()(uint32_t, uint32_t v) {
+    st_s<NT>(wp, v);
+    wp += n;
+  }
+};
+struct WidsToRegs {
+  uint32_t (&w)[TOK_LMAX];
+  __device__ __forceinline__ void operator()(uint32_t lev, uint32_t v) {
+#pragma unroll
+    for (int q = 0; q < TOK_LMAX; ++q)
+      if (lev == uint32_t(q)) w[q] = v;
+  }
+};
+
+template <int G, class SINK>
 __device__ __forceinline__ uint32_t tokenize_grouped(const uint64_t* lds, uint32_t pos, uint32_t end,
-                                                     const IndexView& ix, const uint8_t* tb_lo, uint64_t n,
-                                                     uint32_t* __restrict__ wp) {
+                                                     const IndexView& ix, const uint8_t* tb_lo, SINK&& sink) {
   uint32_t lev = 0, fl = 0;
   bool more = true, wild = false;
   while (more && lev < uint32_t(TOK_LMAX)) {
@@ -683,8 +702,7 @@ __device__ __forceinline__ uint32_t tokenize_grouped(const uint64_t* lds, uint32
         w.start = sl[g] & 0xFFFFu;
         w.len = sl[g] >> 16;
         w.b0 = uint32_t(hd[g] & 0xFF);
-        st_s<NT>(wp, dict_resolve(ix, w, d[g], tb_lo));
-        wp += n;
+        sink(lev, dict_resolve(ix, w, d[g], tb_lo));
         ++lev;
       }
     }
@@ -706,10 +724,9 @@ __device__ __forceinline__ uint32_t tokenize_grouped(const uint64_t* lds, uint32
 
 // One topic: words -> dictionary ids, the next word's first dictionary slot
 // loaded while this word resolves.
-template <class RD>
+template <class RD, class SINK>
 __device__ __forceinline__ uint32_t tokenize_topic(RD& rd, uint64_t pos, uint64_t end, const IndexView& ix,
-                                                   const uint8_t* tb, uint64_t n, uint64_t t,
-                                                   uint32_t* __restrict__ wids) {
+                                                   const uint8_t* tb, SINK&& sink) {
   uint32_t lev = 0, fl = 0;
   WordTok w = next_word(rd, pos, end);
   DictSlot d = dict_first(ix, w);
@@ -727,7 +744,7 @@ __device__ __forceinline__ uint32_t tokenize_topic(RD& rd, uint64_t pos, uint64_
       wn = next_word(rd, pos, end);
       dn = dict_first(ix, wn);
     }
-    if (lev < TOK_LMAX) wids[uint64_t(lev) * n + t] = dict_resolve(ix, w, d, tb);
+    if (lev < TOK_LMAX) sink(lev, dict_resolve(ix, w, d, tb));
     ++lev;
     if (!more) break;
     w = wn;
@@ -765,10 +782,10 @@ __global__ __launch_bounds__(256) void k_tokenize(const uint8_t* __restrict__ tb
     if constexpr (G == 1)
       h = tokenize_staged(s_txt, uint32_t(pos - lo), uint32_t(end - lo), ix, tb + lo, n, wids + t);
     else
-      h = tokenize_grouped<G, NT>(s_txt, uint32_t(pos - lo), uint32_t(end - lo), ix, tb + lo, n, wids + t);
+      h = tokenize_grouped<G>(s_txt, uint32_t(pos - lo), uint32_t(end - lo), ix, tb + lo, WidsToHbm<NT>{wids + t, n});
   } else {
     ByteReader rd{tb, ~0ull, 0};
-    h = tokenize_topic(rd, pos, end, ix, tb, n, t, wids);
+    h = tokenize_topic(rd, pos, end, ix, tb, WidsToHbm<NT>{wids + t, n});
   }
   st_s<NT>(hdr + t, h);
 }
@@ -973,31 +990,31 @@ __device__ __forceinline__ uint32_t lane_prefix(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(uint32_t(mask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mask), 0u));
 }
 
-template <bool EXACT, bool NT>
-__global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict__ tb,
-                                                      const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
-                                                      const uint32_t* __restrict__ hdr,
-                                                      const uint32_t* __restrict__ wids, uint32_t* __restrict__ cnt,
-                                                      uint32_t* __restrict__ stage, uint32_t* __restrict__ ovf_list,
-                                                      uint32_t* __restrict__ ovf_n,
-                                                      unsigned long long* __restrict__ probe_tile,
-                                                      unsigned long long* __restrict__ wild_ctr,
-                                                      uint64_t* __restrict__ tsum, uint64_t t_base) {
-  constexpr uint32_t MC = FAST_MC;
-  __shared__ uint2 s_e[4][2][CW_CAP];      // {hot id | FR_PLUS, exact-child signature}
-  __shared__ uint8_t s_ln[4][2][CW_CAP];   // the entry's topic (lane of the tile)
-  __shared__ uint2 s_lw[4][64];            // per topic: {this level's word id, levels | TOK_DOLLAR}
-  __shared__ uint32_t s_mc[4][64];         // per topic: matches emitted | CW_OVF
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t t = t_base + uint64_t(blockIdx.x) * 256u + threadIdx.x;
-  const uint64_t tile = t >> 6;
-  if (tile * 64 >= n) return;  // wave-uniform: no workgroup barrier below
-  const bool valid = t < n;
-  uint32_t* const MCNT = s_mc[wv];
-  uint2* const LW = s_lw[wv];
-  uint32_t* const stile = stage + tile * (64ull * MC);
+// One wave's walk over its 64-topic tile (k_walk_coop and k_match_fused).
+// h = the topic's tokenizer header; WORDS yields the topic's word id of
+// level 0 (first()) and of the next level (next(level)); the LDS arrays are
+// the wave's own.
+struct CoopLds {
+  uint2 e[2][CW_CAP];      // {hot id | FR_PLUS, exact-child signature}
+  uint8_t ln[2][CW_CAP];   // the entry's topic (lane of the tile)
+  uint2 lw[64];            // per topic: {this level's word id, levels | TOK_DOLLAR}
+  uint32_t mc[64];         // per topic: matches emitted | CW_OVF
+};
 
-  const uint32_t h = valid ? ld_s<NT>(hdr + t) : 0u;
+template <bool EXACT, bool NT, class WORDS>
+__device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& words, bool valid, uint64_t t,
+                                               int lane, const uint8_t* __restrict__ tb,
+                                               const uint64_t* __restrict__ toff, const IndexView& ix,
+                                               uint32_t* __restrict__ cnt, uint32_t* __restrict__ stage,
+                                               uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
+                                               unsigned long long* __restrict__ probe_tile,
+                                               unsigned long long* __restrict__ wild_ctr,
+                                               uint64_t* __restrict__ tsum) {
+  constexpr uint32_t MC = FAST_MC;
+  const uint64_t tile = t >> 6;
+  uint32_t* const MCNT = L.mc;
+  uint2* const LW = L.lw;
+  uint32_t* const stile = stage + tile * (64ull * MC);
   const uint32_t nlev = h & 0xFFu;
   const bool dollar = (h & TOK_DOLLAR) != 0, wild = valid && (h & TOK_WILD), deep = valid && (h & TOK_DEEP);
   const bool walk = valid && !wild && !deep;
@@ -1019,16 +1036,16 @@ __global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict_
   const unsigned long long bw = __ballot(walk);
   if (walk) {
     const uint32_t p = lane_prefix(bw);
-    s_e[wv][0][p] = make_uint2((!dollar && (ix.root_flags & HOT_PLUS)) ? FR_PLUS : 0u, ix.root_sig);
-    s_ln[wv][0][p] = uint8_t(lane);
+    L.e[0][p] = make_uint2((!dollar && (ix.root_flags & HOT_PLUS)) ? FR_PLUS : 0u, ix.root_sig);
+    L.ln[0][p] = uint8_t(lane);
   }
   uint32_t cur_total = uint32_t(__popcll(bw));
-  uint32_t wnext = walk ? ld_s<NT>(wids + t) : NONE;
+  uint32_t wnext = walk ? words.first() : NONE;
   const bool hflat = (ix.flags & IX_HOT_FLAT) != 0;
   int cur = 0;
   for (uint32_t level = 0; cur_total; ++level) {
     LW[lane] = make_uint2(wnext, nlev | (dollar ? TOK_DOLLAR : 0u));
-    if (walk && level + 1 < nlev) wnext = ld_s<NT>(wids + uint64_t(level + 1) * n + t);  // next level's word, in flight
+    if (walk && level + 1 < nlev) wnext = words.next(level);  // next level's word, in flight
     wave_lds_sync();
     const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);
     const int ht = hot_table(lvl + 1);
@@ -1039,10 +1056,10 @@ __global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict_
     const uint32_t capu = uint32_t(cap);
     const uint32_t fmask = ix.efilt_mask[ht];
     const uint32_t* ft = ix.efilt + ix.efilt_off[ht];
-    const uint2* E = s_e[wv][cur];
-    const uint8_t* LNc = s_ln[wv][cur];
-    uint2* EN = s_e[wv][cur ^ 1];
-    uint8_t* LNn = s_ln[wv][cur ^ 1];
+    const uint2* E = L.e[cur];
+    const uint8_t* LNc = L.ln[cur];
+    uint2* EN = L.e[cur ^ 1];
+    uint8_t* LNn = L.ln[cur ^ 1];
     uint32_t nxt_total = 0;
     for (uint32_t base = 0; base < cur_total; base += 64) {
       const uint32_t e = base + uint32_t(lane);
@@ -1141,6 +1158,100 @@ __global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict_
     tsum[tile] = mtot;
     if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
   }
+}
+
+
+struct WordsFromHbm {  // k_walk_coop: the tokenizer's level-major word ids
+  const uint32_t* wp;  // wids + t
+  uint64_t n;
+  bool nt;
+  __device__ __forceinline__ uint32_t first() { return nt ? __builtin_nontemporal_load(wp) : *wp; }
+  __device__ __forceinline__ uint32_t next(uint32_t level) {
+    const uint32_t* p = wp + uint64_t(level + 1) * n;
+    return nt ? __builtin_nontemporal_load(p) : *p;
+  }
+};
+
+template <bool EXACT, bool NT>
+__global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict__ tb,
+                                                      const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
+                                                      const uint32_t* __restrict__ hdr,
+                                                      const uint32_t* __restrict__ wids, uint32_t* __restrict__ cnt,
+                                                      uint32_t* __restrict__ stage, uint32_t* __restrict__ ovf_list,
+                                                      uint32_t* __restrict__ ovf_n,
+                                                      unsigned long long* __restrict__ probe_tile,
+                                                      unsigned long long* __restrict__ wild_ctr,
+                                                      uint64_t* __restrict__ tsum, uint64_t t_base) {
+  __shared__ CoopLds s_w[4];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t t = t_base + uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if ((t >> 6) * 64 >= n) return;  // wave-uniform: no workgroup barrier below
+  const bool valid = t < n;
+  const uint32_t h = valid ? ld_s<NT>(hdr + t) : 0u;
+  WordsFromHbm words{wids + (valid ? t : 0), n, NT};
+  coop_walk_tile<EXACT, NT>(s_w[wv], h, words, valid, t, lane, tb, toff, ix, cnt, stage, ovf_list, ovf_n, probe_tile,
+                            wild_ctr, tsum);
+}
+
+// ---- k_match_fused: tokenize + coop walk in one kernel --------------------
+// The block stages its topics' text in LDS and each lane tokenizes its topic
+// into REGISTERS (word ids of up to TOK_LMAX levels, the header); then each
+// wave walks its tile as k_walk_coop does, in the same LDS.  The word ids
+// and headers never go through HBM (k_tokenize + k_walk_coop write and read
+// back ~48 B per C2 topic of them), and the tokenizer's ALU work of one wave
+// overlaps the walk's gathers of the others.
+struct WordsFromRegs {
+  uint32_t (&w)[TOK_LMAX];
+  __device__ __forceinline__ uint32_t first() { return w[0]; }
+  __device__ __forceinline__ uint32_t next(uint32_t) {  // shift the levels down: w[0] = the next level's word
+#pragma unroll
+    for (int q = 0; q + 1 < TOK_LMAX; ++q) w[q] = w[q + 1];
+    return w[0];
+  }
+};
+
+constexpr size_t FUSED_LDS = sizeof(CoopLds) * 4 > (TOK_STAGE + 8) ? sizeof(CoopLds) * 4 : (TOK_STAGE + 8);
+
+template <int G, bool EXACT, bool NT>
+__global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restrict__ tb,
+                                                        const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
+                                                        uint32_t* __restrict__ cnt, uint32_t* __restrict__ stage,
+                                                        uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
+                                                        unsigned long long* __restrict__ probe_tile,
+                                                        unsigned long long* __restrict__ wild_ctr,
+                                                        uint64_t* __restrict__ tsum) {
+  __shared__ __align__(16) uint8_t s_raw[FUSED_LDS];  // the staged text, then the walk's lists
+  uint64_t* const s_txt = reinterpret_cast<uint64_t*>(s_raw);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t t0 = uint64_t(blockIdx.x) * 256u;
+  const uint64_t t = t0 + threadIdx.x;
+  const uint64_t tl = t0 + 256 < n ? t0 + 256 : n;
+  const uint64_t lo = toff[t0] & ~7ull, hi = toff[tl];
+  const bool staged = hi - lo <= uint64_t(TOK_STAGE) - 8;  // block-uniform
+  if (staged) {
+    const uint64_t nw = ((hi - lo + 7) >> 3) + 1;  // topic buffers are padded by 64 bytes
+    for (uint64_t i = threadIdx.x; i < nw; i += 256) s_txt[i] = ld_s<NT>(reinterpret_cast<const uint64_t*>(tb + lo + 8 * i));
+  }
+  __syncthreads();
+  const bool valid = t < n;
+  uint32_t w[TOK_LMAX];
+#pragma unroll
+  for (int q = 0; q < TOK_LMAX; ++q) w[q] = NONE;
+  uint32_t h = 0;
+  if (valid) {
+    const uint64_t pos = toff[t], end = toff[t + 1];
+    if (staged) {
+      h = tokenize_grouped<G>(s_txt, uint32_t(pos - lo), uint32_t(end - lo), ix, tb + lo, WidsToRegs{w});
+    } else {
+      ByteReader rd{tb, ~0ull, 0};
+      h = tokenize_topic(rd, pos, end, ix, tb, WidsToRegs{w});
+    }
+  }
+  __syncthreads();  // every lane is done with the staged text: the walk reuses the LDS
+  if ((t >> 6) * 64 >= n) return;  // wave-uniform, after the last workgroup barrier
+  WordsFromRegs words{w};
+  coop_walk_tile<EXACT, NT>(reinterpret_cast<CoopLds*>(s_raw)[wv], h, words, valid, t, lane, tb, toff, ix, cnt, stage,
+                            ovf_list, ovf_n, probe_tile, wild_ctr, tsum);
 }
 
 // ---------------------------------------------------------------------------
@@ -1793,11 +1904,12 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
 // compacted list, default), splitw8 (k_tokenize + k_walk, lane-private
 // register frontier, 8-wave register budget), split (budget left to the
 // compiler), split2 (k_walk expanding frontier entries in pairs).
-enum MainKind { MAIN_SPLIT, MAIN_SPLITW8, MAIN_SPLIT2, MAIN_COOP };
+enum MainKind { MAIN_SPLIT, MAIN_SPLITW8, MAIN_SPLIT2, MAIN_COOP, MAIN_FUSED };
 MainKind main_kind() {
   const char* e = getenv("GM_MATCH_MAIN");
   static const struct { const char* name; MainKind kind; } names[] = {
-      {"split", MAIN_SPLIT}, {"splitw8", MAIN_SPLITW8}, {"split2", MAIN_SPLIT2}, {"coop", MAIN_COOP}};
+      {"split", MAIN_SPLIT}, {"splitw8", MAIN_SPLITW8}, {"split2", MAIN_SPLIT2}, {"coop", MAIN_COOP},
+      {"fused", MAIN_FUSED}};
   if (e)
     for (const auto& nk : names)
       if (!strcmp(e, nk.name)) return nk.kind;
@@ -1888,7 +2000,14 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
   }
   for (int i = 0; K > 1 && i <= K; ++i)
     if (!ctx->ov_ev[i] && hipEventCreateWithFlags(&ctx->ov_ev[i], hipEventDisableTiming) != hipSuccess) K = 1;
-  if (K == 1) {
+  if (main_kind() == MAIN_FUSED) {
+    if (nt_streams())
+      hipLaunchKernelGGL((k_match_fused<3, EXACT, true>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, list1,
+                         n1, probe_tile, wild_ctr, tsum);
+    else
+      hipLaunchKernelGGL((k_match_fused<3, EXACT, false>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage,
+                         list1, n1, probe_tile, wild_ctr, tsum);
+  } else if (K == 1) {
     launch_tokenize(st, nblk, tb, to, n, v, hdr, wids, 0);
     GM_WALK(st, nblk, 0ull);
   } else {
@@ -1963,8 +2082,8 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
     return set_err(ctx, EMQX_GM_ENOMEM, "match: workspace");
   PoolBuf probe_tile(ctx->pool, n_tiles * 8 + 8);
   if (!probe_tile.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: probe workspace");
-  PoolBuf hdr, wids;  // split form: per-topic header and word ids [level][topic]
-  {
+  PoolBuf hdr, wids;  // split forms: per-topic header and word ids [level][topic] (the fused kernel keeps them in registers)
+  if (main_kind() != MAIN_FUSED) {
     hdr = PoolBuf(ctx->pool, n * 4 + 16);
     wids = PoolBuf(ctx->pool, uint64_t(TOK_LMAX) * n * 4 + 16);
     if (!hdr.p || !wids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: word-id workspace");

@@ -120,7 +120,8 @@ class ShardedMatcher:
         rl, ri = exchange_rows(self.dist, lens, ids, bounds, W, self.group)
         self.last_exchange_bytes = 4 * (W * S + int(nnz))
         if self.device_tensors:
-            out = ctx.merge_rows(b[r + 1] - b[r], S, W, rl.data_ptr(), ri.data_ptr())
+            # the storage pointer: a tensor with no elements reports data_ptr() 0
+            out = ctx.merge_rows(b[r + 1] - b[r], S, W, rl.data_ptr(), ri.untyped_storage().data_ptr())
         else:
             nl, ni = rl.numel() * 4, max(ri.numel(), 1) * 4
             d_l, d_i = ctx.dev_alloc(nl), ctx.dev_alloc(ni)

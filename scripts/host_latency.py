@@ -15,6 +15,7 @@ sys.path.insert(0, ROOT)
 from emqx_amd import Context  # noqa: E402
 from emqx_amd.engine import gen_filter_codes, render_codes  # noqa: E402
 
+MODE = os.environ.get("LAT_MODE", "both")  # both | host | device
 sizes = [int(x) for x in (sys.argv[1:] or ["1000", "10000", "100000", "1000000", "10000000", "100000000"])]
 ctx = Context(0)
 codes = gen_filter_codes(1, 1_000_000, wildcard_only=True)
@@ -27,18 +28,24 @@ for n in sizes:
     ctx.memcpy_d2h(ho, do, (n + 1) * 8)
     host, dev = [], []
     for k in range(9):
-        t0 = time.perf_counter()
-        h = ctx.match_host(idx, (hb, ho))
-        t1 = time.perf_counter()
-        h.free()
-        r = ctx.match_device(idx, db, do, n)
-        t2 = time.perf_counter()
-        r.free()
-        if k >= 2:
-            host.append(t1 - t0)
-            dev.append(t2 - t1)
-    mh, md = statistics.median(host), statistics.median(dev)
-    print(json.dumps({"topics": n, "host_io_ms": mh * 1e3, "host_io_topics_per_s": n / mh,
+        if MODE != "device":
+            t0 = time.perf_counter()
+            h = ctx.match_host(idx, (hb, ho))
+            t1 = time.perf_counter()
+            h.free()
+            if k >= 2:
+                host.append(t1 - t0)
+        if MODE != "host":
+            t1 = time.perf_counter()
+            r = ctx.match_device(idx, db, do, n)
+            ctx.synchronize()
+            t2 = time.perf_counter()
+            r.free()
+            if k >= 2:
+                dev.append(t2 - t1)
+    mh = statistics.median(host) if host else float("nan")
+    md = statistics.median(dev) if dev else float("nan")
+    print(json.dumps({"mode": MODE, "topics": n, "host_io_ms": mh * 1e3, "host_io_topics_per_s": n / mh,
                       "device_io_ms": md * 1e3, "device_io_topics_per_s": n / md}), flush=True)
     ctx.dev_free(db)
     ctx.dev_free(do)
