@@ -12,8 +12,8 @@ Multi-GPU (weak scaling): one process per GPU, replicated index, each rank
 matches its own 100M-topic slice; no collective on the data path.  `value` is
 the topics of all ranks / the max-over-ranks wall time.
 
-Also reported: a roofline object for the dominant kernels (k_tokenize +
-k_walk, algorithmic bytes per SURVEY.md §8d ÷ their HIP-event time), a CPU
+Also reported: a roofline object for the dominant kernel (k_match_fused:
+tokenizer + trie walk, algorithmic bytes per SURVEY.md §8d ÷ its HIP-event time), a CPU
 baseline (the oracle's faithful emqx_trie restatement -- compact mode, ordered
 key table, fresh prefix strings -- on every core of the process's affinity
 mask over a bounded sample of the same topic stream) and `parity_sample`: the
@@ -294,7 +294,7 @@ def main():
 
     ms_per_step = elapsed * 1000.0 / a.steps
     value = world * n_topics * a.steps / elapsed
-    # algorithmic bytes of one match call's k_tokenize + k_walk:
+    # algorithmic bytes of one match call's main pass, k_match_fused:
     #   B = Σ len(topic) + 8·n (offsets) + 16·P + Σ_matches (4 + len f) + 8·n (row offsets)
     algo = tbytes + 8 * n_topics + 16 * st["probes"] + 4 * nnz + fbytes_matched + 8 * n_topics
     kavg = sum(kern_ms) / len(kern_ms)
@@ -320,7 +320,7 @@ def main():
         "matches_per_sec": world * nnz * a.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_tokenize+k_walk", "kernel_ms": kavg, "algo_bytes_per_launch": algo},
+                     "kernel": "k_match_fused", "kernel_ms": kavg, "algo_bytes_per_launch": algo},
         "detail": {"nnz_per_step": nnz, "matches_per_topic": nnz / n_topics, "probes_per_topic": st["probes"] /
                    n_topics, "overflow_rows": st["n_overflow"], "topic_bytes": tbytes,
                    "index_device_bytes": int(idx.info.device_bytes), "index_nodes": int(idx.info.n_nodes),

@@ -11,6 +11,7 @@
 // Layout (gm_common.h): nodes are numbered breadth-first so the hot upper
 // levels of the trie are contiguous in HBM and stay resident in L2/MALL.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -417,6 +418,16 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
         }
   }
 
+  if (getenv("GM_INDEX_STATS")) {  // diagnostics: the hot tables' sizes (stderr)
+    uint64_t inl_n = 0;
+    for (uint64_t i = 1; i < NN; ++i) inl_n += inl[i];
+    fprintf(stderr, "[gm_index] nodes %llu, inline '+' nodes %llu\n", (unsigned long long)NN,
+            (unsigned long long)inl_n);
+    for (int t = 0; t < HOT_TABLES; ++t)
+      if (hot_n[t])
+        fprintf(stderr, "[gm_index] hot table %d: %llu slots used of %llu (%.1f MB)\n", t,
+                (unsigned long long)hot_n[t], (unsigned long long)hot_cap[t], hot_cap[t] * 32.0 / 1e6);
+  }
   // ---- 3c. exact-edge filters (gm_common.h), for tables whose parents have
   // on average >= 4 exact children and whose filter fits 4 MB
   std::vector<uint64_t> ex_edges(HOT_TABLES, 0), ex_parents(HOT_TABLES, 0);

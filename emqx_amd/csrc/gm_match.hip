@@ -1900,10 +1900,12 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
 }
 
 // Main-pass kernel selection.  GM_MATCH_MAIN (A/B knob, read per call so tests
-// cover every kind): coop (k_tokenize + k_walk_coop, the wave's frontier as one
-// compacted list, default), splitw8 (k_tokenize + k_walk, lane-private
-// register frontier, 8-wave register budget), split (budget left to the
-// compiler), split2 (k_walk expanding frontier entries in pairs).
+// cover every kind): fused (k_match_fused: tokenizer into registers + the
+// compacted wave walk in one kernel, default; C2 10.2 ms vs 12.0 for the
+// split coop pair), coop (k_tokenize + k_walk_coop, the wave's frontier as
+// one compacted list), splitw8 (k_tokenize + k_walk, lane-private register
+// frontier, 8-wave register budget), split (budget left to the compiler),
+// split2 (k_walk expanding frontier entries in pairs).
 enum MainKind { MAIN_SPLIT, MAIN_SPLITW8, MAIN_SPLIT2, MAIN_COOP, MAIN_FUSED };
 MainKind main_kind() {
   const char* e = getenv("GM_MATCH_MAIN");
@@ -1913,7 +1915,7 @@ MainKind main_kind() {
   if (e)
     for (const auto& nk : names)
       if (!strcmp(e, nk.name)) return nk.kind;
-  return MAIN_COOP;
+  return MAIN_FUSED;
 }
 
 constexpr int LISTED_FC = 16;  // frontier capacity of the listed pass
@@ -1928,11 +1930,12 @@ int tok_group() {
   return (v == 1 || v == 5) ? v : 3;
 }
 
-// Non-temporal stream accesses.  GM_NT (A/B knob, read per call): 1 = the
-// topic text, word ids, headers, staging and counts as nt loads / stores.
+// Non-temporal stream accesses.  GM_NT (A/B knob, read per call): the topic
+// text, word ids, headers, staging and counts as nt loads / stores (default;
+// C2: 12.15 -> 12.03 ms for the split pair, 10.45 -> 10.24 ms fused), 0 = plain.
 bool nt_streams() {
   const char* e = getenv("GM_NT");
-  return e && atoi(e) != 0;
+  return !e || atoi(e) != 0;
 }
 
 void launch_tokenize(hipStream_t st, uint64_t nblk, const uint8_t* tb, const uint64_t* to, uint64_t n,
