@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
 TOPICS=${TOPICS:-100000000}
-ARGS="bench.py --topics $TOPICS --steps 2 --warmup 1 --no-cpu"
+ARGS="bench.py --topics $TOPICS --steps 2 --warmup 1 --no-cpu --no-parity --no-host-io"
 run() {  # run <name> <timeout> <rocprof args...>
   local name=$1 t=$2; shift 2
   echo "=== $name"

@@ -49,7 +49,7 @@ def per_launch_sum(path, kernels, min_grid):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("prof", nargs="?", default=os.path.join(ROOT, "gpurun_out", "prof"))
-    p.add_argument("--kernel", default="k_tokenize,k_walk", help="comma-separated kernels of one match call")
+    p.add_argument("--kernel", default="k_match_fused", help="comma-separated kernels of one match call")
     p.add_argument("--topics", type=int, default=100_000_000)
     p.add_argument("--config", default="c2")
     p.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic.json"))
