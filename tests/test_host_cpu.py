@@ -205,3 +205,18 @@ def test_nif_exports_match_erlang_module():
     for name, args in re.findall(r"^([a-z_]+)\(([^)]*)\) -> erlang:nif_error", erl, re.M):
         stubs.add((name, str(len([a for a in args.split(",") if a.strip()]))))
     assert nif == stubs, (nif ^ stubs)
+
+
+def test_host_compiler_under_asan():
+    """The host index compiler (gm_index.cpp) and the overlay id mapping
+    (gm_overlay.cpp) built with AddressSanitizer + UBSan and fed random,
+    empty, NUL-laden, 65,535-byte and 5,000-level filters (SURVEY.md §5;
+    tests/asan/asan_host_compiler.cpp): no sanitizer report, every input gets
+    a valid id."""
+    import subprocess
+    b = subprocess.run(["make", "-C", os.path.join(ROOT, "emqx_amd", "csrc"), "asan"], capture_output=True, text=True)
+    assert b.returncode == 0, b.stderr[-3000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    p = subprocess.run([os.path.join(ROOT, "tests", "asan", "asan_host_compiler")], capture_output=True, text=True,
+                       env=env, timeout=300)
+    assert p.returncode == 0 and "ASAN_HOST_CHECK_OK" in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
