@@ -3,14 +3,20 @@
 // Hot path (replaces emqx_trie:match/1 + emqx_router:match_routes/1,
 // apps/emqx/src/emqx_trie.erl:147-333, apps/emqx/src/emqx_router.erl:128-145):
 //
-//   k_match_reg    main pass: one lane per publish topic, 64 topics per wave
-//                  (a tile).  Streams the topic bytes once, hashes each level
-//                  word, resolves it in the word dictionary (verified
-//                  byte-for-byte) and expands the NFA frontier over exact /
-//                  '+' / '#' edges.  The frontier lives in registers (no LDS),
-//                  so occupancy is bounded by VGPRs alone; visiting a node is
-//                  one 32-B hot-slot load (edge probe and node record in one).
-//                  Matches are staged per tile as [slot][lane].
+//   k_match_fused  main pass (default): a block stages its 256 topics' text in
+//                  LDS; each lane splits its topic into words, hashes them and
+//                  resolves them in the word dictionary (verified
+//                  byte-for-byte) into registers; then each wave walks its
+//                  64-topic tile with the frontier of all 64 topics as ONE
+//                  compacted LDS work list (ballot + mbcnt), one entry per
+//                  lane per round: an exact probe and a '+' probe per entry,
+//                  each one 16-B raw buffer load of a 32-B hot slot (edge probe
+//                  and node record in one line).  Matches are staged per tile
+//                  as [slot][lane].
+//   k_tokenize + k_walk_coop / k_walk
+//                  the same work as two kernels through HBM word ids (A/B
+//                  forms, GM_MATCH_MAIN; k_walk keeps a lane-private frontier
+//                  in registers).
 //   k_match_lds    the same walk with the frontier in LDS (capacity FC).  As
 //                  the LISTED pass it re-walks the topics whose frontier or
 //                  row outgrew the main pass (count read on the device, so no
