@@ -442,7 +442,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   uint32_t efilt_mask[HOT_TABLES] = {0};
   for (int t = 0; t < HOT_TABLES; ++t) {
     if (getenv("GM_NO_EDGE_FILTER")) break;  // A/B knob
-    if (!ex_edges[t] || ex_edges[t] < 4 * ex_parents[t]) continue;
+    if (!ex_edges[t] || (ex_edges[t] < 4 * ex_parents[t] && !getenv("GM_EFILT_ALL"))) continue;  // A/B knob
     const uint64_t words = std::max<uint64_t>(32, next_pow2(ex_edges[t] / 2 + 1));  // 16-32 bits per key
     if (words * 4 > (4ull << 20)) continue;
     efilt_off[t] = efilt_total;
