@@ -97,7 +97,6 @@ struct alignas(32) HotSlot {
 // inline '+' child's record.
 // Read-only view of one index resident in HBM (passed by value to kernels).
 constexpr uint32_t IX_HOT_FLAT = 1u;  // a hot table reaches 2 GiB: flat loads instead of buffer loads
-constexpr uint32_t IX_RH_EXIT = 2u;   // lookups of absent keys use the Robin Hood early exit
 struct IndexView {
   const Node* nodes;
   const DictSlot* dict;
@@ -123,6 +122,7 @@ struct IndexView {
   uint32_t root_hash;   // filter id of "#", or NONE
   uint32_t root_flags;  // HOT_PLUS if "+" starts a filter
   uint32_t flags;       // IX_* below
+  uint32_t rh_mask;     // bit t: hot table t is Robin Hood ordered (absent keys may exit early)
 };
 
 GM_HD uint64_t fmix64(uint64_t k) {
@@ -243,5 +243,17 @@ GM_HD uint32_t edge_filter_hash(uint64_t key) {
 }
 GM_HD uint32_t edge_filter_bits(uint32_t h) { return (1u << (h & 31)) | (1u << ((h >> 5) & 31)); }
 GM_HD uint32_t edge_filter_word(uint32_t h, uint32_t mask) { return (h >> 10) & mask; }
+
+// In-place update (gm_overlay.cpp, patch_update): a filter-id field under the
+// renumbering rmap[old id] -> new id (NONE: deleted).  `none` is the field's
+// empty value (NONE or HF_NONE) and `flag` the flag bit it carries (END_WILD,
+// HOT_PLUS, or 0 for the level-trie fields).
+GM_HD uint32_t renum_field(uint32_t f, uint32_t none, uint32_t flag, const uint32_t* rmap) {
+  if (f == none) return f;
+  const uint32_t fl = f & flag, id = f & ~flag;
+  if (id == (none & ~flag)) return f;
+  const uint32_t r = rmap[id];
+  return r == NONE ? (fl ? (fl | (none & ~flag)) : none) : (fl | r);
+}
 
 }  // namespace gm

@@ -323,10 +323,11 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (uint64_t i = 1; i < NN; ++i)
     if (nodes[i].kind != 2 && !inl[i]) hot_n[hot_table(nodes[i].depth)]++;
   uint64_t hot_off[HOT_TABLES], hot_cap[HOT_TABLES], hot_total = 0;
-  uint64_t hot_load_pct = 40;  // load factor (%); GM_HOT_LOAD_PCT: A/B knob (10..90)
+  uint64_t hot_load_pct = 30;  // load factor (%); GM_HOT_LOAD_PCT: A/B knob (10..90)
   if (const char* e = getenv("GM_HOT_LOAD_PCT")) hot_load_pct = std::min<uint64_t>(90, std::max<uint64_t>(10, strtoull(e, nullptr, 10)));
   for (int t = 0; t < HOT_TABLES; ++t) {
-    // load <= 0.40 (A/B at C2: 0.55 -> 0.40 cut k_walk by 3 %; lower bought nothing);
+    // load <= 0.30 (A/B at C2, fused kernel: 0.40 / 0.35 / 0.30 / 0.25 -> 10.34 / 10.13 / 10.03 /
+    // 9.97 ms; round 1 (split walk): 0.55 -> 0.40 cut k_walk by 3 %);
     // at least 8 slots so the probe loop always finds an empty one
     uint64_t pct = hot_load_pct;
     if (const char* e = getenv("GM_HOT_LOAD_PCT_UPPER"))  // A/B knob: load of the depth 1-2 tables
@@ -493,17 +494,23 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   std::vector<uint16_t> flen(nf);
   for (uint32_t f = 0; f < nf; ++f) flen[f] = uint16_t(std::min<uint64_t>(idx->foff[f + 1] - idx->foff[f], 65535));
 
-  // ---- 6. upload: one allocation, 256-B aligned sections
+  // ---- 6. upload: one allocation, 256-B aligned sections.  A plain index (no
+  // shard ids, no subscriber lists) keeps a host mirror of the blob for
+  // in-place updates, with headroom for appended nodes, words and filters.
+  const bool keep_mirror = ctx && !gids && !sub_off && !getenv("GM_NO_MIRROR");
+  const uint64_t nodes_cap = keep_mirror ? NN + NN / 4 + 1024 : NN;
+  const uint64_t arena_cap = keep_mirror ? arena.size() + arena.size() / 4 + 65536 : arena.size();
+  const uint64_t flen_cap = keep_mirror ? uint64_t(nf) + nf / 4 + 1024 : nf;
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   size_t o_nodes = 0;
-  size_t o_dict = o_nodes + al(NN * sizeof(Node));
+  size_t o_dict = o_nodes + al(nodes_cap * sizeof(Node));
   size_t o_edges = o_dict + al(dcap * sizeof(DictSlot));
   size_t o_hot = o_edges + al(dedges.size() * sizeof(EdgeSlot));
   size_t o_arena = o_hot + al(hot.size() * sizeof(HotSlot));
-  size_t o_soff = o_arena + al(arena.size() + 64);
-  size_t o_sids = o_soff + al(soff.size() * 8);
+  size_t o_soff = o_arena + al(arena_cap + 64);
+  size_t o_sids = o_soff + al((keep_mirror ? flen_cap + 1 : soff.size()) * 8);  // zeros past nf (no subscribers)
   size_t o_flen = o_sids + al(sids.size() * 4 + 4);
-  size_t o_gmap = o_flen + al(flen.size() * 2 + 2);
+  size_t o_gmap = o_flen + al(flen_cap * 2 + 2);
   size_t o_efilt = o_gmap + al(idx->gmap.size() * 4 + 4);
   size_t total = o_efilt + al(efilt.size() * 4 + 4);
 
@@ -530,23 +537,46 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   }
   idx->dev_bytes = total;
   uint8_t* B = static_cast<uint8_t*>(idx->dev_base);
-  auto up = [&](size_t off, const void* src, size_t bytes) {
-    if (bytes && e == hipSuccess) e = hipMemcpy(B + off, src, bytes, hipMemcpyHostToDevice);
+  // the blob assembled on the host (the mirror, when kept) and sent in one copy
+  std::vector<uint8_t> hb(total, 0);
+  auto put = [&](size_t off, const void* src, size_t bytes) {
+    if (bytes) std::memcpy(hb.data() + off, src, bytes);
   };
-  up(o_nodes, dnodes.data(), NN * sizeof(Node));
-  up(o_dict, dict.data(), dcap * sizeof(DictSlot));
-  up(o_edges, dedges.data(), dedges.size() * sizeof(EdgeSlot));
-  up(o_hot, hot.data(), hot.size() * sizeof(HotSlot));
-  up(o_arena, arena.data(), arena.size());
-  up(o_soff, soff.data(), soff.size() * 8);
-  up(o_sids, sids.data(), sids.size() * 4);
-  up(o_flen, flen.data(), flen.size() * 2);
-  up(o_gmap, idx->gmap.data(), idx->gmap.size() * 4);
-  up(o_efilt, efilt.data(), efilt.size() * 4);
+  put(o_nodes, dnodes.data(), NN * sizeof(Node));
+  put(o_dict, dict.data(), dcap * sizeof(DictSlot));
+  put(o_edges, dedges.data(), dedges.size() * sizeof(EdgeSlot));
+  put(o_hot, hot.data(), hot.size() * sizeof(HotSlot));
+  put(o_arena, arena.data(), arena.size());
+  put(o_soff, soff.data(), soff.size() * 8);
+  put(o_sids, sids.data(), sids.size() * 4);
+  put(o_flen, flen.data(), flen.size() * 2);
+  put(o_gmap, idx->gmap.data(), idx->gmap.size() * 4);
+  put(o_efilt, efilt.data(), efilt.size() * 4);
+  e = hipMemcpy(B, hb.data(), total, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
-    hipFree(idx->dev_base);
+    (void)hipFree(idx->dev_base);
     delete idx;
     return set_err(ctx, EMQX_GM_EDEVICE, std::string("index_build: upload: ") + hipGetErrorString(e));
+  }
+  if (keep_mirror) {
+    auto* m = new Mirror;
+    m->blob = std::move(hb);
+    m->o_nodes = o_nodes;
+    m->o_dict = o_dict;
+    m->o_edges = o_edges;
+    m->o_hot = o_hot;
+    m->o_arena = o_arena;
+    m->o_flen = o_flen;
+    m->o_efilt = o_efilt;
+    m->nodes_n = NN;
+    m->nodes_cap = nodes_cap;
+    m->arena_n = arena.size();
+    m->arena_cap = arena_cap;
+    m->flen_cap = flen_cap;
+    m->dict_used = nw;
+    for (int d = 0; d < EDGE_DEPTHS; ++d) m->edge_used[d] = tabs[d].used;
+    for (int t = 0; t < HOT_TABLES; ++t) m->hot_used[t] = hot_n[t];
+    idx->mirror = m;
   }
 
   IndexView& v = idx->view;
@@ -577,7 +607,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (int t = 0; t < HOT_TABLES; ++t)
     if (hot_cap[t] * sizeof(HotSlot) >= (1ull << 31)) v.flags |= IX_HOT_FLAT;
   if (getenv("GM_HOT_FLAT")) v.flags |= IX_HOT_FLAT;  // test knob: exercise the flat-load path
-  if (!getenv("GM_NO_RH_EXIT")) v.flags |= IX_RH_EXIT;  // A/B knob
+  // every per-depth table is Robin Hood ordered; the shared last one is not (GM_NO_RH_EXIT: A/B knob)
+  v.rh_mask = getenv("GM_NO_RH_EXIT") ? 0u : (1u << (HOT_TABLES - 1)) - 1u;
   v.n_nodes = uint32_t(NN);
   v.n_filters = nf;
   v.plus_word = plus_word;
@@ -602,9 +633,10 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
 void free_index(emqx_gm_index* idx) {
   if (!idx) return;
   if (idx->ov) free_overlay(idx);
+  delete idx->mirror;
   if (idx->dev_base) {
-    hipSetDevice(idx->device);
-    hipFree(idx->dev_base);
+    (void)hipSetDevice(idx->device);
+    (void)hipFree(idx->dev_base);
   }
   delete idx;
 }

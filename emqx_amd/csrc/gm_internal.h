@@ -89,6 +89,23 @@ struct emqx_gm_ctx {
 
 namespace gm {
 struct OverlayState;
+
+// Host copy of a plain index's device blob (no shard ids, no subscriber
+// lists), byte for byte, with the headroom an in-place update may use
+// (gm_overlay.cpp, patch_update): appended trie nodes, new words in the
+// arena, more filter lengths.  It belongs to the newest snapshot of its line:
+// an update moves it from the old snapshot (which stays valid for its readers)
+// to the new one.
+struct Mirror {
+  std::vector<uint8_t> blob;
+  size_t o_nodes = 0, o_dict = 0, o_edges = 0, o_hot = 0, o_arena = 0, o_flen = 0, o_efilt = 0;
+  uint64_t nodes_n = 0, nodes_cap = 0;   // v1 level-trie nodes used / capacity
+  uint64_t arena_n = 0, arena_cap = 0;   // word bytes used / capacity
+  uint64_t flen_cap = 0;                 // filter-length entries available
+  uint64_t dict_used = 0;
+  uint64_t edge_used[EDGE_DEPTHS] = {};
+  uint64_t hot_used[HOT_TABLES] = {};
+};
 }
 
 struct emqx_gm_index {
@@ -104,6 +121,7 @@ struct emqx_gm_index {
   std::vector<uint32_t> gmap;   // shard index: global id of each local filter (ascending); empty otherwise
   std::vector<uint64_t> soff;   // subscriber CSR offsets per filter id (host copy; empty without subscribers)
   gm::OverlayState* ov = nullptr;  // overlay snapshot (emqx_gm_index_update); tables above unused then
+  gm::Mirror* mirror = nullptr;    // host copy of the blob (updatable plain index), see gm::Mirror
   emqx_gm_index_info_t info{};
 };
 
@@ -146,6 +164,14 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
                  uint64_t n_ops, emqx_gm_index** out);
 int overlay_filter(const emqx_gm_index* idx, uint32_t id, const uint8_t** bytes, uint64_t* len);
 void free_overlay(emqx_gm_index* idx);
+// gm_match.hip: the device side of an in-place update (patch_update): dst =
+// src (bytes), then the host-patched byte ranges (offset, length) of `host`
+// written over it, then every filter-id field of the hot slots and of nodes
+// [0, n_nodes) renumbered by rmap (n_rmap entries)
+int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t bytes,
+                       const std::vector<std::pair<uint64_t, uint32_t>>& ranges, const uint8_t* host,
+                       const IndexView& v, uint64_t o_hot, uint64_t o_nodes, uint64_t n_nodes,
+                       const std::vector<uint32_t>& rmap);
 // gm_match.hip
 int run_match_overlay(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                       uint32_t flags, emqx_gm_csr* out);

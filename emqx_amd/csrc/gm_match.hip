@@ -423,7 +423,7 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
         const HotSlot* tab = ix.hot + ix.hot_off[ht];
         const HotSlot* ptab = ix.hot + ix.hot_off[hot_table(lvl)];  // the frontier nodes' own table
         const bool hflat = (ix.flags & IX_HOT_FLAT) != 0;
-        const bool hrh = ht < HOT_TABLES - 1 && (ix.flags & IX_RH_EXIT);  // Robin Hood ordered table
+        const bool hrh = ((ix.rh_mask >> ht) & 1u) != 0;  // Robin Hood ordered table
         const uint64_t cap = ix.hot_cap[ht];
         const uint32_t capu = uint32_t(cap);
         for (uint32_t i = 0; i < cur_n; ++i) {
@@ -862,7 +862,7 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
         const HotSlot* tab = ix.hot + ix.hot_off[ht];
         const HotSlot* ptab = ix.hot + ix.hot_off[hot_table(lvl)];  // the frontier nodes' own table
         const bool hflat = (ix.flags & IX_HOT_FLAT) != 0;
-        const bool hrh = ht < HOT_TABLES - 1 && (ix.flags & IX_RH_EXIT);  // Robin Hood ordered table
+        const bool hrh = ((ix.rh_mask >> ht) & 1u) != 0;  // Robin Hood ordered table
         const uint64_t cap = ix.hot_cap[ht];
         const uint32_t capu = uint32_t(cap);
         const bool wok = wid != NONE;
@@ -1057,7 +1057,7 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
     const int ht = hot_table(lvl + 1);
     const HotSlot* tab = ix.hot + ix.hot_off[ht];
     const HotSlot* ptab = ix.hot + ix.hot_off[hot_table(lvl)];  // the frontier nodes' own table
-    const bool hrh = ht < HOT_TABLES - 1 && (ix.flags & IX_RH_EXIT);
+    const bool hrh = ((ix.rh_mask >> ht) & 1u) != 0;
     const uint64_t cap = ix.hot_cap[ht];
     const uint32_t capu = uint32_t(cap);
     const uint32_t fmask = ix.efilt_mask[ht];
@@ -1856,6 +1856,102 @@ int launch_off64_to_32(hipStream_t st, const uint64_t* in, uint64_t n1, uint32_t
   const uint64_t g = std::min<uint64_t>(2048, (n1 + 255) / 256);
   hipLaunchKernelGGL(k_off64_to_32, dim3(g ? g : 1), dim3(256), 0, st, in, n1, out);
   return hipGetLastError() == hipSuccess ? 0 : EMQX_GM_EDEVICE;
+}
+
+// ---- in-place update (gm_overlay.cpp, patch_update) -----------------------
+// The host-patched byte ranges, cut into pieces of <= PATCH_PIECE bytes, one
+// workgroup per piece: desc[3b..3b+2] = (offset in the blob, offset in the
+// payload, bytes).
+constexpr uint32_t PATCH_PIECE = 4096;
+__global__ __launch_bounds__(256) void k_patch_scatter(uint8_t* __restrict__ dst, const uint64_t* __restrict__ desc,
+                                                       const uint8_t* __restrict__ pay) {
+  const uint64_t d = desc[3 * blockIdx.x], p = desc[3 * blockIdx.x + 1], n = desc[3 * blockIdx.x + 2];
+  for (uint64_t i = threadIdx.x; i < n; i += 256) dst[d + i] = pay[p + i];
+}
+// Every filter-id field renumbered (renum_field, the device twin of
+// gm_overlay.cpp's renumber_host): hot slots [0, n_hot), nodes [0, n_nodes).
+__global__ __launch_bounds__(256) void k_renumber(HotSlot* __restrict__ hot, uint64_t n_hot, Node* __restrict__ nodes,
+                                                  uint64_t n_nodes, const uint32_t* __restrict__ rmap) {
+  const uint64_t stride = uint64_t(gridDim.x) * 256u;
+  for (uint64_t s = uint64_t(blockIdx.x) * 256u + threadIdx.x; s < n_hot; s += stride) {
+    HotSlot h = hot[s];
+    if (h.key == EDGE_EMPTY) continue;
+    h.hf = renum_field(h.hf, HF_NONE, HOT_PLUS, rmap);
+    h.end_filter = renum_field(h.end_filter, NONE, END_WILD, rmap);
+    h.p_hf = renum_field(h.p_hf, HF_NONE, HOT_PLUS, rmap);
+    h.p_end = renum_field(h.p_end, NONE, END_WILD, rmap);
+    hot[s] = h;
+  }
+  for (uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x; i < n_nodes; i += stride) {
+    Node nd = nodes[i];
+    nd.hash_filter = renum_field(nd.hash_filter, NONE, 0, rmap);
+    nd.end_filter = renum_field(nd.end_filter, NONE, 0, rmap);
+    nodes[i] = nd;
+  }
+}
+
+int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t bytes,
+                       const std::vector<std::pair<uint64_t, uint32_t>>& ranges, const uint8_t* host,
+                       const IndexView& v, uint64_t o_hot, uint64_t o_nodes, uint64_t n_nodes,
+                       const std::vector<uint32_t>& rmap) {
+  // coalesce (ranges closer than 64 B merge: the bytes between are equal on
+  // both sides, the patch never touched them), then cut into pieces
+  std::vector<std::pair<uint64_t, uint64_t>> seg;  // [begin, end)
+  {
+    std::vector<std::pair<uint64_t, uint32_t>> r(ranges);
+    std::sort(r.begin(), r.end());
+    for (const auto& x : r) {
+      if (!x.second) continue;
+      if (x.first + x.second > bytes) return set_err(ctx, EMQX_GM_EINVAL, "index_update: patch outside the blob");
+      if (!seg.empty() && x.first <= seg.back().second + 64) seg.back().second = std::max(seg.back().second, x.first + x.second);
+      else seg.emplace_back(x.first, x.first + x.second);
+    }
+  }
+  std::vector<uint64_t> desc;
+  uint64_t pay_n = 0;
+  for (const auto& g : seg)
+    for (uint64_t b = g.first; b < g.second; b += PATCH_PIECE) {
+      const uint64_t n = std::min<uint64_t>(PATCH_PIECE, g.second - b);
+      desc.insert(desc.end(), {b, pay_n + (b - g.first), n});
+    }
+  for (const auto& g : seg) pay_n += g.second - g.first;
+  const uint64_t n_pieces = desc.size() / 3;
+  if (n_pieces > 0x7FFFFFFFull) return set_err(ctx, EMQX_GM_EINVAL, "index_update: patch too large");
+  // staging: desc | payload | rmap (one upload)
+  const size_t o_pay = (desc.size() * 8 + 255) & ~size_t(255);
+  const size_t o_rmap = (o_pay + pay_n + 255) & ~size_t(255);
+  const size_t total = o_rmap + rmap.size() * 4 + 4;
+  std::vector<uint8_t> st(total, 0);
+  if (!desc.empty()) std::memcpy(st.data(), desc.data(), desc.size() * 8);
+  {
+    uint64_t q = o_pay;
+    for (const auto& g : seg) {
+      std::memcpy(st.data() + q, host + g.first, g.second - g.first);
+      q += g.second - g.first;
+    }
+  }
+  if (!rmap.empty()) std::memcpy(st.data() + o_rmap, rmap.data(), rmap.size() * 4);
+  PoolBuf dbuf(ctx->pool, total);
+  if (!dbuf.p) return set_err(ctx, EMQX_GM_ENOMEM, "index_update: staging buffer");
+  hipStream_t s = ctx->stream;
+  GM_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+  GM_HIP(ctx, hipMemcpyAsync(dbuf.p, st.data(), total, hipMemcpyHostToDevice, s));
+  uint8_t* D = static_cast<uint8_t*>(dst);
+  const uint8_t* S = dbuf.as<uint8_t>();
+  if (n_pieces) {
+    hipLaunchKernelGGL(k_patch_scatter, dim3(uint32_t(n_pieces)), dim3(256), 0, s, D,
+                       reinterpret_cast<const uint64_t*>(S), S + o_pay);
+    GM_HIP(ctx, hipGetLastError());
+  }
+  uint64_t n_hot = 0;
+  for (int t = 0; t < HOT_TABLES; ++t) n_hot = std::max<uint64_t>(n_hot, v.hot_off[t] + v.hot_cap[t]);
+  const uint64_t g = std::min<uint64_t>(4096, (std::max(n_hot, n_nodes) + 255) / 256);
+  hipLaunchKernelGGL(k_renumber, dim3(uint32_t(g ? g : 1)), dim3(256), 0, s, reinterpret_cast<HotSlot*>(D + o_hot),
+                     n_hot, reinterpret_cast<Node*>(D + o_nodes), n_nodes,
+                     reinterpret_cast<const uint32_t*>(S + o_rmap));
+  GM_HIP(ctx, hipGetLastError());
+  GM_HIP(ctx, hipStreamSynchronize(s));  // the staging buffers go back to the pool / the host
+  return EMQX_GM_OK;
 }
 
 // Sum of per-tile counters into one (one atomic per wave of a small grid).

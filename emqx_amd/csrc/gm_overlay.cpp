@@ -12,6 +12,7 @@
 // Result rows use the ids of the updated set (lexicographic rank), exactly
 // what a full rebuild would return.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <set>
 #include <string>
@@ -55,7 +56,497 @@ bool wildcard(const uint8_t* p, uint64_t len) {
   return false;
 }
 
+// ---------------------------------------------------------------------------
+// In-place update of a plain index: the new snapshot is a device copy of the
+// previous one with the inserted filters' nodes, words and fields patched in
+// and the deleted filters' fields cleared (worked out on the host mirror, the
+// same bytes), then every filter id renumbered to the updated set's ranks by
+// one device pass.  The result is an ordinary flat snapshot: a match on it
+// costs exactly what a match on a rebuilt index costs (one pass, no overlay).
+// ---------------------------------------------------------------------------
+struct Words {  // '/'-separated words of one filter
+  std::vector<std::pair<uint64_t, uint64_t>> w;  // (start, len)
+  Words(const uint8_t* p, uint64_t len) {
+    uint64_t ws = 0;
+    for (uint64_t i = 0; i <= len; ++i)
+      if (i == len || p[i] == '/') {
+        w.emplace_back(ws, i - ws);
+        ws = i + 1;
+      }
+  }
+};
+bool is1(const uint8_t* p, const std::pair<uint64_t, uint64_t>& w, char c) { return w.second == 1 && p[w.first] == c; }
+// well formed for the in-place path: '#' only as the last word (anything else
+// takes the overlay / rebuild path, which handles every byte string)
+bool well_formed(const uint8_t* p, uint64_t len) {
+  Words ws(p, len);
+  for (size_t i = 0; i + 1 < ws.w.size(); ++i)
+    if (is1(p, ws.w[i], '#')) return false;
+  return true;
+}
+
+enum CurKind { CUR_ROOT, CUR_SLOT, CUR_INLINE };
+struct Cur {
+  CurKind kind = CUR_ROOT;
+  uint32_t slot = 0;  // the node's slot, or for an inline node its parent's
+  int table = 0;      // table of `slot`
+  uint32_t v1 = 0;    // level-trie node
+  uint32_t depth = 0;
+  uint32_t pv1 = NONE, pwid = NONE;  // its parent and incoming word (for the parent's child refs)
+  bool plus = false;                 // reached through '+'
+};
+
+struct Patcher {
+  Mirror& M;
+  IndexView& v;  // the new snapshot's view (its host-side fields are patched here)
+  std::vector<std::pair<uint64_t, uint32_t>> dirty;  // blob ranges changed: (offset, bytes)
+  uint32_t rh_clear = 0;                             // tables that took a key outside Robin Hood order
+  uint64_t new_edges = 0;
+  uint32_t max_depth = 0;
+
+  uint8_t* B() { return M.blob.data(); }
+  Node* nodes() { return reinterpret_cast<Node*>(B() + M.o_nodes); }
+  DictSlot* dict() { return reinterpret_cast<DictSlot*>(B() + M.o_dict); }
+  EdgeSlot* edges() { return reinterpret_cast<EdgeSlot*>(B() + M.o_edges); }
+  HotSlot* hot() { return reinterpret_cast<HotSlot*>(B() + M.o_hot); }
+  uint8_t* arena() { return B() + M.o_arena; }
+  uint32_t* efilt() { return reinterpret_cast<uint32_t*>(B() + M.o_efilt); }
+  void mark(const void* p, size_t n) { dirty.emplace_back(uint64_t(static_cast<const uint8_t*>(p) - B()), uint32_t(n)); }
+
+  // ---- word dictionary (dict_resolve's rules: length + head, tail against the arena)
+  uint32_t dict_find(const uint8_t* w, uint64_t len) {
+    const uint64_t head = word_head_host(w, len);
+    for (uint64_t s = dict_slot(dict_hash_host(w, len), v.dict_mask);; s = (s + 1) & v.dict_mask) {
+      const DictSlot& d = dict()[s];
+      if (d.len == DICT_EMPTY_LEN) return NONE;
+      if (d.len == len && d.head == head && (len <= 8 || std::memcmp(arena() + d.word + 8, w + 8, len - 8) == 0))
+        return d.word;
+    }
+  }
+  uint32_t word(const uint8_t* w, uint64_t len) {
+    uint32_t id = dict_find(w, len);
+    if (id != NONE) return id;
+    id = uint32_t(M.arena_n);  // every word owns >= 1 byte: ids stay unique
+    if (len) std::memcpy(arena() + id, w, len);
+    else arena()[id] = 0;
+    M.arena_n += len ? len : 1;
+    mark(arena() + id, len ? len : 1);
+    uint64_t s = dict_slot(dict_hash_host(w, len), v.dict_mask);
+    while (dict()[s].len != DICT_EMPTY_LEN) s = (s + 1) & v.dict_mask;
+    dict()[s] = DictSlot{word_head_host(w, len), uint32_t(len), id};
+    mark(&dict()[s], sizeof(DictSlot));
+    ++M.dict_used;
+    return id;
+  }
+
+  // ---- level trie (v1: slow path, literal lookups)
+  uint32_t edge_get(uint32_t depth, uint32_t parent, uint32_t wid) {
+    const int d = edge_depth(depth);
+    EdgeSlot* tab = edges() + v.etab_off[d];
+    const uint64_t key = edge_key(parent, wid), mask = v.etab_mask[d];
+    for (uint64_t s = edge_slot(key, mask);; s = (s + 1) & mask) {
+      if (tab[s].key == key) return tab[s].child;
+      if (tab[s].key == EDGE_EMPTY) return NONE;
+    }
+  }
+  void edge_put(uint32_t depth, uint32_t parent, uint32_t wid, uint32_t child) {
+    const int d = edge_depth(depth);
+    EdgeSlot* tab = edges() + v.etab_off[d];
+    const uint64_t key = edge_key(parent, wid), mask = v.etab_mask[d];
+    uint64_t s = edge_slot(key, mask);
+    while (tab[s].key != EDGE_EMPTY) s = (s + 1) & mask;
+    tab[s] = EdgeSlot{key, child, 0};
+    mark(&tab[s], sizeof(EdgeSlot));
+    ++M.edge_used[d];
+    ++new_edges;
+  }
+  uint32_t new_node() {
+    const uint32_t id = uint32_t(M.nodes_n++);
+    nodes()[id] = Node{NONE, NONE, NONE, 0};
+    mark(&nodes()[id], sizeof(Node));
+    return id;
+  }
+
+  // ---- hot tables (any key order: the table's early exit is switched off)
+  HotSlot* htab(int t) { return hot() + v.hot_off[t]; }
+  uint32_t hot_find(int t, uint64_t key) {
+    const uint64_t cap = v.hot_cap[t];
+    HotSlot* tab = htab(t);
+    for (uint64_t s = hot_slot(key, cap);; s = s + 1 == cap ? 0 : s + 1) {
+      if (tab[s].key == key) return uint32_t(s);
+      if (tab[s].key == EDGE_EMPTY) return NONE;
+    }
+  }
+  // Slots never move (a slot index is a hot id other keys hold), so the key
+  // goes to the first empty slot from its home.  That keeps the table's Robin
+  // Hood order (hot_resolve's early exit) as long as no resident on the way is
+  // nearer its own home than the new key is at that slot; otherwise the
+  // table's early exit is switched off (rh_clear).
+  uint32_t hot_add(int t, uint64_t key) {
+    const uint64_t cap = v.hot_cap[t];
+    HotSlot* tab = htab(t);
+    const uint64_t home = hot_slot(key, cap);
+    uint64_t s = home, dist = 0;
+    bool rh_ok = true;
+    while (tab[s].key != EDGE_EMPTY) {
+      const uint64_t h2 = hot_slot(tab[s].key, cap);
+      if ((s >= h2 ? s - h2 : s + cap - h2) < dist) rh_ok = false;
+      s = s + 1 == cap ? 0 : s + 1;
+      ++dist;
+    }
+    tab[s] = HotSlot{key, 0, HF_NONE, NONE, 0, HF_NONE, NONE};
+    mark(&tab[s], sizeof(HotSlot));
+    ++M.hot_used[t];
+    if (!rh_ok) rh_clear |= 1u << t;
+    return uint32_t(s);
+  }
+  // a node's first exact child: set NF_HAS_EXACT and the REF_X bit of the
+  // references to it (its parent's edge, and plus_child when it is a '+' child)
+  void gain_exact(const Cur& c) {
+    Node& nd = nodes()[c.v1];
+    if (nd.flags & NF_HAS_EXACT) return;
+    nd.flags |= NF_HAS_EXACT;
+    mark(&nd, sizeof(Node));
+    if (c.pv1 == NONE) return;  // the root: no reference
+    const int d = edge_depth(c.depth - 1);
+    EdgeSlot* tab = edges() + v.etab_off[d];
+    const uint64_t key = edge_key(c.pv1, c.pwid), mask = v.etab_mask[d];
+    for (uint64_t s = edge_slot(key, mask);; s = (s + 1) & mask) {
+      if (tab[s].key == key) {
+        tab[s].child |= REF_X;
+        mark(&tab[s], sizeof(EdgeSlot));
+        break;
+      }
+      if (tab[s].key == EDGE_EMPTY) break;
+    }
+    if (c.plus) {
+      Node& p = nodes()[c.pv1];
+      p.plus_child |= REF_X;
+      mark(&p, sizeof(Node));
+    }
+  }
+  static uint32_t hid(const Cur& c) {
+    return c.kind == CUR_ROOT ? 0u : c.kind == CUR_SLOT ? c.slot : (c.slot | HOT_INLINE);
+  }
+  // the node record's fields: root -> IndexView, slot node -> its slot, inline node -> p_* of its parent's slot
+  uint32_t& f_sig(const Cur& c) {
+    return c.kind == CUR_ROOT ? v.root_sig : c.kind == CUR_SLOT ? htab(c.table)[c.slot].sig : htab(c.table)[c.slot].p_sig;
+  }
+  uint32_t& f_hf(const Cur& c) {
+    return c.kind == CUR_SLOT ? htab(c.table)[c.slot].hf : htab(c.table)[c.slot].p_hf;
+  }
+  uint32_t& f_end(const Cur& c) {
+    return c.kind == CUR_SLOT ? htab(c.table)[c.slot].end_filter : htab(c.table)[c.slot].p_end;
+  }
+  void mark_rec(const Cur& c) {
+    if (c.kind != CUR_ROOT) mark(&htab(c.table)[c.slot], sizeof(HotSlot));
+  }
+  void set_hf(const Cur& c, uint32_t id) {  // 'match_#' of the node (keeps its HOT_PLUS flag)
+    if (c.kind == CUR_ROOT) {
+      v.root_hash = id == HF_NONE ? NONE : id;
+      return;
+    }
+    uint32_t& f = f_hf(c);
+    f = (f & HOT_PLUS) | id;
+    mark_rec(c);
+  }
+
+  // Insert a well-formed filter with (temporary) id fid.
+  void insert(const uint8_t* p, uint64_t len, uint32_t fid, bool wild) {
+    Words ws(p, len);
+    Cur c;
+    for (size_t i = 0; i < ws.w.size(); ++i) {
+      const auto& w = ws.w[i];
+      if (is1(p, w, '#')) {  // the last word: the parent's 'match_#' (no hot node)
+        const uint32_t hw = word(p + w.first, 1);
+        v.hash_word = hw;
+        uint32_t ch = edge_get(c.depth, c.v1, hw);
+        if (ch == NONE) {
+          ch = new_node();
+          edge_put(c.depth, c.v1, hw, ch);
+        }
+        ch &= REF_MASK;
+        nodes()[ch].end_filter = fid;
+        nodes()[ch].flags |= NF_END_WILD;
+        mark(&nodes()[ch], sizeof(Node));
+        nodes()[c.v1].hash_filter = fid;
+        mark(&nodes()[c.v1], sizeof(Node));
+        set_hf(c, fid);
+        max_depth = std::max<uint32_t>(max_depth, c.depth + 1);
+        return;
+      }
+      const bool plus = is1(p, w, '+');
+      const uint32_t wid = word(p + w.first, w.second);
+      if (plus) v.plus_word = wid;
+      uint32_t ch = edge_get(c.depth, c.v1, wid);
+      if (ch == NONE) {
+        ch = new_node();
+        edge_put(c.depth, c.v1, wid, ch);
+        if (plus) {
+          nodes()[c.v1].plus_child = ch;
+          nodes()[c.v1].flags |= NF_HAS_PLUS;
+          mark(&nodes()[c.v1], sizeof(Node));
+        } else {
+          gain_exact(c);
+        }
+      }
+      Cur n;
+      n.v1 = ch & REF_MASK;
+      n.depth = c.depth + 1;
+      n.pv1 = c.v1;
+      n.pwid = wid;
+      n.plus = plus;
+      if (plus && c.kind == CUR_SLOT) {  // the '+' child of a slot-owning node lives in its slot
+        HotSlot& P = htab(c.table)[c.slot];
+        if (!(P.hf & HOT_PLUS)) {
+          P.hf |= HOT_PLUS;
+          P.p_sig = 0;
+          P.p_hf = HF_NONE;
+          P.p_end = NONE;
+          mark(&P, sizeof(HotSlot));
+        }
+        n.kind = CUR_INLINE;
+        n.slot = c.slot;
+        n.table = c.table;
+      } else {
+        const int t = hot_table(c.depth + 1);
+        const uint64_t key = hot_key(hid(c), wid, c.depth);
+        uint32_t sl = hot_find(t, key);
+        if (sl == NONE) sl = hot_add(t, key);
+        if (plus) {  // the parent (root or inline) gains its '+' flag
+          if (c.kind == CUR_ROOT) {
+            v.root_flags |= HOT_PLUS;
+          } else {
+            f_hf(c) |= HOT_PLUS;
+            mark_rec(c);
+          }
+        } else {  // the parent's exact-child signature and the table's exact-edge filter
+          f_sig(c) |= sig_bit(wid);
+          mark_rec(c);
+          if (v.efilt_mask[t]) {
+            const uint32_t fh = edge_filter_hash(key);
+            uint32_t* fw = efilt() + v.efilt_off[t] + edge_filter_word(fh, v.efilt_mask[t]);
+            *fw |= edge_filter_bits(fh);
+            mark(fw, 4);
+          }
+        }
+        n.kind = CUR_SLOT;
+        n.slot = sl;
+        n.table = t;
+      }
+      c = n;
+    }
+    f_end(c) = fid | (wild ? END_WILD : 0u);
+    mark_rec(c);
+    nodes()[c.v1].end_filter = fid;
+    if (wild) nodes()[c.v1].flags |= NF_END_WILD;
+    mark(&nodes()[c.v1], sizeof(Node));
+    max_depth = std::max<uint32_t>(max_depth, c.depth);
+  }
+
+  // Clear an indexed filter's fields (its nodes stay: an empty node matches nothing).
+  void erase(const uint8_t* p, uint64_t len) {
+    Words ws(p, len);
+    const bool wf = well_formed(p, len);
+    Cur c;
+    uint32_t v1 = 0;
+    for (size_t i = 0; i < ws.w.size(); ++i) {
+      const auto& w = ws.w[i];
+      const uint32_t wid = dict_find(p + w.first, w.second);
+      if (wid == NONE) return;  // not indexed
+      const uint32_t ch = edge_get(uint32_t(i), v1, wid);
+      if (ch == NONE) return;
+      const bool last = i + 1 == ws.w.size();
+      if (last && is1(p, w, '#')) {
+        nodes()[v1].hash_filter = NONE;
+        mark(&nodes()[v1], sizeof(Node));
+        nodes()[ch & REF_MASK].end_filter = NONE;
+        mark(&nodes()[ch & REF_MASK], sizeof(Node));
+        if (wf) set_hf(c, HF_NONE);
+        return;
+      }
+      if (wf) {  // follow the hot path (ill-formed filters have no hot fields)
+        const bool plus = is1(p, w, '+');
+        Cur n;
+        if (plus && c.kind == CUR_SLOT) {
+          n.kind = CUR_INLINE;
+          n.slot = c.slot;
+          n.table = c.table;
+        } else {
+          const int t = hot_table(i + 1);
+          const uint32_t sl = hot_find(t, hot_key(hid(c), wid, uint32_t(i)));
+          if (sl == NONE) return;
+          n.kind = CUR_SLOT;
+          n.slot = sl;
+          n.table = t;
+        }
+        c = n;
+      }
+      v1 = ch & REF_MASK;
+    }
+    nodes()[v1].end_filter = NONE;
+    mark(&nodes()[v1], sizeof(Node));
+    if (wf) {
+      f_end(c) = NONE;
+      mark_rec(c);
+    }
+  }
+};
+
+// rmap[temporary id] -> final id (NONE: deleted) over every filter-id field
+// (the host twin of gm_match.hip's k_renumber)
+void renumber_host(Mirror& M, const IndexView& v, const std::vector<uint32_t>& rmap) {
+  HotSlot* hot = reinterpret_cast<HotSlot*>(M.blob.data() + M.o_hot);
+  uint64_t slots = 0;
+  for (int t = 0; t < HOT_TABLES; ++t) slots = std::max(slots, v.hot_off[t] + v.hot_cap[t]);
+  const uint32_t* r = rmap.data();
+  for (uint64_t s = 0; s < slots; ++s) {
+    HotSlot& h = hot[s];
+    if (h.key == EDGE_EMPTY) continue;
+    h.hf = renum_field(h.hf, HF_NONE, HOT_PLUS, r);
+    h.end_filter = renum_field(h.end_filter, NONE, END_WILD, r);
+    h.p_hf = renum_field(h.p_hf, HF_NONE, HOT_PLUS, r);
+    h.p_end = renum_field(h.p_end, NONE, END_WILD, r);
+  }
+  Node* nd = reinterpret_cast<Node*>(M.blob.data() + M.o_nodes);
+  for (uint64_t i = 0; i < M.nodes_n; ++i) {
+    nd[i].hash_filter = renum_field(nd[i].hash_filter, NONE, 0, r);
+    nd[i].end_filter = renum_field(nd[i].end_filter, NONE, 0, r);
+  }
+}
+
 }  // namespace
+
+// Returns 1 (nothing changed) when the snapshot's tables lack room: the caller rebuilds.
+static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>& tomb,
+                        const std::set<std::string>& dset, emqx_gm_index** out) {
+  Mirror& M = *prev->mirror;
+  const uint64_t nb = prev->info.n_filters, K = dset.size();
+  // capacity (upper bounds: every word of every new filter new): otherwise rebuild
+  uint64_t words = 0, bytes = 0;
+  for (const std::string& d : dset) {
+    words += 1 + uint64_t(std::count(d.begin(), d.end(), '/'));
+    bytes += d.size() + 1;
+  }
+  const uint64_t nf_new = nb - tomb.size() + K;
+  if (M.nodes_n + words > M.nodes_cap || M.arena_n + bytes > M.arena_cap || nf_new > M.flen_cap ||
+      (M.dict_used + words) * 2 > prev->view.dict_mask + 1)
+    return 1;
+  for (int d = 0; d < EDGE_DEPTHS; ++d)
+    if ((M.edge_used[d] + words) * 4 > (prev->view.etab_mask[d] + 1) * 3) return 1;
+  for (int t = 0; t < HOT_TABLES; ++t)
+    if (prev->view.hot_cap[t] && (M.hot_used[t] + words) * 5 > prev->view.hot_cap[t] * 3) return 1;
+  for (int t = 1; t < HOT_TABLES; ++t)  // a depth the base never reached has no table
+    if (!prev->view.hot_cap[t])
+      for (const std::string& d : dset)
+        if (uint64_t(std::count(d.begin(), d.end(), '/')) + 1 >= uint64_t(t)) return 1;
+
+  auto* idx = new emqx_gm_index;
+  idx->device = prev->device;
+  idx->view = prev->view;
+  idx->info = prev->info;
+  IndexView& v = idx->view;
+  hipError_t e = hipSetDevice(prev->device);
+  if (e == hipSuccess) e = hipMalloc(&idx->dev_base, prev->dev_bytes);
+  if (e != hipSuccess) {
+    delete idx;
+    return set_err(ctx, EMQX_GM_ENOMEM, std::string("index_update: hipMalloc: ") + hipGetErrorString(e));
+  }
+  idx->dev_bytes = prev->dev_bytes;
+  Patcher P{M, v};
+  // final ids: surviving base filters and the new ones, in byte order
+  std::vector<uint32_t> rmap(nb + K, NONE);
+  {
+    auto tit = tomb.begin();
+    auto dit = dset.begin();
+    uint32_t fin = 0, k = 0;
+    idx->foff.push_back(0);
+    for (uint64_t b = 0; b <= nb; ++b) {
+      const uint8_t* bp = b < nb ? prev->fbytes.data() + prev->foff[b] : nullptr;
+      const uint64_t bl = b < nb ? prev->foff[b + 1] - prev->foff[b] : 0;
+      while (dit != dset.end() &&
+             (b == nb || cmp_bytes(reinterpret_cast<const uint8_t*>(dit->data()), dit->size(), bp, bl) < 0)) {
+        idx->fbytes.insert(idx->fbytes.end(), dit->begin(), dit->end());
+        idx->foff.push_back(idx->fbytes.size());
+        rmap[nb + k] = fin++;
+        ++dit;
+        ++k;
+      }
+      if (b == nb) break;
+      if (tit != tomb.end() && *tit == b) {
+        ++tit;
+        continue;
+      }
+      idx->fbytes.insert(idx->fbytes.end(), bp, bp + bl);
+      idx->foff.push_back(idx->fbytes.size());
+      rmap[b] = fin++;
+    }
+  }
+  // clear the deleted, insert the new (temporary ids nb + k), on the mirror
+  uint64_t twild = 0, dwild = 0;
+  for (uint32_t b : tomb) {
+    const uint8_t* bp = prev->fbytes.data() + prev->foff[b];
+    const uint64_t bl = prev->foff[b + 1] - prev->foff[b];
+    twild += wildcard(bp, bl);
+    P.erase(bp, bl);
+  }
+  {
+    uint32_t k = 0;
+    for (const std::string& d : dset) {
+      const uint8_t* p = reinterpret_cast<const uint8_t*>(d.data());
+      const bool wild = wildcard(p, d.size());
+      dwild += wild;
+      P.insert(p, d.size(), uint32_t(nb + k), wild);
+      ++k;
+    }
+  }
+  if (v.root_hash != NONE) v.root_hash = rmap[v.root_hash];
+  v.rh_mask &= ~P.rh_clear;
+  v.n_nodes = uint32_t(M.nodes_n);
+  v.n_filters = uint32_t(nf_new);
+  // filter lengths (stats), in final ids
+  uint16_t* flen = reinterpret_cast<uint16_t*>(M.blob.data() + M.o_flen);
+  for (uint64_t f = 0; f < nf_new; ++f)
+    flen[f] = uint16_t(std::min<uint64_t>(idx->foff[f + 1] - idx->foff[f], 65535));
+  P.mark(flen, nf_new * 2);
+  // device: copy the previous blob, apply the patched ranges (still in temporary
+  // ids), renumber every filter-id field; then the mirror the same way
+  const int rc = apply_patch_device(ctx, idx->dev_base, prev->dev_base, prev->dev_bytes, P.dirty, M.blob.data(), v,
+                                    M.o_hot, M.o_nodes, M.nodes_n, rmap);
+  if (rc) {  // the mirror no longer matches any snapshot: later updates take the overlay path
+    (void)hipFree(idx->dev_base);
+    delete idx;
+    delete prev->mirror;
+    prev->mirror = nullptr;
+    return rc;
+  }
+  renumber_host(M, v, rmap);
+  // the view's device pointers follow the new blob
+  uint8_t* NB = static_cast<uint8_t*>(idx->dev_base);
+  const uint8_t* OB = static_cast<const uint8_t*>(prev->dev_base);
+  auto rebase = [&](auto p) { return reinterpret_cast<decltype(p)>(NB + (reinterpret_cast<const uint8_t*>(p) - OB)); };
+  v.nodes = rebase(v.nodes);
+  v.dict = rebase(v.dict);
+  v.edges = rebase(v.edges);
+  v.hot = rebase(v.hot);
+  v.arena = rebase(v.arena);
+  v.sub_off = rebase(v.sub_off);
+  v.sub_ids = rebase(v.sub_ids);
+  v.efilt = rebase(v.efilt);
+  idx->dev_flen = reinterpret_cast<uint16_t*>(NB + M.o_flen);
+  emqx_gm_index_info_t& in = idx->info;
+  in.n_filters = nf_new;
+  in.n_wildcard = prev->info.n_wildcard - twild + dwild;
+  in.trie_empty = in.n_wildcard == 0;
+  in.n_nodes = M.nodes_n;
+  in.n_edges = prev->info.n_edges + P.new_edges;
+  in.n_words = M.dict_used;
+  in.max_depth = std::max(prev->info.max_depth, P.max_depth);
+  idx->mirror = prev->mirror;  // the mirror follows the newest snapshot
+  prev->mirror = nullptr;
+  *out = idx;
+  return EMQX_GM_OK;
+}
 
 int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo, const uint8_t* ops,
                  uint64_t n_ops, emqx_gm_index** out) {
@@ -92,7 +583,22 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
     *out = base;
     return EMQX_GM_OK;
   }
-  if (tomb.size() + dset.size() > std::max<uint64_t>(4096, nb / 8)) {
+  // a plain snapshot with its mirror: patched in place into a new flat snapshot
+  // (GM_UPDATE_OVERLAY: the overlay form below instead, A/B and tests)
+  // (a filter with '#' before its last word takes the overlay; no room left in
+  // the snapshot's tables: a rebuild, which restores the headroom)
+  bool no_room = false;
+  if (!prev->ov && prev->mirror && !getenv("GM_UPDATE_OVERLAY") &&
+      tomb.size() + dset.size() <= std::max<uint64_t>(4096, nb / 8)) {
+    bool wf = true;
+    for (const std::string& d : dset) wf = wf && well_formed(reinterpret_cast<const uint8_t*>(d.data()), d.size());
+    if (wf) {
+      const int rc = patch_update(ctx, prev, tomb, dset, out);
+      if (rc <= 0) return rc;
+      no_room = true;
+    }
+  }
+  if (no_room || tomb.size() + dset.size() > std::max<uint64_t>(4096, nb / 8)) {
     // compaction: a flat snapshot of the updated set
     std::vector<uint8_t> bytes;
     std::vector<uint64_t> offs{0};
@@ -224,8 +730,8 @@ void free_overlay(emqx_gm_index* idx) {
   OverlayState* ov = idx->ov;
   idx->ov = nullptr;
   if (ov->dev) {
-    hipSetDevice(idx->device);
-    hipFree(ov->dev);
+    (void)hipSetDevice(idx->device);
+    (void)hipFree(ov->dev);
   }
   if (ov->delta && ov->delta->refs.fetch_sub(1) == 1) free_index(ov->delta);
   if (ov->base && ov->base->refs.fetch_sub(1) == 1) free_index(ov->base);

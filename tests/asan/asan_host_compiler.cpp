@@ -16,6 +16,12 @@
 
 namespace gm {
 int set_err(emqx_gm_ctx*, int code, const std::string&) { return code; }  // gm_api.cpp's, minus the thread-local
+// gm_match.hip's device step of an in-place update: never reached here (no
+// context, so no snapshot keeps a mirror)
+int apply_patch_device(emqx_gm_ctx*, void*, const void*, size_t, const std::vector<std::pair<uint64_t, uint32_t>>&,
+                       const uint8_t*, const IndexView&, uint64_t, uint64_t, uint64_t, const std::vector<uint32_t>&) {
+  return EMQX_GM_EDEVICE;
+}
 }
 
 static int compile(const std::vector<std::string>& fs) {

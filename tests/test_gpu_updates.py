@@ -2,14 +2,42 @@
 emqx_gm_index_update applies insert/delete sequences with the reference's
 semantics (insert idempotent, delete only if present; emqx_trie.erl:107-136)
 and returns a new snapshot whose rows equal a rebuild over the updated set,
-while the previous snapshot keeps answering for the old set (RCU)."""
+while the previous snapshot keeps answering for the old set (RCU).
 
+Two forms (gm_overlay.cpp): the in-place patch (default: the newest plain
+snapshot's tables patched on a device copy -> a flat snapshot, one match pass)
+and the overlay (base + delta index, GM_UPDATE_OVERLAY=1, also the form taken
+for a filter with '#' before its last word or an update of a superseded
+snapshot)."""
+
+import os
 import random
 
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["patch", "overlay"])
+def form(request, monkeypatch):
+    if request.param == "overlay":
+        monkeypatch.setenv("GM_UPDATE_OVERLAY", "1")
+    else:
+        monkeypatch.delenv("GM_UPDATE_OVERLAY", raising=False)
+    return request.param
+
+
+def _is_flat(ctx, idx):
+    """A flat snapshot answers fanout (no subscribers: zero deliveries); an
+    overlay one refuses it (gm_api.cpp)."""
+    from emqx_amd import GpuMatchError
+    try:
+        ctx.fanout(idx, np.zeros(2, np.uint64), np.zeros(0, np.uint32))
+        return True
+    except GpuMatchError as e:
+        assert "EUNSUPPORTED" in str(e)
+        return False
 
 
 @pytest.fixture(scope="module")
@@ -50,7 +78,7 @@ def _rand_ops(rng, current, k):
     return ops
 
 
-def test_update_sequences_vs_oracle(ctx, orc):
+def test_update_sequences_vs_oracle(ctx, orc, form):
     from tests.test_gpu_parity import _rand_filter, _rand_topic
     rng = random.Random(21)
     current = {_rand_filter(rng).encode() for _ in range(500)}
@@ -62,6 +90,8 @@ def test_update_sequences_vs_oracle(ctx, orc):
         new = ctx.update_index(idx, ops)
         _check(ctx, orc, new, current, topics)
         assert [new.filter(i) for i in range(new.n_filters)] == sorted(current)
+        if new is not idx and form == "patch":
+            assert _is_flat(ctx, new)
         if rnd % 4 == 0:  # RCU: the previous snapshot still answers for the previous set
             _check(ctx, orc, idx, before, topics)
         idx.release()
@@ -69,7 +99,7 @@ def test_update_sequences_vs_oracle(ctx, orc):
     idx.release()
 
 
-def test_update_c1_scale_and_compaction(ctx, orc):
+def test_update_c1_scale_and_compaction(ctx, orc, form):
     from emqx_amd.engine import gen_filter_codes, render_codes
     from tests.test_gpu_parity import _rand_filter
     codes = gen_filter_codes(6, 20_000)
@@ -107,7 +137,7 @@ def test_update_c1_scale_and_compaction(ctx, orc):
     new.release()
 
 
-def test_update_edges(ctx, orc):
+def test_update_edges(ctx, orc, form):
     from emqx_amd import GpuMatchError
     idx = ctx.build_index([b"a/#", b"b"])
     same = ctx.update_index(idx, [(b"a/#", True), (b"zz", False)])  # no change: the same snapshot
@@ -116,10 +146,115 @@ def test_update_edges(ctx, orc):
     _check(ctx, orc, gone, set(), [b"a/x", b"b", b""])
     back = ctx.update_index(gone, [(b"b", True), (b"a/#", True), (b"+/+", True)])
     _check(ctx, orc, back, {b"a/#", b"b", b"+/+"}, [b"a/x", b"b", b"q/r", b"$SYS/x"])
-    with pytest.raises(GpuMatchError, match="EUNSUPPORTED"):
-        ctx.fanout(back, np.zeros(2, np.uint64), np.zeros(0, np.uint32))
+    assert _is_flat(ctx, back) == (form == "patch")
+    if form == "overlay":
+        with pytest.raises(GpuMatchError, match="EUNSUPPORTED"):
+            ctx.fanout(back, np.zeros(2, np.uint64), np.zeros(0, np.uint32))
     shard = ctx.build_index_shard([b"a/#"], np.array([3], np.uint32))
     with pytest.raises(GpuMatchError, match="EUNSUPPORTED"):
         ctx.update_index(shard, [(b"b", True)])
     for x in (idx, same, gone, back, shard):
+        x.release()
+
+
+TOPIC_WORDS = ["a", "b", "c", "", "$x", "long-word-over-8-bytes"]
+
+
+def _deep_filter(rng, depth):
+    ws = [rng.choice(TOPIC_WORDS + ["+"]) for _ in range(depth)]
+    if rng.random() < 0.3:
+        ws.append("#")
+    return "/".join(ws).encode()
+
+
+def test_patch_deep_root_inline_and_fallbacks(ctx, orc, monkeypatch):
+    """The in-place patch across every table kind: filters deeper than the
+    per-depth hot tables (the shared last table, the shared last edge table),
+    '#' and '+' at the root, '+' under '+' (inline and slot records), words
+    longer than the 8-byte dictionary head, the empty word; then the fallbacks:
+    a filter with '#' before its last word -> overlay, an update of a
+    superseded snapshot -> overlay, a delta too large for the tables' headroom
+    -> rebuild (flat again, with a fresh mirror)."""
+    monkeypatch.delenv("GM_UPDATE_OVERLAY", raising=False)
+    rng = random.Random(77)
+    current = {_deep_filter(rng, rng.randint(1, 22)) for _ in range(300)}
+    topics = ["/".join(rng.choice(TOPIC_WORDS) for _ in range(rng.randint(1, 24))).encode() for _ in range(3000)]
+    idx = ctx.build_index(sorted(current))
+    steps = [
+        [(b"#", True), (b"+", True), (b"+/+", True), (b"+/+/+/#", True)],
+        [(_deep_filter(rng, rng.randint(14, 24)), True) for _ in range(40)],
+        [(f, False) for f in rng.sample(sorted(current), 50)] + [(b"#", False)],
+        [(b"long-word-over-8-bytes/+/long-word-over-8-bytes-2", True), (b"//+//#", True), (b"", True)],
+    ]
+    for ops in steps:
+        for f, ins in ops:
+            (current.add if ins else current.discard)(f)
+        new = ctx.update_index(idx, ops)
+        _check(ctx, orc, new, current, topics)
+        assert _is_flat(ctx, new)
+        idx.release()
+        idx = new
+    # '#' inside a filter: the overlay form
+    ill = ctx.update_index(idx, [(b"a/#/b", True)])
+    _check(ctx, orc, ill, current | {b"a/#/b"}, topics)
+    assert not _is_flat(ctx, ill)
+    ill.release()
+    # the mirror moved on: an update of the superseded snapshot is an overlay
+    newer = ctx.update_index(idx, [(b"q/r", True)])
+    older = ctx.update_index(idx, [(b"q/s", True)])
+    assert _is_flat(ctx, newer) and not _is_flat(ctx, older)
+    _check(ctx, orc, older, current | {b"q/s"}, topics + [b"q/s", b"q/r"])
+    older.release()
+    idx.release()
+    idx = newer
+    current.add(b"q/r")
+    # no headroom for 4,000 new filters over ~400: the flat rebuild
+    ops = [(_deep_filter(rng, rng.randint(1, 8)), True) for _ in range(4000)]
+    for f, _ in ops:
+        current.add(f)
+    new = ctx.update_index(idx, ops)
+    _check(ctx, orc, new, current, topics)
+    assert _is_flat(ctx, new)
+    idx.release()
+    idx = new
+    ops = [(b"z/+", True)]  # the rebuilt snapshot has a mirror again
+    current.add(b"z/+")
+    new = ctx.update_index(idx, ops)
+    _check(ctx, orc, new, current, topics + [b"z/q"])
+    assert _is_flat(ctx, new)
+    idx.release()
+    new.release()
+
+
+@pytest.mark.timeout(600)
+def test_patch_c2_scale_equals_rebuild(ctx, orc):
+    """At C2 scale (1M wildcard filters), 2,000 deletes + 2,000 inserts patched
+    in place: the patched snapshot's rows on 1M C2 topics are identical to a
+    rebuilt index's (itself parity-checked against the oracle at this size in
+    test_gpu_scale.py), in both match modes."""
+    import time
+    from emqx_amd.engine import gen_filter_codes, render_codes, pack
+    os.environ.pop("GM_UPDATE_OVERLAY", None)
+    codes = gen_filter_codes(1, 1_000_000, wildcard_only=True)
+    fb, fo = render_codes(codes)
+    idx = ctx.build_index((fb, fo))
+    rng = random.Random(9)
+    base = orc.unpack(fb, fo)
+    dels = rng.sample(base, 2000)
+    extra = orc.unpack(*render_codes(gen_filter_codes(77, 2000, wildcard_only=True)))
+    ops = [(f, False) for f in dels] + [(f, True) for f in extra]
+    t0 = time.perf_counter()
+    new = ctx.update_index(idx, ops)
+    t_upd = time.perf_counter() - t0
+    assert _is_flat(ctx, new)
+    current = (set(base) - set(dels)) | set(extra)
+    flat = ctx.build_index(pack(sorted(current)))
+    assert new.n_filters == flat.n_filters == len(current)
+    tb, to = orc.render_codes(orc.gen_topic_codes(1, 0, 1_000_000, codes))
+    for exact in (True, False):
+        ra, ia = ctx.match(new, (tb, to), exact=exact)
+        rb, ib = ctx.match(flat, (tb, to), exact=exact)
+        assert np.array_equal(ra, rb) and np.array_equal(ia, ib)
+    print(f"[patch_c2] update of {len(ops)} ops: {t_upd * 1e3:.1f} ms", flush=True)
+    for x in (idx, new, flat):
         x.release()
