@@ -1909,12 +1909,13 @@ int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t byte
   }
   std::vector<uint64_t> desc;
   uint64_t pay_n = 0;
-  for (const auto& g : seg)
+  for (const auto& g : seg) {
     for (uint64_t b = g.first; b < g.second; b += PATCH_PIECE) {
       const uint64_t n = std::min<uint64_t>(PATCH_PIECE, g.second - b);
       desc.insert(desc.end(), {b, pay_n + (b - g.first), n});
     }
-  for (const auto& g : seg) pay_n += g.second - g.first;
+    pay_n += g.second - g.first;
+  }
   const uint64_t n_pieces = desc.size() / 3;
   if (n_pieces > 0x7FFFFFFFull) return set_err(ctx, EMQX_GM_EINVAL, "index_update: patch too large");
   // staging: desc | payload | rmap (one upload)
