@@ -12,6 +12,8 @@
 // Result rows use the ids of the updated set (lexicographic rank), exactly
 // what a full rebuild would return.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <set>
@@ -96,6 +98,8 @@ struct Cur {
   bool plus = false;                 // reached through '+'
 };
 
+struct NoRoom {};  // a table of the snapshot is full: the update rolls back and rebuilds
+
 struct Patcher {
   Mirror& M;
   IndexView& v;  // the new snapshot's view (its host-side fields are patched here)
@@ -103,7 +107,17 @@ struct Patcher {
   uint32_t rh_clear = 0;                             // tables that took a key outside Robin Hood order
   uint64_t new_edges = 0;
   uint32_t max_depth = 0;
+  // undo log: every write first saves the bytes it overwrites (rollback on NoRoom)
+  std::vector<uint8_t> undo_bytes;
+  uint64_t s_nodes_n, s_arena_n, s_dict_used, s_edge_used[EDGE_DEPTHS], s_hot_used[HOT_TABLES];
 
+  Patcher(Mirror& m, IndexView& view) : M(m), v(view) {
+    s_nodes_n = M.nodes_n;
+    s_arena_n = M.arena_n;
+    s_dict_used = M.dict_used;
+    std::memcpy(s_edge_used, M.edge_used, sizeof(s_edge_used));
+    std::memcpy(s_hot_used, M.hot_used, sizeof(s_hot_used));
+  }
   uint8_t* B() { return M.blob.data(); }
   Node* nodes() { return reinterpret_cast<Node*>(B() + M.o_nodes); }
   DictSlot* dict() { return reinterpret_cast<DictSlot*>(B() + M.o_dict); }
@@ -111,7 +125,28 @@ struct Patcher {
   HotSlot* hot() { return reinterpret_cast<HotSlot*>(B() + M.o_hot); }
   uint8_t* arena() { return B() + M.o_arena; }
   uint32_t* efilt() { return reinterpret_cast<uint32_t*>(B() + M.o_efilt); }
-  void mark(const void* p, size_t n) { dirty.emplace_back(uint64_t(static_cast<const uint8_t*>(p) - B()), uint32_t(n)); }
+  // before writing n bytes at p
+  void touch(const void* p, size_t n) {
+    const uint64_t off = uint64_t(static_cast<const uint8_t*>(p) - B());
+    dirty.emplace_back(off, uint32_t(n));
+    undo_bytes.insert(undo_bytes.end(), B() + off, B() + off + n);
+  }
+  template <class T> T& W(T& r) {
+    touch(&r, sizeof(T));
+    return r;
+  }
+  void rollback() {
+    size_t q = undo_bytes.size();
+    for (size_t k = dirty.size(); k-- > 0;) {
+      q -= dirty[k].second;
+      std::memcpy(B() + dirty[k].first, undo_bytes.data() + q, dirty[k].second);
+    }
+    M.nodes_n = s_nodes_n;
+    M.arena_n = s_arena_n;
+    M.dict_used = s_dict_used;
+    std::memcpy(M.edge_used, s_edge_used, sizeof(s_edge_used));
+    std::memcpy(M.hot_used, s_hot_used, sizeof(s_hot_used));
+  }
 
   // ---- word dictionary (dict_resolve's rules: length + head, tail against the arena)
   uint32_t dict_find(const uint8_t* w, uint64_t len) {
@@ -126,15 +161,16 @@ struct Patcher {
   uint32_t word(const uint8_t* w, uint64_t len) {
     uint32_t id = dict_find(w, len);
     if (id != NONE) return id;
-    id = uint32_t(M.arena_n);  // every word owns >= 1 byte: ids stay unique
+    const uint64_t own = len ? len : 1;  // every word owns >= 1 byte: ids stay unique
+    if (M.arena_n + own > M.arena_cap || (M.dict_used + 1) * 2 > v.dict_mask + 1) throw NoRoom{};
+    id = uint32_t(M.arena_n);
+    touch(arena() + id, own);
     if (len) std::memcpy(arena() + id, w, len);
     else arena()[id] = 0;
-    M.arena_n += len ? len : 1;
-    mark(arena() + id, len ? len : 1);
+    M.arena_n += own;
     uint64_t s = dict_slot(dict_hash_host(w, len), v.dict_mask);
     while (dict()[s].len != DICT_EMPTY_LEN) s = (s + 1) & v.dict_mask;
-    dict()[s] = DictSlot{word_head_host(w, len), uint32_t(len), id};
-    mark(&dict()[s], sizeof(DictSlot));
+    W(dict()[s]) = DictSlot{word_head_host(w, len), uint32_t(len), id};
     ++M.dict_used;
     return id;
   }
@@ -151,26 +187,27 @@ struct Patcher {
   }
   void edge_put(uint32_t depth, uint32_t parent, uint32_t wid, uint32_t child) {
     const int d = edge_depth(depth);
+    if ((M.edge_used[d] + 1) * 4 > (v.etab_mask[d] + 1) * 3) throw NoRoom{};  // load <= 0.75
     EdgeSlot* tab = edges() + v.etab_off[d];
     const uint64_t key = edge_key(parent, wid), mask = v.etab_mask[d];
     uint64_t s = edge_slot(key, mask);
     while (tab[s].key != EDGE_EMPTY) s = (s + 1) & mask;
-    tab[s] = EdgeSlot{key, child, 0};
-    mark(&tab[s], sizeof(EdgeSlot));
+    W(tab[s]) = EdgeSlot{key, child, 0};
     ++M.edge_used[d];
     ++new_edges;
   }
   uint32_t new_node() {
+    if (M.nodes_n >= M.nodes_cap || M.nodes_n >= REF_X) throw NoRoom{};
     const uint32_t id = uint32_t(M.nodes_n++);
-    nodes()[id] = Node{NONE, NONE, NONE, 0};
-    mark(&nodes()[id], sizeof(Node));
+    W(nodes()[id]) = Node{NONE, NONE, NONE, 0};
     return id;
   }
 
-  // ---- hot tables (any key order: the table's early exit is switched off)
+  // ---- hot tables
   HotSlot* htab(int t) { return hot() + v.hot_off[t]; }
   uint32_t hot_find(int t, uint64_t key) {
     const uint64_t cap = v.hot_cap[t];
+    if (!cap) return NONE;
     HotSlot* tab = htab(t);
     for (uint64_t s = hot_slot(key, cap);; s = s + 1 == cap ? 0 : s + 1) {
       if (tab[s].key == key) return uint32_t(s);
@@ -184,6 +221,7 @@ struct Patcher {
   // table's early exit is switched off (rh_clear).
   uint32_t hot_add(int t, uint64_t key) {
     const uint64_t cap = v.hot_cap[t];
+    if (!cap || (M.hot_used[t] + 1) * 5 > cap * 3) throw NoRoom{};  // load <= 0.6
     HotSlot* tab = htab(t);
     const uint64_t home = hot_slot(key, cap);
     uint64_t s = home, dist = 0;
@@ -194,41 +232,19 @@ struct Patcher {
       s = s + 1 == cap ? 0 : s + 1;
       ++dist;
     }
-    tab[s] = HotSlot{key, 0, HF_NONE, NONE, 0, HF_NONE, NONE};
-    mark(&tab[s], sizeof(HotSlot));
+    W(tab[s]) = HotSlot{key, 0, HF_NONE, NONE, 0, HF_NONE, NONE};
     ++M.hot_used[t];
     if (!rh_ok) rh_clear |= 1u << t;
     return uint32_t(s);
   }
-  // a node's first exact child: set NF_HAS_EXACT and the REF_X bit of the
-  // references to it (its parent's edge, and plus_child when it is a '+' child)
-  void gain_exact(const Cur& c) {
-    Node& nd = nodes()[c.v1];
-    if (nd.flags & NF_HAS_EXACT) return;
-    nd.flags |= NF_HAS_EXACT;
-    mark(&nd, sizeof(Node));
-    if (c.pv1 == NONE) return;  // the root: no reference
-    const int d = edge_depth(c.depth - 1);
-    EdgeSlot* tab = edges() + v.etab_off[d];
-    const uint64_t key = edge_key(c.pv1, c.pwid), mask = v.etab_mask[d];
-    for (uint64_t s = edge_slot(key, mask);; s = (s + 1) & mask) {
-      if (tab[s].key == key) {
-        tab[s].child |= REF_X;
-        mark(&tab[s], sizeof(EdgeSlot));
-        break;
-      }
-      if (tab[s].key == EDGE_EMPTY) break;
-    }
-    if (c.plus) {
-      Node& p = nodes()[c.pv1];
-      p.plus_child |= REF_X;
-      mark(&p, sizeof(Node));
-    }
-  }
   static uint32_t hid(const Cur& c) {
     return c.kind == CUR_ROOT ? 0u : c.kind == CUR_SLOT ? c.slot : (c.slot | HOT_INLINE);
   }
-  // the node record's fields: root -> IndexView, slot node -> its slot, inline node -> p_* of its parent's slot
+  // the node's record: root -> IndexView fields, slot node -> its slot, inline
+  // node -> p_* of its parent's slot.  rec() saves the slot before a write.
+  void rec(const Cur& c) {
+    if (c.kind != CUR_ROOT) touch(&htab(c.table)[c.slot], sizeof(HotSlot));
+  }
   uint32_t& f_sig(const Cur& c) {
     return c.kind == CUR_ROOT ? v.root_sig : c.kind == CUR_SLOT ? htab(c.table)[c.slot].sig : htab(c.table)[c.slot].p_sig;
   }
@@ -238,20 +254,35 @@ struct Patcher {
   uint32_t& f_end(const Cur& c) {
     return c.kind == CUR_SLOT ? htab(c.table)[c.slot].end_filter : htab(c.table)[c.slot].p_end;
   }
-  void mark_rec(const Cur& c) {
-    if (c.kind != CUR_ROOT) mark(&htab(c.table)[c.slot], sizeof(HotSlot));
-  }
   void set_hf(const Cur& c, uint32_t id) {  // 'match_#' of the node (keeps its HOT_PLUS flag)
     if (c.kind == CUR_ROOT) {
       v.root_hash = id == HF_NONE ? NONE : id;
       return;
     }
+    rec(c);
     uint32_t& f = f_hf(c);
     f = (f & HOT_PLUS) | id;
-    mark_rec(c);
+  }
+  // a node's first exact child: set NF_HAS_EXACT and the REF_X bit of the
+  // references to it (its parent's edge, and plus_child when it is a '+' child)
+  void gain_exact(const Cur& c) {
+    if (nodes()[c.v1].flags & NF_HAS_EXACT) return;
+    W(nodes()[c.v1]).flags |= NF_HAS_EXACT;
+    if (c.pv1 == NONE) return;  // the root: no reference
+    const int d = edge_depth(c.depth - 1);
+    EdgeSlot* tab = edges() + v.etab_off[d];
+    const uint64_t key = edge_key(c.pv1, c.pwid), mask = v.etab_mask[d];
+    for (uint64_t s = edge_slot(key, mask);; s = (s + 1) & mask) {
+      if (tab[s].key == key) {
+        W(tab[s]).child |= REF_X;
+        break;
+      }
+      if (tab[s].key == EDGE_EMPTY) break;
+    }
+    if (c.plus) W(nodes()[c.pv1]).plus_child |= REF_X;
   }
 
-  // Insert a well-formed filter with (temporary) id fid.
+  // Insert a well-formed filter with (temporary) id fid.  Throws NoRoom.
   void insert(const uint8_t* p, uint64_t len, uint32_t fid, bool wild) {
     Words ws(p, len);
     Cur c;
@@ -265,12 +296,10 @@ struct Patcher {
           ch = new_node();
           edge_put(c.depth, c.v1, hw, ch);
         }
-        ch &= REF_MASK;
-        nodes()[ch].end_filter = fid;
-        nodes()[ch].flags |= NF_END_WILD;
-        mark(&nodes()[ch], sizeof(Node));
-        nodes()[c.v1].hash_filter = fid;
-        mark(&nodes()[c.v1], sizeof(Node));
+        Node& hn = W(nodes()[ch & REF_MASK]);
+        hn.end_filter = fid;
+        hn.flags |= NF_END_WILD;
+        W(nodes()[c.v1]).hash_filter = fid;
         set_hf(c, fid);
         max_depth = std::max<uint32_t>(max_depth, c.depth + 1);
         return;
@@ -283,9 +312,9 @@ struct Patcher {
         ch = new_node();
         edge_put(c.depth, c.v1, wid, ch);
         if (plus) {
-          nodes()[c.v1].plus_child = ch;
-          nodes()[c.v1].flags |= NF_HAS_PLUS;
-          mark(&nodes()[c.v1], sizeof(Node));
+          Node& pn = W(nodes()[c.v1]);
+          pn.plus_child = ch;
+          pn.flags |= NF_HAS_PLUS;
         } else {
           gain_exact(c);
         }
@@ -299,11 +328,11 @@ struct Patcher {
       if (plus && c.kind == CUR_SLOT) {  // the '+' child of a slot-owning node lives in its slot
         HotSlot& P = htab(c.table)[c.slot];
         if (!(P.hf & HOT_PLUS)) {
+          W(P);
           P.hf |= HOT_PLUS;
           P.p_sig = 0;
           P.p_hf = HF_NONE;
           P.p_end = NONE;
-          mark(&P, sizeof(HotSlot));
         }
         n.kind = CUR_INLINE;
         n.slot = c.slot;
@@ -317,17 +346,15 @@ struct Patcher {
           if (c.kind == CUR_ROOT) {
             v.root_flags |= HOT_PLUS;
           } else {
+            rec(c);
             f_hf(c) |= HOT_PLUS;
-            mark_rec(c);
           }
         } else {  // the parent's exact-child signature and the table's exact-edge filter
+          rec(c);
           f_sig(c) |= sig_bit(wid);
-          mark_rec(c);
           if (v.efilt_mask[t]) {
             const uint32_t fh = edge_filter_hash(key);
-            uint32_t* fw = efilt() + v.efilt_off[t] + edge_filter_word(fh, v.efilt_mask[t]);
-            *fw |= edge_filter_bits(fh);
-            mark(fw, 4);
+            W(efilt()[v.efilt_off[t] + edge_filter_word(fh, v.efilt_mask[t])]) |= edge_filter_bits(fh);
           }
         }
         n.kind = CUR_SLOT;
@@ -336,11 +363,11 @@ struct Patcher {
       }
       c = n;
     }
+    rec(c);
     f_end(c) = fid | (wild ? END_WILD : 0u);
-    mark_rec(c);
-    nodes()[c.v1].end_filter = fid;
-    if (wild) nodes()[c.v1].flags |= NF_END_WILD;
-    mark(&nodes()[c.v1], sizeof(Node));
+    Node& en = W(nodes()[c.v1]);
+    en.end_filter = fid;
+    if (wild) en.flags |= NF_END_WILD;
     max_depth = std::max<uint32_t>(max_depth, c.depth);
   }
 
@@ -358,10 +385,8 @@ struct Patcher {
       if (ch == NONE) return;
       const bool last = i + 1 == ws.w.size();
       if (last && is1(p, w, '#')) {
-        nodes()[v1].hash_filter = NONE;
-        mark(&nodes()[v1], sizeof(Node));
-        nodes()[ch & REF_MASK].end_filter = NONE;
-        mark(&nodes()[ch & REF_MASK], sizeof(Node));
+        W(nodes()[v1]).hash_filter = NONE;
+        W(nodes()[ch & REF_MASK]).end_filter = NONE;
         if (wf) set_hf(c, HF_NONE);
         return;
       }
@@ -384,11 +409,10 @@ struct Patcher {
       }
       v1 = ch & REF_MASK;
     }
-    nodes()[v1].end_filter = NONE;
-    mark(&nodes()[v1], sizeof(Node));
+    W(nodes()[v1]).end_filter = NONE;
     if (wf) {
+      rec(c);
       f_end(c) = NONE;
-      mark_rec(c);
     }
   }
 };
@@ -422,37 +446,22 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
                         const std::set<std::string>& dset, emqx_gm_index** out) {
   Mirror& M = *prev->mirror;
   const uint64_t nb = prev->info.n_filters, K = dset.size();
-  // capacity (upper bounds: every word of every new filter new): otherwise rebuild
-  uint64_t words = 0, bytes = 0;
-  for (const std::string& d : dset) {
-    words += 1 + uint64_t(std::count(d.begin(), d.end(), '/'));
-    bytes += d.size() + 1;
-  }
   const uint64_t nf_new = nb - tomb.size() + K;
-  if (M.nodes_n + words > M.nodes_cap || M.arena_n + bytes > M.arena_cap || nf_new > M.flen_cap ||
-      (M.dict_used + words) * 2 > prev->view.dict_mask + 1)
-    return 1;
-  for (int d = 0; d < EDGE_DEPTHS; ++d)
-    if ((M.edge_used[d] + words) * 4 > (prev->view.etab_mask[d] + 1) * 3) return 1;
-  for (int t = 0; t < HOT_TABLES; ++t)
-    if (prev->view.hot_cap[t] && (M.hot_used[t] + words) * 5 > prev->view.hot_cap[t] * 3) return 1;
-  for (int t = 1; t < HOT_TABLES; ++t)  // a depth the base never reached has no table
-    if (!prev->view.hot_cap[t])
-      for (const std::string& d : dset)
-        if (uint64_t(std::count(d.begin(), d.end(), '/')) + 1 >= uint64_t(t)) return 1;
-
+  if (nf_new > M.flen_cap) return 1;  // the other tables are checked per insert (NoRoom)
+  // GM_UPDATE_TIMING: phase times on stderr (diagnostics)
+  const bool timing = getenv("GM_UPDATE_TIMING") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char* what) {
+    if (!timing) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "[gm_update] %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
   auto* idx = new emqx_gm_index;
   idx->device = prev->device;
   idx->view = prev->view;
   idx->info = prev->info;
   IndexView& v = idx->view;
-  hipError_t e = hipSetDevice(prev->device);
-  if (e == hipSuccess) e = hipMalloc(&idx->dev_base, prev->dev_bytes);
-  if (e != hipSuccess) {
-    delete idx;
-    return set_err(ctx, EMQX_GM_ENOMEM, std::string("index_update: hipMalloc: ") + hipGetErrorString(e));
-  }
-  idx->dev_bytes = prev->dev_bytes;
   Patcher P{M, v};
   // final ids: surviving base filters and the new ones, in byte order
   std::vector<uint32_t> rmap(nb + K, NONE);
@@ -482,6 +491,7 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
       rmap[b] = fin++;
     }
   }
+  phase("ids");
   // clear the deleted, insert the new (temporary ids nb + k), on the mirror
   uint64_t twild = 0, dwild = 0;
   for (uint32_t b : tomb) {
@@ -490,7 +500,7 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
     twild += wildcard(bp, bl);
     P.erase(bp, bl);
   }
-  {
+  try {
     uint32_t k = 0;
     for (const std::string& d : dset) {
       const uint8_t* p = reinterpret_cast<const uint8_t*>(d.data());
@@ -499,18 +509,34 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
       P.insert(p, d.size(), uint32_t(nb + k), wild);
       ++k;
     }
+  } catch (const NoRoom&) {  // the mirror back to prev's bytes; the caller rebuilds
+    P.rollback();
+    delete idx;
+    phase("no room");
+    return 1;
   }
   if (v.root_hash != NONE) v.root_hash = rmap[v.root_hash];
   v.rh_mask &= ~P.rh_clear;
   v.n_nodes = uint32_t(M.nodes_n);
   v.n_filters = uint32_t(nf_new);
+  phase("patch");
   // filter lengths (stats), in final ids
   uint16_t* flen = reinterpret_cast<uint16_t*>(M.blob.data() + M.o_flen);
+  P.touch(flen, nf_new * 2);
   for (uint64_t f = 0; f < nf_new; ++f)
     flen[f] = uint16_t(std::min<uint64_t>(idx->foff[f + 1] - idx->foff[f], 65535));
-  P.mark(flen, nf_new * 2);
   // device: copy the previous blob, apply the patched ranges (still in temporary
   // ids), renumber every filter-id field; then the mirror the same way
+  phase("flen");
+  hipError_t e = hipSetDevice(prev->device);
+  if (e == hipSuccess) e = hipMalloc(&idx->dev_base, prev->dev_bytes);
+  if (e != hipSuccess) {
+    P.rollback();
+    delete idx;
+    return set_err(ctx, EMQX_GM_ENOMEM, std::string("index_update: hipMalloc: ") + hipGetErrorString(e));
+  }
+  idx->dev_bytes = prev->dev_bytes;
+  phase("alloc");
   const int rc = apply_patch_device(ctx, idx->dev_base, prev->dev_base, prev->dev_bytes, P.dirty, M.blob.data(), v,
                                     M.o_hot, M.o_nodes, M.nodes_n, rmap);
   if (rc) {  // the mirror no longer matches any snapshot: later updates take the overlay path
@@ -520,7 +546,9 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
     prev->mirror = nullptr;
     return rc;
   }
+  phase("device");
   renumber_host(M, v, rmap);
+  phase("renumber");
   // the view's device pointers follow the new blob
   uint8_t* NB = static_cast<uint8_t*>(idx->dev_base);
   const uint8_t* OB = static_cast<const uint8_t*>(prev->dev_base);
