@@ -18,6 +18,7 @@
 #include <cstring>
 #include <set>
 #include <string>
+#include <thread>
 
 #include "gm_internal.h"
 
@@ -418,25 +419,33 @@ struct Patcher {
 };
 
 // rmap[temporary id] -> final id (NONE: deleted) over every filter-id field
-// (the host twin of gm_match.hip's k_renumber)
+// (the host twin of gm_match.hip's k_renumber), split over a few threads
 void renumber_host(Mirror& M, const IndexView& v, const std::vector<uint32_t>& rmap) {
   HotSlot* hot = reinterpret_cast<HotSlot*>(M.blob.data() + M.o_hot);
+  Node* nd = reinterpret_cast<Node*>(M.blob.data() + M.o_nodes);
   uint64_t slots = 0;
   for (int t = 0; t < HOT_TABLES; ++t) slots = std::max(slots, v.hot_off[t] + v.hot_cap[t]);
   const uint32_t* r = rmap.data();
-  for (uint64_t s = 0; s < slots; ++s) {
-    HotSlot& h = hot[s];
-    if (h.key == EDGE_EMPTY) continue;
-    h.hf = renum_field(h.hf, HF_NONE, HOT_PLUS, r);
-    h.end_filter = renum_field(h.end_filter, NONE, END_WILD, r);
-    h.p_hf = renum_field(h.p_hf, HF_NONE, HOT_PLUS, r);
-    h.p_end = renum_field(h.p_end, NONE, END_WILD, r);
-  }
-  Node* nd = reinterpret_cast<Node*>(M.blob.data() + M.o_nodes);
-  for (uint64_t i = 0; i < M.nodes_n; ++i) {
-    nd[i].hash_filter = renum_field(nd[i].hash_filter, NONE, 0, r);
-    nd[i].end_filter = renum_field(nd[i].end_filter, NONE, 0, r);
-  }
+  const uint64_t n_nodes = M.nodes_n;
+  auto work = [=](unsigned part, unsigned parts) {
+    for (uint64_t s = slots * part / parts, e = slots * (part + 1) / parts; s < e; ++s) {
+      HotSlot& h = hot[s];
+      if (h.key == EDGE_EMPTY) continue;
+      h.hf = renum_field(h.hf, HF_NONE, HOT_PLUS, r);
+      h.end_filter = renum_field(h.end_filter, NONE, END_WILD, r);
+      h.p_hf = renum_field(h.p_hf, HF_NONE, HOT_PLUS, r);
+      h.p_end = renum_field(h.p_end, NONE, END_WILD, r);
+    }
+    for (uint64_t i = n_nodes * part / parts, e = n_nodes * (part + 1) / parts; i < e; ++i) {
+      nd[i].hash_filter = renum_field(nd[i].hash_filter, NONE, 0, r);
+      nd[i].end_filter = renum_field(nd[i].end_filter, NONE, 0, r);
+    }
+  };
+  const unsigned parts = (slots + n_nodes) < (1u << 18) ? 1u : std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (unsigned p = 1; p < parts; ++p) th.emplace_back(work, p, parts);
+  work(0, parts);
+  for (auto& t : th) t.join();
 }
 
 }  // namespace
@@ -463,32 +472,51 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
   idx->info = prev->info;
   IndexView& v = idx->view;
   Patcher P{M, v};
-  // final ids: surviving base filters and the new ones, in byte order
+  // final ids: surviving base filters and the new ones, in byte order; the
+  // base filters between two events (a tombstone, an insert position) move as
+  // one run
   std::vector<uint32_t> rmap(nb + K, NONE);
   {
+    std::vector<uint64_t> ipos;  // per new filter (byte order): base filters sorting before it
+    ipos.reserve(K);
+    for (const std::string& d : dset) {
+      bool found;
+      ipos.push_back(base_rank(prev, reinterpret_cast<const uint8_t*>(d.data()), d.size(), &found));
+    }
+    idx->fbytes.reserve(prev->fbytes.size() + K * 16);
+    idx->foff.reserve(nf_new + 1);
+    idx->foff.push_back(0);
     auto tit = tomb.begin();
     auto dit = dset.begin();
-    uint32_t fin = 0, k = 0;
-    idx->foff.push_back(0);
-    for (uint64_t b = 0; b <= nb; ++b) {
-      const uint8_t* bp = b < nb ? prev->fbytes.data() + prev->foff[b] : nullptr;
-      const uint64_t bl = b < nb ? prev->foff[b + 1] - prev->foff[b] : 0;
-      while (dit != dset.end() &&
-             (b == nb || cmp_bytes(reinterpret_cast<const uint8_t*>(dit->data()), dit->size(), bp, bl) < 0)) {
+    uint64_t b = 0, k = 0;
+    uint32_t fin = 0;
+    auto run = [&](uint64_t e) {  // base filters [b, e), none tombstoned
+      if (e <= b) return;
+      const uint64_t a0 = prev->foff[b], a1 = prev->foff[e];
+      const uint64_t shift = idx->fbytes.size() - a0;
+      idx->fbytes.insert(idx->fbytes.end(), prev->fbytes.begin() + a0, prev->fbytes.begin() + a1);
+      for (uint64_t x = b; x < e; ++x) {
+        idx->foff.push_back(prev->foff[x + 1] + shift);
+        rmap[x] = fin++;
+      }
+      b = e;
+    };
+    while (b < nb || k < K) {
+      const uint64_t next_t = tit != tomb.end() ? *tit : nb;
+      const uint64_t next_i = k < K ? ipos[k] : nb;
+      run(std::min(next_t, next_i));
+      if (k < K && ipos[k] == b) {  // new filters sort before base filter b
         idx->fbytes.insert(idx->fbytes.end(), dit->begin(), dit->end());
         idx->foff.push_back(idx->fbytes.size());
         rmap[nb + k] = fin++;
         ++dit;
         ++k;
-      }
-      if (b == nb) break;
-      if (tit != tomb.end() && *tit == b) {
+      } else if (tit != tomb.end() && *tit == b) {
         ++tit;
-        continue;
+        ++b;
+      } else if (b >= nb && k >= K) {
+        break;
       }
-      idx->fbytes.insert(idx->fbytes.end(), bp, bp + bl);
-      idx->foff.push_back(idx->fbytes.size());
-      rmap[b] = fin++;
     }
   }
   phase("ids");

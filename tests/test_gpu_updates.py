@@ -210,11 +210,17 @@ def test_patch_deep_root_inline_and_fallbacks(ctx, orc, monkeypatch):
     current.add(b"q/r")
     # no headroom for 4,000 new filters over ~400: the flat rebuild
     ops = [(_deep_filter(rng, rng.randint(1, 8)), True) for _ in range(4000)]
+    before = set(current)
     for f, _ in ops:
         current.add(f)
     new = ctx.update_index(idx, ops)
     _check(ctx, orc, new, current, topics)
     assert _is_flat(ctx, new)
+    # the failed patch rolled idx's mirror back: idx still patches correctly
+    again = ctx.update_index(idx, [(b"z/q/+", True), (b"a", False)])
+    assert _is_flat(ctx, again)
+    _check(ctx, orc, again, (before | {b"z/q/+"}) - {b"a"}, topics + [b"z/q/x"])
+    again.release()
     idx.release()
     idx = new
     ops = [(b"z/+", True)]  # the rebuilt snapshot has a mirror again
