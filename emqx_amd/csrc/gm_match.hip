@@ -984,7 +984,14 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
 // row outgrows FAST_MC, is marked (CW_OVF) and queued for the listed pass
 // like k_walk's overflow.  Same hdr / wids input, same stage / cnt / tile-sum
 // output as k_walk, so the listed pass, the scan and k_assemble are shared.
-constexpr int CW_CAP = 192;                // frontier entries per wave and level
+// Frontier entries per wave and level: 9 B each, two lists, so a 4-wave
+// block's LDS is 72 * CW_CAP + 3 KB; 236 keeps it under 20 KB, i.e. 8 blocks
+// (32 waves) per CU in 160 KB.  (192 -> 236 cut C3's list overflow rows; the
+// overflowed topics are re-walked by the listed pass.)
+#ifndef GM_CW_CAP
+#define GM_CW_CAP 236
+#endif
+constexpr int CW_CAP = GM_CW_CAP;
 constexpr uint32_t CW_OVF = 0x40000000u;   // in a topic's LDS match counter: queued for the listed pass
 
 __device__ __forceinline__ void wave_lds_sync() {
