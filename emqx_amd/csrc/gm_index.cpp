@@ -444,7 +444,9 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (int t = 0; t < HOT_TABLES; ++t) {
     if (getenv("GM_NO_EDGE_FILTER")) break;  // A/B knob
     if (!ex_edges[t] || (ex_edges[t] < 4 * ex_parents[t] && !getenv("GM_EFILT_ALL"))) continue;  // A/B knob
-    const uint64_t words = std::max<uint64_t>(32, next_pow2(ex_edges[t] / 2 + 1));  // 16-32 bits per key
+    uint64_t div = 2;  // 16-32 bits per key; GM_EFILT_DIV: A/B knob (4: 8-16 bits, 8: 4-8 bits)
+    if (const char* e = getenv("GM_EFILT_DIV")) div = std::min<uint64_t>(64, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
+    const uint64_t words = std::max<uint64_t>(32, next_pow2(ex_edges[t] / div + 1));
     if (words * 4 > (4ull << 20)) continue;
     efilt_off[t] = efilt_total;
     efilt_mask[t] = uint32_t(words - 1);

@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -994,6 +995,15 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
 constexpr int CW_CAP = GM_CW_CAP;
 constexpr uint32_t CW_OVF = 0x40000000u;   // in a topic's LDS match counter: queued for the listed pass
 
+#ifdef GM_PROBE_STATS
+// Diagnostic build only (-DGM_PROBE_STATS): a census of the coop walk's
+// probes per level [level][k]: 0 entries, 1 exact candidates (a word), 2 past
+// the signature, 3 past the exact-edge filter (= exact probes issued), 4 exact
+// children found, 5 '+' slot probes issued, 6 '+' children found (slot), 7
+// '+' children taken inline.  Printed by run_match after each call.
+__device__ unsigned long long g_pstats[8][8];
+#endif
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1084,6 +1094,9 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
       const bool last = act && level + 1 == (lw.y & 0xFFu);
       const bool ldollar = (lw.y & TOK_DOLLAR) != 0;
       bool dx = act && wid != NONE && (en.y & sig_bit(wid));
+#ifdef GM_PROBE_STATS
+      const bool st_cand = act && wid != NONE, st_sig = dx;
+#endif
       if (fmask && dx) {  // the table's exact-edge filter (an L2 hit) before a random line
         const uint32_t fh = edge_filter_hash(hot_key(id, wid, lvl));
         const uint32_t fb = edge_filter_bits(fh);
@@ -1109,6 +1122,16 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
       const uint32_t hp = pin ? (id | HOT_INLINE)
                               : dp ? hot_resolve(tab, capu, hot_key(id, ix.plus_word, lvl), sp, rp, last, hflat, hrh)
                                    : NONE;
+#ifdef GM_PROBE_STATS
+      {
+        const unsigned long long c[8] = {__ballot(act), __ballot(st_cand), __ballot(st_sig), __ballot(dx),
+                                         __ballot(hx != NONE), __ballot(dp && !pin), __ballot(dp && !pin && hp != NONE),
+                                         __ballot(pin)};
+        if (lane == 0)
+          for (int k = 0; k < 8; ++k)
+            if (c[k]) atomicAdd(&g_pstats[lvl < 7 ? lvl : 7][k], (unsigned long long)__popcll(c[k]));
+      }
+#endif
       // visits: 'match_#', the end filter on the last level, else the next frontier
 #define GM_CW_EMIT(f)                                   \
   do {                                                  \
@@ -2140,6 +2163,19 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
   }
 #undef GM_WALK
 #undef GM_LAUNCH_WALK
+#ifdef GM_PROBE_STATS
+  {
+    unsigned long long h[8][8], z[8][8] = {};
+    if (hipStreamSynchronize(st) == hipSuccess && hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pstats), sizeof h) == hipSuccess) {
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pstats), z, sizeof z);
+      for (int l = 0; l < 8; ++l)
+        if (h[l][0])
+          fprintf(stderr, "[probe_stats] level %d entries %llu cand %llu sig %llu efilt %llu found %llu plus_slot %llu "
+                  "plus_found %llu plus_inline %llu\n", l, h[l][0], h[l][1], h[l][2], h[l][3], h[l][4], h[l][5], h[l][6],
+                  h[l][7]);
+    }
+  }
+#endif
   hipEventRecord(after_main, st);
   hipLaunchKernelGGL(k_sum_tiles, dim3(256), dim3(256), 0, st, probe_tile, (n + 63) / 64, probe_ctr);
   const uint64_t lblk = std::min<uint64_t>(nblk, 512);
