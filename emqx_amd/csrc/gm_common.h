@@ -185,6 +185,16 @@ GM_HD uint64_t edge_key(uint32_t parent, uint32_t word) { return (uint64_t(paren
 GM_HD uint64_t edge_slot(uint64_t key, uint64_t mask) { return fmix64(key) & mask; }
 
 GM_HD int hot_table(uint32_t depth) { return depth < uint32_t(HOT_TABLES) ? int(depth) : HOT_TABLES - 1; }
+// Is the '+' child of a node at `pdepth` held inline in the node's own slot?
+// Only under a slot-owning node (not the root, not an inline node), and not
+// under a node of depth HOT_TABLES-2: its '+' child's children go to the
+// shared last table, whose keys must tell parents apart by slot number, and an
+// inline hot id there would name a slot of table HOT_TABLES-2 beside the hot
+// ids of the shared table's own inline nodes (same numbers, same INLINE bit).
+// Such a '+' child owns a slot of the shared table instead.
+GM_HD bool plus_inline(uint32_t pdepth, bool parent_owns_slot) {
+  return parent_owns_slot && pdepth != 0 && pdepth != uint32_t(HOT_TABLES - 2);
+}
 // Key of the child of `parent` (a node at depth `pdepth`) through word `word`.
 GM_HD uint64_t hot_key(uint32_t parent, uint32_t word, uint32_t pdepth) {
   return ((uint64_t(parent) << 32) | word) | (pdepth == uint32_t(HOT_TABLES - 2) ? HOT_KEY_MARK : 0ull);

@@ -317,7 +317,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   std::vector<uint8_t> inl(NN, 0);
   for (uint64_t i = 1; i < NN; ++i) {
     const HNode& h = nodes[i];
-    inl[i] = h.kind == 1 && h.parent != 0 && nodes[h.parent].kind != 2 && !inl[h.parent];
+    inl[i] = h.kind == 1 && nodes[h.parent].kind != 2 && plus_inline(nodes[h.parent].depth, h.parent != 0 && !inl[h.parent]);
   }
   uint64_t hot_n[HOT_TABLES] = {0};
   for (uint64_t i = 1; i < NN; ++i)
@@ -499,7 +499,14 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // ---- 6. upload: one allocation, 256-B aligned sections.  A plain index (no
   // shard ids, no subscriber lists) keeps a host mirror of the blob for
   // in-place updates, with headroom for appended nodes, words and filters.
-  const bool keep_mirror = ctx && !gids && !sub_off && !getenv("GM_NO_MIRROR");
+  // (no context but an `out`: a host-only index whose view points into its
+  // mirror -- the CPU test of the in-place update, tests/asan/)
+  const bool host_mirror = !ctx && out && !host_only;
+  if (host_mirror && (gids || sub_off)) {
+    delete idx;
+    return set_err(ctx, EMQX_GM_EINVAL, "index_build: host-only index without subscribers or shard ids only");
+  }
+  const bool keep_mirror = host_mirror || (ctx && !gids && !sub_off && !getenv("GM_NO_MIRROR"));
   const uint64_t nodes_cap = keep_mirror ? NN + NN / 4 + 1024 : NN;
   const uint64_t arena_cap = keep_mirror ? arena.size() + arena.size() / 4 + 65536 : arena.size();
   const uint64_t flen_cap = keep_mirror ? uint64_t(nf) + nf / 4 + 1024 : nf;
@@ -531,14 +538,16 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     delete idx;
     return EMQX_GM_OK;
   }
-  hipError_t e = hipSetDevice(ctx->device);
-  if (e == hipSuccess) e = hipMalloc(&idx->dev_base, total);
-  if (e != hipSuccess) {
-    delete idx;
-    return set_err(ctx, EMQX_GM_ENOMEM, std::string("index_build: hipMalloc: ") + hipGetErrorString(e));
+  hipError_t e = hipSuccess;
+  if (!host_mirror) {
+    e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipMalloc(&idx->dev_base, total);
+    if (e != hipSuccess) {
+      delete idx;
+      return set_err(ctx, EMQX_GM_ENOMEM, std::string("index_build: hipMalloc: ") + hipGetErrorString(e));
+    }
   }
   idx->dev_bytes = total;
-  uint8_t* B = static_cast<uint8_t*>(idx->dev_base);
   // the blob assembled on the host (the mirror, when kept) and sent in one copy
   std::vector<uint8_t> hb(total, 0);
   auto put = [&](size_t off, const void* src, size_t bytes) {
@@ -554,7 +563,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   put(o_flen, flen.data(), flen.size() * 2);
   put(o_gmap, idx->gmap.data(), idx->gmap.size() * 4);
   put(o_efilt, efilt.data(), efilt.size() * 4);
-  e = hipMemcpy(B, hb.data(), total, hipMemcpyHostToDevice);
+  if (!host_mirror) e = hipMemcpy(idx->dev_base, hb.data(), total, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipFree(idx->dev_base);
     delete idx;
@@ -580,6 +589,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     for (int t = 0; t < HOT_TABLES; ++t) m->hot_used[t] = hot_n[t];
     idx->mirror = m;
   }
+  // the view's base: the device blob, or (host-only index) the mirror
+  uint8_t* B = host_mirror ? idx->mirror->blob.data() : static_cast<uint8_t*>(idx->dev_base);
 
   IndexView& v = idx->view;
   v.nodes = reinterpret_cast<const Node*>(B + o_nodes);

@@ -323,7 +323,7 @@ __device__ __forceinline__ HotRec plus_inline_load(const HotSlot* ptab, uint32_t
   return r;
 }
 // Whether the '+' child of frontier entry `id` (a node at depth lvl) is inline.
-__device__ __forceinline__ bool plus_is_inline(uint32_t lvl, uint32_t id) { return lvl != 0 && !(id & HOT_INLINE); }
+__device__ __forceinline__ bool plus_is_inline(uint32_t lvl, uint32_t id) { return plus_inline(lvl, !(id & HOT_INLINE)); }
 
 // Issue (load the home slot of) / take (resolve and visit) one probe of a
 // frontier entry: the exact edge (word wid) or the '+' edge.  An inline '+'

@@ -326,7 +326,7 @@ struct Patcher {
       n.pv1 = c.v1;
       n.pwid = wid;
       n.plus = plus;
-      if (plus && c.kind == CUR_SLOT) {  // the '+' child of a slot-owning node lives in its slot
+      if (plus && plus_inline(c.depth, c.kind == CUR_SLOT)) {  // the '+' child lives in its parent's slot
         HotSlot& P = htab(c.table)[c.slot];
         if (!(P.hf & HOT_PLUS)) {
           W(P);
@@ -394,7 +394,7 @@ struct Patcher {
       if (wf) {  // follow the hot path (ill-formed filters have no hot fields)
         const bool plus = is1(p, w, '+');
         Cur n;
-        if (plus && c.kind == CUR_SLOT) {
+        if (plus && plus_inline(uint32_t(i), c.kind == CUR_SLOT)) {
           n.kind = CUR_INLINE;
           n.slot = c.slot;
           n.table = c.table;
@@ -556,30 +556,33 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
   // device: copy the previous blob, apply the patched ranges (still in temporary
   // ids), renumber every filter-id field; then the mirror the same way
   phase("flen");
-  hipError_t e = hipSetDevice(prev->device);
-  if (e == hipSuccess) e = hipMalloc(&idx->dev_base, prev->dev_bytes);
-  if (e != hipSuccess) {
-    P.rollback();
-    delete idx;
-    return set_err(ctx, EMQX_GM_ENOMEM, std::string("index_update: hipMalloc: ") + hipGetErrorString(e));
+  const bool host = prev->dev_base == nullptr;  // a host-only index (CPU test): the mirror is the index
+  if (!host) {
+    hipError_t e = hipSetDevice(prev->device);
+    if (e == hipSuccess) e = hipMalloc(&idx->dev_base, prev->dev_bytes);
+    if (e != hipSuccess) {
+      P.rollback();
+      delete idx;
+      return set_err(ctx, EMQX_GM_ENOMEM, std::string("index_update: hipMalloc: ") + hipGetErrorString(e));
+    }
+    phase("alloc");
+    const int rc = apply_patch_device(ctx, idx->dev_base, prev->dev_base, prev->dev_bytes, P.dirty, M.blob.data(), v,
+                                      M.o_hot, M.o_nodes, M.nodes_n, rmap);
+    if (rc) {  // the mirror no longer matches any snapshot: later updates take the overlay path
+      (void)hipFree(idx->dev_base);
+      delete idx;
+      delete prev->mirror;
+      prev->mirror = nullptr;
+      return rc;
+    }
+    phase("device");
   }
   idx->dev_bytes = prev->dev_bytes;
-  phase("alloc");
-  const int rc = apply_patch_device(ctx, idx->dev_base, prev->dev_base, prev->dev_bytes, P.dirty, M.blob.data(), v,
-                                    M.o_hot, M.o_nodes, M.nodes_n, rmap);
-  if (rc) {  // the mirror no longer matches any snapshot: later updates take the overlay path
-    (void)hipFree(idx->dev_base);
-    delete idx;
-    delete prev->mirror;
-    prev->mirror = nullptr;
-    return rc;
-  }
-  phase("device");
   renumber_host(M, v, rmap);
   phase("renumber");
-  // the view's device pointers follow the new blob
-  uint8_t* NB = static_cast<uint8_t*>(idx->dev_base);
-  const uint8_t* OB = static_cast<const uint8_t*>(prev->dev_base);
+  // the view's pointers follow the new blob (a host-only index keeps the mirror's)
+  uint8_t* NB = host ? M.blob.data() : static_cast<uint8_t*>(idx->dev_base);
+  const uint8_t* OB = host ? M.blob.data() : static_cast<const uint8_t*>(prev->dev_base);
   auto rebase = [&](auto p) { return reinterpret_cast<decltype(p)>(NB + (reinterpret_cast<const uint8_t*>(p) - OB)); };
   v.nodes = rebase(v.nodes);
   v.dict = rebase(v.dict);
@@ -589,7 +592,7 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
   v.sub_off = rebase(v.sub_off);
   v.sub_ids = rebase(v.sub_ids);
   v.efilt = rebase(v.efilt);
-  idx->dev_flen = reinterpret_cast<uint16_t*>(NB + M.o_flen);
+  idx->dev_flen = host ? nullptr : reinterpret_cast<uint16_t*>(NB + M.o_flen);
   emqx_gm_index_info_t& in = idx->info;
   in.n_filters = nf_new;
   in.n_wildcard = prev->info.n_wildcard - twild + dwild;
@@ -654,7 +657,7 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
       no_room = true;
     }
   }
-  if (no_room || tomb.size() + dset.size() > std::max<uint64_t>(4096, nb / 8)) {
+  if (no_room || tomb.size() + dset.size() > std::max<uint64_t>(4096, nb / 8) || !base->dev_base) {
     // compaction: a flat snapshot of the updated set
     std::vector<uint8_t> bytes;
     std::vector<uint64_t> offs{0};

@@ -1,14 +1,18 @@
 // tests/asan/asan_host_compiler.cpp — TEST ONLY: the host index compiler
-// (emqx_amd/csrc/gm_index.cpp) and the overlay id mapping (gm_overlay.cpp)
-// built with AddressSanitizer + UBSan and fed untrusted filter
-// bytes: random bytes (NUL, '/', '+', '#', 0xFF), empty sets and empty
-// filters, 65,535-byte filters, 5,000-level filters, duplicates.  Host-only:
-// build_index(host_only) never touches a device.  Built and run by
+// (emqx_amd/csrc/gm_index.cpp), the overlay id mapping and the in-place
+// update (gm_overlay.cpp) built with AddressSanitizer + UBSan
+// and fed untrusted filter bytes: random bytes (NUL, '/', '+', '#', 0xFF),
+// empty sets and empty filters, 65,535-byte filters, 5,000-level filters,
+// duplicates; then random insert/delete sequences patched into a host-only
+// index (its mirror is the index) with every table invariant checked after
+// each update.  Never touches a device.  Built and run by
 // tests/test_host_cpu.py::test_host_compiler_under_asan (`make -C
 // emqx_amd/csrc asan`).
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <random>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -42,6 +46,256 @@ static int compile(const std::vector<std::string>& fs) {
     if (perm[i] >= info.n_filters) return -100;
   return 0;
 }
+
+// ---- in-place update: random sequences on a host-only index ---------------
+namespace {
+using namespace gm;
+
+std::vector<std::string> split_words(const std::string& f) {
+  std::vector<std::string> w;
+  size_t a = 0;
+  for (size_t i = 0; i <= f.size(); ++i)
+    if (i == f.size() || f[i] == '/') {
+      w.push_back(f.substr(a, i - a));
+      a = i + 1;
+    }
+  return w;
+}
+uint32_t v_dict_find(const IndexView& v, const std::string& w) {
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(w.data());
+  const uint64_t head = word_head_host(p, w.size());
+  for (uint64_t s = dict_slot(dict_hash_host(p, w.size()), v.dict_mask);; s = (s + 1) & v.dict_mask) {
+    const DictSlot& d = v.dict[s];
+    if (d.len == DICT_EMPTY_LEN) return NONE;
+    if (d.len == w.size() && d.head == head &&
+        (w.size() <= 8 || std::memcmp(v.arena + d.word + 8, p + 8, w.size() - 8) == 0))
+      return d.word;
+  }
+}
+uint32_t v_edge_get(const IndexView& v, uint32_t depth, uint32_t parent, uint32_t wid) {
+  const int d = edge_depth(depth);
+  const EdgeSlot* tab = v.edges + v.etab_off[d];
+  const uint64_t key = edge_key(parent, wid), mask = v.etab_mask[d];
+  for (uint64_t s = edge_slot(key, mask);; s = (s + 1) & mask) {
+    if (tab[s].key == key) return tab[s].child;
+    if (tab[s].key == EDGE_EMPTY) return NONE;
+  }
+}
+// the device lookup (gm_match.hip hot_resolve): with rh, an absent key stops
+// at the first resident nearer its own home than the probe
+uint32_t v_hot_lookup(const IndexView& v, int t, uint64_t key, bool rh) {
+  const uint64_t cap = v.hot_cap[t];
+  if (!cap) return NONE;
+  const HotSlot* tab = v.hot + v.hot_off[t];
+  uint64_t s = hot_slot(key, cap), dist = 0;
+  for (uint64_t step = 0; step < cap; ++step) {
+    if (tab[s].key == key) return uint32_t(s);
+    if (tab[s].key == EDGE_EMPTY) return NONE;
+    if (rh) {
+      const uint64_t h = hot_slot(tab[s].key, cap);
+      if ((s >= h ? s - h : s + cap - h) < dist) return NONE;
+    }
+    s = s + 1 == cap ? 0 : s + 1;
+    ++dist;
+  }
+  return NONE;
+}
+bool is_wild(const std::vector<std::string>& ws) {
+  for (auto& w : ws)
+    if (w == "+" || w == "#") return true;
+  return false;
+}
+
+// Every table invariant of a (patched) index against the filter set it holds.
+int verify(const emqx_gm_index* idx, const std::set<std::string>& cur, const char* what) {
+  const IndexView& v = idx->view;
+  int bad = 0;
+  auto fail = [&](const std::string& m) {
+    if (bad++ < 5) std::fprintf(stderr, "patch verify (%s): %s\n", what, m.c_str());
+  };
+  if (idx->info.n_filters != cur.size()) fail("n_filters");
+  uint32_t f = 0;
+  for (const std::string& flt : cur) {
+    const std::string got(reinterpret_cast<const char*>(idx->fbytes.data() + idx->foff[f]),
+                          idx->foff[f + 1] - idx->foff[f]);
+    if (got != flt) fail("filter bytes of id " + std::to_string(f));
+    const auto ws = split_words(flt);
+    const bool wild = is_wild(ws);
+    // the level trie (slow path, literal lookups)
+    uint32_t node = 0;
+    for (size_t i = 0; i < ws.size(); ++i) {
+      const uint32_t wid = v_dict_find(v, ws[i]);
+      const uint32_t ch = wid == NONE ? NONE : v_edge_get(v, uint32_t(i), node, wid);
+      if (ch == NONE) {
+        fail("v1 path of " + flt);
+        node = NONE;
+        break;
+      }
+      if (i + 1 == ws.size() && ws[i] == "#") {
+        if (v.nodes[node].hash_filter != f || v.nodes[ch & REF_MASK].end_filter != f) fail("v1 '#' of " + flt);
+        node = NONE;
+        break;
+      }
+      node = ch & REF_MASK;
+    }
+    if (node != NONE && v.nodes[node].end_filter != f) fail("v1 end of " + flt);
+    // the hot path (walk kernels)
+    uint32_t kind = 0, slot = 0;  // 0 root, 1 slot, 2 inline
+    int table = 0;
+    for (size_t i = 0; i < ws.size(); ++i) {
+      const HotSlot* P = kind ? &v.hot[v.hot_off[table] + slot] : nullptr;
+      const uint32_t hf = kind == 1 ? P->hf : kind == 2 ? P->p_hf : 0u;
+      const uint32_t sig = kind == 0 ? v.root_sig : kind == 1 ? P->sig : P->p_sig;
+      if (i + 1 == ws.size() && ws[i] == "#") {
+        const uint32_t id = kind == 0 ? v.root_hash : (hf & ID_MASK);
+        if (id != f) fail("hot '#' of " + flt);
+        kind = 9;
+        break;
+      }
+      const uint32_t wid = v_dict_find(v, ws[i]);
+      const bool plus = ws[i] == "+";
+      const bool pflag = kind == 0 ? (v.root_flags & HOT_PLUS) != 0 : (hf & HOT_PLUS) != 0;
+      if (plus && !pflag) fail("HOT_PLUS on the parent in " + flt);
+      if (plus && plus_inline(uint32_t(i), kind == 1)) {
+        kind = 2;
+        continue;
+      }
+      if (!plus && !(sig & sig_bit(wid))) fail("sig bit in " + flt);
+      const uint32_t hid = kind == 0 ? 0u : kind == 1 ? slot : (slot | HOT_INLINE);
+      const int t = hot_table(uint32_t(i + 1));
+      const uint64_t key = hot_key(hid, wid, uint32_t(i));
+      if (!plus && v.efilt_mask[t]) {
+        const uint32_t fh = edge_filter_hash(key), fb = edge_filter_bits(fh);
+        if ((v.efilt[v.efilt_off[t] + edge_filter_word(fh, v.efilt_mask[t])] & fb) != fb) fail("efilt in " + flt);
+      }
+      const uint32_t s = v_hot_lookup(v, t, key, false);
+      if (s == NONE) {
+        fail("hot slot of " + flt);
+        kind = 9;
+        break;
+      }
+      if (((v.rh_mask >> t) & 1u) && v_hot_lookup(v, t, key, true) != s) fail("Robin Hood exit loses " + flt);
+      kind = 1;
+      slot = s;
+      table = t;
+    }
+    if (kind == 1 || kind == 2) {
+      const HotSlot& H = v.hot[v.hot_off[table] + slot];
+      const uint32_t e = kind == 1 ? H.end_filter : H.p_end;
+      if (e != (f | (wild ? END_WILD : 0u))) fail("hot end of " + flt);
+    }
+    ++f;
+  }
+  // REF_X: an edge / '+' reference carries its child's has-exact flag
+  for (int d = 0; d < EDGE_DEPTHS; ++d)
+    for (uint64_t s = 0; s <= v.etab_mask[d]; ++s) {
+      const EdgeSlot& e = v.edges[v.etab_off[d] + s];
+      if (e.key == EDGE_EMPTY) continue;
+      const bool x = (v.nodes[e.child & REF_MASK].flags & NF_HAS_EXACT) != 0;
+      if (((e.child & REF_X) != 0) != x) fail("edge REF_X");
+    }
+  for (uint32_t i = 0; i < v.n_nodes; ++i) {
+    const Node& n = v.nodes[i];
+    if (n.plus_child != NONE && ((n.plus_child & REF_X) != 0) != ((v.nodes[n.plus_child & REF_MASK].flags & NF_HAS_EXACT) != 0))
+      fail("plus REF_X");
+    for (uint32_t x : {n.end_filter, n.hash_filter})
+      if (x != NONE && x >= cur.size()) fail("stale node filter id");
+  }
+  // no filter id outside the set (deleted ones cleared, the rest renumbered)
+  for (int t = 0; t < HOT_TABLES; ++t)
+    for (uint64_t s = 0; s < v.hot_cap[t]; ++s) {
+      const HotSlot& h = v.hot[v.hot_off[t] + s];
+      if (h.key == EDGE_EMPTY) continue;
+      for (uint32_t x : {h.end_filter, h.p_end})
+        if (x != NONE && (x & ID_MASK) >= cur.size()) fail("stale hot end id");
+      for (uint32_t x : {h.hf, h.p_hf})
+        if ((x & ID_MASK) != HF_NONE && (x & ID_MASK) >= cur.size()) fail("stale hot hf id");
+    }
+  return bad;
+}
+
+std::string rand_filter(std::mt19937_64& rng, int max_depth) {
+  static const char* W[] = {"a", "b", "c", "", "$x", "long-word-over-8-bytes", "w1", "w22", "+"};
+  const int n = 1 + int(rng() % max_depth);
+  std::string f;
+  for (int i = 0; i < n; ++i) f += (i ? "/" : "") + std::string(W[rng() % 9]);
+  if (rng() % 3 == 0) f += "/#";
+  if (rng() % 40 == 0) f = "#";
+  return f;
+}
+
+emqx_gm_index* host_build(const std::set<std::string>& fs) {
+  std::vector<uint8_t> b;
+  std::vector<uint64_t> o{0};
+  for (auto& f : fs) {
+    b.insert(b.end(), f.begin(), f.end());
+    o.push_back(b.size());
+  }
+  b.resize(b.size() + 64, 0);
+  emqx_gm_index* idx = nullptr;
+  if (gm::build_index(nullptr, b.data(), o.data(), fs.size(), nullptr, nullptr, nullptr, &idx)) return nullptr;
+  return idx;
+}
+
+emqx_gm_index* host_update(emqx_gm_index* prev, const std::vector<std::pair<std::string, bool>>& ops) {
+  std::vector<uint8_t> b, k;
+  std::vector<uint64_t> o{0};
+  for (auto& op : ops) {
+    b.insert(b.end(), op.first.begin(), op.first.end());
+    o.push_back(b.size());
+    k.push_back(op.second ? 1 : 0);
+  }
+  b.resize(b.size() + 64, 0);
+  k.push_back(0);
+  emqx_gm_index* out = nullptr;
+  if (gm::update_index(nullptr, prev, b.data(), o.data(), k.data(), ops.size(), &out)) return nullptr;
+  return out;
+}
+
+int patch_sequences() {
+  int bad = 0;
+  std::mt19937_64 rng(7);
+  for (int run = 0; run < 3; ++run) {
+    std::set<std::string> cur;
+    const int depth = run == 2 ? 22 : 6;  // run 2: the shared last tables
+    for (int i = 0; i < 400; ++i) cur.insert(rand_filter(rng, depth));
+    emqx_gm_index* idx = host_build(cur);
+    if (!idx) return 1;
+    bad += verify(idx, cur, "build");
+    for (int round = 0; round < 40; ++round) {
+      std::vector<std::pair<std::string, bool>> ops;
+      const int n = round % 13 == 12 ? 3000 : 1 + int(rng() % 80);  // now and then past the headroom
+      for (int i = 0; i < n; ++i) {
+        if (!cur.empty() && rng() % 5 < 2) {
+          auto it = cur.begin();
+          std::advance(it, rng() % cur.size());
+          const std::string f = *it;
+          const bool ins = rng() % 4 == 0;  // mostly deletes
+          ops.emplace_back(f, ins);
+          if (!ins) cur.erase(f);
+        } else {
+          const std::string f = rand_filter(rng, depth);
+          const bool ins = rng() % 5 != 0;  // some deletes of absent filters
+          ops.emplace_back(f, ins);
+          if (ins) cur.insert(f);
+          else cur.erase(f);
+        }
+      }
+      emqx_gm_index* nx = host_update(idx, ops);
+      if (!nx) {
+        std::fprintf(stderr, "host update failed (run %d round %d)\n", run, round);
+        return bad + 1;
+      }
+      if (nx != idx) gm::free_index(idx);  // host-only: the old view shares the moved mirror
+      else nx->refs.fetch_sub(1);
+      idx = nx;
+      bad += verify(idx, cur, "update");
+    }
+    gm::free_index(idx);
+  }
+  return bad;
+}
+}  // namespace
 
 int main() {
   std::mt19937_64 rng(42);
@@ -113,6 +367,7 @@ int main() {
     delete ov.ov;
     ov.ov = nullptr;
   }
+  bad += patch_sequences();
   std::printf(bad ? "ASAN_HOST_CHECK_FAILED %d\n" : "ASAN_HOST_CHECK_OK\n", bad);
   return bad ? 1 : 0;
 }
