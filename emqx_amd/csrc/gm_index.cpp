@@ -430,8 +430,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
                 (unsigned long long)hot_n[t], (unsigned long long)hot_cap[t], hot_cap[t] * 32.0 / 1e6);
   }
   // ---- 3c. exact-edge filters (gm_common.h), for tables whose parents have
-  // on average >= 4 exact children and whose filter fits 4 MB (gm_common.h's
-  // "16-32 bits per key" is now 4-8, see below)
+  // on average >= 4 exact children and whose filter fits 4 MB
   std::vector<uint64_t> ex_edges(HOT_TABLES, 0), ex_parents(HOT_TABLES, 0);
   for (uint64_t i = 1; i < NN; ++i) {
     const HNode& h = nodes[i];
