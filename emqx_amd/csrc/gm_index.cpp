@@ -323,11 +323,12 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (uint64_t i = 1; i < NN; ++i)
     if (nodes[i].kind != 2 && !inl[i]) hot_n[hot_table(nodes[i].depth)]++;
   uint64_t hot_off[HOT_TABLES], hot_cap[HOT_TABLES], hot_total = 0;
-  uint64_t hot_load_pct = 30;  // load factor (%); GM_HOT_LOAD_PCT: A/B knob (10..90)
+  uint64_t hot_load_pct = 25;  // load factor (%); GM_HOT_LOAD_PCT: A/B knob (10..90)
   if (const char* e = getenv("GM_HOT_LOAD_PCT")) hot_load_pct = std::min<uint64_t>(90, std::max<uint64_t>(10, strtoull(e, nullptr, 10)));
   for (int t = 0; t < HOT_TABLES; ++t) {
-    // load <= 0.30 (A/B at C2, fused kernel: 0.40 / 0.35 / 0.30 / 0.25 -> 10.34 / 10.13 / 10.03 /
-    // 9.97 ms; round 1 (split walk): 0.55 -> 0.40 cut k_walk by 3 %);
+    // load <= 0.25: shorter probe chains beat a smaller footprint (C2, fused
+    // kernel, 4-8 bit/key edge filter: load 0.40 / 0.35 / 0.30 / 0.25 / 0.20 /
+    // 0.15 / 0.10 -> 9.73 / 9.51 / 9.39 / 9.20 / 9.22 / 9.24 / 9.35 ms);
     // at least 8 slots so the probe loop always finds an empty one
     uint64_t pct = hot_load_pct;
     if (const char* e = getenv("GM_HOT_LOAD_PCT_UPPER"))  // A/B knob: load of the depth 1-2 tables
