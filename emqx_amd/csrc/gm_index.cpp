@@ -431,7 +431,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
                 (unsigned long long)hot_n[t], (unsigned long long)hot_cap[t], hot_cap[t] * 32.0 / 1e6);
   }
   // ---- 3c. exact-edge filters (gm_common.h), for tables whose parents have
-  // on average >= 4 exact children and whose filter fits 4 MB
+  // on average >= 4 exact children and whose filter fits the L2 budget
   std::vector<uint64_t> ex_edges(HOT_TABLES, 0), ex_parents(HOT_TABLES, 0);
   for (uint64_t i = 1; i < NN; ++i) {
     const HNode& h = nodes[i];
@@ -451,7 +451,11 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     uint64_t div = 8;  // GM_EFILT_DIV: A/B knob (words = keys / div)
     if (const char* e = getenv("GM_EFILT_DIV")) div = std::min<uint64_t>(64, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
     const uint64_t words = std::max<uint64_t>(32, next_pow2(ex_edges[t] / div + 1));
-    if (words * 4 > (4ull << 20)) continue;
+    // an L2 budget (a filter that does not stay in L2 costs more than it saves:
+    // C3's 4 MB one took its kernel from 14.1 to 14.9 ms); GM_EFILT_MAX_KB: A/B knob
+    uint64_t max_kb = 1024;
+    if (const char* e = getenv("GM_EFILT_MAX_KB")) max_kb = strtoull(e, nullptr, 10);
+    if (words * 4 > max_kb * 1024) continue;
     efilt_off[t] = efilt_total;
     efilt_mask[t] = uint32_t(words - 1);
     efilt_total += words;
