@@ -349,13 +349,15 @@ def main():
     # the cpu_baseline leg (oracle): timed on all host cores at N=1, and, outside the
     # timed region, the last step's CSR checked against it on a strided sample
     want_cpu = rank == 0 and world == 1 and not a.no_cpu
-    want_parity = rank == 0 and not a.no_parity and n_filters <= 2_000_000
+    want_parity = rank == 0 and not a.no_parity
     if want_cpu or want_parity:
         threads = a.cpu_threads or len(os.sched_getaffinity(0))
         r = oracle_router(fpack)
         if want_parity:
+            # C3's 10M-filter oracle runs ~0.5 M topics/s on the box's quota: a 200k-topic sample
             out["parity_sample"] = parity_sample(ctx, r, last, codes, sorted_unique(*fpack), a.seed,
-                                                 rank * n_topics, n_topics, threads)
+                                                 rank * n_topics, n_topics, threads,
+                                                 width=50_000 if n_filters <= 2_000_000 else 10_000)
         if want_cpu:
             out["cpu_baseline"] = cpu_baseline(r, codes, a.seed, a.cpu_seconds, threads)
             out["vs_cpu"] = value / out["cpu_baseline"]["value"]
