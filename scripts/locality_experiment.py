@@ -68,8 +68,43 @@ def run(name, b, o):
                       "probes_per_topic": st["probes"] / N}), flush=True)
 
 
+def first_word_key():
+    """The first word's bytes (up to 8, zero padded) of every topic, as a u64."""
+    key = np.zeros(N, np.uint64)
+    live = np.ones(N, bool)
+    for j in range(8):
+        b = np.where(lens > j, hb[np.minimum(starts + j, tbytes)], 0)
+        live &= b != ord("/")
+        key |= np.where(live, b, 0).astype(np.uint64) << np.uint64(8 * j)
+    return key
+
+
+def xcd_order(buckets, nb=8, blk=256):
+    """Workgroup i (XCD i % 8 under round-robin dispatch) takes 256 topics of bucket i % 8."""
+    lists = [list(np.nonzero(buckets == x)[0]) for x in range(nb)]
+    pos = [0] * nb
+    out = []
+    while len(out) < N:
+        for x in range(nb):
+            src = x
+            if pos[src] >= len(lists[src]):  # bucket drained: any other
+                cands = [y for y in range(nb) if pos[y] < len(lists[y])]
+                if not cands:
+                    break
+                src = cands[0]
+            out.extend(lists[src][pos[src]:pos[src] + blk])
+            pos[src] += blk
+    return np.array(out[:N], np.int64)
+
+
 run("generator", hb, ho)
-for k in (2, 4, 8, 16):
+fw = first_word_key()
+bk = ((fw * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(61)).astype(np.int64)
+b, o = reorder(xcd_order(bk))
+run("xcd_routed_first_word", b, o)
+b, o = reorder(np.argsort(fw, kind="stable"))
+run("grouped_first_word", b, o)
+for k in (8, 16):
     perm = np.argsort(key_bytes(min(k, 8)), kind="stable") if k <= 8 else None
     if k == 16:
         k1, k2 = key_bytes(8), None
