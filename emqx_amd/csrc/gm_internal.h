@@ -122,6 +122,7 @@ struct emqx_gm_index {
   std::vector<uint64_t> soff;   // subscriber CSR offsets per filter id (host copy; empty without subscribers)
   gm::OverlayState* ov = nullptr;  // overlay snapshot (emqx_gm_index_update); tables above unused then
   gm::Mirror* mirror = nullptr;    // host copy of the blob (updatable plain index), see gm::Mirror
+  std::mutex mirror_mu;            // an in-place update holds it while it patches and hands the mirror on
   emqx_gm_index_info_t info{};
 };
 

@@ -647,6 +647,7 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
   // (a filter with '#' before its last word takes the overlay; no room left in
   // the snapshot's tables: a rebuild, which restores the headroom)
   bool no_room = false;
+  std::unique_lock<std::mutex> mirror_lock(prev->mirror_mu);  // updates of one snapshot from several contexts
   if (!prev->ov && prev->mirror && !getenv("GM_UPDATE_OVERLAY") &&
       tomb.size() + dset.size() <= std::max<uint64_t>(4096, nb / 8)) {
     bool wf = true;
@@ -657,6 +658,7 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
       no_room = true;
     }
   }
+  mirror_lock.unlock();
   if (no_room || tomb.size() + dset.size() > std::max<uint64_t>(4096, nb / 8) || !base->dev_base) {
     // compaction: a flat snapshot of the updated set
     std::vector<uint8_t> bytes;
