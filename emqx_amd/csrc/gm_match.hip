@@ -2257,8 +2257,15 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
                         probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ctx->ev[2]);
   GM_HIP(ctx, hipGetLastError());
 
+  // count -> scan, then ONE host round trip reads the pass counters and the
+  // match total together (the slow path below is rare; it re-scans)
+  // (tsum: per-tile match counts, written by the main pass and topped up by the listed and slow passes)
+  int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff.as<uint64_t>());
+  if (rc) return rc;
   uint64_t h_ctr[4] = {0, 0, 0, 0};
+  uint64_t nnz = 0;
   GM_HIP(ctx, hipMemcpyAsync(h_ctr, ctrs.p, 32, hipMemcpyDeviceToHost, st));
+  GM_HIP(ctx, hipMemcpyAsync(&nnz, toff.as<uint64_t>() + n_tiles, 8, hipMemcpyDeviceToHost, st));
   GM_HIP(ctx, hipStreamSynchronize(st));
   const uint64_t n_listed = uint32_t(h_ctr[0]);
   const uint64_t n_ovf = uint32_t(h_ctr[0] >> 32);
@@ -2313,15 +2320,14 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
                          slow_off.as<uint64_t>(), slow_ids.as<uint32_t>());
       GM_HIP(ctx, hipGetLastError());
     }
+    // the slow path added its rows' counts to tsum: scan again
+    rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff.as<uint64_t>());
+    if (rc) return rc;
+    GM_HIP(ctx, hipMemcpyAsync(&nnz, toff.as<uint64_t>() + n_tiles, 8, hipMemcpyDeviceToHost, st));
+    GM_HIP(ctx, hipStreamSynchronize(st));
   }
 
-  // ---- count -> scan -> write
-  // (tsum: per-tile match counts, written by k_walk and topped up by the listed and slow passes)
-  int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff.as<uint64_t>());
-  if (rc) return rc;
-  uint64_t nnz = 0;
-  GM_HIP(ctx, hipMemcpyAsync(&nnz, toff.as<uint64_t>() + n_tiles, 8, hipMemcpyDeviceToHost, st));
-  GM_HIP(ctx, hipStreamSynchronize(st));
+  // ---- write the rows
   PoolBuf ids(ctx->pool, nnz * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
   hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt.as<uint32_t>(), n, toff.as<uint64_t>(),

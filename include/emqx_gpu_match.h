@@ -138,12 +138,18 @@ int emqx_gm_index_build(emqx_gm_ctx *ctx, const uint8_t *filter_bytes, const uin
  * 164-172, emqx_trie.erl:107-136).  Applies n_ops filter inserts (ops[i] = 1,
  * idempotent) and deletes (ops[i] = 0, only if present), in order, to `prev`
  * and returns a NEW snapshot; `prev` is unchanged (readers holding it keep
- * it: RCU).  Small deltas share prev's device tables (tombstones + a delta
- * index); past 1/8 of the base the set is rebuilt flat.  Ids in rows of the
- * new snapshot are ranks in the updated set, as a full rebuild would give.
- * Not available for shard indexes or indexes with subscriber lists
- * (EMQX_GM_EUNSUPPORTED: rebuild those), and emqx_gm_fanout needs a flat
- * snapshot. */
+ * it: RCU).  The newest snapshot of a line is patched in place on a device
+ * copy of its tables: the result is a flat snapshot, a match on it costs what
+ * a match on a rebuilt index costs, and the update costs O(delta) host work +
+ * one device copy of the index.  A plain index keeps a host copy of its device
+ * tables for this (host RAM ~ emqx_gm_index_info().device_bytes), handed on
+ * to each newer snapshot.  Otherwise -- a filter with '#' before its last
+ * word, or an update of a snapshot that is no longer the newest -- the new
+ * snapshot shares prev's tables (tombstones + a delta index; emqx_gm_fanout
+ * refuses it).  Past 1/8 of the set, or when the tables run out of headroom,
+ * the set is rebuilt.  Ids in rows of the new snapshot are ranks in the
+ * updated set, as a full rebuild would give.  Not available for shard indexes
+ * or indexes with subscriber lists (EMQX_GM_EUNSUPPORTED: rebuild those). */
 int emqx_gm_index_update(emqx_gm_ctx *ctx, emqx_gm_index *prev, const uint8_t *filter_bytes,
                          const uint64_t *filter_off, const uint8_t *ops, uint64_t n_ops, emqx_gm_index **out);
 int emqx_gm_index_retain(emqx_gm_index *idx);
