@@ -11,6 +11,7 @@
 // Layout (gm_common.h): nodes are numbered breadth-first so the hot upper
 // levels of the trie are contiguous in HBM and stay resident in L2/MALL.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -92,35 +93,52 @@ bool less_bytes(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
   return la < lb;
 }
 
-// Parallel sort of filter indices by bytes (chunked std::sort + pairwise merges).
+// Parallel sort of filter indices by bytes: (big-endian first 8 bytes, index)
+// pairs, so most comparisons are one integer compare on contiguous memory and
+// only equal prefixes compare the filters' bytes; chunked std::sort + pairwise
+// merges.
 void sort_filters_impl(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t* fo) {
-  auto cmp = [&](uint32_t x, uint32_t y) {
-    return less_bytes(fb + fo[x], fo[x + 1] - fo[x], fb + fo[y], fo[y + 1] - fo[y]);
+  const size_t n = ord.size();
+  struct K {
+    uint64_t key;
+    uint32_t i;
   };
-  size_t n = ord.size();
+  std::vector<K> ks(n);
+  for (size_t k = 0; k < n; ++k) {
+    const uint32_t x = ord[k];
+    const uint64_t len = fo[x + 1] - fo[x];
+    uint64_t key = 0;
+    for (uint64_t b = 0; b < 8; ++b) key = (key << 8) | (b < len ? fb[fo[x] + b] : 0u);
+    ks[k] = K{key, x};
+  }
+  auto cmp = [&](const K& a, const K& b) {
+    if (a.key != b.key) return a.key < b.key;
+    return less_bytes(fb + fo[a.i], fo[a.i + 1] - fo[a.i], fb + fo[b.i], fo[b.i + 1] - fo[b.i]);
+  };
   unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   if (n < 200000 || T == 1) {
-    std::sort(ord.begin(), ord.end(), cmp);
-    return;
-  }
-  std::vector<size_t> b(T + 1);
-  for (unsigned k = 0; k <= T; ++k) b[k] = n * k / T;
-  {
-    std::vector<std::thread> th;
-    for (unsigned k = 0; k < T; ++k)
-      th.emplace_back([&, k] { std::sort(ord.begin() + b[k], ord.begin() + b[k + 1], cmp); });
-    for (auto& t : th) t.join();
-  }
-  for (size_t width = 1; width < T; width *= 2) {
-    std::vector<std::thread> th;
-    for (size_t k = 0; k + width < T; k += 2 * width) {
-      size_t lo = b[k], mid = b[k + width], hi = b[std::min<size_t>(k + 2 * width, T)];
-      th.emplace_back([&, lo, mid, hi] {
-        std::inplace_merge(ord.begin() + lo, ord.begin() + mid, ord.begin() + hi, cmp);
-      });
+    std::sort(ks.begin(), ks.end(), cmp);
+  } else {
+    std::vector<size_t> b(T + 1);
+    for (unsigned k = 0; k <= T; ++k) b[k] = n * k / T;
+    {
+      std::vector<std::thread> th;
+      for (unsigned k = 0; k < T; ++k)
+        th.emplace_back([&, k] { std::sort(ks.begin() + b[k], ks.begin() + b[k + 1], cmp); });
+      for (auto& t : th) t.join();
     }
-    for (auto& t : th) t.join();
+    for (size_t width = 1; width < T; width *= 2) {
+      std::vector<std::thread> th;
+      for (size_t k = 0; k + width < T; k += 2 * width) {
+        size_t lo = b[k], mid = b[k + width], hi = b[std::min<size_t>(k + 2 * width, T)];
+        th.emplace_back([&, lo, mid, hi] {
+          std::inplace_merge(ks.begin() + lo, ks.begin() + mid, ks.begin() + hi, cmp);
+        });
+      }
+      for (auto& t : th) t.join();
+    }
   }
+  for (size_t k = 0; k < n; ++k) ord[k] = ks[k].i;
 }
 
 }  // namespace
@@ -140,6 +158,15 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
 
   auto* idx = new emqx_gm_index;
   idx->device = ctx ? ctx->device : -1;
+  // GM_INDEX_STATS: phase times on stderr (diagnostics)
+  const bool stats = getenv("GM_INDEX_STATS") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char* what) {
+    if (!stats) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "[gm_index] %-12s %9.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
 
   // ---- 1. ids = lexicographic rank of unique filters
   std::vector<uint32_t> ord(n);
@@ -184,6 +211,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       }
   }
 
+  phase("sort+ids");
   // ---- 2. intern words, build the level trie
   std::unordered_map<std::string_view, uint32_t, ViewHash> wid;  // word -> arena offset
   std::vector<uint8_t> arena;
@@ -220,13 +248,41 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     return off;
   };
 
+  // Filters are in byte order, so a filter usually shares its leading words
+  // with the previous one: those words' nodes are taken from the previous
+  // filter's path (no interning, no edge lookup).  Word j of the previous
+  // filter (ending at byte e) is shared when the two agree on every byte up
+  // to e and the word ends at e in both.
+  std::vector<uint32_t> pnode;  // node after word j of the previous filter
+  std::vector<uint64_t> pend;   // end byte of word j
+  std::vector<uint8_t> pwild;   // a wildcard word among words 0..j
+  const uint8_t* ps = nullptr;
+  uint64_t plen = 0;
   for (uint32_t f = 0; f < nf; ++f) {
     const uint8_t* s = FB + idx->foff[f];
     uint64_t len = idx->foff[f + 1] - idx->foff[f];
-    uint32_t node = 0, depth = 0;
-    bool wild = false;
-    uint64_t ws = 0;
-    for (uint64_t i = 0; i <= len; ++i) {
+    uint64_t cp = 0;
+    if (ps) {
+      const uint64_t m = std::min(len, plen);
+      while (cp < m && s[cp] == ps[cp]) ++cp;
+    }
+    size_t j = 0;
+    while (j < pend.size()) {
+      const uint64_t e = pend[j];
+      const bool shared = e < cp || (e == cp && (cp == len || (cp == plen && cp < len && s[cp] == '/')));
+      if (!shared) break;
+      ++j;
+    }
+    pnode.resize(j);
+    pend.resize(j);
+    pwild.resize(j);
+    uint32_t node = j ? pnode[j - 1] : 0, depth = uint32_t(j);
+    bool wild = j ? pwild[j - 1] != 0 : false;
+    const uint64_t ws0 = j ? pend[j - 1] + 1 : 0;
+    uint64_t ws = ws0;
+    ps = s;
+    plen = len;
+    for (uint64_t i = ws0; i <= len; ++i) {
       if (i < len && s[i] != '/') continue;
       const uint8_t* w = s + ws;
       uint64_t wl = i - ws;
@@ -251,12 +307,16 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       node = child;
       ++depth;
       ws = i + 1;
+      pnode.push_back(node);
+      pend.push_back(i);
+      pwild.push_back(wild);
     }
     nodes[node].end_filter = f;
     if (wild) { nodes[node].flags |= NF_END_WILD; ++n_wild; }
     max_depth = std::max(max_depth, depth);
   }
 
+  phase("trie");
   // ---- 3. breadth-first renumbering (stable by creation order within a level)
   uint64_t NN = nodes.size();
   std::vector<uint64_t> per_depth(max_depth + 2, 0);
@@ -279,17 +339,33 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     d.flags = h.flags;
   }
   // edge tables partitioned by the parent's depth
-  std::vector<uint64_t> per_tab(EDGE_DEPTHS, 0);
-  for (auto& s : edges.slots)
-    if (s.key != EDGE_EMPTY) per_tab[edge_depth(nodes[uint32_t(s.key >> 32)].depth)]++;
+  // (each depth's table built on its own thread from its bucket of edges)
+  std::vector<std::vector<std::pair<uint64_t, uint32_t>>> by_tab(EDGE_DEPTHS);
+  {
+    std::vector<uint64_t> per_tab(EDGE_DEPTHS, 0);
+    for (auto& s : edges.slots)
+      if (s.key != EDGE_EMPTY) per_tab[edge_depth(nodes[uint32_t(s.key >> 32)].depth)]++;
+    for (int d = 0; d < EDGE_DEPTHS; ++d) by_tab[d].reserve(per_tab[d]);
+    for (auto& s : edges.slots)
+      if (s.key != EDGE_EMPTY) {
+        const uint32_t par = uint32_t(s.key >> 32);
+        by_tab[edge_depth(nodes[par].depth)].emplace_back(edge_key(newid[par], uint32_t(s.key)), ref(s.child));
+      }
+    std::vector<EdgeSlot>().swap(edges.slots);  // the build-time map is done
+  }
   std::vector<EdgeMap> tabs;
   tabs.reserve(EDGE_DEPTHS);
-  for (int d = 0; d < EDGE_DEPTHS; ++d) tabs.emplace_back(per_tab[d] + 1);
-  for (auto& s : edges.slots)
-    if (s.key != EDGE_EMPTY) {
-      const uint32_t par = uint32_t(s.key >> 32);
-      tabs[edge_depth(nodes[par].depth)].put(edge_key(newid[par], uint32_t(s.key)), ref(s.child));
-    }
+  for (int d = 0; d < EDGE_DEPTHS; ++d) tabs.emplace_back(by_tab[d].size() + 1);
+  {
+    std::vector<std::thread> th;
+    for (int d = 0; d < EDGE_DEPTHS; ++d)
+      if (!by_tab[d].empty())
+        th.emplace_back([&, d] {
+          for (const auto& kv : by_tab[d]) tabs[d].put(kv.first, kv.second);
+          std::vector<std::pair<uint64_t, uint32_t>>().swap(by_tab[d]);
+        });
+    for (auto& t : th) t.join();
+  }
   std::vector<EdgeSlot> dedges;
   uint64_t etab_off[EDGE_DEPTHS], etab_mask[EDGE_DEPTHS], n_edges = 0;
   for (int d = 0; d < EDGE_DEPTHS; ++d) {
@@ -300,6 +376,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     std::vector<EdgeSlot>().swap(tabs[d].slots);
   }
 
+  phase("v1 tables");
   // ---- 3b. hot tables: one 32-B slot per node reached through an exact edge
   // (or a '+' edge from the root or from an inline node), slot index = the
   // node's hot id; the '+' child of a slot-owning node is inline in its
@@ -430,6 +507,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
         fprintf(stderr, "[gm_index] hot table %d: %llu slots used of %llu (%.1f MB)\n", t,
                 (unsigned long long)hot_n[t], (unsigned long long)hot_cap[t], hot_cap[t] * 32.0 / 1e6);
   }
+  phase("hot tables");
   // ---- 3c. exact-edge filters (gm_common.h), for tables whose parents have
   // on average >= 4 exact children and whose filter fits the L2 budget
   std::vector<uint64_t> ex_edges(HOT_TABLES, 0), ex_parents(HOT_TABLES, 0);
@@ -470,6 +548,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     efilt[efilt_off[t] + edge_filter_word(fh, efilt_mask[t])] |= edge_filter_bits(fh);
   }
 
+  phase("edge filter");
   // ---- 4. word dictionary (open addressing by hash, verified by bytes)
   uint64_t nw = word_ids.size();
   uint64_t dcap = next_pow2(nw * 4 + 4);  // load <= 0.25: a second (dependent) slot read is rare
@@ -487,6 +566,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     if (it != wid.end()) hash_word = it->second;
   }
 
+  phase("dictionary");
   // ---- 5. subscriber CSR per unique filter id (duplicates concatenated)
   std::vector<uint64_t> soff(nf + 1, 0);
   std::vector<uint32_t> sids;
@@ -504,6 +584,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   std::vector<uint16_t> flen(nf);
   for (uint32_t f = 0; f < nf; ++f) flen[f] = uint16_t(std::min<uint64_t>(idx->foff[f + 1] - idx->foff[f], 65535));
 
+  phase("subscribers");
   // ---- 6. upload: one allocation, 256-B aligned sections.  A plain index (no
   // shard ids, no subscriber lists) keeps a host mirror of the blob for
   // in-place updates, with headroom for appended nodes, words and filters.
@@ -600,6 +681,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // the view's base: the device blob, or (host-only index) the mirror
   uint8_t* B = host_mirror ? idx->mirror->blob.data() : static_cast<uint8_t*>(idx->dev_base);
 
+  phase("upload");
   IndexView& v = idx->view;
   v.nodes = reinterpret_cast<const Node*>(B + o_nodes);
   v.dict = reinterpret_cast<const DictSlot*>(B + o_dict);
