@@ -321,6 +321,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   uint64_t NN = nodes.size();
   std::vector<uint64_t> per_depth(max_depth + 2, 0);
   for (auto& nd : nodes) per_depth[nd.depth + 1]++;
+  idx->level_nodes = *std::max_element(per_depth.begin(), per_depth.end());
   for (size_t d = 1; d < per_depth.size(); ++d) per_depth[d] += per_depth[d - 1];
   std::vector<uint32_t> newid(NN);
   for (uint64_t i = 0; i < NN; ++i) newid[i] = uint32_t(per_depth[nodes[i].depth]++);

@@ -121,6 +121,7 @@ struct emqx_gm_index {
   std::vector<uint32_t> gmap;   // shard index: global id of each local filter (ascending); empty otherwise
   std::vector<uint64_t> soff;   // subscriber CSR offsets per filter id (host copy; empty without subscribers)
   gm::OverlayState* ov = nullptr;  // overlay snapshot (emqx_gm_index_update); tables above unused then
+  uint64_t level_nodes = 0;        // an upper bound on the trie nodes of any one depth (the slow path's frontier); 0: unknown
   gm::Mirror* mirror = nullptr;    // host copy of the blob (updatable plain index), see gm::Mirror
   std::mutex mirror_mu;            // an in-place update holds it while it patches and hands the mirror on
   emqx_gm_index_info_t info{};

@@ -2277,10 +2277,13 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   PoolBuf slow_off, slow_ids;
   uint32_t* ovf_list = list2.as<uint32_t>();
   if (n_ovf) {
-    const uint64_t fr_cap = uint64_t(idx->view.n_nodes) + 1;
+    // a frontier holds the nodes of one depth: the widest depth bounds it
+    const uint64_t fr_cap = std::min<uint64_t>(uint64_t(idx->view.n_nodes),
+                                               idx->level_nodes ? idx->level_nodes : uint64_t(idx->view.n_nodes)) + 1;
     const uint64_t bm_words = (uint64_t(idx->view.n_filters) + 31) / 32 + 1;
     const uint64_t per_blk = (2 * fr_cap + bm_words) * 4;
-    uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(256, (2ull << 30) / per_blk));
+    // chunks sized by a 1 GiB workspace, up to 16,384 topics (a workgroup each) per launch
+    uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(16384, (1ull << 30) / per_blk));
     chunk = std::min(chunk, n_ovf);
     PoolBuf fr(ctx->pool, chunk * 2 * fr_cap * 4);
     PoolBuf bm(ctx->pool, chunk * bm_words * 4);

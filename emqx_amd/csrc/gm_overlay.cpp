@@ -601,6 +601,7 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
   in.n_edges = prev->info.n_edges + P.new_edges;
   in.n_words = M.dict_used;
   in.max_depth = std::max(prev->info.max_depth, P.max_depth);
+  idx->level_nodes = prev->level_nodes ? prev->level_nodes + (M.nodes_n - P.s_nodes_n) : 0;  // new nodes, any depth
   idx->mirror = prev->mirror;  // the mirror follows the newest snapshot
   prev->mirror = nullptr;
   *out = idx;

@@ -531,3 +531,29 @@ def test_host_path_rejects_bad_offsets_and_survives(ctx):
     ro, ids = ctx.match(idx, (tb, np.array([0, 3, 6, 7], np.uint64)), exact=True)
     assert ro.tolist() == [0, 1, 2, 3] and ids.tolist() == [0, 1, 1]  # a/x; b/y, b via b/#
     idx.release()
+
+
+@pytest.mark.timeout(300)
+def test_adversarial_plus_chains_all_rows(ctx, orc):
+    """Every word sequence of depth 1..8 over {w, +} (each also with '/#'),
+    plus '#': a topic 'w/.../w' matches hundreds of filters, so almost every
+    row overflows the main and listed passes into the device slow path
+    (frontier bounded by the widest trie level, chunks of up to 16,384
+    topics).  60k topics, every row against the oracle, in both modes."""
+    import itertools
+    fs = {b"#"}
+    for d in range(1, 9):
+        for ws in itertools.product([b"w", b"+"], repeat=d):
+            fs.add(b"/".join(ws))
+            fs.add(b"/".join(ws) + b"/#")
+    filters = sorted(fs)
+    rng = random.Random(31)
+    topics = [b"/".join(rng.choice([b"w", b"w", b"w", b"x", b"$x"]) for _ in range(rng.randint(1, 10)))
+              for _ in range(60_000)]
+    idx = ctx.build_index(filters)
+    for exact in (True, False):
+        ro, ids = ctx.match(idx, topics, exact=exact)
+        oro, oids = _oracle_rows(orc, filters, topics, 1 if exact else 0)
+        assert np.array_equal(ro, oro) and np.array_equal(ids, oids)
+        assert ctx.stats()["n_overflow"] > 10_000  # the slow path really ran
+    idx.release()
