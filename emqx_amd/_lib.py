@@ -61,6 +61,7 @@ SIGNATURES = {
     "emqx_gm_synchronize": (_i32, [_vp]),
     "emqx_gm_index_build": (_i32, [_vp, _vp, _vp, _u64, _vp, _vp, _vp, C.POINTER(_vp)]),
     "emqx_gm_index_update": (_i32, [_vp, _vp, _vp, _vp, _vp, _u64, C.POINTER(_vp)]),
+    "emqx_gm_index_update_subs": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u64, C.POINTER(_vp)]),
     "emqx_gm_index_retain": (_i32, [_vp]),
     "emqx_gm_index_release": (_i32, [_vp]),
     "emqx_gm_index_info": (_i32, [_vp, C.POINTER(IndexInfo)]),

@@ -202,6 +202,18 @@ int emqx_gm_index_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* f
   GM_GUARD_END(ctx)
 }
 
+int emqx_gm_index_update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo,
+                              const uint32_t* subs, const uint8_t* ops, uint64_t n_ops, emqx_gm_index** out) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (prev && prev->device != ctx->device)
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: index lives on another device");
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  return gm::update_subs(ctx, prev, fb, fo, subs, ops, n_ops, out);
+  GM_GUARD_END(ctx)
+}
+
 int emqx_gm_index_retain(emqx_gm_index* idx) {
   if (!idx) return EMQX_GM_EINVAL;
   idx->refs.fetch_add(1);

@@ -586,9 +586,11 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (uint32_t f = 0; f < nf; ++f) flen[f] = uint16_t(std::min<uint64_t>(idx->foff[f + 1] - idx->foff[f], 65535));
 
   phase("subscribers");
-  // ---- 6. upload: one allocation, 256-B aligned sections.  A plain index (no
-  // shard ids, no subscriber lists) keeps a host mirror of the blob for
-  // in-place updates, with headroom for appended nodes, words and filters.
+  // ---- 6. upload: one allocation, 256-B aligned sections, the subscriber
+  // CSR last.  An index without shard ids keeps a host mirror of the blob up
+  // to the subscriber CSR for in-place updates, with headroom for appended
+  // nodes, words and filters (an update of the subscriber lists writes a new
+  // CSR of its own, gm_subs.cpp).
   // (no context but an `out`: a host-only index whose view points into its
   // mirror -- the CPU test of the in-place update, tests/asan/)
   const bool host_mirror = !ctx && out && !host_only;
@@ -596,7 +598,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     delete idx;
     return set_err(ctx, EMQX_GM_EINVAL, "index_build: host-only index without subscribers or shard ids only");
   }
-  const bool keep_mirror = host_mirror || (ctx && !gids && !sub_off && !getenv("GM_NO_MIRROR"));
+  const bool keep_mirror = host_mirror || (ctx && !gids && !getenv("GM_NO_MIRROR"));
   const uint64_t nodes_cap = keep_mirror ? NN + NN / 4 + 1024 : NN;
   const uint64_t arena_cap = keep_mirror ? arena.size() + arena.size() / 4 + 65536 : arena.size();
   const uint64_t flen_cap = keep_mirror ? uint64_t(nf) + nf / 4 + 1024 : nf;
@@ -606,12 +608,13 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   size_t o_edges = o_dict + al(dcap * sizeof(DictSlot));
   size_t o_hot = o_edges + al(dedges.size() * sizeof(EdgeSlot));
   size_t o_arena = o_hot + al(hot.size() * sizeof(HotSlot));
-  size_t o_soff = o_arena + al(arena_cap + 64);
-  size_t o_sids = o_soff + al((keep_mirror ? flen_cap + 1 : soff.size()) * 8);  // zeros past nf (no subscribers)
-  size_t o_flen = o_sids + al(sids.size() * 4 + 4);
+  size_t o_flen = o_arena + al(arena_cap + 64);
   size_t o_gmap = o_flen + al(flen_cap * 2 + 2);
   size_t o_efilt = o_gmap + al(idx->gmap.size() * 4 + 4);
-  size_t total = o_efilt + al(efilt.size() * 4 + 4);
+  size_t o_soff = o_efilt + al(efilt.size() * 4 + 4);
+  // (a plain index's offsets stay zero past nf: appended filters have no subscribers)
+  size_t o_sids = o_soff + al((keep_mirror && !sub_off ? flen_cap + 1 : soff.size()) * 8);
+  size_t total = o_sids + al(sids.size() * 4 + 4);
 
   if (host_only) {  // compile-only self check (no device): report the table sizes
     emqx_gm_index_info_t& in = *host_only;
@@ -661,6 +664,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   }
   if (keep_mirror) {
     auto* m = new Mirror;
+    hb.resize(o_soff);  // the mirror stops at the subscriber CSR
+    hb.shrink_to_fit();
     m->blob = std::move(hb);
     m->o_nodes = o_nodes;
     m->o_dict = o_dict;
@@ -689,8 +694,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.edges = reinterpret_cast<const EdgeSlot*>(B + o_edges);
   v.hot = reinterpret_cast<const HotSlot*>(B + o_hot);
   v.arena = B + o_arena;
-  v.sub_off = reinterpret_cast<const uint64_t*>(B + o_soff);
-  v.sub_ids = reinterpret_cast<const uint32_t*>(B + o_sids);
+  v.sub_off = host_mirror ? nullptr : reinterpret_cast<const uint64_t*>(B + o_soff);
+  v.sub_ids = host_mirror ? nullptr : reinterpret_cast<const uint32_t*>(B + o_sids);
   v.gmap = idx->gmap.empty() ? nullptr : reinterpret_cast<const uint32_t*>(B + o_gmap);
   v.dict_mask = dcap - 1;
   for (int d = 0; d < EDGE_DEPTHS; ++d) {
@@ -738,9 +743,10 @@ void free_index(emqx_gm_index* idx) {
   if (!idx) return;
   if (idx->ov) free_overlay(idx);
   delete idx->mirror;
-  if (idx->dev_base) {
+  if (idx->dev_base || idx->dev_subs) {
     (void)hipSetDevice(idx->device);
-    (void)hipFree(idx->dev_base);
+    if (idx->dev_base) (void)hipFree(idx->dev_base);
+    if (idx->dev_subs) (void)hipFree(idx->dev_subs);
   }
   delete idx;
 }

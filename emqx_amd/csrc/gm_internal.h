@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -112,6 +113,7 @@ struct emqx_gm_index {
   std::atomic<int> refs{1};
   int device = 0;
   void* dev_base = nullptr;     // one allocation holding every table
+  void* dev_subs = nullptr;     // a subscriber CSR of its own (after emqx_gm_index_update_subs), or nullptr
   size_t dev_bytes = 0;
   gm::IndexView view{};
   uint16_t* dev_flen = nullptr; // filter lengths (stats only), inside dev_base
@@ -164,6 +166,27 @@ struct OverlayState {
 };
 int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo, const uint8_t* ops,
                  uint64_t n_ops, emqx_gm_index** out);
+// The in-place patch of update_index (prev must hold the mirror and a write
+// lock on it): deletes base ids `tomb`, inserts the filters `dset`.  Returns 1
+// when a table lacks room (nothing changed), <0 on error.  rmap_out (optional)
+// receives old id -> new id for prev's filters (NONE: deleted) followed by the
+// new ids of dset's filters in byte order.
+// trie_only: the new blob holds the tables up to the subscriber CSR only (the
+// caller gives the snapshot a CSR of its own).
+int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>& tomb,
+                 const std::set<std::string>& dset, emqx_gm_index** out, std::vector<uint32_t>* rmap_out = nullptr,
+                 bool trie_only = false);
+bool well_formed_filter(const uint8_t* p, uint64_t len);
+// rank of f among idx's filters; *found = exact hit
+uint64_t filter_rank(const emqx_gm_index* idx, const uint8_t* f, uint64_t len, bool* found);
+// gm_subs.cpp: emqx_gm_index_update_subs
+int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo, const uint32_t* subs,
+                const uint8_t* ops, uint64_t n_ops, emqx_gm_index** out);
+// gm_match.hip: the new subscriber CSR of update_subs (see there)
+int rebuild_subs_device(emqx_gm_ctx* ctx, const emqx_gm_index* prev, emqx_gm_index* idx,
+                        const std::vector<uint64_t>& new_soff, const std::vector<uint32_t>& inv,
+                        const std::vector<uint32_t>& aff_ids, const std::vector<uint64_t>& aff_off,
+                        const std::vector<uint32_t>& aff_buf);
 int overlay_filter(const emqx_gm_index* idx, uint32_t id, const uint8_t** bytes, uint64_t* len);
 void free_overlay(emqx_gm_index* idx);
 // gm_match.hip: the device side of an in-place update (patch_update): dst =

@@ -1985,6 +1985,90 @@ int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t byte
   return EMQX_GM_OK;
 }
 
+// ---- the new subscriber CSR of emqx_gm_index_update_subs (gm_subs.cpp) ----
+// Output element p of the new CSR belongs to filter f (the last segment whose
+// start <= p); its source is f's edited list from the host (f in aff_ids) or
+// element p - nsoff[f] of the previous list of f's old id inv[f].  Every
+// workgroup owns per_block consecutive outputs, as k_fanout_copy does.
+__device__ __forceinline__ uint64_t seg_of(const uint64_t* __restrict__ s, uint64_t a, uint64_t b, uint64_t p) {
+  // s[a] <= p < s[b]: the last segment of [a, b) starting at or before p
+  while (b - a > 1) {
+    const uint64_t m = (a + b) >> 1;
+    if (s[m] <= p) a = m;
+    else b = m;
+  }
+  return a;
+}
+__global__ __launch_bounds__(256) void k_subs_copy(const uint64_t* __restrict__ nsoff, uint64_t nf,
+                                                   const uint32_t* __restrict__ inv, const uint64_t* __restrict__ osoff,
+                                                   const uint32_t* __restrict__ oids, const uint32_t* __restrict__ aff_ids,
+                                                   uint64_t n_aff, const uint64_t* __restrict__ aff_off,
+                                                   const uint32_t* __restrict__ aff_buf, uint64_t total,
+                                                   uint64_t per_block, uint32_t* __restrict__ out) {
+  const uint64_t lo = uint64_t(blockIdx.x) * per_block;
+  if (lo >= total) return;
+  const uint64_t hi = min(total, lo + per_block);
+  __shared__ uint64_t s_seg[2];
+  if (threadIdx.x < 2) s_seg[threadIdx.x] = seg_of(nsoff, 0, nf, threadIdx.x == 0 ? lo : hi - 1);
+  __syncthreads();
+  const uint64_t s0 = s_seg[0], s1 = s_seg[1] + 1;
+  for (uint64_t p = lo + threadIdx.x; p < hi; p += 256) {
+    const uint64_t f = seg_of(nsoff, s0, s1, p);
+    const uint64_t q = p - nsoff[f];
+    uint64_t a = 0, b = n_aff;  // is f a touched filter?
+    while (a < b) {
+      const uint64_t m = (a + b) >> 1;
+      if (aff_ids[m] < f) a = m + 1;
+      else b = m;
+    }
+    out[p] = (a < n_aff && aff_ids[a] == f) ? aff_buf[aff_off[a] + q] : oids[osoff[inv[f]] + q];
+  }
+}
+
+int rebuild_subs_device(emqx_gm_ctx* ctx, const emqx_gm_index* prev, emqx_gm_index* idx,
+                        const std::vector<uint64_t>& new_soff, const std::vector<uint32_t>& inv,
+                        const std::vector<uint32_t>& aff_ids, const std::vector<uint64_t>& aff_off,
+                        const std::vector<uint32_t>& aff_buf) {
+  const uint64_t nf = new_soff.size() - 1, total = new_soff.back();
+  for (uint64_t f = 0; f < nf; ++f)  // host-side check of what the kernel will index
+    if (inv[f] == NONE && !std::binary_search(aff_ids.begin(), aff_ids.end(), uint32_t(f)) &&
+        new_soff[f + 1] != new_soff[f])
+      return set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: a new filter without its list");
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t o_ids = al((nf + 1) * 8);
+  GM_HIP(ctx, hipMalloc(&idx->dev_subs, o_ids + total * 4 + 16));
+  uint8_t* D = static_cast<uint8_t*>(idx->dev_subs);
+  hipStream_t st = ctx->stream;
+  GM_HIP(ctx, hipMemcpyAsync(D, new_soff.data(), (nf + 1) * 8, hipMemcpyHostToDevice, st));
+  // staging: inv | aff_ids | aff_off | aff_buf
+  const size_t o_aid = al(nf * 4 + 4), o_aoff = o_aid + al(aff_ids.size() * 4 + 4),
+               o_abuf = o_aoff + al(aff_off.size() * 8), n_st = o_abuf + aff_buf.size() * 4 + 4;
+  std::vector<uint8_t> h(n_st, 0);
+  std::memcpy(h.data(), inv.data(), nf * 4);
+  if (!aff_ids.empty()) std::memcpy(h.data() + o_aid, aff_ids.data(), aff_ids.size() * 4);
+  std::memcpy(h.data() + o_aoff, aff_off.data(), aff_off.size() * 8);
+  if (!aff_buf.empty()) std::memcpy(h.data() + o_abuf, aff_buf.data(), aff_buf.size() * 4);
+  PoolBuf sbuf(ctx->pool, n_st);
+  if (!sbuf.p) return set_err(ctx, EMQX_GM_ENOMEM, "index_update_subs: staging");
+  GM_HIP(ctx, hipMemcpyAsync(sbuf.p, h.data(), n_st, hipMemcpyHostToDevice, st));
+  if (total) {
+    const uint8_t* S = sbuf.as<uint8_t>();
+    const uint64_t per = fan_per_block(total);
+    hipLaunchKernelGGL(k_subs_copy, dim3((total + per - 1) / per), dim3(256), 0, st,
+                       reinterpret_cast<const uint64_t*>(D), nf, reinterpret_cast<const uint32_t*>(S),
+                       prev->view.sub_off, prev->view.sub_ids, reinterpret_cast<const uint32_t*>(S + o_aid),
+                       uint64_t(aff_ids.size()), reinterpret_cast<const uint64_t*>(S + o_aoff),
+                       reinterpret_cast<const uint32_t*>(S + o_abuf), total, per,
+                       reinterpret_cast<uint32_t*>(D + o_ids));
+    GM_HIP(ctx, hipGetLastError());
+  }
+  GM_HIP(ctx, hipStreamSynchronize(st));  // the staging goes back to the pool / the host
+  idx->view.sub_off = reinterpret_cast<const uint64_t*>(D);
+  idx->view.sub_ids = reinterpret_cast<const uint32_t*>(D + o_ids);
+  idx->info.device_bytes += o_ids + total * 4 + 16;
+  return EMQX_GM_OK;
+}
+
 // Sum of per-tile counters into one (one atomic per wave of a small grid).
 __global__ __launch_bounds__(256) void k_sum_tiles(const unsigned long long* __restrict__ a, uint64_t n,
                                                    unsigned long long* __restrict__ acc) {

@@ -450,9 +450,15 @@ void renumber_host(Mirror& M, const IndexView& v, const std::vector<uint32_t>& r
 
 }  // namespace
 
+bool well_formed_filter(const uint8_t* p, uint64_t len) { return well_formed(p, len); }
+uint64_t filter_rank(const emqx_gm_index* idx, const uint8_t* f, uint64_t len, bool* found) {
+  return base_rank(idx, f, len, found);
+}
+
 // Returns 1 (nothing changed) when the snapshot's tables lack room: the caller rebuilds.
-static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>& tomb,
-                        const std::set<std::string>& dset, emqx_gm_index** out) {
+int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>& tomb,
+                 const std::set<std::string>& dset, emqx_gm_index** out, std::vector<uint32_t>* rmap_out,
+                 bool trie_only) {
   Mirror& M = *prev->mirror;
   const uint64_t nb = prev->info.n_filters, K = dset.size();
   const uint64_t nf_new = nb - tomb.size() + K;
@@ -557,16 +563,17 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
   // ids), renumber every filter-id field; then the mirror the same way
   phase("flen");
   const bool host = prev->dev_base == nullptr;  // a host-only index (CPU test): the mirror is the index
+  const size_t blob_bytes = trie_only ? M.blob.size() : prev->dev_bytes;  // the mirror ends at the CSR
   if (!host) {
     hipError_t e = hipSetDevice(prev->device);
-    if (e == hipSuccess) e = hipMalloc(&idx->dev_base, prev->dev_bytes);
+    if (e == hipSuccess) e = hipMalloc(&idx->dev_base, blob_bytes);
     if (e != hipSuccess) {
       P.rollback();
       delete idx;
       return set_err(ctx, EMQX_GM_ENOMEM, std::string("index_update: hipMalloc: ") + hipGetErrorString(e));
     }
     phase("alloc");
-    const int rc = apply_patch_device(ctx, idx->dev_base, prev->dev_base, prev->dev_bytes, P.dirty, M.blob.data(), v,
+    const int rc = apply_patch_device(ctx, idx->dev_base, prev->dev_base, blob_bytes, P.dirty, M.blob.data(), v,
                                       M.o_hot, M.o_nodes, M.nodes_n, rmap);
     if (rc) {  // the mirror no longer matches any snapshot: later updates take the overlay path
       (void)hipFree(idx->dev_base);
@@ -577,20 +584,22 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
     }
     phase("device");
   }
-  idx->dev_bytes = prev->dev_bytes;
+  idx->dev_bytes = blob_bytes;
   renumber_host(M, v, rmap);
   phase("renumber");
   // the view's pointers follow the new blob (a host-only index keeps the mirror's)
   uint8_t* NB = host ? M.blob.data() : static_cast<uint8_t*>(idx->dev_base);
   const uint8_t* OB = host ? M.blob.data() : static_cast<const uint8_t*>(prev->dev_base);
-  auto rebase = [&](auto p) { return reinterpret_cast<decltype(p)>(NB + (reinterpret_cast<const uint8_t*>(p) - OB)); };
+  auto rebase = [&](auto p) {
+    return p ? reinterpret_cast<decltype(p)>(NB + (reinterpret_cast<const uint8_t*>(p) - OB)) : p;
+  };
   v.nodes = rebase(v.nodes);
   v.dict = rebase(v.dict);
   v.edges = rebase(v.edges);
   v.hot = rebase(v.hot);
   v.arena = rebase(v.arena);
-  v.sub_off = rebase(v.sub_off);
-  v.sub_ids = rebase(v.sub_ids);
+  v.sub_off = trie_only ? nullptr : rebase(v.sub_off);  // trie_only: set by the caller
+  v.sub_ids = trie_only ? nullptr : rebase(v.sub_ids);
   v.efilt = rebase(v.efilt);
   idx->dev_flen = host ? nullptr : reinterpret_cast<uint16_t*>(NB + M.o_flen);
   emqx_gm_index_info_t& in = idx->info;
@@ -601,7 +610,9 @@ static int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<ui
   in.n_edges = prev->info.n_edges + P.new_edges;
   in.n_words = M.dict_used;
   in.max_depth = std::max(prev->info.max_depth, P.max_depth);
+  in.device_bytes = blob_bytes;
   idx->level_nodes = prev->level_nodes ? prev->level_nodes + (M.nodes_n - P.s_nodes_n) : 0;  // new nodes, any depth
+  if (rmap_out) *rmap_out = std::move(rmap);
   idx->mirror = prev->mirror;  // the mirror follows the newest snapshot
   prev->mirror = nullptr;
   *out = idx;

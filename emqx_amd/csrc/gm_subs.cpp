@@ -1,0 +1,210 @@
+// gm_subs.cpp — subscriber maintenance on an index with subscriber lists
+// (SURVEY.md §8a a10 writes, §8f rank 1).
+//
+// The reference: emqx_broker:subscribe/2 inserts {Topic, SubPid} into the
+// emqx_subscriber bag (sharded past 1,024 subscribers) and, for a topic's
+// first subscriber, adds its route (emqx_router:do_add_route/2);
+// unsubscribe/1 deletes the pair and, after the last one, the route
+// (apps/emqx/src/emqx_broker.erl:147-165, 445-454; emqx_broker_helper.erl:
+// 82-91; emqx_router.erl:112-125, 164-172).  Here one call applies a batch of
+// (filter, subscriber, subscribe | unsubscribe) ops and returns a NEW snapshot
+// (RCU, like emqx_gm_index_update):
+//   * each touched filter's list is read back, edited on the host (a pair is
+//     present at most once; a subscribe appends, an unsubscribe removes the
+//     pair and keeps the others' order);
+//   * route changes (first subscriber / last one gone) go through the in-place
+//     trie patch (gm_overlay.cpp, patch_update);
+//   * the new snapshot gets a subscriber CSR of its own, written on the device
+//     (gm_match.hip, rebuild_subs_device): untouched filters' lists copied from
+//     the previous CSR through the id renumbering, touched ones from the host.
+// Anything the patch cannot take (no room, a filter with '#' inside, a
+// snapshot that is no longer the newest) rebuilds the index from the full
+// lists.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <string>
+#include <unordered_map>
+
+#include "gm_internal.h"
+
+namespace gm {
+namespace {
+
+struct FilterEdit {
+  uint32_t old_id = NONE;  // the filter's id in prev, or NONE
+  bool had_subs = false;
+  std::vector<uint32_t> list;                    // prev's list, then appended subscribers
+  std::vector<uint8_t> dead;                     // per list entry: unsubscribed
+  std::unordered_map<uint32_t, uint64_t> where;  // subscriber -> its live entry
+
+  void subscribe(uint32_t s) {
+    auto it = where.find(s);
+    if (it != where.end() && !dead[it->second]) return;  // already subscribed (bag: one pair)
+    where[s] = list.size();
+    list.push_back(s);
+    dead.push_back(0);
+  }
+  void unsubscribe(uint32_t s) {
+    auto it = where.find(s);
+    if (it == where.end() || dead[it->second]) return;  // only if present
+    dead[it->second] = 1;
+  }
+  std::vector<uint32_t> final_list() const {
+    std::vector<uint32_t> o;
+    o.reserve(list.size());
+    for (size_t i = 0; i < list.size(); ++i)
+      if (!dead[i]) o.push_back(list[i]);
+    return o;
+  }
+};
+
+// Filter `id`'s subscriber list in prev, read back from the device.
+int read_lists(emqx_gm_ctx* ctx, const emqx_gm_index* prev, uint32_t id, std::vector<uint32_t>& out) {
+  const uint64_t a = prev->soff[id], b = prev->soff[id + 1];
+  out.resize(b - a);
+  if (b > a) GM_HIP(ctx, hipMemcpy(out.data(), prev->view.sub_ids + a, (b - a) * 4, hipMemcpyDeviceToHost));
+  return EMQX_GM_OK;
+}
+
+// Fallback: the updated set rebuilt from full host lists.
+int rebuild(emqx_gm_ctx* ctx, const emqx_gm_index* prev, const std::map<std::string, FilterEdit>& ed,
+            emqx_gm_index** out) {
+  const uint64_t nb = prev->info.n_filters;
+  std::vector<uint32_t> all(prev->soff.back());
+  if (!all.empty())
+    GM_HIP(ctx, hipMemcpy(all.data(), prev->view.sub_ids, all.size() * 4, hipMemcpyDeviceToHost));
+  std::vector<const FilterEdit*> edit_of(nb, nullptr);
+  for (const auto& kv : ed)
+    if (kv.second.old_id != NONE) edit_of[kv.second.old_id] = &kv.second;
+  std::vector<uint8_t> fb;
+  std::vector<uint64_t> fo{0}, so{0};
+  std::vector<uint32_t> si;
+  auto add = [&](const uint8_t* p, uint64_t len, const uint32_t* l, uint64_t cnt) {
+    fb.insert(fb.end(), p, p + len);
+    fo.push_back(fb.size());
+    si.insert(si.end(), l, l + cnt);
+    so.push_back(si.size());
+  };
+  for (uint64_t f = 0; f < nb; ++f) {
+    const uint8_t* p = prev->fbytes.data() + prev->foff[f];
+    const uint64_t len = prev->foff[f + 1] - prev->foff[f];
+    if (const FilterEdit* e = edit_of[f]) {
+      const std::vector<uint32_t> l = e->final_list();
+      if (e->had_subs && l.empty()) continue;  // the last subscriber left: the route goes
+      add(p, len, l.data(), l.size());
+    } else {
+      add(p, len, all.data() + prev->soff[f], prev->soff[f + 1] - prev->soff[f]);
+    }
+  }
+  for (const auto& kv : ed)
+    if (kv.second.old_id == NONE) {
+      const std::vector<uint32_t> l = kv.second.final_list();
+      if (!l.empty()) add(reinterpret_cast<const uint8_t*>(kv.first.data()), kv.first.size(), l.data(), l.size());
+    }
+  fb.resize(fb.size() + 64, 0);
+  if (si.empty()) si.push_back(0);
+  return build_index(ctx, fb.data(), fo.data(), fo.size() - 1, so.data(), si.data(), nullptr, out);
+}
+
+}  // namespace
+
+int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo, const uint32_t* subs,
+                const uint8_t* ops, uint64_t n_ops, emqx_gm_index** out) {
+  if (!prev || !out) return set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: NULL argument");
+  if (n_ops && (!fb || !fo || !subs || !ops)) return set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: NULL op buffers");
+  if (prev->ov) return set_err(ctx, EMQX_GM_EUNSUPPORTED, "index_update_subs: overlay snapshot");
+  if (!prev->gmap.empty()) return set_err(ctx, EMQX_GM_EUNSUPPORTED, "index_update_subs: shard index");
+  if (prev->soff.empty())
+    return set_err(ctx, EMQX_GM_EUNSUPPORTED,
+                   "index_update_subs: index without subscriber lists (route updates: emqx_gm_index_update)");
+  for (uint64_t i = 0; i < n_ops; ++i)
+    if (fo[i + 1] < fo[i]) return set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: offsets not monotone");
+  // ---- the touched filters' lists, edited in op order
+  std::map<std::string, FilterEdit> ed;  // filter bytes -> edit (byte order: the new filters' order)
+  for (uint64_t i = 0; i < n_ops; ++i) {
+    const uint8_t* f = fb + fo[i];
+    const uint64_t len = fo[i + 1] - fo[i];
+    auto ins = ed.try_emplace(std::string(reinterpret_cast<const char*>(f), len));
+    FilterEdit& e = ins.first->second;
+    if (ins.second) {
+      bool found;
+      const uint64_t r = filter_rank(prev, f, len, &found);
+      if (found) {
+        e.old_id = uint32_t(r);
+        int rc = read_lists(ctx, prev, e.old_id, e.list);
+        if (rc) return rc;
+        e.had_subs = !e.list.empty();
+        e.dead.assign(e.list.size(), 0);
+        for (uint64_t k = 0; k < e.list.size(); ++k) e.where[e.list[k]] = k;
+      }
+    }
+    if (ops[i]) e.subscribe(subs[i]);
+    else e.unsubscribe(subs[i]);
+  }
+  // ---- route changes: a first subscriber adds the route, the last one leaving deletes it
+  std::set<uint32_t> tomb;
+  std::set<std::string> dset;
+  bool wf = true;
+  for (const auto& kv : ed) {
+    uint64_t live = 0;
+    for (uint8_t d : kv.second.dead) live += d ? 0 : 1;
+    if (kv.second.old_id == NONE && live) {
+      dset.insert(kv.first);
+      wf = wf && well_formed_filter(reinterpret_cast<const uint8_t*>(kv.first.data()), kv.first.size());
+    } else if (kv.second.old_id != NONE && kv.second.had_subs && !live) {
+      tomb.insert(kv.second.old_id);
+    }
+  }
+  const uint64_t nb = prev->info.n_filters;
+  emqx_gm_index* idx = nullptr;
+  std::vector<uint32_t> rmap;
+  int rc = 1;
+  {
+    std::unique_lock<std::mutex> lk(prev->mirror_mu);
+    if (prev->mirror && wf && tomb.size() + dset.size() <= std::max<uint64_t>(4096, nb / 8))
+      rc = patch_update(ctx, prev, tomb, dset, &idx, &rmap, /*trie_only=*/true);
+  }
+  if (rc < 0) return rc;
+  if (rc == 1) return rebuild(ctx, prev, ed, out);
+  // ---- the new CSR: new id -> old id, the touched filters' final lists by new id
+  const uint64_t nf = idx->info.n_filters;
+  std::vector<uint32_t> inv(nf, NONE);
+  for (uint64_t f = 0; f < nb; ++f)
+    if (rmap[f] != NONE) inv[rmap[f]] = uint32_t(f);
+  std::vector<std::pair<uint32_t, std::vector<uint32_t>>> aff;
+  {
+    uint64_t k = 0;  // dset's filters in byte order: ids nb + k before renumbering
+    for (const auto& kv : ed) {
+      uint32_t nid = NONE;
+      if (kv.second.old_id != NONE) nid = rmap[kv.second.old_id];
+      else if (dset.count(kv.first)) nid = rmap[nb + k++];
+      if (nid != NONE) aff.emplace_back(nid, kv.second.final_list());
+    }
+  }
+  std::sort(aff.begin(), aff.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<uint32_t> aff_ids, aff_buf;
+  std::vector<uint64_t> aff_off{0};
+  std::vector<uint64_t> cnt(nf, 0);
+  for (uint64_t f = 0; f < nf; ++f)
+    if (inv[f] != NONE) cnt[f] = prev->soff[inv[f] + 1] - prev->soff[inv[f]];
+  for (auto& a : aff) {
+    aff_ids.push_back(a.first);
+    aff_buf.insert(aff_buf.end(), a.second.begin(), a.second.end());
+    aff_off.push_back(aff_buf.size());
+    cnt[a.first] = a.second.size();
+  }
+  std::vector<uint64_t> new_soff(nf + 1, 0);
+  for (uint64_t f = 0; f < nf; ++f) new_soff[f + 1] = new_soff[f] + cnt[f];
+  rc = rebuild_subs_device(ctx, prev, idx, new_soff, inv, aff_ids, aff_off, aff_buf);
+  if (rc) {
+    free_index(idx);  // (its mirror goes too: later updates of this line rebuild)
+    return rc;
+  }
+  idx->info.n_subs = new_soff.back();
+  idx->soff = std::move(new_soff);
+  *out = idx;
+  return EMQX_GM_OK;
+}
+
+}  // namespace gm

@@ -227,6 +227,20 @@ class Context:
               self.h, "index_update")
         return Index(self, h, np.zeros(0, np.uint32))
 
+    def update_subs(self, index: Index, ops) -> Index:
+        """A new snapshot of an index built with subscriber lists, with ``ops``
+        applied in order: (filter, subscriber id, subscribe: bool) -- a filter's
+        first subscriber adds its route, the last one leaving deletes it
+        (emqx_gm_index_update_subs).  ``index`` stays valid (RCU)."""
+        ops = list(ops)
+        fb, fo = pack([f for f, _, _ in ops])
+        subs = np.array([s for _, s, _ in ops] or [0], np.uint32)
+        kinds = np.array([1 if sub else 0 for _, _, sub in ops] or [0], np.uint8)
+        h = C.c_void_p()
+        check(lib().emqx_gm_index_update_subs(self.h, index.h, _ptr(fb), _ptr(fo), _ptr(subs), _ptr(kinds), len(ops),
+                                              C.byref(h)), self.h, "index_update_subs")
+        return Index(self, h, np.zeros(0, np.uint32))
+
     # ------------------------------------------------------------------ match
     def match(self, index: Index, topics, exact: bool = True) -> Tuple[np.ndarray, np.ndarray]:
         """Batch emqx_router:match_routes/1 (exact=True) or emqx_trie:match/1

@@ -152,6 +152,21 @@ int emqx_gm_index_build(emqx_gm_ctx *ctx, const uint8_t *filter_bytes, const uin
  * or indexes with subscriber lists (EMQX_GM_EUNSUPPORTED: rebuild those). */
 int emqx_gm_index_update(emqx_gm_ctx *ctx, emqx_gm_index *prev, const uint8_t *filter_bytes,
                          const uint64_t *filter_off, const uint8_t *ops, uint64_t n_ops, emqx_gm_index **out);
+/* Subscriber maintenance on an index built with subscriber lists
+ * (emqx_broker:subscribe/2, unsubscribe/1 with the route added on a filter's
+ * first subscriber and deleted after its last: apps/emqx/src/
+ * emqx_broker.erl:147-165, 445-454, emqx_router.erl:112-125, 164-172).
+ * Applies n_ops ops in order: ops[i] = 1 subscribes sub_ids[i] to filter i
+ * (idempotent per pair), 0 unsubscribes it (only if present).  A subscribe
+ * appends to the filter's list, an unsubscribe keeps the others' order.
+ * Returns a NEW snapshot (RCU, as emqx_gm_index_update): route changes are
+ * patched into a device copy of the newest snapshot's tables and the new
+ * snapshot gets a subscriber CSR of its own; what the patch cannot take is
+ * rebuilt.  EMQX_GM_EUNSUPPORTED for indexes without subscriber lists (use
+ * emqx_gm_index_update), overlay snapshots and shard indexes. */
+int emqx_gm_index_update_subs(emqx_gm_ctx *ctx, emqx_gm_index *prev, const uint8_t *filter_bytes,
+                              const uint64_t *filter_off, const uint32_t *sub_ids, const uint8_t *ops,
+                              uint64_t n_ops, emqx_gm_index **out);
 int emqx_gm_index_retain(emqx_gm_index *idx);
 int emqx_gm_index_release(emqx_gm_index *idx);
 int emqx_gm_index_info(const emqx_gm_index *idx, emqx_gm_index_info_t *info);

@@ -10,7 +10,7 @@
 %% On {error, _} the wrapper falls back to emqx_trie:match/1 (SURVEY.md §8b).
 -module(emqx_gpu_match).
 
--export([load_index/1, load_index/2, update_index/2, match_batch/2, match_routes_batch/2, fanout_batch/2,
+-export([load_index/1, load_index/2, update_index/2, update_subs/2, match_batch/2, match_routes_batch/2, fanout_batch/2,
          empty/1]).
 -export([match/2]).
 
@@ -36,6 +36,13 @@ load_index(_Filters, _SubIds) -> erlang:nif_error(nif_not_loaded).
 %% Any op other than insert | delete is badarg.
 -spec update_index(reference(), [{binary(), insert | delete}]) -> {ok, reference()} | {error, term()}.
 update_index(_Index, _Ops) -> erlang:nif_error(nif_not_loaded).
+
+%% emqx_gm_index_update_subs on an index from load_index/2: emqx_broker:subscribe/2
+%% and unsubscribe/1 in one batch; a filter's first subscriber adds its route, the
+%% last one leaving deletes it.  Any other op atom is badarg.
+-spec update_subs(reference(), [{binary(), non_neg_integer(), subscribe | unsubscribe}]) ->
+          {ok, reference()} | {error, term()}.
+update_subs(_Index, _Ops) -> erlang:nif_error(nif_not_loaded).
 
 -spec match_batch(reference(), [binary()]) -> [[binary()]] | {error, term()}.
 match_batch(_Index, _Topics) -> erlang:nif_error(nif_not_loaded).

@@ -28,7 +28,7 @@ typedef struct {
 
 static ErlNifResourceType *INDEX_RT;
 static emqx_gm_ctx *CTX;
-static ERL_NIF_TERM A_OK, A_ERROR, A_BADARG, A_INSERT, A_DELETE;
+static ERL_NIF_TERM A_OK, A_ERROR, A_BADARG, A_INSERT, A_DELETE, A_SUBSCRIBE, A_UNSUBSCRIBE;
 
 static void index_dtor(ErlNifEnv *env, void *obj) {
   gm_index_res *r = (gm_index_res *)obj;
@@ -49,6 +49,8 @@ static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
   A_BADARG = enif_make_atom(env, "badarg");
   A_INSERT = enif_make_atom(env, "insert");
   A_DELETE = enif_make_atom(env, "delete");
+  A_SUBSCRIBE = enif_make_atom(env, "subscribe");
+  A_UNSUBSCRIBE = enif_make_atom(env, "unsubscribe");
   return emqx_gm_open(&o, &CTX) == EMQX_GM_OK && INDEX_RT ? 0 : 1;
 }
 
@@ -200,6 +202,53 @@ static ERL_NIF_TERM update_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM ar
   return make_index_term(env, idx);
 }
 
+/* update_subs(Index, [{Filter :: binary(), SubId :: non_neg_integer(), subscribe | unsubscribe}])
+ *   -> {ok, NewIndex} | {error, Reason}
+ * emqx_gm_index_update_subs on an index from load_index/2: emqx_broker's
+ * subscribe/unsubscribe, with the route added on a filter's first subscriber
+ * and deleted after its last. */
+static ERL_NIF_TERM update_subs(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_index_res *r;
+  unsigned len, i = 0;
+  ERL_NIF_TERM h, t = argv[1], fl = enif_make_list(env, 0);
+  uint8_t *fb, *ops;
+  uint32_t *subs;
+  uint64_t *fo, n;
+  emqx_gm_index *idx = NULL;
+  int rc;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], INDEX_RT, (void **)&r) || !enif_get_list_length(env, argv[1], &len))
+    return enif_make_badarg(env);
+  ops = enif_alloc(len + 1);
+  subs = enif_alloc((len + 1) * sizeof(uint32_t));
+  while (enif_get_list_cell(env, t, &h, &t)) {
+    const ERL_NIF_TERM *tup;
+    int arity;
+    unsigned s;
+    if (!enif_get_tuple(env, h, &arity, &tup) || arity != 3 || !enif_get_uint(env, tup[1], &s) ||
+        (!enif_is_identical(tup[2], A_SUBSCRIBE) && !enif_is_identical(tup[2], A_UNSUBSCRIBE))) {
+      enif_free(ops);
+      enif_free(subs);
+      return enif_make_badarg(env);  /* only subscribe | unsubscribe */
+    }
+    fl = enif_make_list_cell(env, tup[0], fl);
+    subs[i] = s;
+    ops[i++] = enif_is_identical(tup[2], A_SUBSCRIBE) ? 1 : 0;
+  }
+  if (!enif_make_reverse_list(env, fl, &fl) || !pack_list(env, fl, &fb, &fo, &n)) {
+    enif_free(ops);
+    enif_free(subs);
+    return enif_make_badarg(env);
+  }
+  rc = emqx_gm_index_update_subs(CTX, r->idx, fb, fo, subs, ops, n, &idx);
+  enif_free(fb);
+  enif_free(fo);
+  enif_free(ops);
+  enif_free(subs);
+  if (rc != EMQX_GM_OK) return error_tuple(env, rc);
+  return make_index_term(env, idx);
+}
+
 static ERL_NIF_TERM do_match(ErlNifEnv *env, const ERL_NIF_TERM argv[], uint32_t flags) {
   gm_index_res *r;
   uint8_t *tb;
@@ -308,6 +357,7 @@ static ErlNifFunc funcs[] = {
     {"load_index", 1, load_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"load_index", 2, load_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"update_index", 2, update_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"update_subs", 2, update_subs, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"match_batch", 2, match_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"match_routes_batch", 2, match_routes_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fanout_batch", 2, fanout_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},

@@ -264,3 +264,140 @@ def test_patch_c2_scale_equals_rebuild(ctx, orc):
     print(f"[patch_c2] update of {len(ops)} ops: {t_upd * 1e3:.1f} ms", flush=True)
     for x in (idx, new, flat):
         x.release()
+
+
+class _Broker:
+    """The reference's bookkeeping for the test: emqx_subscriber lists (a pair
+    at most once, appended on subscribe) and the routed filters (a filter's
+    first subscriber adds its route, the last one leaving deletes it;
+    emqx_broker.erl:147-165, 445-454, emqx_router.erl:112-125, 164-172)."""
+
+    def __init__(self, subs):
+        self.lists = {f: list(l) for f, l in subs.items()}
+        self.indexed = set(subs)
+
+    def apply(self, ops):
+        before = {f: len(self.lists.get(f, [])) for f, _, _ in ops}
+        for f, s, sub in ops:
+            l = self.lists.setdefault(f, [])
+            if sub and s not in l:
+                l.append(s)
+            elif not sub and s in l:
+                l.remove(s)
+        for f in before:
+            n = len(self.lists.get(f, []))
+            if f not in self.indexed and n:
+                self.indexed.add(f)
+            elif f in self.indexed and before[f] and not n:
+                self.indexed.discard(f)
+
+    def csr(self):
+        fs = sorted(self.indexed)
+        so = np.zeros(len(fs) + 1, np.uint64)
+        so[1:] = np.cumsum([len(self.lists.get(f, [])) for f in fs])
+        si = np.array([x for f in fs for x in self.lists.get(f, [])], np.uint32)
+        return fs, so, si
+
+
+def _check_subs(ctx, orc, idx, br, topics):
+    fs, so, si = br.csr()
+    assert idx.n_filters == len(fs) and [idx.filter(i) for i in range(idx.n_filters)] == fs
+    ro, ids = ctx.match(idx, topics, exact=True)
+    oro, oids = _oracle(orc, set(fs), topics, True)
+    assert np.array_equal(ro, oro) and np.array_equal(ids, oids)
+    fro, fids = ctx.fanout(idx, ro, ids)
+    ero, eids = orc.fanout(ro, ids, so, si)
+    assert np.array_equal(fro, ero) and np.array_equal(fids, eids)
+    for i in range(0, len(fs), max(1, len(fs) // 50)):
+        assert idx.subscriber_count(i) == so[i + 1] - so[i]
+
+
+def test_update_subs_vs_oracle(ctx, orc, monkeypatch):
+    """emqx_gm_index_update_subs: random subscribe / unsubscribe batches (new
+    filters, last subscribers leaving, re-subscribes, absent pairs) against
+    the reference's bookkeeping; matches and fan-out rows vs the oracle after
+    every batch; the previous snapshot keeps its own lists (RCU); then the
+    rebuild fallbacks ('#' inside a filter, a superseded snapshot)."""
+    from tests.test_gpu_parity import _rand_filter, _rand_topic
+    monkeypatch.delenv("GM_UPDATE_OVERLAY", raising=False)
+    rng = random.Random(41)
+    subs = {}
+    for _ in range(300):
+        f = _rand_filter(rng).encode()
+        subs[f] = rng.sample(range(5000), rng.randint(0, 6))  # some routes without local subscribers
+    br = _Broker(subs)
+    fs0 = sorted(subs)
+    idx = ctx.build_index(fs0, subs=[subs[f] for f in fs0])
+    topics = [_rand_topic(rng).encode() for _ in range(1500)]
+    _check_subs(ctx, orc, idx, br, topics)
+    for rnd in range(10):
+        ops = []
+        for _ in range(rng.randint(1, 80)):
+            k = rng.random()
+            if k < 0.35 and br.indexed:  # subscribe to a routed filter
+                ops.append((rng.choice(sorted(br.indexed)), rng.randrange(5000), True))
+            elif k < 0.6:  # a new filter's first subscriber (or an existing one)
+                ops.append((_rand_filter(rng).encode(), rng.randrange(5000), True))
+            elif k < 0.85 and br.lists:  # unsubscribe a present pair
+                f = rng.choice(sorted(br.lists))
+                if br.lists[f]:
+                    ops.append((f, rng.choice(br.lists[f]), False))
+            elif br.indexed:  # all subscribers of a filter leave: its route goes
+                f = rng.choice(sorted(br.indexed))
+                ops += [(f, s, False) for s in list(br.lists.get(f, []))]
+                ops.append((f, 99_999, False))  # an absent pair: no-op
+        prev_state = _Broker({})
+        prev_state.lists = {f: list(l) for f, l in br.lists.items()}
+        prev_state.indexed = set(br.indexed)
+        br.apply(ops)
+        new = ctx.update_subs(idx, ops)
+        _check_subs(ctx, orc, new, br, topics)
+        if rnd % 3 == 0:  # RCU: the previous snapshot answers with its own lists
+            _check_subs(ctx, orc, idx, prev_state, topics)
+        idx.release()
+        idx = new
+    # fallbacks: a filter with '#' inside, then an update of a superseded snapshot
+    ops = [(b"a/#/b", 7, True)]
+    br.apply(ops)
+    new = ctx.update_subs(idx, ops)
+    _check_subs(ctx, orc, new, br, topics + [b"a/x/b"])
+    older_state = _Broker({})
+    older_state.lists = {f: list(l) for f, l in br.lists.items()}
+    older_state.indexed = set(br.indexed)
+    newer = ctx.update_subs(new, [(b"z/z", 1, True)])
+    older = ctx.update_subs(new, [(b"z/q", 2, True)])  # new has no mirror now: rebuilt
+    older_state.apply([(b"z/q", 2, True)])
+    _check_subs(ctx, orc, older, older_state, topics + [b"z/q"])
+    for x in (idx, new, newer, older):
+        x.release()
+    with pytest.raises(Exception, match="EUNSUPPORTED"):
+        plain = ctx.build_index([b"a"])
+        try:
+            ctx.update_subs(plain, [(b"a", 1, True)])
+        finally:
+            plain.release()
+
+
+@pytest.mark.timeout(300)
+def test_update_subs_hot_list(ctx, orc):
+    """A C4-shaped hot filter (200k subscribers) loses 2,000 and gains 2,000
+    in one batch: the untouched filters' lists are copied on the device, the
+    hot one comes back from the host; every delivery vs the oracle."""
+    K = 50
+    filters = [b"hot/#"] + [b"hot/%d/x" % k for k in range(K)]
+    subs = {b"hot/#": list(range(200_000))}
+    for k in range(K):
+        subs[b"hot/%d/x" % k] = list(range(300_000 + 10 * k, 300_000 + 10 * k + 10))
+    br = _Broker(subs)
+    fs0 = sorted(filters)
+    idx = ctx.build_index(fs0, subs=[subs[f] for f in fs0])
+    rng = random.Random(5)
+    ops = [(b"hot/#", s, False) for s in rng.sample(range(200_000), 2000)]
+    ops += [(b"hot/#", 500_000 + i, True) for i in range(2000)]
+    ops += [(b"hot/%d/x" % k, 900_000 + k, True) for k in range(0, K, 7)]
+    br.apply(ops)
+    new = ctx.update_subs(idx, ops)
+    topics = [b"hot/%d/x" % k for k in range(K)]
+    _check_subs(ctx, orc, new, br, topics)
+    idx.release()
+    new.release()
