@@ -182,6 +182,11 @@ uint64_t filter_rank(const emqx_gm_index* idx, const uint8_t* f, uint64_t len, b
 // gm_subs.cpp: emqx_gm_index_update_subs
 int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo, const uint32_t* subs,
                 const uint8_t* ops, uint64_t n_ops, emqx_gm_index** out);
+// gm_match.hip: segments [src_off[j], src_off[j] + (dst_off[j+1] - dst_off[j])) of
+// the device array src gathered into host `out` (dst_off[m] elements), one
+// device gather + one copy back
+int gather_segments(emqx_gm_ctx* ctx, const uint32_t* src, const std::vector<uint64_t>& src_off,
+                    const std::vector<uint64_t>& dst_off, uint32_t* out);
 // gm_match.hip: the new subscriber CSR of update_subs (see there)
 int rebuild_subs_device(emqx_gm_ctx* ctx, const emqx_gm_index* prev, emqx_gm_index* idx,
                         const std::vector<uint64_t>& new_soff, const std::vector<uint32_t>& inv,

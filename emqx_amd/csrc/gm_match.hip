@@ -2025,6 +2025,42 @@ __global__ __launch_bounds__(256) void k_subs_copy(const uint64_t* __restrict__ 
   }
 }
 
+__global__ __launch_bounds__(256) void k_gather_segments(const uint32_t* __restrict__ src,
+                                                         const uint64_t* __restrict__ src_off,
+                                                         const uint64_t* __restrict__ dst_off, uint64_t m,
+                                                         uint64_t total, uint64_t per_block,
+                                                         uint32_t* __restrict__ out) {
+  const uint64_t lo = uint64_t(blockIdx.x) * per_block;
+  if (lo >= total) return;
+  const uint64_t hi = min(total, lo + per_block);
+  __shared__ uint64_t s_seg[2];
+  if (threadIdx.x < 2) s_seg[threadIdx.x] = seg_of(dst_off, 0, m, threadIdx.x == 0 ? lo : hi - 1);
+  __syncthreads();
+  const uint64_t s0 = s_seg[0], s1 = s_seg[1] + 1;
+  for (uint64_t p = lo + threadIdx.x; p < hi; p += 256) {
+    const uint64_t j = seg_of(dst_off, s0, s1, p);
+    out[p] = src[src_off[j] + (p - dst_off[j])];
+  }
+}
+
+int gather_segments(emqx_gm_ctx* ctx, const uint32_t* src, const std::vector<uint64_t>& src_off,
+                    const std::vector<uint64_t>& dst_off, uint32_t* out) {
+  const uint64_t m = src_off.size(), total = dst_off.back();
+  if (!total) return EMQX_GM_OK;
+  hipStream_t st = ctx->stream;
+  PoolBuf so(ctx->pool, m * 8 + 8), dof(ctx->pool, (m + 1) * 8), buf(ctx->pool, total * 4 + 16);
+  if (!so.p || !dof.p || !buf.p) return set_err(ctx, EMQX_GM_ENOMEM, "gather_segments: workspace");
+  GM_HIP(ctx, hipMemcpyAsync(so.p, src_off.data(), m * 8, hipMemcpyHostToDevice, st));
+  GM_HIP(ctx, hipMemcpyAsync(dof.p, dst_off.data(), (m + 1) * 8, hipMemcpyHostToDevice, st));
+  const uint64_t per = fan_per_block(total);
+  hipLaunchKernelGGL(k_gather_segments, dim3((total + per - 1) / per), dim3(256), 0, st, src, so.as<uint64_t>(),
+                     dof.as<uint64_t>(), m, total, per, buf.as<uint32_t>());
+  GM_HIP(ctx, hipGetLastError());
+  GM_HIP(ctx, hipMemcpyAsync(out, buf.p, total * 4, hipMemcpyDeviceToHost, st));
+  GM_HIP(ctx, hipStreamSynchronize(st));
+  return EMQX_GM_OK;
+}
+
 int rebuild_subs_device(emqx_gm_ctx* ctx, const emqx_gm_index* prev, emqx_gm_index* idx,
                         const std::vector<uint64_t>& new_soff, const std::vector<uint32_t>& inv,
                         const std::vector<uint32_t>& aff_ids, const std::vector<uint64_t>& aff_off,

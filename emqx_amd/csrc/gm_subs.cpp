@@ -59,13 +59,6 @@ struct FilterEdit {
   }
 };
 
-// Filter `id`'s subscriber list in prev, read back from the device.
-int read_lists(emqx_gm_ctx* ctx, const emqx_gm_index* prev, uint32_t id, std::vector<uint32_t>& out) {
-  const uint64_t a = prev->soff[id], b = prev->soff[id + 1];
-  out.resize(b - a);
-  if (b > a) GM_HIP(ctx, hipMemcpy(out.data(), prev->view.sub_ids + a, (b - a) * 4, hipMemcpyDeviceToHost));
-  return EMQX_GM_OK;
-}
 
 // Fallback: the updated set rebuilt from full host lists.
 int rebuild(emqx_gm_ctx* ctx, const emqx_gm_index* prev, const std::map<std::string, FilterEdit>& ed,
@@ -120,27 +113,47 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
                    "index_update_subs: index without subscriber lists (route updates: emqx_gm_index_update)");
   for (uint64_t i = 0; i < n_ops; ++i)
     if (fo[i + 1] < fo[i]) return set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: offsets not monotone");
-  // ---- the touched filters' lists, edited in op order
+  // ---- the touched filters, their current lists read back in one device gather
   std::map<std::string, FilterEdit> ed;  // filter bytes -> edit (byte order: the new filters' order)
+  std::vector<FilterEdit*> by_op(n_ops);
   for (uint64_t i = 0; i < n_ops; ++i) {
     const uint8_t* f = fb + fo[i];
     const uint64_t len = fo[i + 1] - fo[i];
     auto ins = ed.try_emplace(std::string(reinterpret_cast<const char*>(f), len));
-    FilterEdit& e = ins.first->second;
     if (ins.second) {
       bool found;
       const uint64_t r = filter_rank(prev, f, len, &found);
-      if (found) {
-        e.old_id = uint32_t(r);
-        int rc = read_lists(ctx, prev, e.old_id, e.list);
-        if (rc) return rc;
-        e.had_subs = !e.list.empty();
-        e.dead.assign(e.list.size(), 0);
-        for (uint64_t k = 0; k < e.list.size(); ++k) e.where[e.list[k]] = k;
-      }
+      if (found) ins.first->second.old_id = uint32_t(r);
     }
-    if (ops[i]) e.subscribe(subs[i]);
-    else e.unsubscribe(subs[i]);
+    by_op[i] = &ins.first->second;
+  }
+  {
+    std::vector<FilterEdit*> touched;
+    std::vector<uint64_t> src_off, dst_off{0};
+    for (auto& kv : ed)
+      if (kv.second.old_id != NONE) {
+        const uint32_t id = kv.second.old_id;
+        touched.push_back(&kv.second);
+        src_off.push_back(prev->soff[id]);
+        dst_off.push_back(dst_off.back() + (prev->soff[id + 1] - prev->soff[id]));
+      }
+    std::vector<uint32_t> all(dst_off.back());
+    if (!all.empty()) {
+      const int rc = gather_segments(ctx, prev->view.sub_ids, src_off, dst_off, all.data());
+      if (rc) return rc;
+    }
+    for (size_t j = 0; j < touched.size(); ++j) {
+      FilterEdit& e = *touched[j];
+      e.list.assign(all.begin() + dst_off[j], all.begin() + dst_off[j + 1]);
+      e.had_subs = !e.list.empty();
+      e.dead.assign(e.list.size(), 0);
+      for (uint64_t k = 0; k < e.list.size(); ++k) e.where[e.list[k]] = k;
+    }
+  }
+  // ---- the ops, in order
+  for (uint64_t i = 0; i < n_ops; ++i) {
+    if (ops[i]) by_op[i]->subscribe(subs[i]);
+    else by_op[i]->unsubscribe(subs[i]);
   }
   // ---- route changes: a first subscriber adds the route, the last one leaving deletes it
   std::set<uint32_t> tomb;
