@@ -218,7 +218,14 @@ class Broker:
     the topic, later ones in ``{shard, Topic, I}`` buckets with one
     ``{shard, I}`` marker per bucket (emqx_broker.erl:147-165, 445-454).  The
     snapshot flattens the buckets into one subscriber list per filter, which is
-    what do_dispatch/2,3 (emqx_broker.erl:506-530) folds over."""
+    what do_dispatch/2,3 (emqx_broker.erl:506-530) folds over.
+
+    Snapshots are incremental: the subscribe / unsubscribe calls since the last
+    snapshot are applied with one emqx_gm_index_update_subs (a filter's first
+    subscriber adds its route, its last one leaving deletes it).  Within a
+    filter the incremental list keeps arrival order, so a sharded topic's
+    deliveries may come in another order than subscribers/1 lists them; the
+    delivery multiset is the same (the reference promises no order either)."""
 
     SHARD = 1024  # emqx_broker_helper.erl:54
 
@@ -231,7 +238,7 @@ class Broker:
         self._seq: Dict[bytes, int] = {}
         self._subopt: set = set()
         self._snap: Optional[_Snapshot] = None
-        self._snap_filters: Optional[List[bytes]] = None
+        self._pending: List[Tuple[bytes, int, bool]] = []  # since the snapshot: (filter, subscriber, subscribe)
         self._lock = threading.Lock()
 
     def _context(self) -> Context:
@@ -252,7 +259,7 @@ class Broker:
                 i = (subpid * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF)
                 i = ((i ^ (i >> 29)) % self.shards_num) + 1
                 self._shards.setdefault((t, i), []).append(subpid)
-            self._snap = None
+            self._pending.append((t, subpid, True))
         self.router.add_route(t)
 
     def unsubscribe(self, t, subpid: int) -> None:
@@ -266,7 +273,7 @@ class Broker:
             for k in [k for k in self._shards if k[0] == t]:
                 if subpid in self._shards[k]:
                     self._shards[k].remove(subpid)
-            self._snap = None
+            self._pending.append((t, subpid, False))
             still = bool(self._direct.get(t)) or any(v for k, v in self._shards.items() if k[0] == t)
         if not still:
             self.router.delete_route(t)
@@ -282,10 +289,19 @@ class Broker:
 
     def snapshot(self) -> _Snapshot:
         with self._lock:
+            filters = sorted(self.router._routes)
+            if self._snap is not None and self._pending:
+                idx = self._context().update_subs(self._snap.index, self._pending)
+                if idx.n_filters == len(filters):
+                    self._snap = _Snapshot(self._context(), filters, index=idx)
+                else:  # routes changed behind the broker's back (router.add_route): rebuild
+                    idx.release()
+                    self._snap = None
+                self._pending = []
             if self._snap is None:
-                filters = sorted(self.router._routes)
                 subs = [self.subscribers(f) for f in filters]
                 self._snap = _Snapshot(self._context(), filters, subs)
+                self._pending = []
             return self._snap
 
     def publish_batch(self, topics: Sequence) -> List[List[int]]:

@@ -557,3 +557,41 @@ def test_adversarial_plus_chains_all_rows(ctx, orc):
         assert np.array_equal(ro, oro) and np.array_equal(ids, oids)
         assert ctx.stats()["n_overflow"] > 10_000  # the slow path really ran
     idx.release()
+
+
+def test_broker_incremental_snapshots(ctx):
+    """Broker snapshots between publishes come from emqx_gm_index_update_subs:
+    subscribes past the 1,024-subscriber shard threshold, unsubscribes, a
+    filter's last subscriber leaving (its route goes), wildcard filters;
+    deliveries as multisets against the bookkeeping's subscribers/1."""
+    from emqx_amd.routing import Broker
+    rng = random.Random(8)
+    b = Broker(ctx, schedulers=2)
+    filters = ["hot/t", "hot/+", "hot/#", "a/b", "a/+/c", "#"]
+    truth = {f: [] for f in filters}
+    topics = ["hot/t", "hot/x", "a/b", "a/q/c", "z"]
+
+    def expect(t):
+        from emqx_amd import topic as T
+        return sorted(s for f, l in truth.items() for s in l if T.match(t, f))
+
+    for rnd in range(8):
+        for _ in range(rng.randint(50, 700)):
+            f = rng.choice(filters)
+            if truth[f] and rng.random() < 0.3:
+                s = rng.choice(truth[f])
+                b.unsubscribe(f, s)
+                truth[f].remove(s)
+            else:
+                s = rng.randrange(1, 5000)
+                b.subscribe(f, s)
+                if s not in truth[f]:
+                    truth[f].append(s)
+        if rnd == 5:  # every subscriber of a/b leaves: its route goes
+            for s in list(truth["a/b"]):
+                b.unsubscribe("a/b", s)
+            truth["a/b"] = []
+        for t in topics:
+            assert sorted(b.publish(t)) == expect(t), (rnd, t)
+        assert b.router.has_routes("a/b") == bool(truth["a/b"])
+    assert len(truth["hot/t"]) > 1024  # the shard buckets were exercised
