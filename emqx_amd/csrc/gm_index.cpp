@@ -745,9 +745,10 @@ void free_index(emqx_gm_index* idx) {
   delete idx->mirror;
   if (idx->dev_base || idx->dev_subs) {
     (void)hipSetDevice(idx->device);
-    if (idx->dev_base) (void)hipFree(idx->dev_base);
+    if (idx->dev_base && !idx->blob_owner) (void)hipFree(idx->dev_base);
     if (idx->dev_subs) (void)hipFree(idx->dev_subs);
   }
+  if (idx->blob_owner && idx->blob_owner->refs.fetch_sub(1) == 1) free_index(idx->blob_owner);
   delete idx;
 }
 

@@ -114,6 +114,7 @@ struct emqx_gm_index {
   int device = 0;
   void* dev_base = nullptr;     // one allocation holding every table
   void* dev_subs = nullptr;     // a subscriber CSR of its own (after emqx_gm_index_update_subs), or nullptr
+  emqx_gm_index* blob_owner = nullptr;  // set: dev_base is that (retained) snapshot's blob, shared
   size_t dev_bytes = 0;
   gm::IndexView view{};
   uint16_t* dev_flen = nullptr; // filter lengths (stats only), inside dev_base

@@ -175,8 +175,31 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
   int rc = 1;
   {
     std::unique_lock<std::mutex> lk(prev->mirror_mu);
-    if (prev->mirror && wf && tomb.size() + dset.size() <= std::max<uint64_t>(4096, nb / 8))
+    if (prev->mirror && tomb.empty() && dset.empty()) {
+      // no route changed: the new snapshot shares prev's tables (retained), the
+      // mirror moves on with it; only the subscriber CSR is new
+      idx = new emqx_gm_index;
+      idx->device = prev->device;
+      idx->dev_base = prev->dev_base;
+      idx->dev_bytes = prev->dev_bytes;
+      emqx_gm_index* owner = prev->blob_owner ? prev->blob_owner : prev;
+      owner->refs.fetch_add(1);
+      idx->blob_owner = owner;
+      idx->view = prev->view;
+      idx->info = prev->info;
+      idx->info.device_bytes = prev->dev_bytes;  // the tables; the new CSR is added below
+      idx->fbytes = prev->fbytes;
+      idx->foff = prev->foff;
+      idx->dev_flen = prev->dev_flen;
+      idx->level_nodes = prev->level_nodes;
+      idx->mirror = prev->mirror;
+      prev->mirror = nullptr;
+      rmap.resize(nb);
+      for (uint64_t f = 0; f < nb; ++f) rmap[f] = uint32_t(f);
+      rc = 0;
+    } else if (prev->mirror && wf && tomb.size() + dset.size() <= std::max<uint64_t>(4096, nb / 8)) {
       rc = patch_update(ctx, prev, tomb, dset, &idx, &rmap, /*trie_only=*/true);
+    }
   }
   if (rc < 0) return rc;
   if (rc == 1) return rebuild(ctx, prev, ed, out);

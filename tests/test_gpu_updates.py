@@ -356,6 +356,20 @@ def test_update_subs_vs_oracle(ctx, orc, monkeypatch):
             _check_subs(ctx, orc, idx, prev_state, topics)
         idx.release()
         idx = new
+    # subscriber-only batches (no route changes): the new snapshot shares the
+    # previous one's tables; the previous one is released before the new one is
+    # used, so the shared tables must outlive it
+    for rnd in range(4):
+        ops = []
+        for f in rng.sample(sorted(f for f in br.indexed if br.lists.get(f)), 10):
+            ops.append((f, 10_000 + rnd, True))
+            if len(br.lists[f]) > 1:
+                ops.append((f, br.lists[f][0], False))
+        br.apply(ops)
+        new = ctx.update_subs(idx, ops)
+        idx.release()
+        idx = new
+        _check_subs(ctx, orc, idx, br, topics)
     # fallbacks: a filter with '#' inside, then an update of a superseded snapshot
     ops = [(b"a/#/b", 7, True)]
     br.apply(ops)
