@@ -575,7 +575,12 @@ def test_broker_incremental_snapshots(ctx):
         from emqx_amd import topic as T
         return sorted(s for f, l in truth.items() for s in l if T.match(t, f))
 
+    hot = iter(range(10_000, 20_000))
     for rnd in range(8):
+        for _ in range(250):  # hot/t grows past the shard threshold
+            s = next(hot)
+            b.subscribe("hot/t", s)
+            truth["hot/t"].append(s)
         for _ in range(rng.randint(50, 700)):
             f = rng.choice(filters)
             if truth[f] and rng.random() < 0.3:
