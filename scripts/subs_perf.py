@@ -48,5 +48,20 @@ for k in [int(x) for x in (sys.argv[1:] or ["100", "1000", "10000"])]:
     new.release()
     idx.release()  # the mirror moved to the released snapshot: a fresh base for the next k
     idx = ctx.build_index((fb, fo), subs=(so, si))
+# subscriber-only batches (no route changes): the new snapshot shares the tables
+for k in (100, 1000, 10000):
+    ops = []
+    for i in range(k):
+        f = rng.randrange(n)
+        fbytes = bytes(fb[fo[f]:fo[f + 1]])
+        ops.append((fbytes, 4_000_000 + i, True) if i % 2 else (fbytes, int(si[f * PER + rng.randrange(PER)]), False))
+    t = time.perf_counter()
+    new = ctx.update_subs(idx, ops)
+    t_upd = time.perf_counter() - t
+    print(json.dumps({"k": k, "subscriber_only": True, "update_ms": t_upd * 1e3, "filters": new.n_filters,
+                      "entries": int(new.info.n_subs)}), flush=True)
+    new.release()
+    idx.release()
+    idx = ctx.build_index((fb, fo), subs=(so, si))
 idx.release()
 ctx.close()
