@@ -600,3 +600,61 @@ def test_broker_incremental_snapshots(ctx):
             assert sorted(b.publish(t)) == expect(t), (rnd, t)
         assert b.router.has_routes("a/b") == bool(truth["a/b"])
     assert len(truth["hot/t"]) > 1024  # the shard buckets were exercised
+
+
+@pytest.mark.timeout(300)
+def test_concurrent_calls_one_context(ctx, orc):
+    """SURVEY §8b threading: one context, 8 threads at once (ctypes drops the
+    GIL, so the library's calls really overlap and serialize on the context):
+    host-buffer and device-buffer matches, fan-out, in-place updates and
+    failing calls, each thread's results equal to a single-threaded run, and
+    each failing call's message its own (emqx_gm_last_error is per thread)."""
+    import threading
+    from emqx_amd import GpuMatchError
+    rng = random.Random(99)
+    filters = sorted({_rand_filter(rng).encode() for _ in range(400)})
+    subs = [rng.sample(range(10_000), rng.randint(0, 5)) for _ in filters]
+    topics = [_rand_topic(rng).encode() for _ in range(20_000)]
+    idx = ctx.build_index(filters, subs=subs)
+    plain = ctx.build_index(filters)
+    want_ro, want_ids = ctx.match(idx, topics, exact=True)
+    want_fro, want_fids = ctx.fanout(idx, want_ro, want_ids)
+    errors, done = [], []
+
+    def worker(k):
+        try:
+            r = random.Random(k)
+            for it in range(12):
+                kind = (k + it) % 4
+                if kind == 0:
+                    ro, ids = ctx.match(idx, topics, exact=True)
+                    assert np.array_equal(ro, want_ro) and np.array_equal(ids, want_ids)
+                elif kind == 1:
+                    fro, fids = ctx.fanout(idx, want_ro, want_ids)
+                    assert np.array_equal(fro, want_fro) and np.array_equal(fids, want_fids)
+                elif kind == 2:  # an update of the shared plain index (overlay or patch) and a match on it
+                    new_f = b"k%d/%d/+" % (k, it)
+                    t = b"k%d/%d/x" % (k, it)
+                    new = ctx.update_index(plain, [(new_f, True)])
+                    _, ids0 = ctx.match(plain, [t], exact=True)
+                    _, ids = ctx.match(new, [t], exact=True)
+                    assert [new.filter(i) for i in ids] == sorted([plain.filter(i) for i in ids0] + [new_f])
+                    new.release()
+                else:  # a failing call: bad offsets, this thread's own message
+                    bad = (np.zeros(8, np.uint8), np.array([0, 5, 2], np.uint64))
+                    with pytest.raises(GpuMatchError) as ei:
+                        ctx.match(idx, bad, exact=True)
+                    assert "offset" in str(ei.value) or "EINVAL" in str(ei.value)
+            done.append(k)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((k, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:3]
+    assert sorted(done) == list(range(8))
+    idx.release()
+    plain.release()
