@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-parity", action="store_true", help="skip the oracle check of the last step's sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--no-update", action="store_true", help="skip the incremental-update detail")
     p.add_argument("--no-host-io", action="store_true",
                    help="skip the host-buffer call (PCIe-inclusive rate, reported in detail, never `value`)")
     return p.parse_args()
@@ -346,6 +347,23 @@ def main():
         out["detail"]["host_io_ms"] = best * 1e3
         out["detail"]["host_io_nnz_matches_device"] = ok
         del hb, ho
+    if rank == 0 and world == 1 and not a.no_update:
+        # incremental maintenance, outside the timed region: 100 deletes +
+        # 100 inserts patched into this index, and a match of the same batch on the result
+        rng = np.random.default_rng(7)
+        dels = [idx.filter(int(i)) for i in rng.choice(idx.n_filters, 100, replace=False)]
+        ins = [b"upd/%d/+/#" % i for i in range(100)]
+        t0 = time.perf_counter()
+        new = ctx.update_index(idx, [(f, False) for f in dels] + [(f, True) for f in ins])
+        upd_ms = (time.perf_counter() - t0) * 1e3
+        ks = []
+        for _ in range(3):
+            r = ctx.match_device(new, db, do, n_topics, exact=True)
+            ks.append(ctx.stats()["match_kernel_ms"])
+            r.free()
+        out["detail"]["index_update"] = {"ops": 200, "update_ms": upd_ms, "match_kernel_ms_after": min(ks),
+                                         "vs_flat": min(ks) / min(kern_ms)}
+        new.release()
     # the cpu_baseline leg (oracle): timed on all host cores at N=1, and, outside the
     # timed region, the last step's CSR checked against it on a strided sample
     want_cpu = rank == 0 and world == 1 and not a.no_cpu
