@@ -7,6 +7,8 @@
 #include <new>
 #include <stdexcept>
 
+#include <sys/mman.h>
+
 #include "gm_internal.h"
 #include "../../include/emqx_gm_ext.h"
 
@@ -29,6 +31,50 @@ DevPool::~DevPool() {
   hipSetDevice(device_);
   for (auto& kv : free_) hipFree(kv.second);
   for (auto& kv : live_) hipFree(kv.first);
+}
+
+HostPool::~HostPool() {
+  for (auto& kv : free_) free(kv.second);
+  for (auto& kv : live_) free(kv.first);
+}
+void* HostPool::alloc(size_t bytes) {
+  constexpr size_t HUGE_PAGE = 2u << 20;
+  const size_t r = bytes < HUGE_PAGE ? ((bytes + 4095) & ~size_t(4095)) : ((bytes + HUGE_PAGE - 1) & ~(HUGE_PAGE - 1));
+  auto it = free_.lower_bound(r);
+  if (it != free_.end() && it->first <= r + r / 4) {
+    void* p = it->second;
+    cached_ -= it->first;
+    live_.emplace(p, it->first);
+    free_.erase(it);
+    return p;
+  }
+  void* p = nullptr;
+  if (posix_memalign(&p, r >= HUGE_PAGE ? HUGE_PAGE : 64, r) != 0) return nullptr;
+  if (r >= HUGE_PAGE) (void)madvise(p, r, MADV_HUGEPAGE);
+  live_.emplace(p, r);
+  return p;
+}
+void HostPool::release(void* p) {
+  if (!p) return;
+  auto it = live_.find(p);
+  if (it == live_.end()) {
+    free(p);
+    return;
+  }
+  const size_t r = it->second;
+  live_.erase(it);
+  while (cached_ + r > kCap && !free_.empty()) {  // the largest cached ones go first
+    auto last = std::prev(free_.end());
+    cached_ -= last->first;
+    free(last->second);
+    free_.erase(last);
+  }
+  if (r > kCap) {
+    free(p);
+    return;
+  }
+  free_.emplace(r, p);
+  cached_ += r;
 }
 
 static size_t round_size(size_t b) {
@@ -122,6 +168,7 @@ int emqx_gm_open(const emqx_gm_opts* opts, emqx_gm_ctx** out) {
     }
   }
   ctx->pool = new gm::DevPool(dev);
+  ctx->hpool = new gm::HostPool;
   *out = ctx;
   return EMQX_GM_OK;
   GM_GUARD_END(nullptr)
@@ -135,6 +182,7 @@ int emqx_gm_close(emqx_gm_ctx* ctx) {
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     gm::free_host_pipe(ctx);
     delete ctx->pool;
+    delete ctx->hpool;
     for (auto& e : ctx->ev)
       if (e) hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) hipStreamDestroy(ctx->stream);
@@ -314,8 +362,8 @@ int emqx_gm_csr_free(emqx_gm_ctx* ctx, emqx_gm_csr* csr) {
     if (csr->row_off) ctx->pool->release(csr->row_off);
     if (csr->ids) ctx->pool->release(csr->ids);
   } else {
-    free(csr->row_off);
-    free(csr->ids);
+    ctx->hpool->release(csr->row_off);
+    ctx->hpool->release(csr->ids);
   }
   std::memset(csr, 0, sizeof(*csr));
   return EMQX_GM_OK;

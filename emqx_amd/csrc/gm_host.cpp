@@ -199,13 +199,13 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
   const uint64_t CB = 512ull << 20;
   const unsigned T = W.size();
 
-  // the caller-visible result (malloc'd: emqx_gm_csr_free frees it)
-  uint64_t* r_off = static_cast<uint64_t*>(malloc((n + 1) * 8));
+  // the caller-visible result (from the context's host pool: emqx_gm_csr_free hands it back)
+  uint64_t* r_off = static_cast<uint64_t*>(ctx->hpool->alloc((n + 1) * 8));
   uint64_t ids_cap = std::max<uint64_t>(1024, n * 4);
-  uint32_t* r_ids = static_cast<uint32_t*>(malloc(ids_cap * 4));
+  uint32_t* r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(ids_cap * 4));
   if (!r_off || !r_ids) {
-    free(r_off);
-    free(r_ids);
+    ctx->hpool->release(r_off);
+    ctx->hpool->release(r_ids);
     return set_err(ctx, EMQX_GM_ENOMEM, "match: host result");
   }
   emqx_gm_match_stats tot{};
@@ -227,8 +227,8 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
         ctx->pool->release(s.csr.ids);
         s.csr = emqx_gm_csr{};
       }
-    free(r_off);
-    free(r_ids);
+    ctx->hpool->release(r_off);
+    ctx->hpool->release(r_ids);
     return msg ? set_err(ctx, code, msg) : code;  // nullptr: keep the message of the failing step
   };
 
@@ -364,8 +364,10 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
     if (base + s.nnz > ids_cap) {
       for (auto& q : hp->slot) join(q.out_f);  // nobody writes r_ids while it moves
       while (ids_cap < base + s.nnz) ids_cap *= 2;
-      uint32_t* g = static_cast<uint32_t*>(realloc(r_ids, ids_cap * 4));
+      uint32_t* g = static_cast<uint32_t*>(ctx->hpool->alloc(ids_cap * 4));
       if (!g) return fail(EMQX_GM_ENOMEM, "match: host result grow");
+      if (base) std::memcpy(g, r_ids, base * 4);
+      ctx->hpool->release(r_ids);
       r_ids = g;
     }
     {

@@ -34,6 +34,25 @@ class DevPool {
   size_t cached_ = 0;
 };
 
+// Host result buffers (the CSRs emqx_gm_match / emqx_gm_fanout return in host
+// memory): emqx_gm_csr_free hands them back and the next call reuses them, so a
+// steady stream of calls does no first-touch page faults on fresh pages (2 GB
+// per 100M-topic call).  Large buffers are 2 MiB aligned and advised as huge
+// pages.  At most kCap bytes stay cached.
+class HostPool {
+ public:
+  ~HostPool();
+  void* alloc(size_t bytes);  // nullptr on failure
+  void release(void* p);      // a buffer of this pool (any other pointer: free())
+  size_t cached_bytes() const { return cached_; }
+
+ private:
+  static constexpr size_t kCap = 8ull << 30;
+  std::multimap<size_t, void*> free_;  // rounded size -> ptr
+  std::map<void*, size_t> live_;
+  size_t cached_ = 0;
+};
+
 // RAII handle on a pool buffer.
 struct PoolBuf {
   DevPool* pool = nullptr;
@@ -84,6 +103,7 @@ struct emqx_gm_ctx {
   hipEvent_t ov_ev[9] = {};
   std::recursive_mutex mu;
   gm::DevPool* pool = nullptr;
+  gm::HostPool* hpool = nullptr;
   emqx_gm_match_stats stats{};
   hipEvent_t ev[6]{};
 };

@@ -2130,11 +2130,11 @@ int finish_csr(emqx_gm_ctx* ctx, uint64_t n, uint64_t nnz, PoolBuf& row_off, Poo
     out->on_device = 1;
     return 0;
   }
-  uint64_t* h_off = static_cast<uint64_t*>(malloc((n + 1) * 8));
-  uint32_t* h_ids = static_cast<uint32_t*>(malloc(nnz * 4 + 4));
+  uint64_t* h_off = static_cast<uint64_t*>(ctx->hpool->alloc((n + 1) * 8));
+  uint32_t* h_ids = static_cast<uint32_t*>(ctx->hpool->alloc(nnz * 4 + 4));
   if (!h_off || !h_ids) {
-    free(h_off);
-    free(h_ids);
+    ctx->hpool->release(h_off);
+    ctx->hpool->release(h_ids);
     return set_err(ctx, EMQX_GM_ENOMEM, "csr: host allocation");
   }
   GM_HIP(ctx, hipMemcpyAsync(h_off, row_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
