@@ -2382,37 +2382,16 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   // (tsum: per-tile match counts, written by the main pass and topped up by the listed and slow passes)
   int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff.as<uint64_t>());
   if (rc) return rc;
-  // Batches up to 4M topics are assembled before the host has seen the total:
-  // a row outside the slow path holds <= FAST_MC ids, so n * FAST_MC bounds
-  // the output, and the call needs one host round trip instead of two.  A
-  // call with slow-path rows discards this assembly and goes on below.
-  const bool spec = n <= (uint64_t(1) << 22);
-  PoolBuf ids_spec;
-  if (spec) {
-    ids_spec = PoolBuf(ctx->pool, n * FAST_MC * 4 + 16);
-    if (!ids_spec.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
-    hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt.as<uint32_t>(), n, toff.as<uint64_t>(),
-                       stage.as<uint32_t>(), row_off.as<uint64_t>(), ids_spec.as<uint32_t>(), idx->view.gmap);
-    GM_HIP(ctx, hipGetLastError());
-  }
   uint64_t h_ctr[4] = {0, 0, 0, 0};
   uint64_t nnz = 0;
   GM_HIP(ctx, hipMemcpyAsync(h_ctr, ctrs.p, 32, hipMemcpyDeviceToHost, st));
   GM_HIP(ctx, hipMemcpyAsync(&nnz, toff.as<uint64_t>() + n_tiles, 8, hipMemcpyDeviceToHost, st));
-  GM_HIP(ctx, hipEventRecord(ctx->ev[3], st));
-  GM_HIP(ctx, hipEventSynchronize(ctx->ev[3]));
+  GM_HIP(ctx, hipStreamSynchronize(st));
   const uint64_t n_listed = uint32_t(h_ctr[0]);
   const uint64_t n_ovf = uint32_t(h_ctr[0] >> 32);
   ctx->stats.probes = h_ctr[2];
   ctx->stats.n_wildcard_topics = h_ctr[3];
   ctx->stats.n_overflow = n_listed;
-  if (spec && !n_ovf) {
-    ctx->stats.nnz = nnz;
-    ctx->stats.match_kernel_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
-    ctx->stats.total_device_ms = ev_ms(ctx->ev[0], ctx->ev[3]);
-    return finish_csr(ctx, n, nnz, row_off, ids_spec, dev_io, out);
-  }
-  ids_spec.reset();
 
   // ---- slow path for rows the listed pass could not hold
   PoolBuf slow_off, slow_ids;
