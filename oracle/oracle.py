@@ -82,6 +82,14 @@ def lib():
             "orc_gen_filter_codes": (None, [u64, u64, C.c_int, vp]),
             "orc_gen_topic_codes": (None, [u64, u64, u64, vp, u64, vp]),
             "orc_render_codes": (u64, [vp, u64, vp, vp]),
+            "orc_nfa_new": (vp, [vp, vp, u64]),
+            "orc_nfa_free": (None, [vp]),
+            "orc_nfa_match": (vp, [vp, vp, vp, u64, C.c_int, C.c_int]),
+            "orc_nfa_rows_n": (u64, [vp]),
+            "orc_nfa_rows_nnz": (u64, [vp]),
+            "orc_nfa_rows_off": (vp, [vp]),
+            "orc_nfa_rows_ids": (vp, [vp]),
+            "orc_nfa_rows_free": (None, [vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -270,6 +278,38 @@ class Router:
         nf = len(fo) - 1
         return _csr(lib().orc_match_batch(self.h, mode, _ptr(tb), _ptr(to), n, _ptr(fb), _ptr(fo), nf,
                                           nthreads, int(want_ids)))
+
+
+class CpuNfa:
+    """The optimized CPU hash-NFA (cpu_nfa.cpp): emqx_router:match_routes/1
+    rows over flat hash tables, multi-threaded.  The second CPU figure of the
+    bench's cpu_baseline leg; checked against the faithful restatement."""
+
+    def __init__(self, filters):
+        fb, fo = filters if isinstance(filters, tuple) else pack(filters)
+        fb = np.ascontiguousarray(fb, np.uint8)
+        fo = np.ascontiguousarray(fo, np.uint64)
+        self.h = lib().orc_nfa_new(_ptr(fb), _ptr(fo), len(fo) - 1)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_nfa_free(self.h)
+            self.h = None
+
+    def match_batch(self, topics, nthreads: int = 1, want_ids: bool = True):
+        """(row_off, ids) with ids = rank among the sorted unique filters;
+        want_ids=False: row lengths only (ids empty)."""
+        tb, to = topics if isinstance(topics, tuple) else pack(topics)
+        tb = np.ascontiguousarray(tb, np.uint8)
+        to = np.ascontiguousarray(to, np.uint64)
+        L = lib()
+        h = L.orc_nfa_match(self.h, _ptr(tb), _ptr(to), len(to) - 1, nthreads, int(want_ids))
+        rows, nnz = L.orc_nfa_rows_n(h), L.orc_nfa_rows_nnz(h)
+        ro = np.ctypeslib.as_array(C.cast(L.orc_nfa_rows_off(h), C.POINTER(C.c_uint64)), shape=(rows + 1,)).copy()
+        ids = (np.ctypeslib.as_array(C.cast(L.orc_nfa_rows_ids(h), C.POINTER(C.c_uint32)), shape=(nnz,)).copy()
+               if nnz else np.zeros(0, np.uint32))
+        L.orc_nfa_rows_free(h)
+        return ro, ids
 
 
 class Ranker:

@@ -87,3 +87,35 @@ def test_workload_generator_shapes(orc):
     # counter-based: any window regenerates identically
     tc2 = orc.gen_topic_codes(7, 500, 10, codes)
     assert np.array_equal(tc[500:510], tc2)
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_cpu_nfa_equals_faithful_restatement(orc, seed):
+    """The optimized CPU hash-NFA (oracle/cpu_nfa.cpp, the cpu_baseline leg's
+    second figure) returns the faithful restatement's match_routes rows on the
+    PropEr-shaped sets ('$' topics, empty levels, wildcard topics)."""
+    rng = random.Random(1000 + seed)
+    filters = sorted({rand_filter(rng).encode() for _ in range(rng.randint(1, 60))})
+    topics = [rand_topic(rng).encode() for _ in range(200)] + [b"", b"/", b"#", b"+", b"$SYS", b"a//b"]
+    r = orc.Router(True)
+    for f in filters:
+        r.add_route(f)
+    ro, ids, _ = r.match_batch(topics, filters, mode=1)
+    nfa = orc.CpuNfa(filters)
+    nro, nids = nfa.match_batch(topics, nthreads=3)
+    assert np.array_equal(ro, nro) and np.array_equal(ids, nids), seed
+    cro, cids = nfa.match_batch(topics, nthreads=2, want_ids=False)
+    assert np.array_equal(cro, ro) and len(cids) == 0
+
+
+@pytest.mark.parametrize("wild_only,nf", [(False, 10_000), (True, 50_000)], ids=["C1-mix", "C2-wildcard"])
+def test_cpu_nfa_on_workload_configs(orc, wild_only, nf):
+    codes = orc.gen_filter_codes(1, nf, wildcard_only=wild_only)
+    fb, fo = orc.render_codes(codes)
+    tb, to = orc.render_codes(orc.gen_topic_codes(1, 0, 20_000, codes))
+    r = orc.Router(True)
+    r.add_routes((fb, fo))
+    filters = sorted(set(orc.unpack(fb, fo)))
+    ro, ids, _ = r.match_batch((tb, to), filters, mode=1, nthreads=4)
+    nro, nids = orc.CpuNfa((fb, fo)).match_batch((tb, to), nthreads=4)
+    assert np.array_equal(ro, nro) and np.array_equal(ids, nids)
