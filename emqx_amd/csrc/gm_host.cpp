@@ -342,13 +342,18 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
     tot.match_kernel_ms += cs.match_kernel_ms;
     tot.total_device_ms += cs.total_device_ms;
     s.nnz = s.csr.nnz;
-    if (launch_off64_to_32(ctx->stream, s.csr.row_off, s.nc + 1, s.d_r32.as<uint32_t>()) ||
+    // row offsets cross PCIe as u32 unless the chunk's rows hold 2^32 ids or more
+    // (slow-path rows of thousands of filters): then as they are, u64
+    const bool wide = s.nnz > 0xFFFFFFFFull || env_u64("GM_HOST_WIDE_ROWS", 0) != 0;  // (tests force it)
+    if ((!wide && launch_off64_to_32(ctx->stream, s.csr.row_off, s.nc + 1, s.d_r32.as<uint32_t>())) ||
         hipEventRecord(s.comp, ctx->stream) != hipSuccess)
       return fail(EMQX_GM_EDEVICE, "match: row offsets");
     // rows back to pinned memory on the d2h stream
-    if (!s.out_i.reserve(s.nnz * 4 + 4)) return fail(EMQX_GM_ENOMEM, "match: pinned rows");
+    if (!s.out_i.reserve(s.nnz * 4 + 4) || !s.out_o.reserve((s.nc + 1) * (wide ? 8 : 4)))
+      return fail(EMQX_GM_ENOMEM, "match: pinned rows");
     if (hipStreamWaitEvent(hp->d2h, s.comp, 0) != hipSuccess ||
-        hipMemcpyAsync(s.out_o.p, s.d_r32.p, (s.nc + 1) * 4, hipMemcpyDeviceToHost, hp->d2h) != hipSuccess ||
+        hipMemcpyAsync(s.out_o.p, wide ? static_cast<void*>(s.csr.row_off) : s.d_r32.p, (s.nc + 1) * (wide ? 8 : 4),
+                       hipMemcpyDeviceToHost, hp->d2h) != hipSuccess ||
         (s.nnz && hipMemcpyAsync(s.out_i.p, s.csr.ids, s.nnz * 4, hipMemcpyDeviceToHost, hp->d2h) != hipSuccess) ||
         hipEventRecord(s.d2h, hp->d2h) != hipSuccess)
       return fail(EMQX_GM_EDEVICE, "match: rows to host");
@@ -373,6 +378,7 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
     {
       const uint64_t parts = s.nc < 65536 ? 1 : T;
       const uint32_t* ro = s.out_o.as<uint32_t>();
+      const uint64_t* ro64 = s.out_o.as<uint64_t>();
       const uint32_t* ri = s.out_i.as<uint32_t>();
       const hipEvent_t ev = s.d2h;
       const uint64_t sc0 = s.c0, snc = s.nc, sbase = base;
@@ -381,8 +387,9 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
         const uint64_t a = snc * p / parts, e = snc * (p + 1) / parts;
         s.out_f.push_back(W.submit([=] {
           hipEventSynchronize(ev);
-          for (uint64_t j = a; j < e; ++j) r_off[sc0 + j] = sbase + ro[j];
-          if (e > a) std::memcpy(dst_ids + sbase + ro[a], ri + ro[a], uint64_t(ro[e] - ro[a]) * 4);
+          auto row = [&](uint64_t j) -> uint64_t { return wide ? ro64[j] : uint64_t(ro[j]); };
+          for (uint64_t j = a; j < e; ++j) r_off[sc0 + j] = sbase + row(j);
+          if (e > a) std::memcpy(dst_ids + sbase + row(a), ri + row(a), (row(e) - row(a)) * 4);
         }));
       }
     }

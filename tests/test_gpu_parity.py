@@ -484,13 +484,15 @@ def test_fanout_split_two_ranks():
 
 
 # ------------------------------------------------------------------ host-buffer path (gm_host.cpp)
-@pytest.mark.parametrize("chunk", ["1024", "5000", "4194304"])
-def test_host_path_chunks_equal_device_path(ctx, orc, monkeypatch, chunk):
+@pytest.mark.parametrize("chunk,wide", [("1024", "0"), ("5000", "0"), ("4194304", "0"), ("5000", "1")])
+def test_host_path_chunks_equal_device_path(ctx, orc, monkeypatch, chunk, wide):
     """emqx_gm_match on host buffers -- chunked (GM_HOST_CHUNK topics), staged
     through pinned memory with u32 chunk-relative offsets, three chunks in
     flight -- gives the rows of one DEVICE_IO call over the same batch, which
     a strided sample ties to the oracle.  Small chunks put many chunk
-    boundaries (and partial last chunks) in one call."""
+    boundaries (and partial last chunks) in one call.  wide: the row offsets
+    return as u64 (the form a chunk of 2^32 ids or more takes)."""
+    monkeypatch.setenv("GM_HOST_WIDE_ROWS", wide)
     from emqx_amd.engine import gen_filter_codes, render_codes
     codes = gen_filter_codes(7, 20_000)
     fb, fo = render_codes(codes)
