@@ -1248,7 +1248,7 @@ struct WordsFromRegs {
 
 constexpr size_t FUSED_LDS = sizeof(CoopLds) * 4 > (TOK_STAGE + 8) ? sizeof(CoopLds) * 4 : (TOK_STAGE + 8);
 
-template <int G, bool EXACT, bool NT>
+template <int G, bool EXACT, bool NT, bool TOKPRIO>
 __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restrict__ tb,
                                                         const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
                                                         uint32_t* __restrict__ cnt, uint32_t* __restrict__ stage,
@@ -1259,6 +1259,13 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
   __shared__ __align__(16) uint8_t s_raw[FUSED_LDS];  // the staged text, then the walk's lists
   uint64_t* const s_txt = reinterpret_cast<uint64_t*>(s_raw);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // TOKPRIO: staging and tokenizing at wave priority 1, the walk at 0.  A block
+  // holds its 20 KB of LDS (one of the CU's 8 block slots) through both phases
+  // but only the walk keeps lines in flight, so the SIMD's issue arbiter favours
+  // the waves that are still getting their block to the walk (C2 9.20 -> 9.10
+  // ms, C3 13.68 -> 13.54; raising late walk levels instead was slower:
+  // profiles/r02_ab/prio*_c*.txt)
+  if constexpr (TOKPRIO) __builtin_amdgcn_s_setprio(1);
   const uint64_t t0 = uint64_t(blockIdx.x) * 256u;
   const uint64_t t = t0 + threadIdx.x;
   const uint64_t tl = t0 + 256 < n ? t0 + 256 : n;
@@ -1284,6 +1291,7 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
     }
   }
   __syncthreads();  // every lane is done with the staged text: the walk reuses the LDS
+  if constexpr (TOKPRIO) __builtin_amdgcn_s_setprio(0);
   if ((t >> 6) * 64 >= n) return;  // wave-uniform, after the last workgroup barrier
   WordsFromRegs words{w};
   coop_walk_tile<EXACT, NT>(reinterpret_cast<CoopLds*>(s_raw)[wv], h, words, valid, t, lane, tb, toff, ix, cnt, stage,
@@ -2257,12 +2265,19 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
   for (int i = 0; K > 1 && i <= K; ++i)
     if (!ctx->ov_ev[i] && hipEventCreateWithFlags(&ctx->ov_ev[i], hipEventDisableTiming) != hipSuccess) K = 1;
   if (main_kind() == MAIN_FUSED) {
-    if (nt_streams())
-      hipLaunchKernelGGL((k_match_fused<3, EXACT, true>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, list1,
-                         n1, probe_tile, wild_ctr, tsum);
-    else
-      hipLaunchKernelGGL((k_match_fused<3, EXACT, false>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage,
-                         list1, n1, probe_tile, wild_ctr, tsum);
+    const char* pe = getenv("GM_FUSED_PRIO");  // A/B knob (read per call): 0 = every phase at priority 0
+    const bool tp = !pe || atoi(pe) != 0;
+#define GM_FUSED(NT, P)                                                                                            \
+  hipLaunchKernelGGL((k_match_fused<3, EXACT, NT, P>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, list1, \
+                     n1, probe_tile, wild_ctr, tsum)
+    if (nt_streams()) {
+      if (tp) GM_FUSED(true, true);
+      else GM_FUSED(true, false);
+    } else {
+      if (tp) GM_FUSED(false, true);
+      else GM_FUSED(false, false);
+    }
+#undef GM_FUSED
   } else if (K == 1) {
     launch_tokenize(st, nblk, tb, to, n, v, hdr, wids, 0);
     GM_WALK(st, nblk, 0ull);

@@ -660,3 +660,31 @@ def test_concurrent_calls_one_context(ctx, orc):
     assert sorted(done) == list(range(8))
     idx.release()
     plain.release()
+
+
+def test_fused_priority_knob_same_rows(ctx, orc, monkeypatch):
+    """GM_FUSED_PRIO=0 (every phase at wave priority 0) and the default
+    (staging + tokenizer at priority 1) give the same rows, which equal the oracle."""
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    codes = gen_filter_codes(6, 30_000, wildcard_only=True)
+    fb, fo = render_codes(codes)
+    filters = sorted(set(orc.unpack(fb, fo)))
+    idx = ctx.build_index(filters)
+    n = 100_000
+    db, do, tot = ctx.gen_topics_device(codes, 6, 0, n)
+    rows = []
+    for prio in ("0", "1"):
+        monkeypatch.setenv("GM_FUSED_PRIO", prio)
+        res = ctx.match_device(idx, db, do, n, exact=True)
+        rows.append(res.to_host())
+        res.free()
+    assert np.array_equal(rows[0][0], rows[1][0]) and np.array_equal(rows[0][1], rows[1][1])
+    tb, to = orc.render_codes(orc.gen_topic_codes(6, 0, n, codes))
+    r = orc.Router(True)
+    for f in filters:
+        r.add_route(f)
+    oro, oids, _ = r.match_batch((tb, to), filters, mode=1, nthreads=8)
+    assert np.array_equal(rows[1][0], oro) and np.array_equal(rows[1][1], oids)
+    ctx.dev_free(db)
+    ctx.dev_free(do)
+    idx.release()
