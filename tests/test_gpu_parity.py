@@ -688,3 +688,20 @@ def test_fused_priority_knob_same_rows(ctx, orc, monkeypatch):
     ctx.dev_free(db)
     ctx.dev_free(do)
     idx.release()
+
+
+def test_config_c1_fixture(ctx, orc):
+    """The committed C1 fixture (tests/golden/config_c1.json: 2,000 topics over
+    the 1M-topic stream, rows as filter strings) against the full C1 index."""
+    import json
+    import os
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "config_c1.json")) as f:
+        fx = json.load(f)
+    codes = gen_filter_codes(fx["seed"], fx["filters"], wildcard_only=fx["wildcard_only"])
+    filters = sorted(set(orc.unpack(*render_codes(codes))))
+    idx = ctx.build_index(filters)
+    ro, ids = ctx.match(idx, [t.encode() for t in fx["topics"]], exact=True)
+    got = [[filters[k].decode() for k in ids[ro[i]:ro[i + 1]]] for i in range(len(fx["topics"]))]
+    assert got == fx["matches"]
+    idx.release()

@@ -8,6 +8,7 @@
   ids in range).
 * C3: a 10M-filter mixed index on one GPU, one 100M-topic match, a 256k-topic
   strided sample row for row.
+* C2 and C3 also match the committed fixtures (tests/golden/config_c2/c3.json).
 * C5: 8 shard indexes built one after another on one device, each matching the
   same batch, their rows merged on the device by global id (emqx_gm_merge_rows
   with 8 pieces) == the unsharded index's rows, and a window == the oracle.
@@ -80,6 +81,21 @@ def _check_windows(orc, res, router, ranker, codes, seed, n, width, count):
     return checked
 
 
+def _fixture_rows(ctx, idx, spack, name):
+    """The committed config fixture (tests/golden/config_<name>.json: 2,000
+    topics strided over the whole stream, rows as filter strings) matched
+    through the host-buffer call against this full index."""
+    import json
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"config_{name}.json")) as f:
+        fx = json.load(f)
+    sb, so = spack
+    ro, ids = ctx.match(idx, [t.encode() for t in fx["topics"]], exact=True)
+    got = [[bytes(sb[int(so[k]):int(so[k + 1])]).decode() for k in ids[ro[i]:ro[i + 1]]]
+           for i in range(len(fx["topics"]))]
+    assert got == fx["matches"], name
+    return len(got)
+
+
 def _global_properties(res, n, n_filters):
     ro = np.zeros(n + 1, np.uint64)
     res.ctx.memcpy_d2h(ro, ctypes.cast(res.csr.row_off, ctypes.c_void_p).value, (n + 1) * 8)
@@ -123,6 +139,7 @@ def test_c2_full_index_full_batch(ctx, orc):
     checked = _check_windows(orc, res, box["r"], box["rank"], codes, seed, n, 100_000, 20)
     assert checked == 2_000_000
     res.free()
+    assert _fixture_rows(ctx, idx, _sorted_unique(*fpack), "c2") == 2000
     idx.release()
 
 
@@ -148,6 +165,7 @@ def test_c3_10m_index_sample(ctx, orc):
     checked = _check_windows(orc, res, box["r"], box["rank"], codes, seed, n, 32_000, 8)
     assert checked == 256_000
     res.free()
+    assert _fixture_rows(ctx, idx, _sorted_unique(*fpack), "c3") == 2000
     idx.release()
 
 
