@@ -192,6 +192,7 @@ int emqx_gm_close(emqx_gm_ctx* ctx) {
     }
     for (auto& e : ctx->ov_ev)
       if (e) hipEventDestroy(e);
+    if (ctx->pin) hipHostFree(ctx->pin);
   }
   delete ctx;
   return EMQX_GM_OK;

@@ -106,6 +106,8 @@ struct emqx_gm_ctx {
   gm::HostPool* hpool = nullptr;
   emqx_gm_match_stats stats{};
   hipEvent_t ev[6]{};
+  void* pin = nullptr;  // pinned host words for a call's small read-backs (calls are serialized by mu)
+  double ids_per_topic = 4.0;  // speculative ids capacity of a match call (run_match), from recent calls
 };
 
 namespace gm {

@@ -469,7 +469,9 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
   wave_excl_scan(probes, ptot);
   wave_excl_scan(wilds, wtot);
   if (lane == 0) {
-    if (LISTED) atomicAdd(probe_ctr, (unsigned long long)ptot);  // few waves
+    if (LISTED) {
+      if (ptot) atomicAdd(probe_ctr, (unsigned long long)ptot);  // (an idle listed grid adds nothing: 2,048
+    }                                                             //  same-address atomics cost ~20 us)
     else if (((uint64_t(blockIdx.x) * 256u + tid) >> 6) * 64 < n)
       probe_ctr[(uint64_t(blockIdx.x) * 256u + tid) >> 6] = ptot;  // per-tile slot, see k_match_reg
     if (wtot) atomicAdd(wild_ctr, (unsigned long long)wtot);
@@ -1447,11 +1449,13 @@ __device__ __forceinline__ void assemble_tile(const uint32_t* __restrict__ stage
 // output) written through LDS as coalesced 256-B rows.  A tile holding a
 // slow-path row (its ids land later, k_copy_slow) stores lane by lane so
 // that row's range is left alone.
+// cap: the ids buffer's capacity; a tile whose rows would pass it writes no
+// ids (the host, seeing a total past cap, assembles again into a larger buffer).
 __global__ __launch_bounds__(256) void k_assemble(const uint32_t* __restrict__ cnt, uint64_t n,
                                                   const uint64_t* __restrict__ tile_off,
                                                   const uint32_t* __restrict__ stage,
                                                   uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids,
-                                                  const uint32_t* __restrict__ gmap) {
+                                                  const uint32_t* __restrict__ gmap, uint64_t cap) {
   __shared__ uint32_t s_out[4][64 * FAST_MC];
   const int lane = threadIdx.x & 63;
   uint32_t* const out = s_out[threadIdx.x >> 6];
@@ -1468,6 +1472,7 @@ __global__ __launch_bounds__(256) void k_assemble(const uint32_t* __restrict__ c
   if (t == n - 1) row_off[n] = base + call;
   const bool any_slow = __ballot(slow) != 0;
   const uint64_t tb0 = tile_off[tile];
+  if (tb0 + tall > cap) return;  // wave-uniform
 #define GM_ASM(W) assemble_tile<W>(stage, tile, lane, cf, any_slow, base, pa, tall, out, ids, tb0, gmap)
   if (__ballot(cf > 8))
     GM_ASM(FAST_MC);
@@ -2359,11 +2364,17 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   PoolBuf cnt(ctx->pool, n * 4 + 16);
   PoolBuf stage(ctx->pool, n_tiles * 64ull * FAST_MC * 4);
   PoolBuf list1(ctx->pool, n * 4 + 16), list2(ctx->pool, n * 4 + 16);
-  PoolBuf ctrs(ctx->pool, 64);
   PoolBuf tsum(ctx->pool, n_tiles * 8 + 8);
-  PoolBuf toff(ctx->pool, (n_tiles + 1) * 8);
-  if (!cnt.p || !stage.p || !list1.p || !list2.p || !ctrs.p || !tsum.p || !toff.p)
+  // tile offsets [n_tiles + 1] and, right behind the total, the pass counters:
+  // one read-back brings the match total and the counters together
+  PoolBuf toff(ctx->pool, (n_tiles + 1) * 8 + 64);
+  if (!cnt.p || !stage.p || !list1.p || !list2.p || !tsum.p || !toff.p)
     return set_err(ctx, EMQX_GM_ENOMEM, "match: workspace");
+  if (!ctx->pin && hipHostMalloc(&ctx->pin, 256, hipHostMallocDefault) != hipSuccess) {
+    ctx->pin = nullptr;
+    return set_err(ctx, EMQX_GM_ENOMEM, "match: pinned read-back words");
+  }
+  uint8_t* const ctrs_p = toff.as<uint8_t>() + (n_tiles + 1) * 8;
   PoolBuf probe_tile(ctx->pool, n_tiles * 8 + 8);
   if (!probe_tile.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: probe workspace");
   PoolBuf hdr, wids;  // split forms: per-topic header and word ids [level][topic] (the fused kernel keeps them in registers)
@@ -2374,11 +2385,11 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   }
   // counters: u32 n1 @0 (main-pass overflow), u32 n2 @4 (listed-pass
   // overflow), u64 probes @16, u64 wildcard topics @24
-  uint32_t* n1 = ctrs.as<uint32_t>();
+  uint32_t* n1 = reinterpret_cast<uint32_t*>(ctrs_p);
   uint32_t* n2 = n1 + 1;
-  unsigned long long* probe_ctr = reinterpret_cast<unsigned long long*>(ctrs.as<uint8_t>() + 16);
-  unsigned long long* wild_ctr = reinterpret_cast<unsigned long long*>(ctrs.as<uint8_t>() + 24);
-  GM_HIP(ctx, hipMemsetAsync(ctrs.p, 0, 64, st));
+  unsigned long long* probe_ctr = reinterpret_cast<unsigned long long*>(ctrs_p + 16);
+  unsigned long long* wild_ctr = reinterpret_cast<unsigned long long*>(ctrs_p + 24);
+  GM_HIP(ctx, hipMemsetAsync(ctrs_p, 0, 64, st));
 
   GM_HIP(ctx, hipEventRecord(ctx->ev[0], st));
   GM_HIP(ctx, hipEventRecord(ctx->ev[1], st));
@@ -2397,11 +2408,37 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   // (tsum: per-tile match counts, written by the main pass and topped up by the listed and slow passes)
   int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff.as<uint64_t>());
   if (rc) return rc;
-  uint64_t h_ctr[4] = {0, 0, 0, 0};
-  uint64_t nnz = 0;
-  GM_HIP(ctx, hipMemcpyAsync(h_ctr, ctrs.p, 32, hipMemcpyDeviceToHost, st));
-  GM_HIP(ctx, hipMemcpyAsync(&nnz, toff.as<uint64_t>() + n_tiles, 8, hipMemcpyDeviceToHost, st));
+  // Speculative assembly: the rows are written before the host has read the
+  // match total, into an ids buffer sized from this context's recent matches
+  // per topic (x1.25), so a call makes ONE host round trip.  The total, the
+  // pass counters and the assembly come back together; a batch with a listed-
+  // pass overflow (slow-path rows) or more matches than the buffer holds is
+  // assembled again below, once the host knows the total.
+  // (at most FAST_MC per topic: a longer row is a slow-path row, assembled again anyway)
+  const uint64_t cap_spec = 1024 + uint64_t(double(n) * std::min(ctx->ids_per_topic, double(FAST_MC)));
+  PoolBuf ids(ctx->pool, cap_spec * 4 + 16);
+  if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
+  hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt.as<uint32_t>(), n, toff.as<uint64_t>(),
+                     stage.as<uint32_t>(), row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec);
+  GM_HIP(ctx, hipGetLastError());
+  uint64_t* const pin = static_cast<uint64_t*>(ctx->pin);  // [0] match total, [1..4] the counters
+  GM_HIP(ctx, hipMemcpyAsync(pin, toff.as<uint64_t>() + n_tiles, 40, hipMemcpyDeviceToHost, st));
+  GM_HIP(ctx, hipEventRecord(ctx->ev[3], st));
   GM_HIP(ctx, hipStreamSynchronize(st));
+  uint64_t nnz = pin[0];
+  const uint64_t h_ctr[4] = {pin[1], pin[2], pin[3], pin[4]};
+  if (uint32_t(h_ctr[0] >> 32) == 0 && nnz <= cap_spec) {  // no slow-path row, and the rows fit: done
+    ctx->stats.probes = h_ctr[2];
+    ctx->stats.n_wildcard_topics = h_ctr[3];
+    ctx->stats.n_overflow = uint32_t(h_ctr[0]);
+    ctx->ids_per_topic = std::max(1.0, 1.25 * double(nnz) / double(n));
+    ctx->stats.nnz = nnz;
+    ctx->stats.match_kernel_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
+    ctx->stats.total_device_ms = ev_ms(ctx->ev[0], ctx->ev[3]);
+    return finish_csr(ctx, n, nnz, row_off, ids, dev_io, out);
+  }
+  ids.reset();
+  if (nnz > cap_spec) ctx->ids_per_topic = std::max(ctx->ids_per_topic, 1.25 * double(nnz) / double(n));
   const uint64_t n_listed = uint32_t(h_ctr[0]);
   const uint64_t n_ovf = uint32_t(h_ctr[0] >> 32);
   ctx->stats.probes = h_ctr[2];
@@ -2465,11 +2502,11 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
     GM_HIP(ctx, hipStreamSynchronize(st));
   }
 
-  // ---- write the rows
-  PoolBuf ids(ctx->pool, nnz * 4 + 16);
+  // ---- write the rows (again: the speculative pass above did not fit or missed slow-path rows)
+  ids = PoolBuf(ctx->pool, nnz * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
   hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt.as<uint32_t>(), n, toff.as<uint64_t>(),
-                     stage.as<uint32_t>(), row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap);
+                     stage.as<uint32_t>(), row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, nnz);
   GM_HIP(ctx, hipGetLastError());
   if (n_ovf) {
     hipLaunchKernelGGL(k_copy_slow, dim3(n_ovf), dim3(256), 0, st, ovf_list, n_ovf, row_off.as<uint64_t>(),

@@ -705,3 +705,25 @@ def test_config_c1_fixture(ctx, orc):
     got = [[filters[k].decode() for k in ids[ro[i]:ro[i + 1]]] for i in range(len(fx["topics"]))]
     assert got == fx["matches"]
     idx.release()
+
+
+def test_speculative_ids_capacity_redo(ctx, orc):
+    """run_match writes the rows before the host reads the match total, into an
+    ids buffer sized from the context's recent matches per topic.  A batch
+    after a match-free one (capacity ~1 id per topic) with ~8 matches per topic
+    overflows it and is assembled again; both calls equal the oracle, and so
+    does a third call (capacity grown)."""
+    filters = sorted({b"a/#", b"a/+/#", b"+/b/#", b"a/b/#", b"+/+/#", b"a/+/c", b"+/b/c", b"a/b/c", b"#"})
+    idx = ctx.build_index(filters)
+    n = 100_000
+    none = [b"$x/%d" % i for i in range(n)]   # '$' topics: no root '#' or '+', nothing else matches
+    many = [b"a/b/c" if i % 3 else b"a/b/c/%d" % i for i in range(n)]
+    r = orc.Router(True)
+    for f in filters:
+        r.add_route(f)
+    for topics in (none, many, many):
+        ro, ids = ctx.match(idx, topics, exact=True)
+        oro, oids, _ = r.match_batch(topics, filters, mode=1, nthreads=8)
+        assert np.array_equal(ro, oro) and np.array_equal(ids, oids)
+    assert int(oro[-1]) > 7 * n
+    idx.release()
