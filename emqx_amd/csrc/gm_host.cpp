@@ -385,12 +385,16 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
       uint32_t* dst_ids = r_ids;
       for (uint64_t p = 0; p < parts; ++p) {
         const uint64_t a = snc * p / parts, e = snc * (p + 1) / parts;
-        s.out_f.push_back(W.submit([=] {
+        auto unpack = [=] {
           hipEventSynchronize(ev);
           auto row = [&](uint64_t j) -> uint64_t { return wide ? ro64[j] : uint64_t(ro[j]); };
           for (uint64_t j = a; j < e; ++j) r_off[sc0 + j] = sbase + row(j);
           if (e > a) std::memcpy(dst_ids + sbase + row(a), ri + row(a), (row(e) - row(a)) * 4);
-        }));
+        };
+        // a call of one small chunk unpacks on the calling thread (no hand-off to a
+        // worker: nothing else is in flight to overlap with)
+        if (m == 1 && parts == 1) unpack();
+        else s.out_f.push_back(W.submit(unpack));
       }
     }
     base += s.nnz;
