@@ -332,7 +332,22 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
         launch_off32_to_64(ctx->stream, s.d_o32.as<uint32_t>(), s.nc + 1, s.d_o64.as<uint64_t>()))
       return fail(EMQX_GM_EDEVICE, "match: offsets to device");
     s.csr = emqx_gm_csr{};
-    rc = run_match(ctx, idx, s.d_b.as<uint8_t>(), s.d_o64.as<uint64_t>(), s.nc, flags | EMQX_GM_DEVICE_IO, &s.csr);
+    // a one-chunk call queues the rows' copy-out behind the speculative assembly,
+    // inside run_match's one host round trip (no second round trip for the rows)
+    MatchTail tail;
+    const bool one = m == 1 && env_u64("GM_HOST_WIDE_ROWS", 0) == 0;
+    if (one)
+      tail.enqueue = [&](const uint64_t* d_ro, const uint32_t* d_ids, uint64_t cap) -> int {
+        if (!s.out_i.reserve(cap * 4 + 4)) return set_err(ctx, EMQX_GM_ENOMEM, "match: pinned rows");
+        if (launch_off64_to_32(ctx->stream, d_ro, s.nc + 1, s.d_r32.as<uint32_t>()) ||
+            hipMemcpyAsync(s.out_o.p, s.d_r32.p, (s.nc + 1) * 4, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            (cap && hipMemcpyAsync(s.out_i.p, d_ids, cap * 4, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) ||
+            hipEventRecord(s.d2h, ctx->stream) != hipSuccess)
+          return set_err(ctx, EMQX_GM_EDEVICE, "match: rows to host");
+        return 0;
+      };
+    rc = run_match(ctx, idx, s.d_b.as<uint8_t>(), s.d_o64.as<uint64_t>(), s.nc, flags | EMQX_GM_DEVICE_IO, &s.csr,
+                   one ? &tail : nullptr);
     if (rc) return fail(rc, nullptr);
     const emqx_gm_match_stats& cs = ctx->stats;
     tot.nnz += cs.nnz;
@@ -345,18 +360,20 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
     // row offsets cross PCIe as u32 unless the chunk's rows hold 2^32 ids or more
     // (slow-path rows of thousands of filters): then as they are, u64
     const bool wide = s.nnz > 0xFFFFFFFFull || env_u64("GM_HOST_WIDE_ROWS", 0) != 0;  // (tests force it)
-    if ((!wide && launch_off64_to_32(ctx->stream, s.csr.row_off, s.nc + 1, s.d_r32.as<uint32_t>())) ||
-        hipEventRecord(s.comp, ctx->stream) != hipSuccess)
-      return fail(EMQX_GM_EDEVICE, "match: row offsets");
-    // rows back to pinned memory on the d2h stream
-    if (!s.out_i.reserve(s.nnz * 4 + 4) || !s.out_o.reserve((s.nc + 1) * (wide ? 8 : 4)))
-      return fail(EMQX_GM_ENOMEM, "match: pinned rows");
-    if (hipStreamWaitEvent(hp->d2h, s.comp, 0) != hipSuccess ||
-        hipMemcpyAsync(s.out_o.p, wide ? static_cast<void*>(s.csr.row_off) : s.d_r32.p, (s.nc + 1) * (wide ? 8 : 4),
-                       hipMemcpyDeviceToHost, hp->d2h) != hipSuccess ||
-        (s.nnz && hipMemcpyAsync(s.out_i.p, s.csr.ids, s.nnz * 4, hipMemcpyDeviceToHost, hp->d2h) != hipSuccess) ||
-        hipEventRecord(s.d2h, hp->d2h) != hipSuccess)
-      return fail(EMQX_GM_EDEVICE, "match: rows to host");
+    if (!tail.used) {  // the rows are still on the device
+      if ((!wide && launch_off64_to_32(ctx->stream, s.csr.row_off, s.nc + 1, s.d_r32.as<uint32_t>())) ||
+          hipEventRecord(s.comp, ctx->stream) != hipSuccess)
+        return fail(EMQX_GM_EDEVICE, "match: row offsets");
+      // rows back to pinned memory on the d2h stream
+      if (!s.out_i.reserve(s.nnz * 4 + 4) || !s.out_o.reserve((s.nc + 1) * (wide ? 8 : 4)))
+        return fail(EMQX_GM_ENOMEM, "match: pinned rows");
+      if (hipStreamWaitEvent(hp->d2h, s.comp, 0) != hipSuccess ||
+          hipMemcpyAsync(s.out_o.p, wide ? static_cast<void*>(s.csr.row_off) : s.d_r32.p, (s.nc + 1) * (wide ? 8 : 4),
+                         hipMemcpyDeviceToHost, hp->d2h) != hipSuccess ||
+          (s.nnz && hipMemcpyAsync(s.out_i.p, s.csr.ids, s.nnz * 4, hipMemcpyDeviceToHost, hp->d2h) != hipSuccess) ||
+          hipEventRecord(s.d2h, hp->d2h) != hipSuccess)
+        return fail(EMQX_GM_EDEVICE, "match: rows to host");
+    }
     // the previous chunk's device rows are in pinned memory once its d2h event fires
     if (prev >= 0) {
       Slot& p = hp->slot[prev];

@@ -9,6 +9,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/emqx_gpu_match.h"
@@ -160,8 +161,17 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
 void sort_filters(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t* fo);
 void free_index(emqx_gm_index* idx);
 // gm_match.hip
+// A caller's work queued on the context stream right behind the speculative
+// assembly of a DEVICE_IO match, before run_match's one host round trip (the
+// host path queues the rows' copy-out there).  enqueue(row_off, ids, cap) gets
+// the device rows and the ids capacity; `used` says whether those rows are the
+// call's result (no reassembly happened).
+struct MatchTail {
+  std::function<int(const uint64_t* row_off, const uint32_t* ids, uint64_t cap)> enqueue;
+  bool used = false;
+};
 int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
-              uint32_t flags, emqx_gm_csr* out);
+              uint32_t flags, emqx_gm_csr* out, MatchTail* tail = nullptr);
 int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
                emqx_gm_csr* out, uint32_t part = 0, uint32_t n_parts = 1, uint64_t* first_out = nullptr);
 int run_merge_rows(emqx_gm_ctx* ctx, uint64_t n_rows, uint64_t stride, uint32_t n_pieces, const uint32_t* d_lens,

@@ -2368,7 +2368,7 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
 }  // namespace
 
 int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, const uint64_t* to_in, uint64_t n,
-              uint32_t flags, emqx_gm_csr* out) {
+              uint32_t flags, emqx_gm_csr* out, MatchTail* tail) {
   const bool dev_io = flags & EMQX_GM_DEVICE_IO;
   const bool exact = flags & EMQX_GM_WITH_EXACT;
   hipStream_t st = ctx->stream;
@@ -2464,6 +2464,10 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt.as<uint32_t>(), n, toff.as<uint64_t>(),
                      stage.as<uint32_t>(), row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec);
   GM_HIP(ctx, hipGetLastError());
+  if (tail && tail->enqueue) {
+    rc = tail->enqueue(row_off.as<uint64_t>(), ids.as<uint32_t>(), cap_spec);
+    if (rc) return rc;
+  }
   uint64_t* const pin = static_cast<uint64_t*>(ctx->pin);  // [0] match total, [1..4] the counters
   GM_HIP(ctx, hipMemcpyAsync(pin, toff.as<uint64_t>() + n_tiles, 40, hipMemcpyDeviceToHost, st));
   GM_HIP(ctx, hipEventRecord(ctx->ev[3], st));
@@ -2478,6 +2482,7 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
     ctx->stats.nnz = nnz;
     ctx->stats.match_kernel_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
     ctx->stats.total_device_ms = ev_ms(ctx->ev[0], ctx->ev[3]);
+    if (tail) tail->used = true;
     return finish_csr(ctx, n, nnz, row_off, ids, dev_io, out);
   }
   ids.reset();
