@@ -1,10 +1,10 @@
 #!/bin/bash
-# r02lat: per-call overhead (idle listed-pass atomics, one pinned read-back):
-# parity subset, the C1 kernel trace, the host latency table, C1 and C2 bench lines.
+# Per-call overhead: the GPU parity and shard tests, the C1 kernel trace (kernel
+# + copy timeline), the host latency table, C1 and C2 bench lines.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-O=gpurun_out/r02lat
+O=gpurun_out/latency
 mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sharded.py -q -m gpu --timeout 500 --timeout-method thread > $O/pytest.log 2>&1 || { tail -5 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
