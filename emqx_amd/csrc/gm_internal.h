@@ -87,6 +87,7 @@ struct PoolBuf {
 constexpr int FAST_FC = 8;    // frontier capacity per lane (LDS)
 constexpr int FAST_MC = 16;   // match capacity per lane (LDS)
 constexpr uint32_t OVF_BIT = 0x80000000u;
+constexpr uint32_t LIST_BIT = 0x40000000u;  // compact staging: the row is listed-pass row (cnt & ~LIST_BIT)
 constexpr uint32_t CNT_MASK = 0x7FFFFFFFu;
 
 }  // namespace gm

@@ -261,7 +261,7 @@ __device__ __forceinline__ uint32_t hot_resolve(const HotSlot* tab, uint32_t cap
 // lane)]).
 #define GM_EMIT(f)                                \
   do {                                            \
-    if (m_n < MC) srow[m_n * 64u] = (f);          \
+    if (m_n < MC) srow[m_n * sstr] = (f);         \
     ++m_n;                                        \
   } while (0)
 
@@ -364,7 +364,10 @@ __device__ __forceinline__ bool plus_is_inline(uint32_t lvl, uint32_t id) { retu
     ++nn;                                                                  \
   } while (0)
 
-template <bool EXACT, int FC, bool LISTED>
+// CMP (the main pass staged compactly): the listed rows go to their own
+// buffer, row `item` of lstage (FAST_MC ids, stride 1), their length to
+// lcnt[item] and cnt[t] = LIST_BIT | item; items past lcap go to the slow path.
+template <bool EXACT, int FC, bool LISTED, bool CMP = false>
 __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ tb,
                                                    const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
                                                    uint32_t* __restrict__ cnt, uint32_t* __restrict__ stage,
@@ -373,8 +376,10 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
                                                    uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
                                                    unsigned long long* __restrict__ probe_ctr,
                                                    unsigned long long* __restrict__ wild_ctr,
-                                                   uint64_t* __restrict__ tsum) {
+                                                   uint64_t* __restrict__ tsum, uint32_t* __restrict__ lstage = nullptr,
+                                                   uint32_t* __restrict__ lcnt = nullptr, uint64_t lcap = 0) {
   constexpr int MC = FAST_MC;
+  constexpr uint32_t sstr = CMP ? 1u : 64u;
   // frontier entry: {hot id | FR_PLUS, exact-child signature}, double buffered
   __shared__ uint2 s_fr[2][FC][256];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -385,7 +390,12 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
        item += uint64_t(gridDim.x) * 256u) {
     const uint64_t t = LISTED ? uint64_t(list_in[item]) : item;
     const uint64_t tile = t >> 6;
-    uint32_t* const srow = stage + stage_index(tile, 0, int(t & 63));
+    if (CMP && item >= lcap) {  // no listed row left: the slow path
+      cnt[t] = OVF_BIT;
+      ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
+      continue;
+    }
+    uint32_t* const srow = CMP ? lstage + item * uint64_t(MC) : stage + stage_index(tile, 0, int(t & 63));
     uint32_t m_n = 0, tprobes = 0;
     bool ovf = false, wild = false;
     uint64_t pos = toff[t];
@@ -457,7 +467,12 @@ __global__ __launch_bounds__(256) void k_match_lds(const uint8_t* __restrict__ t
       tprobes += 2 * nfinal + 1;
       if (m_n > MC) ovf = true;
     }
-    cnt[t] = ovf ? OVF_BIT : m_n;
+    if (CMP) {
+      cnt[t] = ovf ? OVF_BIT : (LIST_BIT | uint32_t(item));
+      if (!ovf) lcnt[item] = m_n;
+    } else {
+      cnt[t] = ovf ? OVF_BIT : m_n;
+    }
     if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
     else if (LISTED) atomicAdd(reinterpret_cast<unsigned long long*>(tsum + tile), (unsigned long long)m_n);
     probes += tprobes;
@@ -829,6 +844,7 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
   const uint64_t tile = t >> 6;
   const bool valid = t < n;
   uint32_t* const srow = stage + stage_index(tile, 0, lane);
+  constexpr uint32_t sstr = 64u;
   uint32_t m_n = 0, probes = 0;
   bool ovf = false, wild = false;
 
@@ -996,6 +1012,8 @@ __global__ __launch_bounds__(256, MINW) void k_walk(const uint8_t* __restrict__ 
 #endif
 constexpr int CW_CAP = GM_CW_CAP;
 constexpr uint32_t CW_OVF = 0x40000000u;   // in a topic's LDS match counter: queued for the listed pass
+// compact staging entry: filter id (< 2^22) | lane << 22 | the match's rank in its row << 28
+constexpr uint32_t CMP_SHIFT = 22, CMP_RANK = 28;
 
 #ifdef GM_PROBE_STATS
 // Diagnostic build only (-DGM_PROBE_STATS): a census of the coop walk's
@@ -1026,7 +1044,12 @@ struct CoopLds {
   uint32_t mc[64];         // per topic: matches emitted | CW_OVF
 };
 
-template <bool EXACT, bool NT, class WORDS>
+// CMP (compact staging, k_match_fused): the tile's matches go to ONE list in
+// emission order, each entry (filter id | lane | rank in the row), written by
+// ballot + mbcnt; tlen[tile] = the list's length.  k_assemble_c sorts them
+// into rows.  A tile whose list would pass 64 x FAST_MC entries sends every
+// topic to the listed pass.  Otherwise ([slot][lane]): one column per topic.
+template <bool EXACT, bool NT, class WORDS, bool CMP = false>
 __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& words, bool valid, uint64_t t,
                                                int lane, const uint8_t* __restrict__ tb,
                                                const uint64_t* __restrict__ toff, const IndexView& ix,
@@ -1034,8 +1057,9 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
                                                uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
                                                unsigned long long* __restrict__ probe_tile,
                                                unsigned long long* __restrict__ wild_ctr,
-                                               uint64_t* __restrict__ tsum) {
+                                               uint64_t* __restrict__ tsum, uint32_t* __restrict__ tlen = nullptr) {
   constexpr uint32_t MC = FAST_MC;
+  constexpr uint32_t TCAP = 64u * FAST_MC;  // a tile's staging entries
   const uint64_t tile = t >> 6;
   uint32_t* const MCNT = L.mc;
   uint2* const LW = L.lw;
@@ -1044,16 +1068,19 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
   const bool dollar = (h & TOK_DOLLAR) != 0, wild = valid && (h & TOK_WILD), deep = valid && (h & TOK_DEEP);
   const bool walk = valid && !wild && !deep;
   uint32_t m0 = deep ? CW_OVF : 0u;  // deep topics: the listed pass tokenizes them itself
+  uint32_t f0 = NONE;
   if (wild && EXACT) {  // a wildcard publish topic: the literal route only (emqx_router.erl:128-134)
-    const uint32_t f = literal_lookup(ix, tb, toff[t], toff[t + 1]);
-    if (f != NONE) {
-      stile[lane] = f;
-      m0 = 1;
-    }
+    f0 = literal_lookup(ix, tb, toff[t], toff[t + 1]);
   }
-  if (walk && !dollar && ix.root_hash != NONE) {  // '#' at the virtual root ('$' rule: emqx_trie.erl:271-278)
-    stile[lane] = ix.root_hash;
-    m0 = 1;
+  if (walk && !dollar && ix.root_hash != NONE) f0 = ix.root_hash;  // '#' at the virtual root ('$' rule: emqx_trie.erl:271-278)
+  uint32_t wbase = 0;  // CMP: entries in the tile's list (wave-uniform)
+  if (f0 != NONE) m0 = 1;
+  if constexpr (CMP) {  // (rank 0 of the lane's row)
+    const unsigned long long b0 = __ballot(f0 != NONE);
+    if (f0 != NONE) st_s<NT>(stile + lane_prefix(b0), f0 | (uint32_t(lane) << CMP_SHIFT));
+    wbase = uint32_t(__popcll(b0));
+  } else {
+    if (f0 != NONE) stile[lane] = f0;
   }
   MCNT[lane] = m0;
   uint32_t probes = walk ? 1u : 0u;  // + the exact-route probe
@@ -1135,6 +1162,33 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
       }
 #endif
       // visits: 'match_#', the end filter on the last level, else the next frontier
+      if constexpr (CMP) {
+        const bool ex = hx != NONE, ep = hp != NONE;
+        const bool e1 = ex && (rx.a.w & ID_MASK) != HF_NONE;
+        const bool e2 = ex && last && rx.ef != NONE && (EXACT || (rx.ef & END_WILD) || (ldollar && level == 0));
+        const bool e3 = ep && (rp.a.w & ID_MASK) != HF_NONE;
+        const bool e4 = ep && last && rp.ef != NONE && (EXACT || (rp.ef & END_WILD) || (ldollar && level == 0));
+        probes += last ? 2u * (uint32_t(ex) + uint32_t(ep)) : 0u;
+        // the row's counter hands this lane's matches their ranks in the row
+        const uint32_t ne = uint32_t(e1) + uint32_t(e2) + uint32_t(e3) + uint32_t(e4);
+        uint32_t rk = ne ? atomicAdd(&MCNT[tl], ne) : 0u;
+        const uint32_t tag = uint32_t(tl) << CMP_SHIFT;
+#define GM_CW_PUT(c, f)                                                                         \
+  do {                                                                                          \
+    const unsigned long long b_ = __ballot(c);                                                  \
+    if (c) {                                                                                    \
+      const uint32_t k_ = wbase + lane_prefix(b_);                                              \
+      if (k_ < TCAP) st_s<NT>(stile + k_, (f) | tag | ((rk < MC ? rk : MC - 1) << CMP_RANK));   \
+      ++rk;                                                                                     \
+    }                                                                                           \
+    wbase += uint32_t(__popcll(b_));                                                            \
+  } while (0)
+        GM_CW_PUT(e1, rx.a.w & ID_MASK);
+        GM_CW_PUT(e2, rx.ef & ID_MASK);
+        GM_CW_PUT(e3, rp.a.w & ID_MASK);
+        GM_CW_PUT(e4, rp.ef & ID_MASK);
+#undef GM_CW_PUT
+      } else {
 #define GM_CW_EMIT(f)                                   \
   do {                                                  \
     const uint32_t k_ = atomicAdd(&MCNT[tl], 1u);       \
@@ -1149,10 +1203,11 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
       probes += 2u;                                                                             \
     }                                                                                           \
   } while (0)
-      if (hx != NONE) GM_CW_VISIT(rx);
-      if (hp != NONE) GM_CW_VISIT(rp);
+        if (hx != NONE) GM_CW_VISIT(rx);
+        if (hp != NONE) GM_CW_VISIT(rp);
 #undef GM_CW_VISIT
 #undef GM_CW_EMIT
+      }
       const bool cx = hx != NONE && !last, cp = hp != NONE && !last;
       const unsigned long long bx = __ballot(cx), bp = __ballot(cp);
       const uint32_t nx = uint32_t(__popcll(bx));
@@ -1182,11 +1237,13 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
   }
   wave_lds_sync();
   const uint32_t m_n = MCNT[lane];
-  const bool ovf = valid && m_n > MC;  // CW_OVF or a row past the staging capacity
+  // CW_OVF or a row past the staging capacity; CMP: the tile's list past its capacity
+  const bool ovf = valid && (m_n > MC || (CMP && wbase > TCAP));
   if (valid) {
     st_s<NT>(cnt + t, ovf ? OVF_BIT : m_n);
     if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
   }
+  if (CMP && lane == 0) st_s<NT>(tlen + tile, wbase < TCAP ? wbase : TCAP);
   uint32_t ptot, mtot;
   wave_excl_scan(probes, ptot);
   wave_excl_scan(valid && !ovf ? m_n : 0u, mtot);
@@ -1250,14 +1307,14 @@ struct WordsFromRegs {
 
 constexpr size_t FUSED_LDS = sizeof(CoopLds) * 4 > (TOK_STAGE + 8) ? sizeof(CoopLds) * 4 : (TOK_STAGE + 8);
 
-template <int G, bool EXACT, bool NT, bool TOKPRIO>
+template <int G, bool EXACT, bool NT, bool TOKPRIO, bool CMP>
 __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restrict__ tb,
                                                         const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
                                                         uint32_t* __restrict__ cnt, uint32_t* __restrict__ stage,
                                                         uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
                                                         unsigned long long* __restrict__ probe_tile,
                                                         unsigned long long* __restrict__ wild_ctr,
-                                                        uint64_t* __restrict__ tsum) {
+                                                        uint64_t* __restrict__ tsum, uint32_t* __restrict__ tlen) {
   __shared__ __align__(16) uint8_t s_raw[FUSED_LDS];  // the staged text, then the walk's lists
   uint64_t* const s_txt = reinterpret_cast<uint64_t*>(s_raw);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1296,8 +1353,8 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
   if constexpr (TOKPRIO) __builtin_amdgcn_s_setprio(0);
   if ((t >> 6) * 64 >= n) return;  // wave-uniform, after the last workgroup barrier
   WordsFromRegs words{w};
-  coop_walk_tile<EXACT, NT>(reinterpret_cast<CoopLds*>(s_raw)[wv], h, words, valid, t, lane, tb, toff, ix, cnt, stage,
-                            ovf_list, ovf_n, probe_tile, wild_ctr, tsum);
+  coop_walk_tile<EXACT, NT, WordsFromRegs, CMP>(reinterpret_cast<CoopLds*>(s_raw)[wv], h, words, valid, t, lane, tb,
+                                                toff, ix, cnt, stage, ovf_list, ovf_n, probe_tile, wild_ctr, tsum, tlen);
 }
 
 // ---------------------------------------------------------------------------
@@ -1535,6 +1592,107 @@ __global__ __launch_bounds__(256) void k_assemble(const uint32_t* __restrict__ c
   else
     GM_ASM(1);
 #undef GM_ASM
+}
+
+// One lane's row of k_assemble_c once the wave's longest row fits W slots:
+// W gathers (LDS, or the listed row), the W-wide network, W writes back (or,
+// beside a slow row, straight to the output).
+template <int W>
+__device__ __forceinline__ void assemble_rows_c(uint32_t* out, const uint32_t* __restrict__ lrow, bool listed,
+                                                uint32_t lpa, uint32_t cf, bool any_slow, uint32_t* __restrict__ ids,
+                                                uint64_t base, const uint32_t* __restrict__ gmap) {
+  uint32_t m[FAST_MC];
+#pragma unroll
+  for (int k = 0; k < FAST_MC; ++k)
+    m[k] = (k < W && uint32_t(k) < cf) ? (listed ? lrow[k] : out[lpa + k]) : 0xFFFFFFFFu;
+  if (W > 1) sort_row<W>(m);
+  if (any_slow) {  // leave the slow rows' ranges alone: lane by lane
+#pragma unroll
+    for (int k = 0; k < W; ++k)
+      if (uint32_t(k) < cf) ids[base + k] = gmap ? gmap[m[k]] : m[k];
+    return;
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int k = 0; k < W; ++k)
+    if (uint32_t(k) < cf) out[lpa + k] = gmap ? gmap[m[k]] : m[k];  // (no slow row: lpa == pa)
+}
+
+// Compact staging (k_match_fused<CMP>): the tile's list holds its matches in
+// emission order as (filter id | lane | rank in its row), tlen[tile] of them, the
+// partial rows of topics that went on to the listed pass included.  Each
+// wave places its main-pass rows' entries in LDS at the row's offset (one
+// LDS counter per row), sorts each row in registers, and writes the tile's
+// ids as one coalesced range; a listed row comes from its own lstage row.
+// The list is ~11.5 B per C2 topic against the ~20 B of [slot][lane] rows
+// k_assemble reads.
+__global__ __launch_bounds__(256) void k_assemble_c(const uint32_t* __restrict__ cnt, uint64_t n,
+                                                    const uint64_t* __restrict__ tile_off,
+                                                    const uint32_t* __restrict__ stage,
+                                                    const uint32_t* __restrict__ tlen,
+                                                    const uint32_t* __restrict__ lstage,
+                                                    const uint32_t* __restrict__ lcnt,
+                                                    uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids,
+                                                    const uint32_t* __restrict__ gmap, uint64_t cap) {
+  __shared__ uint32_t s_out[4][64 * FAST_MC];
+  __shared__ uint32_t s_pa[4][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t* const out = s_out[wv];
+  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  const uint64_t tile = t >> 6;
+  if (tile * 64 >= n) return;  // wave-uniform; no block barrier below
+  // every load the wave needs up front: its counts, the list length and the
+  // list's first 256 entries (a C2 tile holds ~184), in one round trip
+  const uint32_t* const lst = stage + tile * (64ull * FAST_MC);
+  constexpr int PRE = 4;
+  uint32_t pre[PRE];
+#pragma unroll
+  for (int q = 0; q < PRE; ++q) pre[q] = ld_s<true>(lst + q * 64 + lane);
+  const uint32_t len = tlen[tile];
+  const uint32_t c = t < n ? cnt[t] : 0;
+  const bool slow = (c & OVF_BIT) != 0, listed = !slow && (c & LIST_BIT);
+  const uint32_t call = slow ? (c & CNT_MASK) : listed ? lcnt[c & ~LIST_BIT] : c;
+  const uint32_t cf = slow ? 0 : call;  // rows placed here (a slow row's ids land later, k_copy_slow)
+  uint32_t tall, lall;
+  const uint32_t pa = wave_excl_scan(call, tall);
+  const uint32_t lpa = wave_excl_scan(cf, lall);  // the row's place in LDS (slow rows take none)
+  const uint64_t tb0 = tile_off[tile];
+  const uint64_t base = tb0 + pa;
+  if (t < n) row_off[t] = base;
+  if (t == n - 1) row_off[n] = base + call;
+  if (tb0 + tall > cap) return;  // wave-uniform
+  const bool any_slow = __ballot(slow) != 0;
+  // main-pass rows: scatter the list into LDS at each row's offset
+  s_pa[wv][lane] = (slow || listed || t >= n) ? NONE : lpa;
+  wave_lds_sync();
+  // each entry carries its rank in its row
+#define GM_PLACE(e)                                                               \
+  do {                                                                            \
+    const uint32_t rp = s_pa[wv][((e) >> CMP_SHIFT) & 63u];                       \
+    if (rp != NONE) out[rp + ((e) >> CMP_RANK)] = (e) & ((1u << CMP_SHIFT) - 1u); \
+  } while (0)
+#pragma unroll
+  for (int q = 0; q < PRE; ++q)
+    if (uint32_t(q * 64 + lane) < len) GM_PLACE(pre[q]);
+  for (uint32_t i = PRE * 64 + lane; i < len; i += 64) {
+    const uint32_t e = ld_s<true>(lst + i);
+    GM_PLACE(e);
+  }
+#undef GM_PLACE
+  wave_lds_sync();
+  // each row sorted in registers (W = the wave's longest row, a power of two)
+  const uint32_t* const lrow = listed ? lstage + uint64_t(c & ~LIST_BIT) * FAST_MC : nullptr;
+#define GM_ASMC(W) assemble_rows_c<W>(out, lrow, listed, lpa, cf, any_slow, ids, base, gmap)
+  if (__ballot(cf > 8)) GM_ASMC(FAST_MC);
+  else if (__ballot(cf > 4)) GM_ASMC(8);
+  else if (__ballot(cf > 2)) GM_ASMC(4);
+  else if (__ballot(cf > 1)) GM_ASMC(2);
+  else GM_ASMC(1);
+#undef GM_ASMC
+  if (any_slow) return;
+  wave_lds_sync();
+  uint32_t* const dst = ids + tb0;
+  for (uint32_t i = lane; i < tall; i += 64) st_s<true>(dst + i, out[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -2246,6 +2404,29 @@ bool nt_streams() {
   return !e || atoi(e) != 0;
 }
 
+// Compact staging of the fused main pass (k_match_fused<CMP> + k_assemble_c).
+// GM_STAGE_COMPACT (A/B knob, read per call so tests cover both; default on):
+// used when the index's filter ids fit CMP_SHIFT bits.
+bool stage_compact() {
+  const char* e = getenv("GM_STAGE_COMPACT");
+  return !e || atoi(e) != 0;
+}
+struct CmpBufs {
+  uint32_t* tlen;    // per tile: entries in its list
+  uint32_t* lstage;  // listed rows, FAST_MC ids each
+  uint32_t* lcnt;    // listed row lengths
+  uint64_t lcap;     // listed rows available
+};
+void launch_assemble(hipStream_t st, uint64_t nblk, const CmpBufs* cb, const uint32_t* cnt, uint64_t n,
+                     const uint64_t* toff, const uint32_t* stage, uint64_t* row_off, uint32_t* ids,
+                     const uint32_t* gmap, uint64_t cap) {
+  if (cb)
+    hipLaunchKernelGGL(k_assemble_c, dim3(nblk), dim3(256), 0, st, cnt, n, toff, stage, cb->tlen, cb->lstage, cb->lcnt,
+                       row_off, ids, gmap, cap);
+  else
+    hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt, n, toff, stage, row_off, ids, gmap, cap);
+}
+
 void launch_tokenize(hipStream_t st, uint64_t nblk, const uint8_t* tb, const uint64_t* to, uint64_t n,
                      const IndexView& v, uint32_t* hdr, uint32_t* wids, uint64_t t_base) {
   const bool nt = nt_streams();
@@ -2281,7 +2462,7 @@ template <bool EXACT>
 void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const uint64_t* to, uint64_t n,
                   uint32_t* cnt, uint32_t* stage, uint32_t* list1, uint32_t* n1, uint32_t* list2, uint32_t* n2,
                   unsigned long long* probe_ctr, unsigned long long* wild_ctr, uint32_t* hdr, uint32_t* wids,
-                  unsigned long long* probe_tile, uint64_t* tsum, hipEvent_t after_main) {
+                  unsigned long long* probe_tile, uint64_t* tsum, hipEvent_t after_main, const CmpBufs* cb) {
   hipStream_t st = ctx->stream;
   const uint64_t nblk = (n + 255) / 256;
 #define GM_LAUNCH_WALK(W, P, sw, g, base)                                                                        \
@@ -2314,15 +2495,21 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
   if (main_kind() == MAIN_FUSED) {
     const char* pe = getenv("GM_FUSED_PRIO");  // A/B knob (read per call): 0 = every phase at priority 0
     const bool tp = !pe || atoi(pe) != 0;
-#define GM_FUSED(NT, P)                                                                                            \
-  hipLaunchKernelGGL((k_match_fused<3, EXACT, NT, P>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, list1, \
-                     n1, probe_tile, wild_ctr, tsum)
-    if (nt_streams()) {
-      if (tp) GM_FUSED(true, true);
-      else GM_FUSED(true, false);
+    uint32_t* const tl = cb ? cb->tlen : nullptr;
+#define GM_FUSED(NT, P, C)                                                                                            \
+  hipLaunchKernelGGL((k_match_fused<3, EXACT, NT, P, C>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, list1, \
+                     n1, probe_tile, wild_ctr, tsum, tl)
+    if (cb) {
+      if (nt_streams() && tp) GM_FUSED(true, true, true);
+      else if (nt_streams()) GM_FUSED(true, false, true);
+      else if (tp) GM_FUSED(false, true, true);
+      else GM_FUSED(false, false, true);
+    } else if (nt_streams()) {
+      if (tp) GM_FUSED(true, true, false);
+      else GM_FUSED(true, false, false);
     } else {
-      if (tp) GM_FUSED(false, true);
-      else GM_FUSED(false, false);
+      if (tp) GM_FUSED(false, true, false);
+      else GM_FUSED(false, false, false);
     }
 #undef GM_FUSED
   } else if (K == 1) {
@@ -2361,8 +2548,12 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
   hipEventRecord(after_main, st);
   (void)probe_tile;  // summed into the probe counter by the tile scan (run_match)
   const uint64_t lblk = std::min<uint64_t>(nblk, 512);
-  hipLaunchKernelGGL((k_match_lds<EXACT, LISTED_FC, true>), dim3(lblk), dim3(256), 0, st, tb, to, n, v, cnt, stage,
-                     list1, n1, list2, n2, probe_ctr, wild_ctr, tsum);
+  if (cb)
+    hipLaunchKernelGGL((k_match_lds<EXACT, LISTED_FC, true, true>), dim3(lblk), dim3(256), 0, st, tb, to, n, v, cnt,
+                       stage, list1, n1, list2, n2, probe_ctr, wild_ctr, tsum, cb->lstage, cb->lcnt, cb->lcap);
+  else
+    hipLaunchKernelGGL((k_match_lds<EXACT, LISTED_FC, true>), dim3(lblk), dim3(256), 0, st, tb, to, n, v, cnt, stage,
+                       list1, n1, list2, n2, probe_ctr, wild_ctr, tsum);
 }
 
 }  // namespace
@@ -2433,16 +2624,30 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   unsigned long long* wild_ctr = reinterpret_cast<unsigned long long*>(ctrs_p + 24);
   GM_HIP(ctx, hipMemsetAsync(ctrs_p, 0, 64, st));
 
+  PoolBuf c_tlen, c_lstage, c_lcnt;
+  CmpBufs cmpb{};
+  const bool cmp = main_kind() == MAIN_FUSED && stage_compact() && uint64_t(idx->view.n_filters) < (1ull << CMP_SHIFT);
+  if (cmp) {
+    const char* le = getenv("GM_LISTED_CAP");  // (tests: listed rows past it go to the slow path)
+    cmpb.lcap = std::min<uint64_t>(n, le ? strtoull(le, nullptr, 10) : (1u << 20));
+    c_tlen = PoolBuf(ctx->pool, n_tiles * 4 + 16);
+    c_lstage = PoolBuf(ctx->pool, cmpb.lcap * FAST_MC * 4 + 16);
+    c_lcnt = PoolBuf(ctx->pool, cmpb.lcap * 4 + 16);
+    if (!c_tlen.p || !c_lstage.p || !c_lcnt.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: compact staging");
+    cmpb.tlen = c_tlen.as<uint32_t>();
+    cmpb.lstage = c_lstage.as<uint32_t>();
+    cmpb.lcnt = c_lcnt.as<uint32_t>();
+  }
   GM_HIP(ctx, hipEventRecord(ctx->ev[0], st));
   GM_HIP(ctx, hipEventRecord(ctx->ev[1], st));
   if (exact)
     launch_match<true>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
                        list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
-                       probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ctx->ev[2]);
+                       probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ctx->ev[2], cmp ? &cmpb : nullptr);
   else
     launch_match<false>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(),
                         n1, list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
-                        probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ctx->ev[2]);
+                        probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ctx->ev[2], cmp ? &cmpb : nullptr);
   GM_HIP(ctx, hipGetLastError());
 
   // count -> scan, then ONE host round trip reads the pass counters and the
@@ -2461,8 +2666,8 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   const uint64_t cap_spec = 1024 + uint64_t(double(n) * std::min(ctx->ids_per_topic, double(FAST_MC)));
   PoolBuf ids(ctx->pool, cap_spec * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
-  hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt.as<uint32_t>(), n, toff.as<uint64_t>(),
-                     stage.as<uint32_t>(), row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec);
+  launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff.as<uint64_t>(), stage.as<uint32_t>(),
+                  row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec);
   GM_HIP(ctx, hipGetLastError());
   if (tail && tail->enqueue) {
     rc = tail->enqueue(row_off.as<uint64_t>(), ids.as<uint32_t>(), cap_spec);
@@ -2553,8 +2758,8 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   // ---- write the rows (again: the speculative pass above did not fit or missed slow-path rows)
   ids = PoolBuf(ctx->pool, nnz * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
-  hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt.as<uint32_t>(), n, toff.as<uint64_t>(),
-                     stage.as<uint32_t>(), row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, nnz);
+  launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff.as<uint64_t>(), stage.as<uint32_t>(),
+                  row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, nnz);
   GM_HIP(ctx, hipGetLastError());
   if (n_ovf) {
     hipLaunchKernelGGL(k_copy_slow, dim3(n_ovf), dim3(256), 0, st, ovf_list, n_ovf, row_off.as<uint64_t>(),

@@ -727,3 +727,43 @@ def test_speculative_ids_capacity_redo(ctx, orc):
         assert np.array_equal(ro, oro) and np.array_equal(ids, oids)
     assert int(oro[-1]) > 7 * n
     idx.release()
+
+
+@pytest.mark.parametrize("listed_cap", [None, "3"])
+def test_compact_staging_vs_columns(ctx, orc, monkeypatch, listed_cap):
+    """GM_STAGE_COMPACT: the fused main pass stages each tile's matches as one
+    list (filter id | lane) and k_assemble_c sorts them into rows; the listed
+    pass keeps its rows apart (past GM_LISTED_CAP of them: the slow path).
+    Both layouts give the oracle's rows on: a C2-shaped sample; 10-level topics
+    (listed-pass rows); and tiles of 32 topics with 16 matches beside 32 with
+    33 (their list passes 64 x 16 entries: every topic of the tile is re-walked
+    by the listed pass, the 33-match rows finish on the slow path)."""
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    import itertools
+    if listed_cap:
+        monkeypatch.setenv("GM_LISTED_CAP", listed_cap)
+    codes = gen_filter_codes(8, 20_000, wildcard_only=True)
+    filters = set(orc.unpack(*render_codes(codes)))
+    deep = ["/".join(["d%d" % i] + ["x"] * 9) for i in range(3)]
+    filters |= {d.encode() for d in deep} | {b"d0/+/x/#", b"d1/x/+/x/x/#"}
+    a16 = ["m/a/b", "m/+/b", "m/a/+", "m/#", "m/+/+", "+/a/b", "+/+/b", "+/a/+", "#", "+/#", "m/a/#", "+/+/+",
+           "m/a/b/#", "+/a/#", "m/+/b/#", "+/+/b/#"]
+    b33 = ["n/%s/%s/%s" % c for c in itertools.product(["3", "+"], ["x", "+"], ["y", "+"])]
+    b33 += [f + "/#" for f in b33] + ["+/%s/%s/%s" % c for c in itertools.product(["3", "+"], ["x", "+"], ["y", "+"])]
+    b33 += ["n/#", "n/3/#", "n/+/#", "n/3/x/#", "n/+/x/#", "n/3/+/#", "n/+/+/#"]
+    filters = sorted(filters | {f.encode() for f in a16 + b33})
+    tb, to = orc.render_codes(orc.gen_topic_codes(8, 0, 40_000, codes))
+    topics = orc.unpack(tb, to) + [d.encode() for d in deep] * 50
+    topics += [b"z/z"] * (-len(topics) % 64)  # the next tiles start on a 64-topic boundary
+    topics += [b"m/a/b", b"n/3/x/y"] * 32 + [b"m/a/b"] * 32 + [b"n/3/x/y"] * 32
+    r = orc.Router(True)
+    for f in filters:
+        r.add_route(f)
+    assert len(r.match_routes(b"m/a/b")) == 16 and len(r.match_routes(b"n/3/x/y")) == 33
+    oro, oids, _ = r.match_batch(topics, filters, mode=1, nthreads=8)
+    idx = ctx.build_index(filters)
+    for mode in ("1", "0"):
+        monkeypatch.setenv("GM_STAGE_COMPACT", mode)
+        ro, ids = ctx.match(idx, topics, exact=True)
+        assert np.array_equal(ro, oro) and np.array_equal(ids, oids), mode
+    idx.release()
