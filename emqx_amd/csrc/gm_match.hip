@@ -1057,7 +1057,8 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
                                                uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
                                                unsigned long long* __restrict__ probe_tile,
                                                unsigned long long* __restrict__ wild_ctr,
-                                               uint64_t* __restrict__ tsum, uint32_t* __restrict__ tlen = nullptr) {
+                                               uint64_t* __restrict__ tsum, uint32_t* __restrict__ tlen = nullptr,
+                                               uint8_t* __restrict__ cnt8 = nullptr) {
   constexpr uint32_t MC = FAST_MC;
   constexpr uint32_t TCAP = 64u * FAST_MC;  // a tile's staging entries
   const uint64_t tile = t >> 6;
@@ -1240,7 +1241,9 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
   // CW_OVF or a row past the staging capacity; CMP: the tile's list past its capacity
   const bool ovf = valid && (m_n > MC || (CMP && wbase > TCAP));
   if (valid) {
-    st_s<NT>(cnt + t, ovf ? OVF_BIT : m_n);
+    // CMP: one byte per row (0xFF: the listed and slow passes write the row's cnt word)
+    if constexpr (CMP) st_s<NT>(cnt8 + t, uint8_t(ovf ? 0xFFu : m_n));
+    else st_s<NT>(cnt + t, ovf ? OVF_BIT : m_n);
     if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
   }
   if (CMP && lane == 0) st_s<NT>(tlen + tile, wbase < TCAP ? wbase : TCAP);
@@ -1314,7 +1317,8 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
                                                         uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ ovf_n,
                                                         unsigned long long* __restrict__ probe_tile,
                                                         unsigned long long* __restrict__ wild_ctr,
-                                                        uint64_t* __restrict__ tsum, uint32_t* __restrict__ tlen) {
+                                                        uint64_t* __restrict__ tsum, uint32_t* __restrict__ tlen,
+                                                        uint8_t* __restrict__ cnt8) {
   __shared__ __align__(16) uint8_t s_raw[FUSED_LDS];  // the staged text, then the walk's lists
   uint64_t* const s_txt = reinterpret_cast<uint64_t*>(s_raw);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1354,7 +1358,8 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
   if ((t >> 6) * 64 >= n) return;  // wave-uniform, after the last workgroup barrier
   WordsFromRegs words{w};
   coop_walk_tile<EXACT, NT, WordsFromRegs, CMP>(reinterpret_cast<CoopLds*>(s_raw)[wv], h, words, valid, t, lane, tb,
-                                                toff, ix, cnt, stage, ovf_list, ovf_n, probe_tile, wild_ctr, tsum, tlen);
+                                                toff, ix, cnt, stage, ovf_list, ovf_n, probe_tile, wild_ctr, tsum, tlen,
+                                                cnt8);
 }
 
 // ---------------------------------------------------------------------------
@@ -1626,55 +1631,57 @@ __device__ __forceinline__ void assemble_rows_c(uint32_t* out, const uint32_t* _
 // ids as one coalesced range; a listed row comes from its own lstage row.
 // The list is ~11.5 B per C2 topic against the ~20 B of [slot][lane] rows
 // k_assemble reads.
-__global__ __launch_bounds__(256) void k_assemble_c(const uint32_t* __restrict__ cnt, uint64_t n,
-                                                    const uint64_t* __restrict__ tile_off,
-                                                    const uint32_t* __restrict__ stage,
-                                                    const uint32_t* __restrict__ tlen,
-                                                    const uint32_t* __restrict__ lstage,
-                                                    const uint32_t* __restrict__ lcnt,
-                                                    uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids,
-                                                    const uint32_t* __restrict__ gmap, uint64_t cap) {
-  __shared__ uint32_t s_out[4][64 * FAST_MC];
-  __shared__ uint32_t s_pa[4][64];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t* const out = s_out[wv];
-  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x;
-  const uint64_t tile = t >> 6;
-  if (tile * 64 >= n) return;  // wave-uniform; no block barrier below
-  // every load the wave needs up front: its counts, the list length and the
-  // list's first 256 entries (a C2 tile holds ~184), in one round trip
+struct AsmCLoads {  // one tile's loads of k_assemble_c, issued before any is used
+  static constexpr int PRE = 4;
+  uint32_t pre[PRE];  // the list's first 256 entries (a C2 tile holds ~184)
+  uint32_t len, c;
+  uint64_t tb0;
+};
+__device__ __forceinline__ void asm_c_load(AsmCLoads& L, uint64_t tile, uint64_t n, int lane,
+                                           const uint8_t* __restrict__ cnt8, const uint64_t* __restrict__ tile_off,
+                                           const uint32_t* __restrict__ stage, const uint32_t* __restrict__ tlen) {
   const uint32_t* const lst = stage + tile * (64ull * FAST_MC);
-  constexpr int PRE = 4;
-  uint32_t pre[PRE];
 #pragma unroll
-  for (int q = 0; q < PRE; ++q) pre[q] = ld_s<true>(lst + q * 64 + lane);
-  const uint32_t len = tlen[tile];
-  const uint32_t c = t < n ? cnt[t] : 0;
+  for (int q = 0; q < AsmCLoads::PRE; ++q) L.pre[q] = ld_s<true>(lst + q * 64 + lane);
+  L.len = tlen[tile];
+  const uint64_t t = tile * 64 + lane;
+  L.c = t < n ? ld_s<true>(cnt8 + t) : 0u;  // 0xFF: the row's cnt word (asm_c_tile)
+  L.tb0 = tile_off[tile];
+}
+
+// One tile of k_assemble_c from its loads (out, s_pa: the wave's LDS).
+__device__ __forceinline__ void asm_c_tile(const AsmCLoads& L, uint64_t tile, uint64_t n, int lane, uint32_t* out,
+                                           uint32_t* s_pa, const uint32_t* __restrict__ cnt,
+                                           const uint32_t* __restrict__ stage,
+                                           const uint32_t* __restrict__ lstage, const uint32_t* __restrict__ lcnt,
+                                           uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids,
+                                           const uint32_t* __restrict__ gmap, uint64_t cap) {
+  const uint64_t t = tile * 64 + lane;
+  const uint32_t c = L.c == 0xFFu ? cnt[t] : L.c;  // a listed or slow row: its cnt word
   const bool slow = (c & OVF_BIT) != 0, listed = !slow && (c & LIST_BIT);
   const uint32_t call = slow ? (c & CNT_MASK) : listed ? lcnt[c & ~LIST_BIT] : c;
   const uint32_t cf = slow ? 0 : call;  // rows placed here (a slow row's ids land later, k_copy_slow)
   uint32_t tall, lall;
   const uint32_t pa = wave_excl_scan(call, tall);
   const uint32_t lpa = wave_excl_scan(cf, lall);  // the row's place in LDS (slow rows take none)
-  const uint64_t tb0 = tile_off[tile];
-  const uint64_t base = tb0 + pa;
+  const uint64_t base = L.tb0 + pa;
   if (t < n) row_off[t] = base;
   if (t == n - 1) row_off[n] = base + call;
-  if (tb0 + tall > cap) return;  // wave-uniform
+  if (L.tb0 + tall > cap) return;  // wave-uniform
   const bool any_slow = __ballot(slow) != 0;
-  // main-pass rows: scatter the list into LDS at each row's offset
-  s_pa[wv][lane] = (slow || listed || t >= n) ? NONE : lpa;
+  // main-pass rows: scatter the list into LDS at each row's offset + the entry's rank
+  s_pa[lane] = (slow || listed || t >= n) ? NONE : lpa;
   wave_lds_sync();
-  // each entry carries its rank in its row
 #define GM_PLACE(e)                                                               \
   do {                                                                            \
-    const uint32_t rp = s_pa[wv][((e) >> CMP_SHIFT) & 63u];                       \
+    const uint32_t rp = s_pa[((e) >> CMP_SHIFT) & 63u];                           \
     if (rp != NONE) out[rp + ((e) >> CMP_RANK)] = (e) & ((1u << CMP_SHIFT) - 1u); \
   } while (0)
 #pragma unroll
-  for (int q = 0; q < PRE; ++q)
-    if (uint32_t(q * 64 + lane) < len) GM_PLACE(pre[q]);
-  for (uint32_t i = PRE * 64 + lane; i < len; i += 64) {
+  for (int q = 0; q < AsmCLoads::PRE; ++q)
+    if (uint32_t(q * 64 + lane) < L.len) GM_PLACE(L.pre[q]);
+  const uint32_t* const lst = stage + tile * (64ull * FAST_MC);
+  for (uint32_t i = AsmCLoads::PRE * 64 + lane; i < L.len; i += 64) {
     const uint32_t e = ld_s<true>(lst + i);
     GM_PLACE(e);
   }
@@ -1691,8 +1698,39 @@ __global__ __launch_bounds__(256) void k_assemble_c(const uint32_t* __restrict__
 #undef GM_ASMC
   if (any_slow) return;
   wave_lds_sync();
-  uint32_t* const dst = ids + tb0;
+  uint32_t* const dst = ids + L.tb0;
   for (uint32_t i = lane; i < tall; i += 64) st_s<true>(dst + i, out[i]);
+}
+
+// ASM_TPW tiles per wave, every tile's loads issued together (one round trip
+// for all).  2 was slower at C2: 0.83-0.84 ms against 0.79-0.80 for 1, at 6
+// waves/SIMD (74 VGPRs) or at 8 with spills.
+constexpr int ASM_TPW = 1;
+__global__ __launch_bounds__(256) void k_assemble_c(const uint8_t* __restrict__ cnt8, const uint32_t* __restrict__ cnt,
+                                                    uint64_t n,
+                                                    const uint64_t* __restrict__ tile_off,
+                                                    const uint32_t* __restrict__ stage,
+                                                    const uint32_t* __restrict__ tlen,
+                                                    const uint32_t* __restrict__ lstage,
+                                                    const uint32_t* __restrict__ lcnt,
+                                                    uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids,
+                                                    const uint32_t* __restrict__ gmap, uint64_t cap) {
+  __shared__ uint32_t s_out[4][64 * FAST_MC];
+  __shared__ uint32_t s_pa[4][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t n_tiles = (n + 63) / 64;
+  const uint64_t tile0 = (uint64_t(blockIdx.x) * 4 + wv) * ASM_TPW;
+  if (tile0 >= n_tiles) return;  // wave-uniform; no block barrier below
+  AsmCLoads L[ASM_TPW];
+#pragma unroll
+  for (int k = 0; k < ASM_TPW; ++k)
+    if (tile0 + k < n_tiles) asm_c_load(L[k], tile0 + k, n, lane, cnt8, tile_off, stage, tlen);
+#pragma unroll
+  for (int k = 0; k < ASM_TPW; ++k) {
+    if (tile0 + k >= n_tiles) break;
+    if (k) wave_lds_sync();  // the previous tile is done with the wave's LDS
+    asm_c_tile(L[k], tile0 + k, n, lane, s_out[wv], s_pa[wv], cnt, stage, lstage, lcnt, row_off, ids, gmap, cap);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2412,6 +2450,7 @@ bool stage_compact() {
   return !e || atoi(e) != 0;
 }
 struct CmpBufs {
+  uint8_t* cnt8;     // per topic: its row length, 0xFF = see cnt (listed / slow rows)
   uint32_t* tlen;    // per tile: entries in its list
   uint32_t* lstage;  // listed rows, FAST_MC ids each
   uint32_t* lcnt;    // listed row lengths
@@ -2421,8 +2460,8 @@ void launch_assemble(hipStream_t st, uint64_t nblk, const CmpBufs* cb, const uin
                      const uint64_t* toff, const uint32_t* stage, uint64_t* row_off, uint32_t* ids,
                      const uint32_t* gmap, uint64_t cap) {
   if (cb)
-    hipLaunchKernelGGL(k_assemble_c, dim3(nblk), dim3(256), 0, st, cnt, n, toff, stage, cb->tlen, cb->lstage, cb->lcnt,
-                       row_off, ids, gmap, cap);
+    hipLaunchKernelGGL(k_assemble_c, dim3((nblk + ASM_TPW - 1) / ASM_TPW), dim3(256), 0, st, cb->cnt8, cnt, n, toff,
+                       stage, cb->tlen, cb->lstage, cb->lcnt, row_off, ids, gmap, cap);
   else
     hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt, n, toff, stage, row_off, ids, gmap, cap);
 }
@@ -2496,9 +2535,10 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
     const char* pe = getenv("GM_FUSED_PRIO");  // A/B knob (read per call): 0 = every phase at priority 0
     const bool tp = !pe || atoi(pe) != 0;
     uint32_t* const tl = cb ? cb->tlen : nullptr;
+    uint8_t* const c8 = cb ? cb->cnt8 : nullptr;
 #define GM_FUSED(NT, P, C)                                                                                            \
   hipLaunchKernelGGL((k_match_fused<3, EXACT, NT, P, C>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, list1, \
-                     n1, probe_tile, wild_ctr, tsum, tl)
+                     n1, probe_tile, wild_ctr, tsum, tl, c8)
     if (cb) {
       if (nt_streams() && tp) GM_FUSED(true, true, true);
       else if (nt_streams()) GM_FUSED(true, false, true);
@@ -2624,16 +2664,18 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   unsigned long long* wild_ctr = reinterpret_cast<unsigned long long*>(ctrs_p + 24);
   GM_HIP(ctx, hipMemsetAsync(ctrs_p, 0, 64, st));
 
-  PoolBuf c_tlen, c_lstage, c_lcnt;
+  PoolBuf c_tlen, c_lstage, c_lcnt, c_cnt8;
   CmpBufs cmpb{};
   const bool cmp = main_kind() == MAIN_FUSED && stage_compact() && uint64_t(idx->view.n_filters) < (1ull << CMP_SHIFT);
   if (cmp) {
     const char* le = getenv("GM_LISTED_CAP");  // (tests: listed rows past it go to the slow path)
     cmpb.lcap = std::min<uint64_t>(n, le ? strtoull(le, nullptr, 10) : (1u << 20));
     c_tlen = PoolBuf(ctx->pool, n_tiles * 4 + 16);
+    c_cnt8 = PoolBuf(ctx->pool, n + 64);
     c_lstage = PoolBuf(ctx->pool, cmpb.lcap * FAST_MC * 4 + 16);
     c_lcnt = PoolBuf(ctx->pool, cmpb.lcap * 4 + 16);
-    if (!c_tlen.p || !c_lstage.p || !c_lcnt.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: compact staging");
+    if (!c_tlen.p || !c_lstage.p || !c_lcnt.p || !c_cnt8.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: compact staging");
+    cmpb.cnt8 = c_cnt8.as<uint8_t>();
     cmpb.tlen = c_tlen.as<uint32_t>();
     cmpb.lstage = c_lstage.as<uint32_t>();
     cmpb.lcnt = c_lcnt.as<uint32_t>();
