@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 O=gpurun_out/asm_ab
 mkdir -p $O
-env ${PARITY_ENV:-} timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -q -m gpu -k "compact_staging or speculative or config_c1 or assemble" --timeout 250 --timeout-method thread > $O/pytest.log 2>&1 || { grep -E "FAILED|Error|error" $O/pytest.log | head -20; tail -5 $O/pytest.log; exit 1; }
+env ${PARITY_ENV:-} timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -q -m gpu -k "${PARITY_K:-compact_staging or speculative or config_c1 or assemble}" --timeout 250 --timeout-method thread > $O/pytest.log 2>&1 || { grep -E "FAILED|Error|error" $O/pytest.log | head -20; tail -5 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 i=0
 for lib in "$@"; do
