@@ -2640,14 +2640,18 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   PoolBuf tsum(ctx->pool, n_tiles * 8 + 8);
   // tile offsets [n_tiles + 1] and, right behind the total, the pass counters:
   // one read-back brings the match total and the counters together
-  PoolBuf toff(ctx->pool, (n_tiles + 1) * 8 + 64);
+  PoolBuf toff(ctx->pool, (n_tiles + 1) * 8 + 128);
   if (!cnt.p || !stage.p || !list1.p || !list2.p || !tsum.p || !toff.p)
     return set_err(ctx, EMQX_GM_ENOMEM, "match: workspace");
   if (!ctx->pin && hipHostMalloc(&ctx->pin, 256, hipHostMallocDefault) != hipSuccess) {
     ctx->pin = nullptr;
     return set_err(ctx, EMQX_GM_ENOMEM, "match: pinned read-back words");
   }
-  uint8_t* const ctrs_p = toff.as<uint8_t>() + (n_tiles + 1) * 8;
+  // the counters start 64-B aligned, so zeroing them is one fill launch (an
+  // unaligned 64-B memset is split into three)
+  const uintptr_t ctrs_a = (reinterpret_cast<uintptr_t>(toff.p) + (n_tiles + 1) * 8 + 63) & ~uintptr_t(63);
+  uint8_t* const ctrs_p = reinterpret_cast<uint8_t*>(ctrs_a);
+  uint64_t* const toff_p = reinterpret_cast<uint64_t*>(ctrs_p) - (n_tiles + 1);
   PoolBuf probe_tile(ctx->pool, n_tiles * 8 + 8);
   if (!probe_tile.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: probe workspace");
   PoolBuf hdr, wids;  // split forms: per-topic header and word ids [level][topic] (the fused kernel keeps them in registers)
@@ -2695,7 +2699,7 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   // count -> scan, then ONE host round trip reads the pass counters and the
   // match total together (the slow path below is rare; it re-scans)
   // (tsum: per-tile match counts, written by the main pass and topped up by the listed and slow passes)
-  int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff.as<uint64_t>(),
+  int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p,
                      SideSum{probe_tile.as<unsigned long long>(), n_tiles, probe_ctr});
   if (rc) return rc;
   // Speculative assembly: the rows are written before the host has read the
@@ -2708,7 +2712,7 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   const uint64_t cap_spec = 1024 + uint64_t(double(n) * std::min(ctx->ids_per_topic, double(FAST_MC)));
   PoolBuf ids(ctx->pool, cap_spec * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
-  launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff.as<uint64_t>(), stage.as<uint32_t>(),
+  launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
                   row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec);
   GM_HIP(ctx, hipGetLastError());
   if (tail && tail->enqueue) {
@@ -2716,7 +2720,7 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
     if (rc) return rc;
   }
   uint64_t* const pin = static_cast<uint64_t*>(ctx->pin);  // [0] match total, [1..4] the counters
-  GM_HIP(ctx, hipMemcpyAsync(pin, toff.as<uint64_t>() + n_tiles, 40, hipMemcpyDeviceToHost, st));
+  GM_HIP(ctx, hipMemcpyAsync(pin, toff_p + n_tiles, 40, hipMemcpyDeviceToHost, st));
   GM_HIP(ctx, hipEventRecord(ctx->ev[3], st));
   GM_HIP(ctx, hipStreamSynchronize(st));
   uint64_t nnz = pin[0];
@@ -2791,16 +2795,16 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
       GM_HIP(ctx, hipGetLastError());
     }
     // the slow path added its rows' counts to tsum: scan again
-    rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff.as<uint64_t>());
+    rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p);
     if (rc) return rc;
-    GM_HIP(ctx, hipMemcpyAsync(&nnz, toff.as<uint64_t>() + n_tiles, 8, hipMemcpyDeviceToHost, st));
+    GM_HIP(ctx, hipMemcpyAsync(&nnz, toff_p + n_tiles, 8, hipMemcpyDeviceToHost, st));
     GM_HIP(ctx, hipStreamSynchronize(st));
   }
 
   // ---- write the rows (again: the speculative pass above did not fit or missed slow-path rows)
   ids = PoolBuf(ctx->pool, nnz * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
-  launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff.as<uint64_t>(), stage.as<uint32_t>(),
+  launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
                   row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, nnz);
   GM_HIP(ctx, hipGetLastError());
   if (n_ovf) {
