@@ -39,8 +39,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=None,
+                   help="timed steps (default 5; C1's 0.13-ms step: 200, so the timed region is not noise)")
+    p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2; C1: 20)")
     p.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     p.add_argument("--filters", type=int, default=None)
     p.add_argument("--topics", type=int, default=None, help="topics per GPU per step")
@@ -53,7 +54,12 @@ def parse():
     p.add_argument("--no-update", action="store_true", help="skip the incremental-update detail")
     p.add_argument("--no-host-io", action="store_true",
                    help="skip the host-buffer call (PCIe-inclusive rate, reported in detail, never `value`)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.steps is None:
+        a.steps = 200 if a.config == "c1" else 5
+    if a.warmup is None:
+        a.warmup = 20 if a.config == "c1" else 2
+    return a
 
 
 # Rehearsal knobs (tests/test_gpu_bench.py): GM_BENCH_BACKEND=gloo runs the
