@@ -1447,9 +1447,12 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_local(LOAD load, uint64_t n_in,
 
 template <class LOAD>
 __global__ __launch_bounds__(SCAN1_T) void k_scan_one(LOAD load, uint64_t n_in, uint64_t n_out,
-                                                       uint64_t* __restrict__ out, SideSum side) {
+                                                       uint64_t* __restrict__ out, SideSum side,
+                                                       uint64_t* __restrict__ mirror) {
   __shared__ uint64_t s_w[2 * (SCAN1_T / 64)];
-  block_scan<SCAN1_T, SCAN1_V>(load, uint64_t(threadIdx.x) * SCAN1_V, n_in, n_out, 0, out, s_w, side);
+  const uint64_t tot = block_scan<SCAN1_T, SCAN1_V>(load, uint64_t(threadIdx.x) * SCAN1_V, n_in, n_out, 0, out, s_w,
+                                                    side);
+  if (mirror && threadIdx.x == 0) *mirror = tot;  // the grand total, also at the caller's out[n]
 }
 
 __global__ __launch_bounds__(SCAN_T) void k_scan_add(uint64_t* __restrict__ out, uint64_t n_out,
@@ -1480,11 +1483,17 @@ struct LoadSegLen {  // subscriber count of the filter of match entry i
 };
 
 // Exclusive scan of n_in loaded values into out[0..n_in] (out[n_in] = total).
+// split (optional): for a two-level scan, leave out[0..n_in) block-local and
+// hand back the blocks' offsets in *split (out[i] + (*split)[i / SCAN_B] is the
+// scan; out[n_in] is the grand total) -- the consumer adds them, one launch
+// (k_scan_add) fewer.  split->p stays null when the scan was not split.
 template <class LOAD>
-int scan_excl(emqx_gm_ctx* ctx, LOAD load, uint64_t n_in, uint64_t* out, SideSum side = SideSum{}) {
+int scan_excl(emqx_gm_ctx* ctx, LOAD load, uint64_t n_in, uint64_t* out, SideSum side = SideSum{},
+              PoolBuf* split = nullptr) {
   const uint64_t n_out = n_in + 1;
   if (n_out <= uint64_t(SCAN1_B)) {  // one launch
-    hipLaunchKernelGGL(k_scan_one<LOAD>, dim3(1), dim3(SCAN1_T), 0, ctx->stream, load, n_in, n_out, out, side);
+    hipLaunchKernelGGL(k_scan_one<LOAD>, dim3(1), dim3(SCAN1_T), 0, ctx->stream, load, n_in, n_out, out, side,
+                       static_cast<uint64_t*>(nullptr));
     GM_HIP(ctx, hipGetLastError());
     return 0;
   }
@@ -1493,6 +1502,13 @@ int scan_excl(emqx_gm_ctx* ctx, LOAD load, uint64_t n_in, uint64_t* out, SideSum
   if (!sums.p || !offs.p) return set_err(ctx, EMQX_GM_ENOMEM, "scan: workspace");
   hipLaunchKernelGGL(k_scan_local<LOAD>, dim3(nb), dim3(SCAN_T), 0, ctx->stream, load, n_in, n_out, out,
                      sums.as<uint64_t>(), side);
+  if (split && nb + 1 <= uint64_t(SCAN1_B)) {  // the blocks' offsets, and the total into out[n_in]
+    hipLaunchKernelGGL(k_scan_one<LoadU64>, dim3(1), dim3(SCAN1_T), 0, ctx->stream, LoadU64{sums.as<uint64_t>()}, nb,
+                       nb + 1, offs.as<uint64_t>(), SideSum{}, out + n_in);
+    GM_HIP(ctx, hipGetLastError());
+    *split = std::move(offs);
+    return 0;
+  }
   if (nb > 1) {
     int rc = scan_excl(ctx, LoadU64{sums.as<uint64_t>()}, nb, offs.as<uint64_t>());
     if (rc) return rc;
@@ -1643,14 +1659,15 @@ struct AsmCLoads {  // one tile's loads of k_assemble_c, issued before any is us
 };
 __device__ __forceinline__ void asm_c_load(AsmCLoads& L, uint64_t tile, uint64_t n, int lane,
                                            const uint8_t* __restrict__ cnt8, const uint64_t* __restrict__ tile_off,
-                                           const uint32_t* __restrict__ stage, const uint32_t* __restrict__ tlen) {
+                                           const uint32_t* __restrict__ stage, const uint32_t* __restrict__ tlen,
+                                           const uint64_t* __restrict__ blk) {
   const uint32_t* const lst = stage + tile * (64ull * FAST_MC);
 #pragma unroll
   for (int q = 0; q < AsmCLoads::PRE; ++q) L.pre[q] = ld_s<true>(lst + q * 64 + lane);
   L.len = tlen[tile];
   const uint64_t t = tile * 64 + lane;
   L.c = t < n ? ld_s<true>(cnt8 + t) : 0u;  // 0xFF: the row's cnt word (asm_c_tile)
-  L.tb0 = tile_off[tile];
+  L.tb0 = tile_off[tile] + (blk ? blk[tile / SCAN_B] : 0);  // blk: a split scan's block offsets
 }
 
 // One tile of k_assemble_c from its loads (out, s_pa: the wave's LDS).
@@ -1718,7 +1735,8 @@ __global__ __launch_bounds__(256) void k_assemble_c(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ lstage,
                                                     const uint32_t* __restrict__ lcnt,
                                                     uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids,
-                                                    const uint32_t* __restrict__ gmap, uint64_t cap) {
+                                                    const uint32_t* __restrict__ gmap, uint64_t cap,
+                                                    const uint64_t* __restrict__ blk) {
   __shared__ uint32_t s_out[4][64 * FAST_MC];
   __shared__ uint32_t s_pa[4][64];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1728,7 +1746,7 @@ __global__ __launch_bounds__(256) void k_assemble_c(const uint8_t* __restrict__ 
   AsmCLoads L[ASM_TPW];
 #pragma unroll
   for (int k = 0; k < ASM_TPW; ++k)
-    if (tile0 + k < n_tiles) asm_c_load(L[k], tile0 + k, n, lane, cnt8, tile_off, stage, tlen);
+    if (tile0 + k < n_tiles) asm_c_load(L[k], tile0 + k, n, lane, cnt8, tile_off, stage, tlen, blk);
 #pragma unroll
   for (int k = 0; k < ASM_TPW; ++k) {
     if (tile0 + k >= n_tiles) break;
@@ -2462,10 +2480,11 @@ struct CmpBufs {
 };
 void launch_assemble(hipStream_t st, uint64_t nblk, const CmpBufs* cb, const uint32_t* cnt, uint64_t n,
                      const uint64_t* toff, const uint32_t* stage, uint64_t* row_off, uint32_t* ids,
-                     const uint32_t* gmap, uint64_t cap) {
+                     const uint32_t* gmap, uint64_t cap, const uint64_t* blk = nullptr) {
+  // blk (compact staging only): toff is a split scan's block-local part, blk its block offsets
   if (cb)
     hipLaunchKernelGGL(k_assemble_c, dim3((nblk + ASM_TPW - 1) / ASM_TPW), dim3(256), 0, st, cb->cnt8, cnt, n, toff,
-                       stage, cb->tlen, cb->lstage, cb->lcnt, row_off, ids, gmap, cap);
+                       stage, cb->tlen, cb->lstage, cb->lcnt, row_off, ids, gmap, cap, blk);
   else
     hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt, n, toff, stage, row_off, ids, gmap, cap);
 }
@@ -2704,9 +2723,15 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   // count -> scan, then ONE host round trip reads the pass counters and the
   // match total together (the slow path below is rare; it re-scans)
   // (tsum: per-tile match counts, written by the main pass and topped up by the listed and slow passes)
+  // (compact staging: a two-level scan is left split, k_assemble_c adds the
+  // block offsets -- one launch fewer; GM_SCAN_SPLIT=0 turns it off)
+  PoolBuf scan_blk;
+  const char* se = getenv("GM_SCAN_SPLIT");
+  const bool split = cmp && (!se || atoi(se) != 0);
   int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p,
-                     SideSum{probe_tile.as<unsigned long long>(), n_tiles, probe_ctr});
+                     SideSum{probe_tile.as<unsigned long long>(), n_tiles, probe_ctr}, split ? &scan_blk : nullptr);
   if (rc) return rc;
+  const uint64_t* const blk = scan_blk.as<uint64_t>();
   // Speculative assembly: the rows are written before the host has read the
   // match total, into an ids buffer sized from this context's recent matches
   // per topic (x1.25), so a call makes ONE host round trip.  The total, the
@@ -2718,7 +2743,7 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   PoolBuf ids(ctx->pool, cap_spec * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
   launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
-                  row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec);
+                  row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec, blk);
   GM_HIP(ctx, hipGetLastError());
   if (tail && tail->enqueue) {
     rc = tail->enqueue(row_off.as<uint64_t>(), ids.as<uint32_t>(), cap_spec);
@@ -2809,8 +2834,9 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   // ---- write the rows (again: the speculative pass above did not fit or missed slow-path rows)
   ids = PoolBuf(ctx->pool, nnz * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
+  // (after a slow-path rescan toff is whole; otherwise it is still the split first scan)
   launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
-                  row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, nnz);
+                  row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, nnz, n_ovf ? nullptr : blk);
   GM_HIP(ctx, hipGetLastError());
   if (n_ovf) {
     hipLaunchKernelGGL(k_copy_slow, dim3(n_ovf), dim3(256), 0, st, ovf_list, n_ovf, row_off.as<uint64_t>(),

@@ -707,17 +707,24 @@ def test_config_c1_fixture(ctx, orc):
     idx.release()
 
 
-def test_speculative_ids_capacity_redo(ctx, orc):
+@pytest.mark.parametrize("n,listed_cap", [(100_000, None), (300_000, None), (300_000, "3")])
+def test_speculative_ids_capacity_redo(ctx, orc, monkeypatch, n, listed_cap):
     """run_match writes the rows before the host reads the match total, into an
     ids buffer sized from the context's recent matches per topic.  A batch
     after a match-free one (capacity ~1 id per topic) with ~8 matches per topic
     overflows it and is assembled again; both calls equal the oracle, and so
-    does a third call (capacity grown)."""
+    does a third call (capacity grown).  At 300k topics (4,688 tiles) the tile
+    scan is left split and k_assemble_c adds the block offsets, on the first
+    assembly and on the redo; with GM_LISTED_CAP=3 the 10-level topics past
+    the listed pass's cap take the slow path, whose rescan is whole."""
+    if listed_cap:
+        monkeypatch.setenv("GM_LISTED_CAP", listed_cap)
     filters = sorted({b"a/#", b"a/+/#", b"+/b/#", b"a/b/#", b"+/+/#", b"a/+/c", b"+/b/c", b"a/b/c", b"#"})
     idx = ctx.build_index(filters)
-    n = 100_000
     none = [b"$x/%d" % i for i in range(n)]   # '$' topics: no root '#' or '+', nothing else matches
     many = [b"a/b/c" if i % 3 else b"a/b/c/%d" % i for i in range(n)]
+    if listed_cap:
+        many[-10:] = [b"a/b/c/d/e/f/g/h/i/%d" % i for i in range(10)]
     r = orc.Router(True)
     for f in filters:
         r.add_route(f)
