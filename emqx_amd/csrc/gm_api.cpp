@@ -33,9 +33,11 @@ DevPool::~DevPool() {
   for (auto& kv : live_) hipFree(kv.first);
 }
 
+// Buffers still handed out (live_) are NOT freed: a caller may hold a host CSR
+// past emqx_gm_close, so they are detached and leak as plain malloc'd memory
+// (what the CSRs were before the pool existed).
 HostPool::~HostPool() {
   for (auto& kv : free_) free(kv.second);
-  for (auto& kv : live_) free(kv.first);
 }
 void* HostPool::alloc(size_t bytes) {
   constexpr size_t HUGE_PAGE = 2u << 20;
@@ -44,14 +46,14 @@ void* HostPool::alloc(size_t bytes) {
   if (it != free_.end() && it->first <= r + r / 4) {
     void* p = it->second;
     cached_ -= it->first;
-    live_.emplace(p, it->first);
+    live_[p] = it->first;
     free_.erase(it);
     return p;
   }
   void* p = nullptr;
   if (posix_memalign(&p, r >= HUGE_PAGE ? HUGE_PAGE : 64, r) != 0) return nullptr;
   if (r >= HUGE_PAGE) (void)madvise(p, r, MADV_HUGEPAGE);
-  live_.emplace(p, r);
+  live_[p] = r;  // overwrite: an address freed behind the pool's back may come back
   return p;
 }
 void HostPool::release(void* p) {
@@ -357,6 +359,10 @@ int emqx_gm_fanout_part(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_g
 int emqx_gm_csr_free(emqx_gm_ctx* ctx, emqx_gm_csr* csr) {
   if (!ctx || !csr) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  // a result CSR records its context (priv): its buffers belong to that
+  // context's pools, and handing them to another one would corrupt both
+  if (csr->priv && csr->priv != static_cast<void*>(ctx))
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "csr_free: the CSR belongs to another context");
   if (csr->on_device) {
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);

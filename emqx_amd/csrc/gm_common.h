@@ -123,6 +123,19 @@ struct IndexView {
   uint32_t root_flags;  // HOT_PLUS if "+" starts a filter
   uint32_t flags;       // IX_* below
   uint32_t rh_mask;     // bit t: hot table t is Robin Hood ordered (absent keys may exit early)
+  // Minimal-perfect-hash tables (mph_cap[t] != 0): slots [0, mph_cap) are
+  // placed by hash-and-displace (mph_slot: one probe, no chain, load ~0.97),
+  // slots [mph_cap, hot_cap) are a linear-probing overflow region for keys
+  // an in-place update could not put at their perfect slot (mph_ovf bit t set
+  // once it holds any).  One 64-bit word per bucket: the displacement (low 16
+  // bits) and a 48-bit Bloom filter over the bucket's keys, so ONE L2 read
+  // both rules out most absent keys (the exact-edge filter's job) and gives
+  // the slot.  See mph_* below.
+  const uint64_t* mph_word;          // per bucket: displacement | Bloom bits << 16
+  uint64_t mph_off[HOT_TABLES];      // word offset of each table's buckets
+  uint32_t mph_nb[HOT_TABLES];       // buckets of each MPH table
+  uint32_t mph_cap[HOT_TABLES];      // perfect-hash slots of each table; 0 = not an MPH table
+  uint32_t mph_ovf;                  // bit t: table t's overflow region holds keys
 };
 
 GM_HD uint64_t fmix64(uint64_t k) {
@@ -239,6 +252,71 @@ GM_HD uint64_t hot_slot(uint64_t key, uint64_t cap) {
 #else
   return (uint64_t(h) * cap) >> 32;
 #endif
+}
+
+// Hash-and-displace placement of the small upper hot tables (the depth-2
+// table, ~66k keys at C2/C3, shared by every topic's first two probes): the
+// key's bucket (hot_hash scaled to the bucket count) holds a 16-bit
+// displacement d, and the key's slot is mph_hash(key, d) scaled to the
+// table's perfect-hash region.  The builder picks each bucket's d so that all
+// its keys land on distinct free slots (largest buckets first), which fills
+// the region to ~0.97 with ONE probe per lookup: the table is a quarter of its
+// open-addressing size (0.25 load) and stays in each XCD's L2.
+constexpr uint32_t MPH_LAMBDA = 4;     // keys per bucket (2 B of bucket word per key)
+GM_HD uint32_t mph_hash(uint64_t key, uint32_t d) {
+  uint32_t h = (uint32_t(key >> 32) * 0x7FEB352Du) ^ (uint32_t(key) * 0x846CA68Bu) ^ (d * 0x9E3779B9u);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  return h;
+}
+GM_HD uint32_t scale32(uint32_t h, uint32_t n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umulhi(h, n);
+#else
+  return uint32_t((uint64_t(h) * n) >> 32);
+#endif
+}
+GM_HD uint32_t mph_bucket(uint64_t key, uint32_t nb) { return scale32(hot_hash(key), nb); }
+GM_HD uint32_t mph_slot(uint64_t key, uint32_t d, uint32_t cap) { return scale32(mph_hash(key, d), cap); }
+// the key's two Bloom bits in its bucket word (bits 16..63)
+GM_HD uint64_t mph_bloom(uint64_t key) {
+  const uint32_t h = (uint32_t(key >> 32) * 0x85EBCA6Bu) ^ (uint32_t(key) * 0xC2B2AE35u);
+  const uint32_t a = ((h >> 26) * 3u) >> 2, b = (((h >> 20) & 63u) * 3u) >> 2;  // 0..47 each
+  return (1ull << (16 + a)) | (1ull << (16 + b));
+}
+GM_HD bool mph_may_hold(uint64_t word, uint64_t key) {
+  const uint64_t m = mph_bloom(key);
+  return (word & m) == m;
+}
+// the overflow region [mph_cap, hot_cap): linear probing from this home
+GM_HD uint32_t mph_ovf_home(uint64_t key, uint32_t mcap, uint32_t cap) {
+  return mcap + scale32(hot_hash(key) ^ 0x5BD1E995u, cap - mcap);
+}
+
+// Host-side lookup of `key` in hot table t of view v, over a host copy of the
+// tables: slots from `base`, bucket words from `words` (the in-place update's
+// mirror, the host-only test index): the key's slot, or NONE.
+inline uint32_t hot_lookup_host(const IndexView& v, const HotSlot* base, const uint64_t* words, int t, uint64_t key) {
+  const uint64_t cap = v.hot_cap[t];
+  if (!cap) return NONE;
+  const HotSlot* tab = base + v.hot_off[t];
+  const uint32_t mc = v.mph_cap[t];
+  if (mc) {
+    const uint64_t w = words[v.mph_off[t] + mph_bucket(key, v.mph_nb[t])];
+    if (!mph_may_hold(w, key)) return NONE;
+    const uint32_t s = mph_slot(key, uint32_t(w & 0xFFFFu), mc);
+    if (tab[s].key == key) return s;
+    if (!((v.mph_ovf >> t) & 1u)) return NONE;
+    for (uint64_t o = mph_ovf_home(key, mc, uint32_t(cap));; o = o + 1 == cap ? mc : o + 1) {
+      if (tab[o].key == key) return uint32_t(o);
+      if (tab[o].key == EDGE_EMPTY) return NONE;
+    }
+  }
+  for (uint64_t s = hot_slot(key, cap);; s = s + 1 == cap ? 0 : s + 1) {
+    if (tab[s].key == key) return uint32_t(s);
+    if (tab[s].key == EDGE_EMPTY) return NONE;
+  }
 }
 
 // Exact-edge filter: for a hot table whose parents have many exact children

@@ -434,7 +434,7 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
   out->row_off = r_off;
   out->ids = r_ids;
   out->on_device = 0;
-  out->priv = nullptr;
+  out->priv = ctx;  // the owning context (emqx_gm_csr_free checks it)
   return 0;
 }
 

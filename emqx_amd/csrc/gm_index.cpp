@@ -401,6 +401,28 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (uint64_t i = 1; i < NN; ++i)
     if (nodes[i].kind != 2 && !inl[i]) hot_n[hot_table(nodes[i].depth)]++;
   uint64_t hot_off[HOT_TABLES], hot_cap[HOT_TABLES], hot_total = 0;
+  // Minimal-perfect-hash tables (gm_common.h, mph_*): a per-depth table of
+  // [GM_MPH_MIN_KEYS, GM_MPH_MAX_KEYS] keys is placed by hash-and-displace at
+  // load ~0.97 (C2/C3: the depth-2 table, 66.5k keys, 8.5 MB at 0.25 load ->
+  // 2.2 MB, which one XCD's 4 MB L2 keeps); smaller tables stay in L2 anyway and
+  // larger ones do not fit it either way.  GM_NO_MPH / the two bounds: A/B knobs.
+  uint32_t mph_cap[HOT_TABLES] = {0}, mph_nb[HOT_TABLES] = {0};
+  uint64_t mph_off[HOT_TABLES] = {0}, mph_total = 0;
+  {
+    uint64_t lo = 4096, hi = 131072;
+    if (const char* e = getenv("GM_MPH_MIN_KEYS")) lo = strtoull(e, nullptr, 10);
+    if (const char* e = getenv("GM_MPH_MAX_KEYS")) hi = strtoull(e, nullptr, 10);
+    for (int t = 1; t < HOT_TABLES - 1; ++t) {  // (the shared last table mixes depths: open addressing)
+      if (getenv("GM_NO_MPH") || hot_n[t] < lo || hot_n[t] > hi) continue;
+      mph_cap[t] = uint32_t(hot_n[t] + hot_n[t] / 32 + 16);
+      mph_nb[t] = uint32_t((hot_n[t] + MPH_LAMBDA - 1) / MPH_LAMBDA);
+      mph_off[t] = mph_total;
+      mph_total += mph_nb[t];
+    }
+  }
+  uint32_t mph_ovf = 0;
+  uint64_t mph_ovf_n[HOT_TABLES] = {0};
+  std::vector<uint64_t> mph_word(mph_total + 1, 0);
   uint64_t hot_load_pct = 25;  // load factor (%); GM_HOT_LOAD_PCT: A/B knob (10..90)
   if (const char* e = getenv("GM_HOT_LOAD_PCT")) hot_load_pct = std::min<uint64_t>(90, std::max<uint64_t>(10, strtoull(e, nullptr, 10)));
   for (int t = 0; t < HOT_TABLES; ++t) {
@@ -412,6 +434,9 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     if (const char* e = getenv("GM_HOT_LOAD_PCT_UPPER"))  // A/B knob: load of the depth 1-2 tables
       if (t <= 2) pct = std::min<uint64_t>(90, std::max<uint64_t>(10, strtoull(e, nullptr, 10)));
     hot_cap[t] = hot_n[t] ? std::max<uint64_t>(8, hot_n[t] * 100 / pct + 1) : 0;
+    // an MPH table: its perfect-hash region plus an overflow region for in-place
+    // inserts (load <= 0.5 there, Patcher::hot_add)
+    if (mph_cap[t]) hot_cap[t] = mph_cap[t] + std::max<uint64_t>(64, hot_n[t] / 16);
     if (hot_cap[t] > SLOT_MASK) throw std::length_error("hot table exceeds 2^30 slots");
     hot_off[t] = hot_total;
     hot_total += hot_cap[t];
@@ -434,10 +459,86 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // is in (the next depth's keys hold them).  The shared last table keeps
   // plain linear probing (its earlier depths' ids are already referenced).
   std::vector<uint32_t> occ;  // old node index per slot of the table being placed
+  auto fill_slot = [&](HotSlot& o, const HNode& h) {
+    o.sig = h.sig;
+    o.hf = hf_of(h);
+    o.end_filter = end_of(h);
+  };
   for (uint32_t d = 1; d <= max_depth; ++d) {
     const int t = hot_table(d);
     HotSlot* tab = hot.data() + hot_off[t];
     const uint64_t cap = hot_cap[t];
+    if (mph_cap[t]) {  // hash-and-displace (the depth is one table: t < HOT_TABLES-1)
+      std::vector<std::pair<uint64_t, uint32_t>> ks;  // (key, node) of the depth's slot owners
+      for (uint32_t k = by_depth_off[d]; k < by_depth_off[d + 1]; ++k) {
+        const uint32_t i = by_depth[k];
+        const HNode& h = nodes[i];
+        if (h.kind == 2 || hid[h.parent] == NONE) continue;
+        if (inl[i]) {
+          HotSlot& p = hot[hot_off[hot_table(d - 1)] + hid[h.parent]];
+          p.p_sig = h.sig;
+          p.p_hf = hf_of(h);
+          p.p_end = end_of(h);
+          hid[i] = hid[h.parent] | HOT_INLINE;
+          continue;
+        }
+        ks.emplace_back(hot_key(hid[h.parent], h.word, d - 1), i);
+      }
+      const uint32_t mc = mph_cap[t], nb = mph_nb[t];
+      std::vector<uint32_t> boff(nb + 1, 0), bk(ks.size());
+      for (const auto& kv : ks) boff[mph_bucket(kv.first, nb) + 1]++;
+      for (uint32_t b = 0; b < nb; ++b) boff[b + 1] += boff[b];
+      {
+        std::vector<uint32_t> cur(boff.begin(), boff.end() - 1);
+        for (uint32_t j = 0; j < ks.size(); ++j) bk[cur[mph_bucket(ks[j].first, nb)]++] = j;
+      }
+      std::vector<uint32_t> order(nb);
+      for (uint32_t b = 0; b < nb; ++b) order[b] = b;
+      std::stable_sort(order.begin(), order.end(),
+                       [&](uint32_t a, uint32_t b) { return boff[a + 1] - boff[a] > boff[b + 1] - boff[b]; });
+      std::vector<uint8_t> used(mc, 0);
+      uint32_t sl[64];
+      auto put = [&](uint32_t s, uint32_t j) {
+        tab[s].key = ks[j].first;
+        fill_slot(tab[s], nodes[ks[j].second]);
+        hid[ks[j].second] = s;
+      };
+      for (uint32_t b : order) {
+        const uint32_t sz = boff[b + 1] - boff[b];
+        if (!sz) break;  // (sorted by size)
+        bool ok = false;
+        if (sz <= 64) {
+          for (uint32_t dd = 0; dd < 65536 && !ok; ++dd) {
+            ok = true;
+            for (uint32_t q = 0; q < sz && ok; ++q) {
+              const uint32_t s2 = mph_slot(ks[bk[boff[b] + q]].first, dd, mc);
+              ok = !used[s2];
+              for (uint32_t r = 0; r < q && ok; ++r) ok = sl[r] != s2;
+              sl[q] = s2;
+            }
+            if (ok) {
+              mph_word[mph_off[t] + b] = dd;
+              for (uint32_t q = 0; q < sz; ++q) {
+                used[sl[q]] = 1;
+                put(sl[q], bk[boff[b] + q]);
+              }
+            }
+          }
+        }
+        for (uint32_t q = 0; q < sz; ++q) mph_word[mph_off[t] + b] |= mph_bloom(ks[bk[boff[b] + q]].first);
+        if (!ok) {  // (not expected at this load) the bucket's keys go to the overflow region
+          mph_ovf |= 1u << t;
+          for (uint32_t q = 0; q < sz; ++q) {
+            const uint32_t j = bk[boff[b] + q];
+            uint64_t s2 = mph_ovf_home(ks[j].first, mc, uint32_t(cap));
+            while (tab[s2].key != EDGE_EMPTY) s2 = s2 + 1 == cap ? mc : s2 + 1;
+            put(uint32_t(s2), j);
+            ++mph_ovf_n[t];
+          }
+        }
+      }
+      continue;
+    }
     const bool rh = t < HOT_TABLES - 1;
     if (rh) occ.assign(cap, NONE);
     auto home_dist = [&](uint64_t key, uint64_t pos) {
@@ -505,8 +606,9 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
             (unsigned long long)inl_n);
     for (int t = 0; t < HOT_TABLES; ++t)
       if (hot_n[t])
-        fprintf(stderr, "[gm_index] hot table %d: %llu slots used of %llu (%.1f MB)\n", t,
-                (unsigned long long)hot_n[t], (unsigned long long)hot_cap[t], hot_cap[t] * 32.0 / 1e6);
+        fprintf(stderr, "[gm_index] hot table %d: %llu slots used of %llu (%.1f MB)%s\n", t,
+                (unsigned long long)hot_n[t], (unsigned long long)hot_cap[t], hot_cap[t] * 32.0 / 1e6,
+                mph_cap[t] ? ((mph_ovf >> t) & 1u ? " mph+overflow" : " mph") : "");
   }
   phase("hot tables");
   // ---- 3c. exact-edge filters (gm_common.h), for tables whose parents have
@@ -524,6 +626,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (int t = 0; t < HOT_TABLES; ++t) {
     if (getenv("GM_NO_EDGE_FILTER")) break;  // A/B knob
     if (!ex_edges[t] || (ex_edges[t] < 4 * ex_parents[t] && !getenv("GM_EFILT_ALL"))) continue;  // A/B knob
+    if (mph_cap[t]) continue;  // an MPH table's bucket words carry its filter
     // 4-8 bits per key: the filter is a dependent read in front of every exact
     // probe and pays only while it stays in L2 (C2 A/B, bits per key -> kernel ms:
     // 16-32 10.04, 8-16 9.54, 4-8 9.37, 2-4 9.40, 1-2 9.60, no filter 9.50)
@@ -611,7 +714,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   size_t o_flen = o_arena + al(arena_cap + 64);
   size_t o_gmap = o_flen + al(flen_cap * 2 + 2);
   size_t o_efilt = o_gmap + al(idx->gmap.size() * 4 + 4);
-  size_t o_soff = o_efilt + al(efilt.size() * 4 + 4);
+  size_t o_mph = o_efilt + al(efilt.size() * 4 + 4);
+  size_t o_soff = o_mph + al(mph_word.size() * 8);
   // (a plain index's offsets stay zero past nf: appended filters have no subscribers)
   size_t o_sids = o_soff + al((keep_mirror && !sub_off ? flen_cap + 1 : soff.size()) * 8);
   size_t total = o_sids + al(sids.size() * 4 + 4);
@@ -656,6 +760,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   put(o_flen, flen.data(), flen.size() * 2);
   put(o_gmap, idx->gmap.data(), idx->gmap.size() * 4);
   put(o_efilt, efilt.data(), efilt.size() * 4);
+  put(o_mph, mph_word.data(), mph_word.size() * 8);
   if (!host_mirror) e = hipMemcpy(idx->dev_base, hb.data(), total, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipFree(idx->dev_base);
@@ -674,6 +779,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     m->o_arena = o_arena;
     m->o_flen = o_flen;
     m->o_efilt = o_efilt;
+    m->o_mph = o_mph;
     m->nodes_n = NN;
     m->nodes_cap = nodes_cap;
     m->arena_n = arena.size();
@@ -682,6 +788,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     m->dict_used = nw;
     for (int d = 0; d < EDGE_DEPTHS; ++d) m->edge_used[d] = tabs[d].used;
     for (int t = 0; t < HOT_TABLES; ++t) m->hot_used[t] = hot_n[t];
+    for (int t = 0; t < HOT_TABLES; ++t) m->mph_ovf_used[t] = mph_ovf_n[t];
     idx->mirror = m;
   }
   // the view's base: the device blob, or (host-only index) the mirror
@@ -709,6 +816,13 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     v.efilt_mask[t] = efilt_mask[t];
   }
   v.efilt = reinterpret_cast<const uint32_t*>(B + o_efilt);
+  v.mph_word = reinterpret_cast<const uint64_t*>(B + o_mph);
+  v.mph_ovf = mph_ovf;
+  for (int t = 0; t < HOT_TABLES; ++t) {
+    v.mph_off[t] = mph_off[t];
+    v.mph_nb[t] = mph_nb[t];
+    v.mph_cap[t] = mph_cap[t];
+  }
   v.root_sig = nodes[0].sig;
   v.root_hash = nodes[0].hash_child == NONE ? NONE : nodes[nodes[0].hash_child].end_filter;
   v.root_flags = nodes[0].plus_child != NONE ? HOT_PLUS : 0u;

@@ -123,13 +123,14 @@ struct OverlayState;
 // to the new one.
 struct Mirror {
   std::vector<uint8_t> blob;
-  size_t o_nodes = 0, o_dict = 0, o_edges = 0, o_hot = 0, o_arena = 0, o_flen = 0, o_efilt = 0;
+  size_t o_nodes = 0, o_dict = 0, o_edges = 0, o_hot = 0, o_arena = 0, o_flen = 0, o_efilt = 0, o_mph = 0;
   uint64_t nodes_n = 0, nodes_cap = 0;   // v1 level-trie nodes used / capacity
   uint64_t arena_n = 0, arena_cap = 0;   // word bytes used / capacity
   uint64_t flen_cap = 0;                 // filter-length entries available
   uint64_t dict_used = 0;
   uint64_t edge_used[EDGE_DEPTHS] = {};
   uint64_t hot_used[HOT_TABLES] = {};
+  uint64_t mph_ovf_used[HOT_TABLES] = {};  // keys in each MPH table's overflow region
 };
 }
 
@@ -147,6 +148,8 @@ struct emqx_gm_index {
   std::vector<uint64_t> foff;
   std::vector<uint32_t> gmap;   // shard index: global id of each local filter (ascending); empty otherwise
   std::vector<uint64_t> soff;   // subscriber CSR offsets per filter id (host copy; empty without subscribers)
+  std::vector<uint8_t> pinned;  // per filter: its route is held by another destination (emqx_gm_index_update_subs
+                                // ROUTE_ADD); empty: a built index, where a filter without subscribers is route-only
   gm::OverlayState* ov = nullptr;  // overlay snapshot (emqx_gm_index_update); tables above unused then
   uint64_t level_nodes = 0;        // an upper bound on the trie nodes of any one depth (the slow path's frontier); 0: unknown
   gm::Mirror* mirror = nullptr;    // host copy of the blob (updatable plain index), see gm::Mirror
@@ -216,6 +219,7 @@ uint64_t filter_rank(const emqx_gm_index* idx, const uint8_t* f, uint64_t len, b
 // gm_subs.cpp: emqx_gm_index_update_subs
 int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo, const uint32_t* subs,
                 const uint8_t* ops, uint64_t n_ops, emqx_gm_index** out);
+bool is_pinned(const emqx_gm_index* idx, uint64_t f);
 // gm_match.hip: segments [src_off[j], src_off[j] + (dst_off[j+1] - dst_off[j])) of
 // the device array src gathered into host `out` (dst_off[m] elements), one
 // device gather + one copy back

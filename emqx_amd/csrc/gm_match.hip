@@ -256,6 +256,40 @@ __device__ __forceinline__ uint32_t hot_resolve(const HotSlot* tab, uint32_t cap
   return s;
 }
 
+// The home slot of `key` in hot table ht (wave-uniform): an MPH table first
+// reads the key's bucket displacement (a small array that stays in L2), then
+// its one perfect slot; an open-addressing table hashes straight to the home.
+__device__ __forceinline__ uint32_t hot_home(const IndexView& ix, int ht, uint64_t key, uint64_t cap) {
+  if (const uint32_t mc = ix.mph_cap[ht]) {
+    const uint64_t w = ix.mph_word[ix.mph_off[ht] + mph_bucket(key, ix.mph_nb[ht])];
+    return mph_slot(key, uint32_t(w) & 0xFFFFu, mc);
+  }
+  return uint32_t(hot_slot(key, cap));
+}
+// An MPH table's bucket word for `key` (one L2 read): whether the table may
+// hold the key (its Bloom bits) and, if so, the key's perfect slot.
+__device__ __forceinline__ bool mph_gate(const IndexView& ix, int ht, uint64_t key, uint32_t mc, uint32_t& s) {
+  const uint64_t w = ix.mph_word[ix.mph_off[ht] + mph_bucket(key, ix.mph_nb[ht])];
+  s = mph_slot(key, uint32_t(w) & 0xFFFFu, mc);
+  return mph_may_hold(w, key);
+}
+// hot_resolve for either kind of table: an MPH table's key is at its perfect
+// slot, or (once an in-place update put keys there) in the overflow region.
+__device__ __forceinline__ uint32_t hot_resolve_x(const IndexView& ix, int ht, const HotSlot* tab, uint32_t cap,
+                                                  uint64_t key, uint32_t s, HotRec& r, bool with_end, bool flat,
+                                                  bool rh) {
+  if (const uint32_t mc = ix.mph_cap[ht]) {
+    if (hot_is(r, key)) return s;
+    if (!((ix.mph_ovf >> ht) & 1u)) return NONE;
+    for (s = mph_ovf_home(key, mc, cap);; s = s + 1 == cap ? mc : s + 1) {
+      r = hot_load(tab, s, with_end, flat);
+      if (hot_is(r, key)) return s;
+      if (hot_empty(r)) return NONE;
+    }
+  }
+  return hot_resolve(tab, cap, key, s, r, with_end, flat, rh);
+}
+
 // Per-lane match staging: emit one filter id into the topic's row (slot m_n
 // of the topic's lane column in its tile; srow = &stage[stage_index(tile, 0,
 // lane)]).
@@ -335,7 +369,7 @@ __device__ __forceinline__ bool plus_is_inline(uint32_t lvl, uint32_t id) { retu
         sx = NONE;                                                                      \
         rx = plus_inline_load(ptab, (e_id), hflat);                                        \
       } else {                                                                          \
-        sx = uint32_t(hot_slot(hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), cap)); \
+        sx = hot_home(ix, ht, hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), cap);    \
         rx = hot_load(tab, sx, last, hflat);                                            \
       }                                                                                 \
     }                                                                                   \
@@ -347,7 +381,7 @@ __device__ __forceinline__ bool plus_is_inline(uint32_t lvl, uint32_t id) { retu
       if ((plus) && sx == NONE) {                                                                         \
         GM_VISIT((e_id) | HOT_INLINE, rx);                                                                \
       } else {                                                                                            \
-        const uint32_t hs_ = hot_resolve(tab, capu, hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), sx, rx, last, hflat, hrh); \
+        const uint32_t hs_ = hot_resolve_x(ix, ht, tab, capu, hot_key((e_id), (plus) ? ix.plus_word : wid, lvl), sx, rx, last, hflat, hrh); \
         if (hs_ != NONE) GM_VISIT(hs_, rx);                                                               \
       }                                                                                                   \
     }                                                                                                     \
@@ -1127,31 +1161,35 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
 #ifdef GM_PROBE_STATS
       const bool st_cand = act && wid != NONE, st_sig = dx;
 #endif
-      if (fmask && dx) {  // the table's exact-edge filter (an L2 hit) before a random line
-        const uint32_t fh = edge_filter_hash(hot_key(id, wid, lvl));
-        const uint32_t fb = edge_filter_bits(fh);
-        dx = (ft[edge_filter_word(fh, fmask)] & fb) == fb;
-      }
-      const bool dp = act && (en.x & FR_PLUS);
+      bool dp = act && (en.x & FR_PLUS);
       probes += act ? 3u : 0u;
-      // issue both probes, then resolve
-      uint32_t sx = 0, sp = 0;
-      HotRec rx{}, rp{};
       const bool pin = dp && plus_is_inline(lvl, id);
-      if (dx) {
-        sx = uint32_t(hot_slot(hot_key(id, wid, lvl), cap));
-        rx = hot_load(tab, sx, last, hflat);
+      const uint64_t kx = hot_key(id, wid, lvl), kp = hot_key(id, ix.plus_word, lvl);
+      uint32_t sx = 0, sp = 0;
+      if (const uint32_t mc = ix.mph_cap[ht]) {
+        // an MPH table (wave-uniform): one L2 read of the key's bucket word
+        // filters the probe and gives its slot, in place of the exact-edge filter
+        if (dx) dx = mph_gate(ix, ht, kx, mc, sx);
+        if (dp && !pin) dp = mph_gate(ix, ht, kp, mc, sp);
+      } else {
+        if (fmask && dx) {  // the table's exact-edge filter (an L2 hit) before a random line
+          const uint32_t fh = edge_filter_hash(kx);
+          const uint32_t fb = edge_filter_bits(fh);
+          dx = (ft[edge_filter_word(fh, fmask)] & fb) == fb;
+        }
+        if (dx) sx = uint32_t(hot_slot(kx, cap));
+        if (dp && !pin) sp = uint32_t(hot_slot(kp, cap));
       }
+      // issue both probes, then resolve
+      HotRec rx{}, rp{};
+      if (dx) rx = hot_load(tab, sx, last, hflat);
       if (pin) {
         rp = plus_inline_load(ptab, id, hflat);
       } else if (dp) {
-        sp = uint32_t(hot_slot(hot_key(id, ix.plus_word, lvl), cap));
         rp = hot_load(tab, sp, last, hflat);
       }
-      const uint32_t hx = dx ? hot_resolve(tab, capu, hot_key(id, wid, lvl), sx, rx, last, hflat, hrh) : NONE;
-      const uint32_t hp = pin ? (id | HOT_INLINE)
-                              : dp ? hot_resolve(tab, capu, hot_key(id, ix.plus_word, lvl), sp, rp, last, hflat, hrh)
-                                   : NONE;
+      const uint32_t hx = dx ? hot_resolve_x(ix, ht, tab, capu, kx, sx, rx, last, hflat, hrh) : NONE;
+      const uint32_t hp = pin ? (id | HOT_INLINE) : dp ? hot_resolve_x(ix, ht, tab, capu, kp, sp, rp, last, hflat, hrh) : NONE;
 #ifdef GM_PROBE_STATS
       {
         const unsigned long long c[8] = {__ballot(act), __ballot(st_cand), __ballot(st_sig), __ballot(dx),
@@ -2396,7 +2434,7 @@ int finish_csr(emqx_gm_ctx* ctx, uint64_t n, uint64_t nnz, PoolBuf& row_off, Poo
                emqx_gm_csr* out) {
   out->n_rows = n;
   out->nnz = nnz;
-  out->priv = nullptr;
+  out->priv = ctx;  // the owning context (emqx_gm_csr_free checks it)
   if (device_out) {
     out->row_off = static_cast<uint64_t*>(row_off.release_ownership());
     out->ids = static_cast<uint32_t*>(ids.release_ownership());
@@ -2740,14 +2778,18 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   // assembled again below, once the host knows the total.
   // (at most FAST_MC per topic: a longer row is a slow-path row, assembled again anyway)
   const uint64_t cap_spec = 1024 + uint64_t(double(n) * std::min(ctx->ids_per_topic, double(FAST_MC)));
+  // (no room for the speculative buffer: skip speculation, the rows are
+  // assembled below at their exact size once the total is known)
   PoolBuf ids(ctx->pool, cap_spec * 4 + 16);
-  if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
-  launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
-                  row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec, blk);
-  GM_HIP(ctx, hipGetLastError());
-  if (tail && tail->enqueue) {
-    rc = tail->enqueue(row_off.as<uint64_t>(), ids.as<uint32_t>(), cap_spec);
-    if (rc) return rc;
+  const bool spec = ids.p != nullptr;
+  if (spec) {
+    launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
+                    row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec, blk);
+    GM_HIP(ctx, hipGetLastError());
+    if (tail && tail->enqueue) {
+      rc = tail->enqueue(row_off.as<uint64_t>(), ids.as<uint32_t>(), cap_spec);
+      if (rc) return rc;
+    }
   }
   uint64_t* const pin = static_cast<uint64_t*>(ctx->pin);  // [0] match total, [1..4] the counters
   GM_HIP(ctx, hipMemcpyAsync(pin, toff_p + n_tiles, 40, hipMemcpyDeviceToHost, st));
@@ -2755,7 +2797,7 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   GM_HIP(ctx, hipStreamSynchronize(st));
   uint64_t nnz = pin[0];
   const uint64_t h_ctr[4] = {pin[1], pin[2], pin[3], pin[4]};
-  if (uint32_t(h_ctr[0] >> 32) == 0 && nnz <= cap_spec) {  // no slow-path row, and the rows fit: done
+  if (spec && uint32_t(h_ctr[0] >> 32) == 0 && nnz <= cap_spec) {  // no slow-path row, and the rows fit: done
     ctx->stats.probes = h_ctr[2];
     ctx->stats.n_wildcard_topics = h_ctr[3];
     ctx->stats.n_overflow = uint32_t(h_ctr[0]);

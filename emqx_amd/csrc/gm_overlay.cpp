@@ -110,7 +110,8 @@ struct Patcher {
   uint32_t max_depth = 0;
   // undo log: every write first saves the bytes it overwrites (rollback on NoRoom)
   std::vector<uint8_t> undo_bytes;
-  uint64_t s_nodes_n, s_arena_n, s_dict_used, s_edge_used[EDGE_DEPTHS], s_hot_used[HOT_TABLES];
+  uint64_t s_nodes_n, s_arena_n, s_dict_used, s_edge_used[EDGE_DEPTHS], s_hot_used[HOT_TABLES],
+      s_mph_ovf_used[HOT_TABLES];
 
   Patcher(Mirror& m, IndexView& view) : M(m), v(view) {
     s_nodes_n = M.nodes_n;
@@ -118,6 +119,7 @@ struct Patcher {
     s_dict_used = M.dict_used;
     std::memcpy(s_edge_used, M.edge_used, sizeof(s_edge_used));
     std::memcpy(s_hot_used, M.hot_used, sizeof(s_hot_used));
+    std::memcpy(s_mph_ovf_used, M.mph_ovf_used, sizeof(s_mph_ovf_used));
   }
   uint8_t* B() { return M.blob.data(); }
   Node* nodes() { return reinterpret_cast<Node*>(B() + M.o_nodes); }
@@ -147,6 +149,7 @@ struct Patcher {
     M.dict_used = s_dict_used;
     std::memcpy(M.edge_used, s_edge_used, sizeof(s_edge_used));
     std::memcpy(M.hot_used, s_hot_used, sizeof(s_hot_used));
+    std::memcpy(M.mph_ovf_used, s_mph_ovf_used, sizeof(s_mph_ovf_used));
   }
 
   // ---- word dictionary (dict_resolve's rules: length + head, tail against the arena)
@@ -206,15 +209,8 @@ struct Patcher {
 
   // ---- hot tables
   HotSlot* htab(int t) { return hot() + v.hot_off[t]; }
-  uint32_t hot_find(int t, uint64_t key) {
-    const uint64_t cap = v.hot_cap[t];
-    if (!cap) return NONE;
-    HotSlot* tab = htab(t);
-    for (uint64_t s = hot_slot(key, cap);; s = s + 1 == cap ? 0 : s + 1) {
-      if (tab[s].key == key) return uint32_t(s);
-      if (tab[s].key == EDGE_EMPTY) return NONE;
-    }
-  }
+  uint64_t* mwords() { return reinterpret_cast<uint64_t*>(B() + M.o_mph); }
+  uint32_t hot_find(int t, uint64_t key) { return hot_lookup_host(v, hot(), mwords(), t, key); }
   // Slots never move (a slot index is a hot id other keys hold), so the key
   // goes to the first empty slot from its home.  That keeps the table's Robin
   // Hood order (hot_resolve's early exit) as long as no resident on the way is
@@ -222,8 +218,25 @@ struct Patcher {
   // table's early exit is switched off (rh_clear).
   uint32_t hot_add(int t, uint64_t key) {
     const uint64_t cap = v.hot_cap[t];
-    if (!cap || (M.hot_used[t] + 1) * 5 > cap * 3) throw NoRoom{};  // load <= 0.6
     HotSlot* tab = htab(t);
+    if (const uint32_t mc = v.mph_cap[t]) {
+      // a perfect-hash table: the key's own slot when it is free, else the
+      // overflow region (load <= 0.5; lookups probe it once its bit is set)
+      uint64_t& bw = mwords()[v.mph_off[t] + mph_bucket(key, v.mph_nb[t])];
+      W(bw) |= mph_bloom(key);  // the bucket's filter admits the new key (wherever it goes)
+      uint64_t s = mph_slot(key, uint32_t(bw & 0xFFFFu), mc);
+      if (tab[s].key != EDGE_EMPTY) {
+        if (M.mph_ovf_used[t] + 1 > (cap - mc) / 2) throw NoRoom{};
+        s = mph_ovf_home(key, mc, uint32_t(cap));
+        while (tab[s].key != EDGE_EMPTY) s = s + 1 == cap ? mc : s + 1;
+        ++M.mph_ovf_used[t];
+        v.mph_ovf |= 1u << t;
+      }
+      W(tab[s]) = HotSlot{key, 0, HF_NONE, NONE, 0, HF_NONE, NONE};
+      ++M.hot_used[t];
+      return uint32_t(s);
+    }
+    if (!cap || (M.hot_used[t] + 1) * 5 > cap * 3) throw NoRoom{};  // load <= 0.6
     const uint64_t home = hot_slot(key, cap);
     uint64_t s = home, dist = 0;
     bool rh_ok = true;
@@ -601,6 +614,7 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
   v.sub_off = trie_only ? nullptr : rebase(v.sub_off);  // trie_only: set by the caller
   v.sub_ids = trie_only ? nullptr : rebase(v.sub_ids);
   v.efilt = rebase(v.efilt);
+  v.mph_word = rebase(v.mph_word);
   idx->dev_flen = host ? nullptr : reinterpret_cast<uint16_t*>(NB + M.o_flen);
   emqx_gm_index_info_t& in = idx->info;
   in.n_filters = nf_new;

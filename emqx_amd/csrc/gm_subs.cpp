@@ -34,6 +34,8 @@ namespace {
 struct FilterEdit {
   uint32_t old_id = NONE;  // the filter's id in prev, or NONE
   bool had_subs = false;
+  bool was_pinned = false;  // prev holds the filter's route for another destination
+  int pin = -1;             // route_add (1) / route_delete (0) ops seen; -1: unchanged
   std::vector<uint32_t> list;                    // prev's list, then appended subscribers
   std::vector<uint8_t> dead;                     // per list entry: unsubscribed
   std::unordered_map<uint32_t, uint64_t> where;  // subscriber -> its live entry
@@ -50,6 +52,14 @@ struct FilterEdit {
     if (it == where.end() || dead[it->second]) return;  // only if present
     dead[it->second] = 1;
   }
+  bool pinned() const { return pin < 0 ? was_pinned : pin != 0; }
+  bool live() const {
+    for (uint8_t d : dead)
+      if (!d) return true;
+    return false;
+  }
+  // the filter stays a route while a local subscriber or another destination holds it
+  bool present() const { return live() || pinned(); }
   std::vector<uint32_t> final_list() const {
     std::vector<uint32_t> o;
     o.reserve(list.size());
@@ -63,6 +73,7 @@ struct FilterEdit {
 // Fallback: the updated set rebuilt from full host lists.
 int rebuild(emqx_gm_ctx* ctx, const emqx_gm_index* prev, const std::map<std::string, FilterEdit>& ed,
             emqx_gm_index** out) {
+  std::vector<uint8_t> pin_in;  // per input filter, in the order they are added below
   const uint64_t nb = prev->info.n_filters;
   std::vector<uint32_t> all(prev->soff.back());
   if (!all.empty())
@@ -73,7 +84,8 @@ int rebuild(emqx_gm_ctx* ctx, const emqx_gm_index* prev, const std::map<std::str
   std::vector<uint8_t> fb;
   std::vector<uint64_t> fo{0}, so{0};
   std::vector<uint32_t> si;
-  auto add = [&](const uint8_t* p, uint64_t len, const uint32_t* l, uint64_t cnt) {
+  auto add = [&](const uint8_t* p, uint64_t len, const uint32_t* l, uint64_t cnt, bool pinned) {
+    pin_in.push_back(pinned ? 1 : 0);
     fb.insert(fb.end(), p, p + len);
     fo.push_back(fb.size());
     si.insert(si.end(), l, l + cnt);
@@ -83,24 +95,34 @@ int rebuild(emqx_gm_ctx* ctx, const emqx_gm_index* prev, const std::map<std::str
     const uint8_t* p = prev->fbytes.data() + prev->foff[f];
     const uint64_t len = prev->foff[f + 1] - prev->foff[f];
     if (const FilterEdit* e = edit_of[f]) {
+      if (!e->present()) continue;  // the last subscriber left and no other destination: the route goes
       const std::vector<uint32_t> l = e->final_list();
-      if (e->had_subs && l.empty()) continue;  // the last subscriber left: the route goes
-      add(p, len, l.data(), l.size());
+      add(p, len, l.data(), l.size(), e->pinned());
     } else {
-      add(p, len, all.data() + prev->soff[f], prev->soff[f + 1] - prev->soff[f]);
+      add(p, len, all.data() + prev->soff[f], prev->soff[f + 1] - prev->soff[f], is_pinned(prev, f));
     }
   }
   for (const auto& kv : ed)
-    if (kv.second.old_id == NONE) {
+    if (kv.second.old_id == NONE && kv.second.present()) {
       const std::vector<uint32_t> l = kv.second.final_list();
-      if (!l.empty()) add(reinterpret_cast<const uint8_t*>(kv.first.data()), kv.first.size(), l.data(), l.size());
+      add(reinterpret_cast<const uint8_t*>(kv.first.data()), kv.first.size(), l.data(), l.size(), kv.second.pinned());
     }
   fb.resize(fb.size() + 64, 0);
   if (si.empty()) si.push_back(0);
-  return build_index(ctx, fb.data(), fo.data(), fo.size() - 1, so.data(), si.data(), nullptr, out);
+  std::vector<uint32_t> perm(pin_in.size() + 1);
+  const int rc = build_index(ctx, fb.data(), fo.data(), fo.size() - 1, so.data(), si.data(), perm.data(), out);
+  if (rc) return rc;
+  (*out)->pinned.assign((*out)->info.n_filters, 0);
+  for (size_t i = 0; i < pin_in.size(); ++i) (*out)->pinned[perm[i]] = pin_in[i];
+  return 0;
 }
 
 }  // namespace
+
+bool is_pinned(const emqx_gm_index* idx, uint64_t f) {
+  if (!idx->pinned.empty()) return idx->pinned[f] != 0;
+  return idx->soff.empty() || idx->soff[f + 1] == idx->soff[f];  // built: a filter without subscribers is route-only
+}
 
 int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo, const uint32_t* subs,
                 const uint8_t* ops, uint64_t n_ops, emqx_gm_index** out) {
@@ -146,26 +168,31 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
       FilterEdit& e = *touched[j];
       e.list.assign(all.begin() + dst_off[j], all.begin() + dst_off[j + 1]);
       e.had_subs = !e.list.empty();
+      e.was_pinned = is_pinned(prev, e.old_id);
       e.dead.assign(e.list.size(), 0);
       for (uint64_t k = 0; k < e.list.size(); ++k) e.where[e.list[k]] = k;
     }
   }
   // ---- the ops, in order
   for (uint64_t i = 0; i < n_ops; ++i) {
-    if (ops[i]) by_op[i]->subscribe(subs[i]);
-    else by_op[i]->unsubscribe(subs[i]);
+    switch (ops[i]) {
+      case EMQX_GM_SUB_UNSUBSCRIBE: by_op[i]->unsubscribe(subs[i]); break;
+      case EMQX_GM_SUB_SUBSCRIBE: by_op[i]->subscribe(subs[i]); break;
+      case EMQX_GM_SUB_ROUTE_ADD: by_op[i]->pin = 1; break;
+      case EMQX_GM_SUB_ROUTE_DELETE: by_op[i]->pin = 0; break;
+      default: return set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: op kind");
+    }
   }
   // ---- route changes: a first subscriber adds the route, the last one leaving deletes it
   std::set<uint32_t> tomb;
   std::set<std::string> dset;
   bool wf = true;
   for (const auto& kv : ed) {
-    uint64_t live = 0;
-    for (uint8_t d : kv.second.dead) live += d ? 0 : 1;
-    if (kv.second.old_id == NONE && live) {
+    const bool present = kv.second.present();
+    if (kv.second.old_id == NONE && present) {
       dset.insert(kv.first);
       wf = wf && well_formed_filter(reinterpret_cast<const uint8_t*>(kv.first.data()), kv.first.size());
-    } else if (kv.second.old_id != NONE && kv.second.had_subs && !live) {
+    } else if (kv.second.old_id != NONE && !present) {
       tomb.insert(kv.second.old_id);
     }
   }
@@ -238,6 +265,19 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
     return rc;
   }
   idx->info.n_subs = new_soff.back();
+  // the route-only marks of the new ids: untouched filters keep prev's, touched ones their final state
+  idx->pinned.assign(nf, 0);
+  for (uint64_t f = 0; f < nf; ++f)
+    if (inv[f] != NONE) idx->pinned[f] = is_pinned(prev, inv[f]) ? 1 : 0;
+  {
+    uint64_t k = 0;
+    for (const auto& kv : ed) {
+      uint32_t nid = NONE;
+      if (kv.second.old_id != NONE) nid = rmap[kv.second.old_id];
+      else if (dset.count(kv.first)) nid = rmap[nb + k++];
+      if (nid != NONE) idx->pinned[nid] = kv.second.pinned() ? 1 : 0;
+    }
+  }
   idx->soff = std::move(new_soff);
   *out = idx;
   return EMQX_GM_OK;

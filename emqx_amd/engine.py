@@ -227,15 +227,20 @@ class Context:
               self.h, "index_update")
         return Index(self, h, np.zeros(0, np.uint32))
 
+    SUB_OPS = {"unsubscribe": 0, "subscribe": 1, "route_add": 2, "route_delete": 3}
+
     def update_subs(self, index: Index, ops) -> Index:
         """A new snapshot of an index built with subscriber lists, with ``ops``
-        applied in order: (filter, subscriber id, subscribe: bool) -- a filter's
-        first subscriber adds its route, the last one leaving deletes it
+        applied in order: (filter, subscriber id, op) with op True/"subscribe",
+        False/"unsubscribe", or "route_add"/"route_delete" (the filter is routed to
+        another destination: it stays in the index without a local subscriber) --
+        a filter's first holder adds its route, the last one leaving deletes it
         (emqx_gm_index_update_subs).  ``index`` stays valid (RCU)."""
         ops = list(ops)
         fb, fo = pack([f for f, _, _ in ops])
         subs = np.array([s for _, s, _ in ops] or [0], np.uint32)
-        kinds = np.array([1 if sub else 0 for _, _, sub in ops] or [0], np.uint8)
+        kinds = np.array([(1 if k else 0) if isinstance(k, bool) else self.SUB_OPS[k] for _, _, k in ops] or [0],
+                         np.uint8)
         h = C.c_void_p()
         check(lib().emqx_gm_index_update_subs(self.h, index.h, _ptr(fb), _ptr(fo), _ptr(subs), _ptr(kinds), len(ops),
                                               C.byref(h)), self.h, "index_update_subs")

@@ -292,9 +292,18 @@ class Broker:
             filters = sorted(self.router._routes)
             if self._snap is not None and self._pending:
                 idx = self._context().update_subs(self._snap.index, self._pending)
-                if idx.n_filters == len(filters):
+                # the filters the library's snapshot holds: the previous ones, each
+                # touched filter kept iff it still has a subscriber (its route)
+                held = set(self._snap.filters)
+                for t in {t for t, _, _ in self._pending}:
+                    if self._direct.get(t) or any(v for k, v in self._shards.items() if k[0] == t):
+                        held.add(t)
+                    else:
+                        held.discard(t)
+                if idx.n_filters == len(held) and held == set(filters):
                     self._snap = _Snapshot(self._context(), filters, index=idx)
-                else:  # routes changed behind the broker's back (router.add_route): rebuild
+                else:  # routes changed behind the broker's back (router.add_route / a racing
+                    # add or delete_route outside the broker lock): rebuild from the lists
                     idx.release()
                     self._snap = None
                 self._pending = []

@@ -156,14 +156,25 @@ int emqx_gm_index_update(emqx_gm_ctx *ctx, emqx_gm_index *prev, const uint8_t *f
  * (emqx_broker:subscribe/2, unsubscribe/1 with the route added on a filter's
  * first subscriber and deleted after its last: apps/emqx/src/
  * emqx_broker.erl:147-165, 445-454, emqx_router.erl:112-125, 164-172).
- * Applies n_ops ops in order: ops[i] = 1 subscribes sub_ids[i] to filter i
- * (idempotent per pair), 0 unsubscribes it (only if present).  A subscribe
- * appends to the filter's list, an unsubscribe keeps the others' order.
+ * Applies n_ops ops in order: ops[i] = EMQX_GM_SUB_SUBSCRIBE subscribes
+ * sub_ids[i] to filter i (idempotent per pair), EMQX_GM_SUB_UNSUBSCRIBE
+ * unsubscribes it (only if present).  A subscribe appends to the filter's
+ * list, an unsubscribe keeps the others' order.  EMQX_GM_SUB_ROUTE_ADD /
+ * ROUTE_DELETE (sub_ids[i] ignored) mark / unmark filter i as routed to
+ * another destination (a remote node or a shared group: do_add_route/2 with
+ * a dest other than the local node): a filter is in the index while it has a
+ * local subscriber OR that mark, so its matches still come back (with an
+ * empty subscriber segment) for the caller's lookup_routes/1.  In a built
+ * index, a filter given no subscribers carries the mark.
  * Returns a NEW snapshot (RCU, as emqx_gm_index_update): route changes are
  * patched into a device copy of the newest snapshot's tables and the new
  * snapshot gets a subscriber CSR of its own; what the patch cannot take is
  * rebuilt.  EMQX_GM_EUNSUPPORTED for indexes without subscriber lists (use
  * emqx_gm_index_update), overlay snapshots and shard indexes. */
+#define EMQX_GM_SUB_UNSUBSCRIBE 0u
+#define EMQX_GM_SUB_SUBSCRIBE 1u
+#define EMQX_GM_SUB_ROUTE_ADD 2u
+#define EMQX_GM_SUB_ROUTE_DELETE 3u
 int emqx_gm_index_update_subs(emqx_gm_ctx *ctx, emqx_gm_index *prev, const uint8_t *filter_bytes,
                               const uint64_t *filter_off, const uint32_t *sub_ids, const uint8_t *ops,
                               uint64_t n_ops, emqx_gm_index **out);

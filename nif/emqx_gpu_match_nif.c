@@ -28,7 +28,8 @@ typedef struct {
 
 static ErlNifResourceType *INDEX_RT;
 static emqx_gm_ctx *CTX;
-static ERL_NIF_TERM A_OK, A_ERROR, A_BADARG, A_INSERT, A_DELETE, A_SUBSCRIBE, A_UNSUBSCRIBE;
+static ERL_NIF_TERM A_OK, A_ERROR, A_BADARG, A_INSERT, A_DELETE, A_SUBSCRIBE, A_UNSUBSCRIBE, A_ROUTE_ADD,
+    A_ROUTE_DELETE;
 
 static void index_dtor(ErlNifEnv *env, void *obj) {
   gm_index_res *r = (gm_index_res *)obj;
@@ -51,6 +52,8 @@ static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
   A_DELETE = enif_make_atom(env, "delete");
   A_SUBSCRIBE = enif_make_atom(env, "subscribe");
   A_UNSUBSCRIBE = enif_make_atom(env, "unsubscribe");
+  A_ROUTE_ADD = enif_make_atom(env, "route_add");
+  A_ROUTE_DELETE = enif_make_atom(env, "route_delete");
   return emqx_gm_open(&o, &CTX) == EMQX_GM_OK && INDEX_RT ? 0 : 1;
 }
 
@@ -202,11 +205,14 @@ static ERL_NIF_TERM update_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM ar
   return make_index_term(env, idx);
 }
 
-/* update_subs(Index, [{Filter :: binary(), SubId :: non_neg_integer(), subscribe | unsubscribe}])
+/* update_subs(Index, [{Filter :: binary(), SubId :: non_neg_integer(),
+ *                       subscribe | unsubscribe | route_add | route_delete}])
  *   -> {ok, NewIndex} | {error, Reason}
  * emqx_gm_index_update_subs on an index from load_index/2: emqx_broker's
  * subscribe/unsubscribe, with the route added on a filter's first subscriber
- * and deleted after its last. */
+ * and deleted after its last; route_add / route_delete (SubId ignored) mark a
+ * filter routed to another destination (a remote node, a shared group), which
+ * keeps it in the index without a local subscriber. */
 static ERL_NIF_TERM update_subs(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
   gm_index_res *r;
   unsigned len, i = 0;
@@ -225,15 +231,21 @@ static ERL_NIF_TERM update_subs(ErlNifEnv *env, int argc, const ERL_NIF_TERM arg
     const ERL_NIF_TERM *tup;
     int arity;
     unsigned s;
-    if (!enif_get_tuple(env, h, &arity, &tup) || arity != 3 || !enif_get_uint(env, tup[1], &s) ||
-        (!enif_is_identical(tup[2], A_SUBSCRIBE) && !enif_is_identical(tup[2], A_UNSUBSCRIBE))) {
-      enif_free(ops);
-      enif_free(subs);
-      return enif_make_badarg(env);  /* only subscribe | unsubscribe */
-    }
+    uint8_t kind;
+    if (!enif_get_tuple(env, h, &arity, &tup) || arity != 3 || !enif_get_uint(env, tup[1], &s)) goto bad;
+    if (enif_is_identical(tup[2], A_SUBSCRIBE)) kind = EMQX_GM_SUB_SUBSCRIBE;
+    else if (enif_is_identical(tup[2], A_UNSUBSCRIBE)) kind = EMQX_GM_SUB_UNSUBSCRIBE;
+    else if (enif_is_identical(tup[2], A_ROUTE_ADD)) kind = EMQX_GM_SUB_ROUTE_ADD;
+    else if (enif_is_identical(tup[2], A_ROUTE_DELETE)) kind = EMQX_GM_SUB_ROUTE_DELETE;
+    else goto bad;
     fl = enif_make_list_cell(env, tup[0], fl);
     subs[i] = s;
-    ops[i++] = enif_is_identical(tup[2], A_SUBSCRIBE) ? 1 : 0;
+    ops[i++] = kind;
+    continue;
+  bad:
+    enif_free(ops);
+    enif_free(subs);
+    return enif_make_badarg(env);
   }
   if (!enif_make_reverse_list(env, fl, &fl) || !pack_list(env, fl, &fb, &fo, &n)) {
     enif_free(ops);
@@ -328,8 +340,13 @@ static ERL_NIF_TERM fanout_batch(ErlNifEnv *env, int argc, const ERL_NIF_TERM ar
       uint64_t l, c, j;
       ERL_NIF_TERM subs = enif_make_list(env, 0);
       const uint32_t f = m.ids[k - 1];
-      emqx_gm_index_filter(r->idx, f, &p, &l);
-      emqx_gm_index_subscriber_count(r->idx, f, &c);
+      if (emqx_gm_index_filter(r->idx, f, &p, &l) != EMQX_GM_OK ||
+          emqx_gm_index_subscriber_count(r->idx, f, &c) != EMQX_GM_OK || c > d_pos - d.row_off[i]) {
+        enif_free(rows);
+        emqx_gm_csr_free(CTX, &m);
+        emqx_gm_csr_free(CTX, &d);
+        return error_tuple(env, EMQX_GM_EINVAL);
+      }
       for (j = 0; j < c; ++j) subs = enif_make_list_cell(env, enif_make_uint(env, d.ids[d_pos - 1 - j]), subs);
       d_pos -= c;
       row = enif_make_list_cell(env, enif_make_tuple2(env, enif_make_resource_binary(env, r, p, l), subs), row);

@@ -86,6 +86,7 @@ uint32_t v_edge_get(const IndexView& v, uint32_t depth, uint32_t parent, uint32_
 uint32_t v_hot_lookup(const IndexView& v, int t, uint64_t key, bool rh) {
   const uint64_t cap = v.hot_cap[t];
   if (!cap) return NONE;
+  if (v.mph_cap[t]) return hot_lookup_host(v, v.hot, v.mph_word, t, key);  // a perfect-hash table
   const HotSlot* tab = v.hot + v.hot_off[t];
   uint64_t s = hot_slot(key, cap), dist = 0;
   for (uint64_t step = 0; step < cap; ++step) {

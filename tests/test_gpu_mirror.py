@@ -89,37 +89,84 @@ def test_topic_rule_index_vs_predicate(ctx, orc):
 
 @pytest.mark.gpu
 def test_publish_batcher_c_abi_sequence_vs_oracle(orc):
-    """The NIF's fanout_batch/2 sequence (index built with subscriber lists ->
-    emqx_gm_match WITH_EXACT -> emqx_gm_fanout -> rows cut into per-filter
-    groups by emqx_gm_index_subscriber_count) behind the aggregator: every
-    publish's deliveries equal the oracle's dispatch fold, group by group."""
+    """The aggregator end to end on the GPU (emqx_amd/batcher.py, the mirror of
+    nif/emqx_gpu_match_batcher.erl): GpuRoutes keeps ONE index over the route
+    filters -- local subscribers as fan-out lists, remote-node and shared-group
+    destinations as route marks -- derived by update_subs from the previous
+    snapshot after every subscription change (never rebuilt); each publish's
+    local deliveries equal the oracle's match_routes + dispatch fold, and its
+    remote / shared routes come back as route entries (forward, shared
+    dispatch) exactly for the filters the oracle matches."""
     from emqx_amd import Context
-    from emqx_amd.batcher import FanoutGroups, PublishBatcher
+    from emqx_amd.batcher import GpuRoutes, PublishBatcher
     rng = np.random.default_rng(5)
-    filters = sorted({b"a/#", b"a/+", b"a/b", b"+/b", b"#", b"c/d", b"a/+/c", b"$SYS/#", b"c/+"})
-    subs = [sorted(set(rng.integers(0, 500, size=int(rng.integers(0, 40))).tolist())) for _ in filters]
-    topics = [b"a/b", b"a/x", b"c/d", b"q", b"a/b/c", b"$SYS/a", b"c/e", b"a/+"] * 40
+    filters = sorted({b"a/#", b"a/+", b"a/b", b"+/b", b"#", b"c/d", b"a/+/c", b"$SYS/#", b"c/+", b"r/+", b"s/#"})
+    topics = [b"a/b", b"a/x", b"c/d", b"q", b"a/b/c", b"$SYS/a", b"c/e", b"a/+", b"r/1", b"s/x/y"] * 40
     with Context(0) as ctx:
-        idx = ctx.build_index(filters, subs=subs)
-        inbox = {i: [] for i in range(500)}
-        b = PublishBatcher(FanoutGroups(ctx, idx, filters), max_batch=64, window_s=0.002, subscribers=inbox)
-        futs = [b.publish(t, k) for k, t in enumerate(topics)]
-        results = [f.result(timeout=60) for f in futs]
-        b.close()
-        assert b.batches >= len(topics) // 64
-        r = orc.Router(True)
+        routes = GpuRoutes(ctx)
+        local = {f: set() for f in filters}       # filter -> local subscriber names
+        other = {f: [] for f in filters}          # filter -> non-local destinations
         for f in filters:
-            r.add_route(f)
-        oro, oids, _ = r.match_batch(topics, filters, mode=1)
-        so = np.zeros(len(filters) + 1, np.uint64)
-        so[1:] = np.cumsum([len(s) for s in subs])
-        si = np.array([x for s in subs for x in s] or [0], np.uint32)
-        ero, eids = orc.fanout(oro, oids, so, si)
-        for k, t in enumerate(topics):
-            want = [(filters[f], ("ok", len(subs[f])) if subs[f] else ("error", "no_subscribers"))
-                    for f in oids[oro[k]:oro[k + 1]]]
-            assert results[k] == want, t
-        got = sorted((sid, k) for sid, box in inbox.items() for _, k in box)
-        exp = sorted((int(s), k) for k in range(len(topics)) for s in eids[ero[k]:ero[k + 1]])
-        assert got == exp
-        idx.release()
+            if f in (b"r/+",):
+                continue  # a remote-only filter
+            for sname in sorted(set(rng.integers(0, 300, size=int(rng.integers(0, 30))).tolist())):
+                routes.subscribe(f, sname)
+                local[f].add(sname)
+        for f, d in [(b"r/+", b"n2"), (b"a/+", b"n2"), (b"a/+", b"n3"), (b"s/#", (b"g1", b"node")),
+                     (b"s/#", (b"g1", b"n2")), (b"c/d", (b"g2", b"n3"))]:
+            routes.route_add(f, d)
+            other[f].append(d)
+        inbox = {k: [] for k in range(300)}
+        fwd, shared = [], []
+
+        def run(tag):
+            b = PublishBatcher(routes.groups, max_batch=64, window_s=0.002, subscribers=routes.subs,
+                               deliver=lambda sub, f, m: inbox[sub].append((f, m)) or True,
+                               lookup_routes=lambda f: ([b"node"] if local[f] else []) + other[f],
+                               others=routes.other,
+                               forward=lambda n, f, m: fwd.append((n, f, m)) or ("ok", 1),
+                               shared_dispatch=lambda g, f, m: shared.append((g, f, m)) or ("ok", 1))
+            for box in inbox.values():
+                box.clear()
+            fwd.clear()
+            shared.clear()
+            res = b.publish_batch([(t, (tag, k)) for k, t in enumerate(topics)])
+            b.close()
+            live = sorted(f for f in filters if local[f] or other[f])
+            r = orc.Router(True)
+            for f in live:
+                r.add_route(f)
+            oro, oids, _ = r.match_batch(topics, live, mode=1)
+            for k, t in enumerate(topics):
+                matched = [live[i] for i in oids[oro[k]:oro[k + 1]]]
+                want = [(b"node", f, ("ok", len(local[f]))) for f in matched if local[f]]
+                want += [(d, f, ("ok", 1)) for f in matched for d in other[f] if not isinstance(d, tuple)]
+                want += [("share", f, ("ok", 1)) for f in matched for g in sorted({d[0] for d in other[f]
+                                                                                 if isinstance(d, tuple)})]
+                assert sorted(res[k], key=repr) == sorted(want, key=repr), t
+                for f in matched:
+                    for d in other[f]:
+                        if isinstance(d, tuple):
+                            continue
+                        assert (d, f, (tag, k)) in fwd
+            got = sorted((s, m) for s, box in inbox.items() for _, m in box)
+            exp = sorted((s, (tag, k)) for k, t in enumerate(topics)
+                         for i in oids[oro[k]:oro[k + 1]] for s in local[live[i]])
+            assert got == exp
+
+        run("first")
+        u0 = routes.updates
+        # subscription changes between batches: a last local subscriber leaving a
+        # filter that keeps a remote route, a new filter, a remote route dropped
+        for sname in sorted(local[b"a/+"]):
+            routes.unsubscribe(b"a/+", sname)
+        local[b"a/+"].clear()
+        routes.subscribe(b"new/+", 7)
+        filters.append(b"new/+")
+        local[b"new/+"], other[b"new/+"] = {7}, []
+        routes.route_delete(b"r/+", b"n2")
+        other[b"r/+"] = []
+        topics += [b"new/1"] * 5
+        run("second")
+        assert routes.updates == u0 + 1 and routes.builds == 1  # one update_subs, no rebuild
+        assert routes.index.n_filters == len([f for f in filters if local[f] or other[f]])

@@ -125,8 +125,11 @@ def _rand_topic(rng):
     return "/".join(ws)
 
 
+@pytest.mark.parametrize("mph", [False, True], ids=["open_addressing", "mph_all_tables"])
 @pytest.mark.parametrize("exact", [True, False], ids=["match_routes", "trie_match"])
-def test_random_small_sets(ctx, orc, exact):
+def test_random_small_sets(ctx, orc, exact, mph, monkeypatch):
+    if mph:  # every per-depth hot table placed by hash-and-displace (default: 4k..128k-key tables)
+        monkeypatch.setenv("GM_MPH_MIN_KEYS", "1")
     rng = random.Random(11)
     for _ in range(40):
         filters = [_rand_filter(rng) for _ in range(rng.randint(1, 60))]
@@ -134,7 +137,10 @@ def test_random_small_sets(ctx, orc, exact):
         _check(ctx, orc, filters, topics, exact)
 
 
-def test_edge_cases(ctx, orc):
+@pytest.mark.parametrize("mph", [False, True], ids=["open_addressing", "mph_all_tables"])
+def test_edge_cases(ctx, orc, mph, monkeypatch):
+    if mph:
+        monkeypatch.setenv("GM_MPH_MIN_KEYS", "1")
     filters = ["#", "+", "+/+", "/#", "/+", "$SYS/#", "$SYS/+", "$SYS", "sport/", "sport/+", "sport/#", "a/+/#",
                "", "+/#", "a//b", "a/+/b", "x/y", "a/+", "a/#/b", "é/+"]
     topics = ["", "/", "//", "sport", "sport/", "sport/x", "$SYS", "$SYS/", "$SYS/a", "$SYS/a/b", "a", "a/b",
@@ -774,3 +780,32 @@ def test_compact_staging_vs_columns(ctx, orc, monkeypatch, listed_cap):
         ro, ids = ctx.match(idx, topics, exact=True)
         assert np.array_equal(ro, oro) and np.array_equal(ids, oids), mode
     idx.release()
+
+
+def test_host_csr_ownership_across_contexts(ctx, orc):
+    """A result CSR records its context: freeing it through another context is
+    refused (its buffers belong to the first context's pool), and host rows
+    still held after emqx_gm_close stay readable (the pool detaches them)."""
+    import ctypes as C
+    from emqx_amd import Context
+    from emqx_amd._lib import Csr, lib, WITH_EXACT, EINVAL
+    from emqx_amd.engine import pack, _ptr
+    filters = [b"a/+", b"a/#", b"b/c"]
+    topics = [b"a/x", b"b/c", b"q"] * 100
+    other = Context(0)
+    try:
+        idx = other.build_index(filters)
+        tb, to = pack(topics)
+        csr = Csr()
+        assert lib().emqx_gm_match(other.h, idx.h, _ptr(tb), _ptr(to), len(topics), WITH_EXACT, C.byref(csr)) == 0
+        assert lib().emqx_gm_csr_free(ctx.h, C.byref(csr)) == EINVAL  # not this context's CSR
+        ro = np.ctypeslib.as_array(csr.row_off, shape=(len(topics) + 1,)).copy()
+        idx.release()
+    finally:
+        other.close()
+    # after close the rows are detached, not freed: still readable and unchanged
+    ro2 = np.ctypeslib.as_array(csr.row_off, shape=(len(topics) + 1,)).copy()
+    ids = np.ctypeslib.as_array(csr.ids, shape=(int(csr.nnz),)).copy()
+    assert np.array_equal(ro, ro2)
+    oro, oids = _oracle_rows(orc, sorted(filters), topics, 1)
+    assert np.array_equal(ro2, oro) and np.array_equal(ids, oids)

@@ -19,13 +19,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["patch", "overlay"])
+@pytest.fixture(params=["patch", "patch_mph", "overlay"])
 def form(request, monkeypatch):
     if request.param == "overlay":
         monkeypatch.setenv("GM_UPDATE_OVERLAY", "1")
     else:
         monkeypatch.delenv("GM_UPDATE_OVERLAY", raising=False)
-    return request.param
+    if request.param == "patch_mph":  # every per-depth table hash-and-displace placed: inserts take the overflow region
+        monkeypatch.setenv("GM_MPH_MIN_KEYS", "1")
+    return "patch" if request.param == "patch_mph" else request.param
 
 
 def _is_flat(ctx, idx):
@@ -275,20 +277,26 @@ class _Broker:
     def __init__(self, subs):
         self.lists = {f: list(l) for f, l in subs.items()}
         self.indexed = set(subs)
+        # routed to another destination (a remote node, a shared group): a
+        # filter built without local subscribers, or marked by route_add
+        self.pinned = {f for f, l in subs.items() if not l}
 
     def apply(self, ops):
-        before = {f: len(self.lists.get(f, [])) for f, _, _ in ops}
-        for f, s, sub in ops:
+        touched = {f for f, _, _ in ops}
+        for f, s, kind in ops:
             l = self.lists.setdefault(f, [])
-            if sub and s not in l:
+            if kind == "route_add":
+                self.pinned.add(f)
+            elif kind == "route_delete":
+                self.pinned.discard(f)
+            elif kind and s not in l:
                 l.append(s)
-            elif not sub and s in l:
+            elif not kind and s in l:
                 l.remove(s)
-        for f in before:
-            n = len(self.lists.get(f, []))
-            if f not in self.indexed and n:
+        for f in touched:  # a route while a local subscriber or another destination holds it
+            if self.lists.get(f) or f in self.pinned:
                 self.indexed.add(f)
-            elif f in self.indexed and before[f] and not n:
+            else:
                 self.indexed.discard(f)
 
     def csr(self):
@@ -342,13 +350,19 @@ def test_update_subs_vs_oracle(ctx, orc, monkeypatch):
                 f = rng.choice(sorted(br.lists))
                 if br.lists[f]:
                     ops.append((f, rng.choice(br.lists[f]), False))
-            elif br.indexed:  # all subscribers of a filter leave: its route goes
+            elif k < 0.92 and br.indexed:  # all subscribers of a filter leave: its route goes (unless pinned)
                 f = rng.choice(sorted(br.indexed))
                 ops += [(f, s, False) for s in list(br.lists.get(f, []))]
                 ops.append((f, 99_999, False))  # an absent pair: no-op
+            elif k < 0.96:  # another destination takes / holds a route (new or existing filter)
+                f = rng.choice(sorted(br.indexed)) if br.indexed and rng.random() < 0.5 else _rand_filter(rng).encode()
+                ops.append((f, 0, "route_add"))
+            elif br.pinned:  # ... and leaves it
+                ops.append((rng.choice(sorted(br.pinned)), 0, "route_delete"))
         prev_state = _Broker({})
         prev_state.lists = {f: list(l) for f, l in br.lists.items()}
         prev_state.indexed = set(br.indexed)
+        prev_state.pinned = set(br.pinned)
         br.apply(ops)
         new = ctx.update_subs(idx, ops)
         _check_subs(ctx, orc, new, br, topics)
@@ -378,6 +392,7 @@ def test_update_subs_vs_oracle(ctx, orc, monkeypatch):
     older_state = _Broker({})
     older_state.lists = {f: list(l) for f, l in br.lists.items()}
     older_state.indexed = set(br.indexed)
+    older_state.pinned = set(br.pinned)
     newer = ctx.update_subs(new, [(b"z/z", 1, True)])
     older = ctx.update_subs(new, [(b"z/q", 2, True)])  # new has no mirror now: rebuilt
     older_state.apply([(b"z/q", 2, True)])

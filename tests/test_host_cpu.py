@@ -209,7 +209,8 @@ def test_nif_exports_match_erlang_module():
     assert nif == stubs, (nif ^ stubs)
 
 
-def test_host_compiler_under_asan():
+@pytest.mark.parametrize("mph_min", [None, "1"], ids=["default", "mph_all_tables"])
+def test_host_compiler_under_asan(mph_min):
     """The host index compiler (gm_index.cpp) and the overlay id mapping
     (gm_overlay.cpp) built with AddressSanitizer + UBSan and fed random,
     empty, NUL-laden, 65,535-byte and 5,000-level filters (SURVEY.md §5;
@@ -219,6 +220,8 @@ def test_host_compiler_under_asan():
     b = subprocess.run(["make", "-C", os.path.join(ROOT, "emqx_amd", "csrc"), "asan"], capture_output=True, text=True)
     assert b.returncode == 0, b.stderr[-3000:]
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    if mph_min:  # every per-depth table placed by hash-and-displace, in-place inserts into its overflow region
+        env["GM_MPH_MIN_KEYS"] = mph_min
     p = subprocess.run([os.path.join(ROOT, "tests", "asan", "asan_host_compiler")], capture_output=True, text=True,
                        env=env, timeout=300)
     assert p.returncode == 0 and "ASAN_HOST_CHECK_OK" in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
