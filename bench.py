@@ -43,6 +43,10 @@ def parse():
                    help="timed steps (default 5; C1's 0.13-ms step: 200, so the timed region is not noise)")
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2; C1: 20)")
     p.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    p.add_argument("--plan", default="replicated", choices=["replicated", "hash"],
+                   help="C5: the unsharded index replicated on every GPU with the batch partitioned (north_star: "
+                        "replicate while the index fits 288 GB; 100M filters = 38 GB), or filters hash-sharded "
+                        "with the rows exchanged (all-to-all) and merged")
     p.add_argument("--filters", type=int, default=None)
     p.add_argument("--topics", type=int, default=None, help="topics per GPU per step")
     p.add_argument("--seed", type=int, default=1)
@@ -276,6 +280,19 @@ def parity_sample(ctx, r, res, codes, fpack_sorted, seed, first_topic, n_topics,
             "mismatched_windows": bad[:8]}
 
 
+def fixture_check(ctx, idx, name):
+    """The committed config fixture (tests/golden/config_<name>.json: strided
+    topics of the config's stream, their match_routes rows as filter strings)
+    matched through the host-buffer call against this index."""
+    with open(os.path.join(ROOT, "tests", "golden", f"config_{name}.json")) as f:
+        fx = json.load(f)
+    ro, ids = ctx.match(idx, [t.encode() for t in fx["topics"]], exact=True)
+    got = [[idx.filter(int(k)).decode() for k in ids[ro[i]:ro[i + 1]]] for i in range(len(fx["topics"]))]
+    bad = [i for i, (g, w) in enumerate(zip(got, fx["matches"])) if g != w]
+    return {"topics": len(got), "fixture": f"tests/golden/config_{name}.json", "ok": not bad,
+            "mismatched_topics": bad[:8]}
+
+
 def ctypes_ptr(p) -> int:
     import ctypes
     return ctypes.cast(p, ctypes.c_void_p).value or 0
@@ -291,10 +308,10 @@ def main():
     cfg = a.config
     if cfg == "c4":
         return bench_c4(a, world, rank, local, pg)
-    if cfg == "c5":
+    if cfg == "c5" and a.plan == "hash":
         return bench_c5(a, world, rank, local, pg)
-    n_filters = a.filters or {"c1": 10_000, "c2": 1_000_000, "c3": 10_000_000}[cfg]
-    n_topics = a.topics or {"c1": 1_000_000, "c2": 100_000_000, "c3": 100_000_000}[cfg]
+    n_filters = a.filters or {"c1": 10_000, "c2": 1_000_000, "c3": 10_000_000, "c5": 100_000_000}[cfg]
+    n_topics = a.topics or {"c1": 1_000_000, "c2": 100_000_000, "c3": 100_000_000, "c5": 100_000_000}[cfg]
     wildcard_only = cfg == "c2"
 
     ctx = Context(local)
@@ -353,7 +370,9 @@ def main():
         "vs_baseline": None, "dtype": "u8", "data": "synthetic (seeded §8d generator, topics generated on device)",
         "config": {"workload": {"c1": "C1: 10k mixed filters, 1M topics", "c2": "C2: 1M wildcard filters, "
                                 "100M-topic publish batch per GPU", "c3": "C3: 10M mixed filters, replicated index, "
-                                "100M topics per GPU"}[cfg] + " (match_routes semantics, CSR of sorted filter ids)",
+                                "100M topics per GPU", "c5": "C5: 100M mixed filters, replicated index (the "
+                                "unsharded index fits one GPU), 100M topics per GPU"}[cfg]
+                   + " (match_routes semantics, CSR of sorted filter ids)",
                    "filters": int(idx.n_filters), "topics_per_gpu": n_topics,
                    "parallelism": f"replicated index, batch partitioned over {world} GPU(s)"},
         "matches_per_sec": world * nnz * a.steps / elapsed,
@@ -385,7 +404,7 @@ def main():
         out["detail"]["host_io_ms"] = best * 1e3
         out["detail"]["host_io_nnz_matches_device"] = ok
         del hb, ho
-    if rank == 0 and world == 1 and not a.no_update:
+    if rank == 0 and world == 1 and not a.no_update and cfg != "c5":
         # incremental maintenance, outside the timed region: 100 deletes +
         # 100 inserts patched into this index, and a match of the same batch on the result
         rng = np.random.default_rng(7)
@@ -402,10 +421,14 @@ def main():
         out["detail"]["index_update"] = {"ops": 200, "update_ms": upd_ms, "match_kernel_ms_after": min(ks),
                                          "vs_flat": min(ks) / min(kern_ms)}
         new.release()
+    if cfg == "c5" and rank == 0 and not a.no_parity:
+        # the oracle over 100M keys does not fit the box's memory: the committed C5
+        # fixture (2,000 strided topics of the stream, rows as filter strings) instead
+        out["parity_sample"] = fixture_check(ctx, idx, "c5")
     # the cpu_baseline leg (oracle): timed on all host cores at N=1, and, outside the
     # timed region, the last step's CSR checked against it on a strided sample
-    want_cpu = rank == 0 and world == 1 and not a.no_cpu
-    want_parity = rank == 0 and not a.no_parity
+    want_cpu = rank == 0 and world == 1 and not a.no_cpu and cfg != "c5"
+    want_parity = rank == 0 and not a.no_parity and cfg != "c5"
     if want_cpu or want_parity:
         threads = a.cpu_threads or len(os.sched_getaffinity(0))
         r = oracle_router(fpack)

@@ -292,8 +292,7 @@ int emqx_gm_index_filter(const emqx_gm_index* idx, uint32_t id, const uint8_t** 
     id = uint32_t(it - idx->gmap.begin());
   }
   if (id >= idx->info.n_filters) return EMQX_GM_EINVAL;
-  *bytes = idx->fbytes.data() + idx->foff[id];
-  *len = idx->foff[id + 1] - idx->foff[id];
+  *bytes = idx->ft.at(id, len);
   return EMQX_GM_OK;
 }
 

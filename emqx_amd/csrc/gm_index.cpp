@@ -174,7 +174,9 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   sort_filters_impl(ord, fb, fo);
   std::vector<uint32_t> id_of(n);
   uint32_t nf = 0;
-  idx->foff.push_back(0);
+  auto sorted = std::make_shared<SortedFilters>();  // becomes idx->ft's base
+  std::vector<uint8_t>& FBV = sorted->bytes;
+  std::vector<uint64_t>& FOV = sorted->off;
   for (uint64_t k = 0; k < n; ++k) {
     uint32_t i = ord[k];
     bool dup = false;
@@ -184,12 +186,13 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       dup = lp == li && std::memcmp(fb + fo[p], fb + fo[i], li) == 0;
     }
     if (!dup) {
-      idx->fbytes.insert(idx->fbytes.end(), fb + fo[i], fb + fo[i + 1]);
-      idx->foff.push_back(idx->fbytes.size());
+      FBV.insert(FBV.end(), fb + fo[i], fb + fo[i + 1]);
+      FOV.push_back(FBV.size());
       ++nf;
     }
     id_of[i] = nf - 1;
   }
+  idx->ft.set_base(sorted);  // (the same vectors: FBV / FOV stay valid)
   if (perm_out)
     for (uint64_t i = 0; i < n; ++i) perm_out[i] = id_of[i];
   // shard index: rows carry the filters' global ids, which
@@ -221,8 +224,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   std::vector<uint64_t> word_head;
   uint64_t total_words = 0;
   for (uint32_t f = 0; f < nf; ++f) {
-    uint64_t a = idx->foff[f], b = idx->foff[f + 1];
-    total_words += 1 + std::count(idx->fbytes.begin() + a, idx->fbytes.begin() + b, uint8_t('/'));
+    uint64_t a = FOV[f], b = FOV[f + 1];
+    total_words += 1 + std::count(FBV.begin() + a, FBV.begin() + b, uint8_t('/'));
   }
   wid.reserve(std::min<uint64_t>(total_words, 1u << 26));
   EdgeMap edges(std::min<uint64_t>(total_words + 1, 1ull << 30));
@@ -230,7 +233,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   nodes.reserve(std::min<uint64_t>(total_words + 1, 1ull << 30));
   uint64_t n_wild = 0;
   uint32_t max_depth = 0;
-  const uint8_t* FB = idx->fbytes.data();
+  const uint8_t* FB = FBV.data();
 
   auto intern = [&](const uint8_t* p, uint64_t len) -> uint32_t {
     std::string_view v(reinterpret_cast<const char*>(p), len);
@@ -239,7 +242,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     uint32_t off = uint32_t(arena.size());
     arena.insert(arena.end(), p, p + len);
     if (len == 0) arena.push_back(0);  // every word owns >= 1 byte: ids stay unique
-    wid.emplace(v, off);  // view into idx->fbytes (stable for the build)
+    wid.emplace(v, off);  // view into FBV (stable for the build)
     word_hash.push_back(dict_hash_host(p, len));
     word_ids.push_back(off);
     word_len.push_back(uint32_t(len));
@@ -259,8 +262,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   const uint8_t* ps = nullptr;
   uint64_t plen = 0;
   for (uint32_t f = 0; f < nf; ++f) {
-    const uint8_t* s = FB + idx->foff[f];
-    uint64_t len = idx->foff[f + 1] - idx->foff[f];
+    const uint8_t* s = FB + FOV[f];
+    uint64_t len = FOV[f + 1] - FOV[f];
     uint64_t cp = 0;
     if (ps) {
       const uint64_t m = std::min(len, plen);
@@ -686,7 +689,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     }
   }
   std::vector<uint16_t> flen(nf);
-  for (uint32_t f = 0; f < nf; ++f) flen[f] = uint16_t(std::min<uint64_t>(idx->foff[f + 1] - idx->foff[f], 65535));
+  for (uint32_t f = 0; f < nf; ++f) flen[f] = uint16_t(std::min<uint64_t>(FOV[f + 1] - FOV[f], 65535));
 
   phase("subscribers");
   // ---- 6. upload: one allocation, 256-B aligned sections, the subscriber

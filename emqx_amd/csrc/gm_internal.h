@@ -14,6 +14,7 @@
 
 #include "../../include/emqx_gpu_match.h"
 #include "gm_common.h"
+#include "gm_filters.h"
 
 namespace gm {
 
@@ -115,6 +116,42 @@ struct emqx_gm_ctx {
 namespace gm {
 struct OverlayState;
 
+// The id change of an in-place update, from O(delta) lists: prev ids `dels`
+// deleted (ascending), new filter k (byte order) inserted with addpos[k] prev
+// filters sorting before it and temporary id nb + k.  map(): prev id -> new id
+// (NONE: deleted) = id - (dels below it) + (inserts at or before it); a
+// temporary nb + k -> addpos[k] - (dels below addpos[k]) + k.  The device
+// builds the whole table with a kernel (apply_patch_device); table() is the
+// host twin, materialized only where the host needs it.
+struct IdShift {
+  uint64_t nb = 0;
+  std::vector<uint64_t> dels, addpos;
+  uint32_t map(uint64_t id) const {
+    if (id >= nb) {
+      const uint64_t k = id - nb, p = addpos[k];
+      return uint32_t(p - (std::lower_bound(dels.begin(), dels.end(), p) - dels.begin()) + k);
+    }
+    if (std::binary_search(dels.begin(), dels.end(), id)) return NONE;
+    return uint32_t(id - (std::lower_bound(dels.begin(), dels.end(), id) - dels.begin()) +
+                    (std::upper_bound(addpos.begin(), addpos.end(), id) - addpos.begin()));
+  }
+  std::vector<uint32_t> table() const {
+    std::vector<uint32_t> r(nb + addpos.size());
+    uint64_t d = 0, a = 0;
+    for (uint64_t id = 0; id < nb; ++id) {
+      while (a < addpos.size() && addpos[a] <= id) ++a;
+      if (d < dels.size() && dels[d] == id) {
+        r[id] = NONE;
+        ++d;
+        continue;
+      }
+      r[id] = uint32_t(id - d + a);
+    }
+    for (uint64_t k = 0; k < addpos.size(); ++k) r[nb + k] = map(nb + k);
+    return r;
+  }
+};
+
 // Host copy of a plain index's device blob (no shard ids, no subscriber
 // lists), byte for byte, with the headroom an in-place update may use
 // (gm_overlay.cpp, patch_update): appended trie nodes, new words in the
@@ -143,9 +180,10 @@ struct emqx_gm_index {
   size_t dev_bytes = 0;
   gm::IndexView view{};
   uint16_t* dev_flen = nullptr; // filter lengths (stats only), inside dev_base
+  mutable std::atomic<bool> flen_stale{false};  // dev_flen not yet rewritten after an in-place update
+  mutable std::mutex flen_mu;
   // host copies
-  std::vector<uint8_t> fbytes;  // sorted unique filters
-  std::vector<uint64_t> foff;
+  gm::FilterTable ft;           // the sorted unique filters (id = rank), gm_filters.h
   std::vector<uint32_t> gmap;   // shard index: global id of each local filter (ascending); empty otherwise
   std::vector<uint64_t> soff;   // subscriber CSR offsets per filter id (host copy; empty without subscribers)
   std::vector<uint8_t> pinned;  // per filter: its route is held by another destination (emqx_gm_index_update_subs
@@ -234,12 +272,13 @@ int overlay_filter(const emqx_gm_index* idx, uint32_t id, const uint8_t** bytes,
 void free_overlay(emqx_gm_index* idx);
 // gm_match.hip: the device side of an in-place update (patch_update): dst =
 // src (bytes), then the host-patched byte ranges (offset, length) of `host`
-// written over it, then every filter-id field of the hot slots and of nodes
-// [0, n_nodes) renumbered by rmap (n_rmap entries)
+// written over it, the OR ops (offset of a word, bits) applied, then every
+// filter-id field of the hot slots and of nodes [0, n_nodes) renumbered by
+// the shift (its table built on the device)
 int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t bytes,
                        const std::vector<std::pair<uint64_t, uint32_t>>& ranges, const uint8_t* host,
                        const IndexView& v, uint64_t o_hot, uint64_t o_nodes, uint64_t n_nodes,
-                       const std::vector<uint32_t>& rmap);
+                       const IdShift& shift, const std::vector<std::pair<uint64_t, uint32_t>>& orops);
 // gm_match.hip
 int run_match_overlay(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                       uint32_t flags, emqx_gm_csr* out);

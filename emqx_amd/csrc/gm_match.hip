@@ -2217,6 +2217,42 @@ __global__ __launch_bounds__(256) void k_patch_scatter(uint8_t* __restrict__ dst
   const uint64_t d = desc[3 * blockIdx.x], p = desc[3 * blockIdx.x + 1], n = desc[3 * blockIdx.x + 2];
   for (uint64_t i = threadIdx.x; i < n; i += 256) dst[d + i] = pay[p + i];
 }
+// The id table of an in-place update (IdShift::map, gm_internal.h), built on
+// the device from the O(delta) lists: dels (prev ids deleted, ascending) and
+// addpos (per new filter, byte order: prev filters sorting before it).
+__device__ __forceinline__ uint32_t count_below(const uint32_t* a, uint32_t n, uint32_t x) {  // a[i] < x
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (a[m] < x) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+__global__ __launch_bounds__(256) void k_shift_table(uint32_t* __restrict__ rmap, uint64_t nb,
+                                                     const uint32_t* __restrict__ dels, uint32_t nd,
+                                                     const uint32_t* __restrict__ addpos, uint32_t na) {
+  const uint64_t id = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (id >= nb + na) return;
+  if (id >= nb) {
+    const uint32_t k = uint32_t(id - nb), p = addpos[k];
+    rmap[id] = p - count_below(dels, nd, p) + k;
+    return;
+  }
+  const uint32_t x = uint32_t(id), below = count_below(dels, nd, x);
+  if (below < nd && dels[below] == x) {
+    rmap[id] = NONE;
+    return;
+  }
+  rmap[id] = x - below + count_below(addpos, na, x + 1);  // inserts at or before it
+}
+// Flag bits set on words whose other bits are filter ids (HOT_PLUS on hf /
+// p_hf): the host mirror's ids are stale (not renumbered), so these go as ORs.
+__global__ __launch_bounds__(256) void k_patch_or(uint32_t* __restrict__ dst, const uint64_t* __restrict__ ops,
+                                                  uint64_t n) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (i < n) atomicOr(dst + (ops[2 * i] >> 2), uint32_t(ops[2 * i + 1]));
+}
 // Every filter-id field renumbered (renum_field, the device twin of
 // gm_overlay.cpp's renumber_host): hot slots [0, n_hot), nodes [0, n_nodes).
 __global__ __launch_bounds__(256) void k_renumber(HotSlot* __restrict__ hot, uint64_t n_hot, Node* __restrict__ nodes,
@@ -2242,9 +2278,10 @@ __global__ __launch_bounds__(256) void k_renumber(HotSlot* __restrict__ hot, uin
 int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t bytes,
                        const std::vector<std::pair<uint64_t, uint32_t>>& ranges, const uint8_t* host,
                        const IndexView& v, uint64_t o_hot, uint64_t o_nodes, uint64_t n_nodes,
-                       const std::vector<uint32_t>& rmap) {
-  // coalesce (ranges closer than 64 B merge: the bytes between are equal on
-  // both sides, the patch never touched them), then cut into pieces
+                       const IdShift& shift, const std::vector<std::pair<uint64_t, uint32_t>>& orops) {
+  // coalesce overlapping / adjacent ranges only (the bytes between two written
+  // fields may differ: the host mirror's untouched filter ids are stale), then
+  // cut into pieces
   std::vector<std::pair<uint64_t, uint64_t>> seg;  // [begin, end)
   {
     std::vector<std::pair<uint64_t, uint32_t>> r(ranges);
@@ -2252,10 +2289,12 @@ int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t byte
     for (const auto& x : r) {
       if (!x.second) continue;
       if (x.first + x.second > bytes) return set_err(ctx, EMQX_GM_EINVAL, "index_update: patch outside the blob");
-      if (!seg.empty() && x.first <= seg.back().second + 64) seg.back().second = std::max(seg.back().second, x.first + x.second);
+      if (!seg.empty() && x.first <= seg.back().second) seg.back().second = std::max(seg.back().second, x.first + x.second);
       else seg.emplace_back(x.first, x.first + x.second);
     }
   }
+  for (const auto& o : orops)
+    if ((o.first & 3) || o.first + 4 > bytes) return set_err(ctx, EMQX_GM_EINVAL, "index_update: OR op outside the blob");
   std::vector<uint64_t> desc;
   uint64_t pay_n = 0;
   for (const auto& g : seg) {
@@ -2267,11 +2306,16 @@ int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t byte
   }
   const uint64_t n_pieces = desc.size() / 3;
   if (n_pieces > 0x7FFFFFFFull) return set_err(ctx, EMQX_GM_EINVAL, "index_update: patch too large");
-  // staging: desc | payload | rmap (one upload)
+  // staging: desc | payload | dels | addpos | OR ops (one upload); the id table after them (device-built)
+  const uint64_t nd = shift.dels.size(), na = shift.addpos.size(), n_map = shift.nb + na;
   const size_t o_pay = (desc.size() * 8 + 255) & ~size_t(255);
-  const size_t o_rmap = (o_pay + pay_n + 255) & ~size_t(255);
-  const size_t total = o_rmap + rmap.size() * 4 + 4;
-  std::vector<uint8_t> st(total, 0);
+  const size_t o_dels = (o_pay + pay_n + 255) & ~size_t(255);
+  const size_t o_adds = (o_dels + nd * 4 + 4 + 255) & ~size_t(255);
+  const size_t o_ors = (o_adds + na * 4 + 4 + 255) & ~size_t(255);
+  const size_t up = o_ors + orops.size() * 16 + 16;
+  const size_t o_rmap = (up + 255) & ~size_t(255);
+  const size_t total = o_rmap + n_map * 4 + 4;
+  std::vector<uint8_t> st(up, 0);
   if (!desc.empty()) std::memcpy(st.data(), desc.data(), desc.size() * 8);
   {
     uint64_t q = o_pay;
@@ -2280,12 +2324,17 @@ int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t byte
       q += g.second - g.first;
     }
   }
-  if (!rmap.empty()) std::memcpy(st.data() + o_rmap, rmap.data(), rmap.size() * 4);
+  for (uint64_t k = 0; k < nd; ++k) reinterpret_cast<uint32_t*>(st.data() + o_dels)[k] = uint32_t(shift.dels[k]);
+  for (uint64_t k = 0; k < na; ++k) reinterpret_cast<uint32_t*>(st.data() + o_adds)[k] = uint32_t(shift.addpos[k]);
+  for (size_t k = 0; k < orops.size(); ++k) {
+    const uint64_t w[2] = {orops[k].first, orops[k].second};
+    std::memcpy(st.data() + o_ors + 16 * k, w, 16);
+  }
   PoolBuf dbuf(ctx->pool, total);
   if (!dbuf.p) return set_err(ctx, EMQX_GM_ENOMEM, "index_update: staging buffer");
   hipStream_t s = ctx->stream;
   GM_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
-  GM_HIP(ctx, hipMemcpyAsync(dbuf.p, st.data(), total, hipMemcpyHostToDevice, s));
+  GM_HIP(ctx, hipMemcpyAsync(dbuf.p, st.data(), up, hipMemcpyHostToDevice, s));
   uint8_t* D = static_cast<uint8_t*>(dst);
   const uint8_t* S = dbuf.as<uint8_t>();
   if (n_pieces) {
@@ -2293,12 +2342,24 @@ int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t byte
                        reinterpret_cast<const uint64_t*>(S), S + o_pay);
     GM_HIP(ctx, hipGetLastError());
   }
+  if (!orops.empty()) {
+    hipLaunchKernelGGL(k_patch_or, dim3(uint32_t((orops.size() + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<uint32_t*>(D), reinterpret_cast<const uint64_t*>(S + o_ors),
+                       uint64_t(orops.size()));
+    GM_HIP(ctx, hipGetLastError());
+  }
+  uint32_t* const RM = reinterpret_cast<uint32_t*>(dbuf.as<uint8_t>() + o_rmap);
+  if (n_map) {
+    hipLaunchKernelGGL(k_shift_table, dim3(uint32_t((n_map + 255) / 256)), dim3(256), 0, s, RM, shift.nb,
+                       reinterpret_cast<const uint32_t*>(S + o_dels), uint32_t(nd),
+                       reinterpret_cast<const uint32_t*>(S + o_adds), uint32_t(na));
+    GM_HIP(ctx, hipGetLastError());
+  }
   uint64_t n_hot = 0;
   for (int t = 0; t < HOT_TABLES; ++t) n_hot = std::max<uint64_t>(n_hot, v.hot_off[t] + v.hot_cap[t]);
   const uint64_t g = std::min<uint64_t>(4096, (std::max(n_hot, n_nodes) + 255) / 256);
   hipLaunchKernelGGL(k_renumber, dim3(uint32_t(g ? g : 1)), dim3(256), 0, s, reinterpret_cast<HotSlot*>(D + o_hot),
-                     n_hot, reinterpret_cast<Node*>(D + o_nodes), n_nodes,
-                     reinterpret_cast<const uint32_t*>(S + o_rmap));
+                     n_hot, reinterpret_cast<Node*>(D + o_nodes), n_nodes, RM);
   GM_HIP(ctx, hipGetLastError());
   GM_HIP(ctx, hipStreamSynchronize(s));  // the staging buffers go back to the pool / the host
   return EMQX_GM_OK;
@@ -2899,6 +2960,17 @@ int scan_lengths(emqx_gm_ctx* ctx, const uint64_t* len, uint64_t n, uint64_t* ou
 
 int sum_filter_lengths(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint32_t* d_ids, uint64_t nnz,
                        uint64_t* out) {
+  if (idx->flen_stale) {  // after an in-place update: the lengths in this snapshot's ids, once
+    std::lock_guard<std::mutex> lk(idx->flen_mu);
+    if (idx->flen_stale) {
+      const uint64_t nf = idx->info.n_filters;
+      std::vector<uint16_t> fl(nf + 1, 0);
+      idx->ft.for_each([&](uint64_t f, const uint8_t*, uint64_t l) { fl[f] = uint16_t(std::min<uint64_t>(l, 65535)); });
+      GM_HIP(ctx, hipMemcpyAsync(idx->dev_flen, fl.data(), nf * 2, hipMemcpyHostToDevice, ctx->stream));
+      GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      idx->flen_stale = false;
+    }
+  }
   PoolBuf acc(ctx->pool, 16);
   if (!acc.p) return set_err(ctx, EMQX_GM_ENOMEM, "sum_flen");
   GM_HIP(ctx, hipMemsetAsync(acc.p, 0, 8, ctx->stream));

@@ -33,20 +33,9 @@ int cmp_bytes(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
 
 // Number of base filters sorting strictly before f; *found = exact hit.
 uint64_t base_rank(const emqx_gm_index* base, const uint8_t* f, uint64_t len, bool* found) {
-  uint64_t lo = 0, hi = base->info.n_filters;
-  while (lo < hi) {
-    const uint64_t m = (lo + hi) / 2;
-    const uint64_t a = base->foff[m], b = base->foff[m + 1];
-    if (cmp_bytes(base->fbytes.data() + a, b - a, f, len) < 0) lo = m + 1;
-    else hi = m;
-  }
-  *found = false;
-  if (lo < base->info.n_filters) {
-    const uint64_t a = base->foff[lo], b = base->foff[lo + 1];
-    *found = cmp_bytes(base->fbytes.data() + a, b - a, f, len) == 0;
-  }
-  return lo;
+  return base->ft.rank_of(f, len, found);
 }
+const uint8_t* filter_at(const emqx_gm_index* idx, uint64_t id, uint64_t* len) { return idx->ft.at(id, len); }
 
 // emqx_topic:wildcard/1 on the filter bytes
 bool wildcard(const uint8_t* p, uint64_t len) {
@@ -104,7 +93,15 @@ struct NoRoom {};  // a table of the snapshot is full: the update rolls back and
 struct Patcher {
   Mirror& M;
   IndexView& v;  // the new snapshot's view (its host-side fields are patched here)
-  std::vector<std::pair<uint64_t, uint32_t>> dirty;  // blob ranges changed: (offset, bytes)
+  // Blob ranges written (offset, bytes): uploaded over the device copy.  Writes
+  // are field-granular on the id-bearing records (HotSlot, Node): the mirror's
+  // filter-id fields are NOT renumbered after an update (only the device blob
+  // is, by k_renumber), so a record's untouched id fields are stale on the host
+  // and must not be uploaded.  A flag set on a field that also holds an id
+  // (HOT_PLUS in hf / p_hf) goes to the device as an OR instead (orops).
+  std::vector<std::pair<uint64_t, uint32_t>> dirty;
+  std::vector<std::pair<uint64_t, uint32_t>> orops;  // (offset of a 32-bit word, bits to set)
+  std::vector<std::pair<uint64_t, uint32_t>> undo_rng;  // every saved range, in order (rollback)
   uint32_t rh_clear = 0;                             // tables that took a key outside Robin Hood order
   uint64_t new_edges = 0;
   uint32_t max_depth = 0;
@@ -128,11 +125,23 @@ struct Patcher {
   HotSlot* hot() { return reinterpret_cast<HotSlot*>(B() + M.o_hot); }
   uint8_t* arena() { return B() + M.o_arena; }
   uint32_t* efilt() { return reinterpret_cast<uint32_t*>(B() + M.o_efilt); }
+  void save(uint64_t off, size_t n) {
+    undo_rng.emplace_back(off, uint32_t(n));
+    undo_bytes.insert(undo_bytes.end(), B() + off, B() + off + n);
+  }
   // before writing n bytes at p
   void touch(const void* p, size_t n) {
     const uint64_t off = uint64_t(static_cast<const uint8_t*>(p) - B());
     dirty.emplace_back(off, uint32_t(n));
-    undo_bytes.insert(undo_bytes.end(), B() + off, B() + off + n);
+    save(off, n);
+  }
+  // set `bits` in a word whose other bits may be a (host-stale) filter id
+  void orw(uint32_t& w, uint32_t bits) {
+    if ((w & bits) == bits) return;
+    const uint64_t off = uint64_t(reinterpret_cast<const uint8_t*>(&w) - B());
+    save(off, 4);
+    orops.emplace_back(off, bits);
+    w |= bits;
   }
   template <class T> T& W(T& r) {
     touch(&r, sizeof(T));
@@ -140,9 +149,9 @@ struct Patcher {
   }
   void rollback() {
     size_t q = undo_bytes.size();
-    for (size_t k = dirty.size(); k-- > 0;) {
-      q -= dirty[k].second;
-      std::memcpy(B() + dirty[k].first, undo_bytes.data() + q, dirty[k].second);
+    for (size_t k = undo_rng.size(); k-- > 0;) {
+      q -= undo_rng[k].second;
+      std::memcpy(B() + undo_rng[k].first, undo_bytes.data() + q, undo_rng[k].second);
     }
     M.nodes_n = s_nodes_n;
     M.arena_n = s_arena_n;
@@ -255,9 +264,11 @@ struct Patcher {
     return c.kind == CUR_ROOT ? 0u : c.kind == CUR_SLOT ? c.slot : (c.slot | HOT_INLINE);
   }
   // the node's record: root -> IndexView fields, slot node -> its slot, inline
-  // node -> p_* of its parent's slot.  rec() saves the slot before a write.
-  void rec(const Cur& c) {
-    if (c.kind != CUR_ROOT) touch(&htab(c.table)[c.slot], sizeof(HotSlot));
+  // node -> p_* of its parent's slot.  F() records a field before a write
+  // (the root's fields live in the view: nothing to record).
+  uint32_t& F(const Cur& c, uint32_t& f) {
+    if (c.kind != CUR_ROOT) touch(&f, 4);
+    return f;
   }
   uint32_t& f_sig(const Cur& c) {
     return c.kind == CUR_ROOT ? v.root_sig : c.kind == CUR_SLOT ? htab(c.table)[c.slot].sig : htab(c.table)[c.slot].p_sig;
@@ -273,15 +284,14 @@ struct Patcher {
       v.root_hash = id == HF_NONE ? NONE : id;
       return;
     }
-    rec(c);
-    uint32_t& f = f_hf(c);
+    uint32_t& f = F(c, f_hf(c));
     f = (f & HOT_PLUS) | id;
   }
   // a node's first exact child: set NF_HAS_EXACT and the REF_X bit of the
   // references to it (its parent's edge, and plus_child when it is a '+' child)
   void gain_exact(const Cur& c) {
     if (nodes()[c.v1].flags & NF_HAS_EXACT) return;
-    W(nodes()[c.v1]).flags |= NF_HAS_EXACT;
+    W(nodes()[c.v1].flags) |= NF_HAS_EXACT;
     if (c.pv1 == NONE) return;  // the root: no reference
     const int d = edge_depth(c.depth - 1);
     EdgeSlot* tab = edges() + v.etab_off[d];
@@ -293,7 +303,7 @@ struct Patcher {
       }
       if (tab[s].key == EDGE_EMPTY) break;
     }
-    if (c.plus) W(nodes()[c.pv1]).plus_child |= REF_X;
+    if (c.plus) W(nodes()[c.pv1].plus_child) |= REF_X;
   }
 
   // Insert a well-formed filter with (temporary) id fid.  Throws NoRoom.
@@ -310,10 +320,10 @@ struct Patcher {
           ch = new_node();
           edge_put(c.depth, c.v1, hw, ch);
         }
-        Node& hn = W(nodes()[ch & REF_MASK]);
-        hn.end_filter = fid;
-        hn.flags |= NF_END_WILD;
-        W(nodes()[c.v1]).hash_filter = fid;
+        Node& hn = nodes()[ch & REF_MASK];
+        W(hn.end_filter) = fid;
+        W(hn.flags) |= NF_END_WILD;
+        W(nodes()[c.v1].hash_filter) = fid;
         set_hf(c, fid);
         max_depth = std::max<uint32_t>(max_depth, c.depth + 1);
         return;
@@ -326,9 +336,9 @@ struct Patcher {
         ch = new_node();
         edge_put(c.depth, c.v1, wid, ch);
         if (plus) {
-          Node& pn = W(nodes()[c.v1]);
-          pn.plus_child = ch;
-          pn.flags |= NF_HAS_PLUS;
+          Node& pn = nodes()[c.v1];
+          W(pn.plus_child) = ch;
+          W(pn.flags) |= NF_HAS_PLUS;
         } else {
           gain_exact(c);
         }
@@ -342,11 +352,10 @@ struct Patcher {
       if (plus && plus_inline(c.depth, c.kind == CUR_SLOT)) {  // the '+' child lives in its parent's slot
         HotSlot& P = htab(c.table)[c.slot];
         if (!(P.hf & HOT_PLUS)) {
-          W(P);
-          P.hf |= HOT_PLUS;
-          P.p_sig = 0;
-          P.p_hf = HF_NONE;
-          P.p_end = NONE;
+          orw(P.hf, HOT_PLUS);
+          W(P.p_sig) = 0;
+          W(P.p_hf) = HF_NONE;
+          W(P.p_end) = NONE;
         }
         n.kind = CUR_INLINE;
         n.slot = c.slot;
@@ -360,12 +369,10 @@ struct Patcher {
           if (c.kind == CUR_ROOT) {
             v.root_flags |= HOT_PLUS;
           } else {
-            rec(c);
-            f_hf(c) |= HOT_PLUS;
+            orw(f_hf(c), HOT_PLUS);
           }
         } else {  // the parent's exact-child signature and the table's exact-edge filter
-          rec(c);
-          f_sig(c) |= sig_bit(wid);
+          F(c, f_sig(c)) |= sig_bit(wid);
           if (v.efilt_mask[t]) {
             const uint32_t fh = edge_filter_hash(key);
             W(efilt()[v.efilt_off[t] + edge_filter_word(fh, v.efilt_mask[t])]) |= edge_filter_bits(fh);
@@ -377,11 +384,10 @@ struct Patcher {
       }
       c = n;
     }
-    rec(c);
-    f_end(c) = fid | (wild ? END_WILD : 0u);
-    Node& en = W(nodes()[c.v1]);
-    en.end_filter = fid;
-    if (wild) en.flags |= NF_END_WILD;
+    if (c.kind != CUR_ROOT) F(c, f_end(c)) = fid | (wild ? END_WILD : 0u);
+    Node& en = nodes()[c.v1];
+    W(en.end_filter) = fid;
+    if (wild) W(en.flags) |= NF_END_WILD;
     max_depth = std::max<uint32_t>(max_depth, c.depth);
   }
 
@@ -399,8 +405,8 @@ struct Patcher {
       if (ch == NONE) return;
       const bool last = i + 1 == ws.w.size();
       if (last && is1(p, w, '#')) {
-        W(nodes()[v1]).hash_filter = NONE;
-        W(nodes()[ch & REF_MASK]).end_filter = NONE;
+        W(nodes()[v1].hash_filter) = NONE;
+        W(nodes()[ch & REF_MASK].end_filter) = NONE;
         if (wf) set_hf(c, HF_NONE);
         return;
       }
@@ -423,11 +429,8 @@ struct Patcher {
       }
       v1 = ch & REF_MASK;
     }
-    W(nodes()[v1]).end_filter = NONE;
-    if (wf) {
-      rec(c);
-      f_end(c) = NONE;
-    }
+    W(nodes()[v1].end_filter) = NONE;
+    if (wf && c.kind != CUR_ROOT) F(c, f_end(c)) = NONE;
   }
 };
 
@@ -491,59 +494,27 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
   idx->info = prev->info;
   IndexView& v = idx->view;
   Patcher P{M, v};
-  // final ids: surviving base filters and the new ones, in byte order; the
-  // base filters between two events (a tombstone, an insert position) move as
-  // one run
-  std::vector<uint32_t> rmap(nb + K, NONE);
-  {
-    std::vector<uint64_t> ipos;  // per new filter (byte order): base filters sorting before it
-    ipos.reserve(K);
-    for (const std::string& d : dset) {
-      bool found;
-      ipos.push_back(base_rank(prev, reinterpret_cast<const uint8_t*>(d.data()), d.size(), &found));
-    }
-    idx->fbytes.reserve(prev->fbytes.size() + K * 16);
-    idx->foff.reserve(nf_new + 1);
-    idx->foff.push_back(0);
-    auto tit = tomb.begin();
-    auto dit = dset.begin();
-    uint64_t b = 0, k = 0;
-    uint32_t fin = 0;
-    auto run = [&](uint64_t e) {  // base filters [b, e), none tombstoned
-      if (e <= b) return;
-      const uint64_t a0 = prev->foff[b], a1 = prev->foff[e];
-      const uint64_t shift = idx->fbytes.size() - a0;
-      idx->fbytes.insert(idx->fbytes.end(), prev->fbytes.begin() + a0, prev->fbytes.begin() + a1);
-      for (uint64_t x = b; x < e; ++x) {
-        idx->foff.push_back(prev->foff[x + 1] + shift);
-        rmap[x] = fin++;
-      }
-      b = e;
-    };
-    while (b < nb || k < K) {
-      const uint64_t next_t = tit != tomb.end() ? *tit : nb;
-      const uint64_t next_i = k < K ? ipos[k] : nb;
-      run(std::min(next_t, next_i));
-      if (k < K && ipos[k] == b) {  // new filters sort before base filter b
-        idx->fbytes.insert(idx->fbytes.end(), dit->begin(), dit->end());
-        idx->foff.push_back(idx->fbytes.size());
-        rmap[nb + k] = fin++;
-        ++dit;
-        ++k;
-      } else if (tit != tomb.end() && *tit == b) {
-        ++tit;
-        ++b;
-      } else if (b >= nb && k >= K) {
-        break;
-      }
-    }
+  // final ids (IdShift: prev id -> new id, temporaries nb + k -> new id) from
+  // O(delta) lists, and the new snapshot's host filter table derived from
+  // prev's (FilterTable::apply: shared base + delta, gm_filters.h)
+  IdShift shift;
+  shift.nb = nb;
+  shift.dels.assign(tomb.begin(), tomb.end());
+  shift.addpos.reserve(K);
+  for (const std::string& d : dset) {
+    bool found;
+    shift.addpos.push_back(base_rank(prev, reinterpret_cast<const uint8_t*>(d.data()), d.size(), &found));
   }
+  idx->ft = prev->ft.apply(shift.dels, dset);
+  const bool host = prev->dev_base == nullptr;  // a host-only index (CPU test): the mirror is the index
+  std::vector<uint32_t> rmap;  // materialized only where the host needs it (host-only index, update_subs)
+  if (host || rmap_out) rmap = shift.table();
   phase("ids");
   // clear the deleted, insert the new (temporary ids nb + k), on the mirror
   uint64_t twild = 0, dwild = 0;
   for (uint32_t b : tomb) {
-    const uint8_t* bp = prev->fbytes.data() + prev->foff[b];
-    const uint64_t bl = prev->foff[b + 1] - prev->foff[b];
+    uint64_t bl;
+    const uint8_t* bp = filter_at(prev, b, &bl);
     twild += wildcard(bp, bl);
     P.erase(bp, bl);
   }
@@ -562,20 +533,17 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
     phase("no room");
     return 1;
   }
-  if (v.root_hash != NONE) v.root_hash = rmap[v.root_hash];
+  if (v.root_hash != NONE) v.root_hash = shift.map(v.root_hash);
   v.rh_mask &= ~P.rh_clear;
   v.n_nodes = uint32_t(M.nodes_n);
   v.n_filters = uint32_t(nf_new);
   phase("patch");
-  // filter lengths (stats), in final ids
-  uint16_t* flen = reinterpret_cast<uint16_t*>(M.blob.data() + M.o_flen);
-  P.touch(flen, nf_new * 2);
-  for (uint64_t f = 0; f < nf_new; ++f)
-    flen[f] = uint16_t(std::min<uint64_t>(idx->foff[f + 1] - idx->foff[f], 65535));
+  // filter lengths (stats only, emqx_gm_matched_filter_bytes): rewritten in
+  // final ids when first asked for (sum_filter_lengths), not per update
+  idx->flen_stale = true;
   // device: copy the previous blob, apply the patched ranges (still in temporary
   // ids), renumber every filter-id field; then the mirror the same way
   phase("flen");
-  const bool host = prev->dev_base == nullptr;  // a host-only index (CPU test): the mirror is the index
   const size_t blob_bytes = trie_only ? M.blob.size() : prev->dev_bytes;  // the mirror ends at the CSR
   if (!host) {
     hipError_t e = hipSetDevice(prev->device);
@@ -587,7 +555,7 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
     }
     phase("alloc");
     const int rc = apply_patch_device(ctx, idx->dev_base, prev->dev_base, blob_bytes, P.dirty, M.blob.data(), v,
-                                      M.o_hot, M.o_nodes, M.nodes_n, rmap);
+                                      M.o_hot, M.o_nodes, M.nodes_n, shift, P.orops);
     if (rc) {  // the mirror no longer matches any snapshot: later updates take the overlay path
       (void)hipFree(idx->dev_base);
       delete idx;
@@ -598,7 +566,11 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
     phase("device");
   }
   idx->dev_bytes = blob_bytes;
-  renumber_host(M, v, rmap);
+  // A host-only index (CPU tests) IS its mirror: renumber it.  A device index's
+  // mirror keeps its filter-id fields stale: the patcher never reads them and
+  // uploads only the fields it writes (Patcher::dirty / orops), so the host
+  // side of an update stays O(delta) instead of a pass over the whole blob.
+  if (host) renumber_host(M, v, rmap);
   phase("renumber");
   // the view's pointers follow the new blob (a host-only index keeps the mirror's)
   uint8_t* NB = host ? M.blob.data() : static_cast<uint8_t*>(idx->dev_base);
@@ -692,21 +664,21 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
     std::vector<uint64_t> offs{0};
     auto dit = dset.begin();
     auto tit = tomb.begin();
-    for (uint64_t b = 0; b <= nb; ++b) {
-      const uint8_t* bp = b < nb ? base->fbytes.data() + base->foff[b] : nullptr;
-      const uint64_t bl = b < nb ? base->foff[b + 1] - base->foff[b] : 0;
-      while (dit != dset.end() &&
-             (b == nb || cmp_bytes(reinterpret_cast<const uint8_t*>(dit->data()), dit->size(), bp, bl) < 0)) {
+    base->ft.for_each([&](uint64_t b, const uint8_t* bp, uint64_t bl) {
+      while (dit != dset.end() && cmp_bytes(reinterpret_cast<const uint8_t*>(dit->data()), dit->size(), bp, bl) < 0) {
         bytes.insert(bytes.end(), dit->begin(), dit->end());
         offs.push_back(bytes.size());
         ++dit;
       }
-      if (b == nb) break;
       if (tit != tomb.end() && *tit == b) {
         ++tit;
-        continue;
+        return;
       }
       bytes.insert(bytes.end(), bp, bp + bl);
+      offs.push_back(bytes.size());
+    });
+    for (; dit != dset.end(); ++dit) {
+      bytes.insert(bytes.end(), dit->begin(), dit->end());
       offs.push_back(bytes.size());
     }
     bytes.resize(bytes.size() + 64, 0);
@@ -750,7 +722,9 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
   uint64_t twild = 0;
   for (uint32_t b : ov->tomb) {
     tbm[b >> 5] |= 1u << (b & 31);
-    twild += wildcard(base->fbytes.data() + base->foff[b], base->foff[b + 1] - base->foff[b]);
+    uint64_t bl;
+    const uint8_t* bp = filter_at(base, b, &bl);
+    twild += wildcard(bp, bl);
   }
   for (uint64_t w = 1; w < words; ++w) tpre[w] = tpre[w - 1] + uint32_t(__builtin_popcount(tbm[w - 1]));
   const size_t bytes = (2 * words + K + 1) * 4;
@@ -809,8 +783,7 @@ int overlay_filter(const emqx_gm_index* idx, uint32_t id, const uint8_t** bytes,
   }
   while (lo < base->info.n_filters && std::binary_search(ov.tomb.begin(), ov.tomb.end(), uint32_t(lo))) ++lo;
   if (lo >= base->info.n_filters || final_id(lo) != id) return EMQX_GM_EINVAL;
-  *bytes = base->fbytes.data() + base->foff[lo];
-  *len = base->foff[lo + 1] - base->foff[lo];
+  *bytes = filter_at(base, lo, len);
   return EMQX_GM_OK;
 }
 

@@ -91,17 +91,15 @@ int rebuild(emqx_gm_ctx* ctx, const emqx_gm_index* prev, const std::map<std::str
     si.insert(si.end(), l, l + cnt);
     so.push_back(si.size());
   };
-  for (uint64_t f = 0; f < nb; ++f) {
-    const uint8_t* p = prev->fbytes.data() + prev->foff[f];
-    const uint64_t len = prev->foff[f + 1] - prev->foff[f];
+  prev->ft.for_each([&](uint64_t f, const uint8_t* p, uint64_t len) {
     if (const FilterEdit* e = edit_of[f]) {
-      if (!e->present()) continue;  // the last subscriber left and no other destination: the route goes
+      if (!e->present()) return;  // the last subscriber left and no other destination: the route goes
       const std::vector<uint32_t> l = e->final_list();
       add(p, len, l.data(), l.size(), e->pinned());
     } else {
       add(p, len, all.data() + prev->soff[f], prev->soff[f + 1] - prev->soff[f], is_pinned(prev, f));
     }
-  }
+  });
   for (const auto& kv : ed)
     if (kv.second.old_id == NONE && kv.second.present()) {
       const std::vector<uint32_t> l = kv.second.final_list();
@@ -215,9 +213,9 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
       idx->view = prev->view;
       idx->info = prev->info;
       idx->info.device_bytes = prev->dev_bytes;  // the tables; the new CSR is added below
-      idx->fbytes = prev->fbytes;
-      idx->foff = prev->foff;
+      idx->ft = prev->ft;
       idx->dev_flen = prev->dev_flen;
+      idx->flen_stale = prev->flen_stale.load();
       idx->level_nodes = prev->level_nodes;
       idx->mirror = prev->mirror;
       prev->mirror = nullptr;

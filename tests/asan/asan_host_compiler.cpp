@@ -23,7 +23,8 @@ int set_err(emqx_gm_ctx*, int code, const std::string&) { return code; }  // gm_
 // gm_match.hip's device step of an in-place update: never reached here (no
 // context, so no snapshot keeps a mirror)
 int apply_patch_device(emqx_gm_ctx*, void*, const void*, size_t, const std::vector<std::pair<uint64_t, uint32_t>>&,
-                       const uint8_t*, const IndexView&, uint64_t, uint64_t, uint64_t, const std::vector<uint32_t>&) {
+                       const uint8_t*, const IndexView&, uint64_t, uint64_t, uint64_t, const IdShift&,
+                       const std::vector<std::pair<uint64_t, uint32_t>>&) {
   return EMQX_GM_EDEVICE;
 }
 }
@@ -117,8 +118,9 @@ int verify(const emqx_gm_index* idx, const std::set<std::string>& cur, const cha
   if (idx->info.n_filters != cur.size()) fail("n_filters");
   uint32_t f = 0;
   for (const std::string& flt : cur) {
-    const std::string got(reinterpret_cast<const char*>(idx->fbytes.data() + idx->foff[f]),
-                          idx->foff[f + 1] - idx->foff[f]);
+    uint64_t gl;
+    const uint8_t* gp = idx->ft.at(f, &gl);
+    const std::string got(reinterpret_cast<const char*>(gp), gl);
     if (got != flt) fail("filter bytes of id " + std::to_string(f));
     const auto ws = split_words(flt);
     const bool wild = is_wild(ws);
@@ -253,6 +255,68 @@ emqx_gm_index* host_update(emqx_gm_index* prev, const std::vector<std::pair<std:
   return out;
 }
 
+// gm_filters.h FilterTable: random delete / insert batches against a std::set,
+// with a small compaction threshold so shared-base tables, deltas over deltas
+// and compactions all occur; every id, every rank_of and the in-order walk checked.
+int filter_table_check() {
+  int bad = 0;
+  std::mt19937_64 rng(11);
+  std::set<std::string> ref;
+  for (int i = 0; i < 300; ++i) ref.insert(rand_filter(rng, 4));
+  auto sf = std::make_shared<SortedFilters>();
+  for (auto& f : ref) sf->push(reinterpret_cast<const uint8_t*>(f.data()), f.size());
+  FilterTable ft;
+  ft.set_base(sf);
+  for (int round = 0; round < 200; ++round) {
+    std::vector<uint64_t> dels;
+    std::set<std::string> adds, gone;
+    const int nd = int(rng() % 6), na = int(rng() % 6);
+    for (int i = 0; i < nd && !ref.empty(); ++i) {
+      auto it = ref.begin();
+      std::advance(it, rng() % ref.size());
+      gone.insert(*it);
+    }
+    for (auto& g : gone) dels.push_back(uint64_t(std::distance(ref.begin(), ref.find(g))));
+    std::sort(dels.begin(), dels.end());
+    for (int i = 0; i < na; ++i) {
+      std::string f = rand_filter(rng, 4);
+      if (!ref.count(f) || gone.count(f)) adds.insert(f);  // a deleted filter may come back
+    }
+    for (auto& g : gone) ref.erase(g);
+    for (auto& a : adds) ref.insert(a);
+    ft = ft.apply(dels, adds, 8);
+    if (ft.size() != ref.size()) {
+      if (bad++ < 5) std::fprintf(stderr, "filter table: size %llu vs %zu\n", (unsigned long long)ft.size(), ref.size());
+      continue;
+    }
+    uint64_t r = 0;
+    for (auto& f : ref) {
+      uint64_t l;
+      const uint8_t* p = ft.at(r, &l);
+      bool found;
+      const uint64_t rk = ft.rank_of(reinterpret_cast<const uint8_t*>(f.data()), f.size(), &found);
+      if (std::string(reinterpret_cast<const char*>(p), l) != f || rk != r || !found)
+        if (bad++ < 5) std::fprintf(stderr, "filter table: id %llu\n", (unsigned long long)r);
+      ++r;
+    }
+    std::string absent = rand_filter(rng, 4) + "/zz";
+    bool found;
+    const uint64_t rk = ft.rank_of(reinterpret_cast<const uint8_t*>(absent.data()), absent.size(), &found);
+    if (found || rk != uint64_t(std::distance(ref.begin(), ref.lower_bound(absent))))
+      if (bad++ < 5) std::fprintf(stderr, "filter table: absent rank\n");
+    uint64_t walked = 0;
+    auto it = ref.begin();
+    ft.for_each([&](uint64_t id, const uint8_t* p, uint64_t l) {
+      if (id != walked || it == ref.end() || std::string(reinterpret_cast<const char*>(p), l) != *it)
+        if (bad++ < 5) std::fprintf(stderr, "filter table: walk at %llu\n", (unsigned long long)id);
+      ++walked;
+      if (it != ref.end()) ++it;
+    });
+    if (walked != ref.size() && bad++ < 5) std::fprintf(stderr, "filter table: walk length\n");
+  }
+  return bad;
+}
+
 int patch_sequences() {
   int bad = 0;
   std::mt19937_64 rng(7);
@@ -336,10 +400,10 @@ int main() {
   {
     emqx_gm_index base;
     std::vector<std::string> fs = {"a", "a/+", "b/#", "c", "d/e/f", "x"};
-    base.foff.push_back(0);
-    for (auto& f : fs) {
-      base.fbytes.insert(base.fbytes.end(), f.begin(), f.end());
-      base.foff.push_back(base.fbytes.size());
+    {
+      auto sf = std::make_shared<gm::SortedFilters>();
+      for (auto& f : fs) sf->push(reinterpret_cast<const uint8_t*>(f.data()), f.size());
+      base.ft.set_base(sf);
     }
     base.info.n_filters = fs.size();
     emqx_gm_index ov;
@@ -368,6 +432,7 @@ int main() {
     delete ov.ov;
     ov.ov = nullptr;
   }
+  bad += filter_table_check();
   bad += patch_sequences();
   std::printf(bad ? "ASAN_HOST_CHECK_FAILED %d\n" : "ASAN_HOST_CHECK_OK\n", bad);
   return bad ? 1 : 0;
