@@ -355,12 +355,18 @@ def main():
     algo = tbytes + 8 * n_topics + 16 * st["probes"] + 4 * nnz + fbytes_matched + 8 * n_topics
     kavg = sum(kern_ms) / len(kern_ms)
     achieved = algo / (kavg / 1e3) / 1e9
-    traffic = None
+    # roofline.traffic: the PMC bytes of this very build (scripts/profile.sh ->
+    # scripts/traffic.py stamps the library's hash); a stale file gives null
+    traffic, lines, traffic_note = None, None, "no profile of this build (scripts/gpu_full.sh)"
     try:
+        import hashlib
         with open(a.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("config") == cfg and tj.get("n_topics") == n_topics:
-            traffic = tj.get("hbm_bytes_per_launch")
+        with open(os.path.join(ROOT, "emqx_amd", "libemqx_gpu_match.so"), "rb") as f:
+            sha = hashlib.sha256(f.read()).hexdigest()[:16]
+        if tj.get("config") == cfg and tj.get("n_topics") == n_topics and tj.get("lib_sha16") == sha:
+            traffic, lines = tj.get("hbm_bytes_per_launch"), tj.get("lines_per_topic")
+            traffic_note = f"PMC of this build ({os.path.relpath(a.traffic_json, ROOT)}, lib {sha})"
     except (OSError, ValueError):
         pass
 
@@ -377,7 +383,10 @@ def main():
                    "parallelism": f"replicated index, batch partitioned over {world} GPU(s)"},
         "matches_per_sec": world * nnz * a.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
+                     "lines_per_topic": lines,
+                     # the SURVEY §8d formula credits Σ len(f) of the matched filters, bytes no kernel reads
+                     "frac_without_filter_bytes": (algo - fbytes_matched) / (kavg / 1e3) / 1e9 / HBM_PEAK_GBS,
                      "kernel": "k_match_fused", "kernel_ms": kavg, "algo_bytes_per_launch": algo},
         "detail": {"nnz_per_step": nnz, "matches_per_topic": nnz / n_topics, "probes_per_topic": st["probes"] /
                    n_topics, "overflow_rows": st["n_overflow"], "topic_bytes": tbytes,
@@ -421,14 +430,15 @@ def main():
         out["detail"]["index_update"] = {"ops": 200, "update_ms": upd_ms, "match_kernel_ms_after": min(ks),
                                          "vs_flat": min(ks) / min(kern_ms)}
         new.release()
-    if cfg == "c5" and rank == 0 and not a.no_parity:
+    big = cfg == "c5" and n_filters >= 50_000_000  # the oracle over this many keys does not fit the box
+    if big and rank == 0 and not a.no_parity:
         # the oracle over 100M keys does not fit the box's memory: the committed C5
         # fixture (2,000 strided topics of the stream, rows as filter strings) instead
         out["parity_sample"] = fixture_check(ctx, idx, "c5")
     # the cpu_baseline leg (oracle): timed on all host cores at N=1, and, outside the
     # timed region, the last step's CSR checked against it on a strided sample
-    want_cpu = rank == 0 and world == 1 and not a.no_cpu and cfg != "c5"
-    want_parity = rank == 0 and not a.no_parity and cfg != "c5"
+    want_cpu = rank == 0 and world == 1 and not a.no_cpu and not big
+    want_parity = rank == 0 and not a.no_parity and not big
     if want_cpu or want_parity:
         threads = a.cpu_threads or len(os.sched_getaffinity(0))
         r = oracle_router(fpack)

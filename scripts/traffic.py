@@ -23,22 +23,23 @@ import statistics
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_launch(path, kernel, min_grid):
+def per_launch(path, kernel, min_grid, counter=None):
     vals = []
     if not os.path.exists(path):
         return vals
     with open(path) as f:
         for r in csv.DictReader(f):
-            if kernel in r["Kernel_Name"] and int(r["Grid_Size"]) >= min_grid:
+            if kernel in r["Kernel_Name"] and int(r["Grid_Size"]) >= min_grid and \
+                    (counter is None or r["Counter_Name"] == counter):
                 vals.append(float(r["Counter_Value"]))
     return vals
 
 
-def per_launch_sum(path, kernels, min_grid):
+def per_launch_sum(path, kernels, min_grid, counter=None):
     """Per-launch average of each kernel, summed over the kernels of one match call."""
     total, counts = 0.0, []
     for k in kernels:
-        v = per_launch(path, k, min_grid)
+        v = per_launch(path, k, min_grid, counter)
         if not v:
             return None, counts
         total += statistics.mean(v)
@@ -61,9 +62,15 @@ def main():
         raise SystemExit(f"no full-batch {a.kernel} launches in {a.prof}")
     fetch_b = fetch * 1024 * 2  # KB -> B, gfx950 x2 correction
     write_b = write * 1024
+    rdreq, _ = per_launch_sum(os.path.join(a.prof, "pmc_ea", "run_counter_collection.csv"), ks, a.topics, "TCC_EA0_RDREQ_sum")
+    import hashlib
+    with open(os.path.join(ROOT, "emqx_amd", "libemqx_gpu_match.so"), "rb") as f:
+        lib_sha = hashlib.sha256(f.read()).hexdigest()[:16]
     out = {"config": a.config, "n_topics": a.topics, "kernel": a.kernel,
            "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
            "hbm_bytes_per_launch": fetch_b + write_b, "launches": [nf, nw],
+           "lines_per_topic": None if rdreq is None else rdreq / a.topics,
+           "lib_sha16": lib_sha,
            "note": "FETCH_SIZE x1024 x2 (gfx950 correction) + WRITE_SIZE x1024 per launch; L2 fabric side, "
                    "Infinity-Cache hits included"}
     with open(a.out, "w") as f:

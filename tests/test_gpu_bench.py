@@ -47,10 +47,21 @@ def test_bench_two_ranks_c2():
 @pytest.mark.gpu
 @pytest.mark.timeout(400)
 def test_bench_two_ranks_c5_exchange():
-    out = _run_ranks(["--config", "c5", "--filters", "50000", "--topics", "200000"], world=2)
+    out = _run_ranks(["--config", "c5", "--plan", "hash", "--filters", "50000", "--topics", "200000"], world=2)
     assert out["n_gpus"] == 2 and out["scaling"] == "strong"
     assert out["detail"]["exchange_bytes_per_step_rank0"] > 0
     assert out["matches_per_sec"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_two_ranks_c5_replicated():
+    """C5's default plan (north_star: replicate while the index fits): the
+    unsharded index on every rank, the batch partitioned, weak scaling."""
+    out = _run_ranks(["--config", "c5", "--filters", "50000", "--topics", "200000"], world=2)
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
+    assert out["config"]["topics_per_gpu"] == 200_000 and "replicated" in out["config"]["workload"]
+    assert out["parity_sample"]["ok"]
 
 
 @pytest.mark.gpu
