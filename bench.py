@@ -56,9 +56,12 @@ def parse():
     p.add_argument("--no-parity", action="store_true", help="skip the oracle check of the last step's sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--no-update", action="store_true", help="skip the incremental-update detail")
+    p.add_argument("--no-pipeline", action="store_true",
+                   help="one call at a time (emqx_gm_match) instead of two in flight (submit / wait)")
     p.add_argument("--no-host-io", action="store_true",
                    help="skip the host-buffer call (PCIe-inclusive rate, reported in detail, never `value`)")
     a = p.parse_args()
+    a.no_pipeline = a.no_pipeline or bool(os.environ.get("GM_BENCH_NO_PIPELINE"))  # (A/B scripts set env knobs)
     if a.steps is None:
         a.steps = 200 if a.config == "c1" else 5
     if a.warmup is None:
@@ -338,11 +341,23 @@ def main():
     kern_ms = []
     last = None
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        if last is not None:
-            last.free()
-        last = ctx.match_device(idx, db, do, n_topics, exact=True)
-        kern_ms.append(ctx.stats()["match_kernel_ms"])
+    if a.no_pipeline:
+        for _ in range(a.steps):
+            if last is not None:
+                last.free()
+            last = ctx.match_device(idx, db, do, n_topics, exact=True)
+            kern_ms.append(ctx.stats()["match_kernel_ms"])
+    else:
+        # two calls in flight (emqx_gm_match_submit / _wait): step i+1's kernels
+        # are queued before the host finishes step i, as a serving loop does
+        cur = ctx.match_submit(idx, db, do, n_topics, exact=True)
+        for i in range(a.steps):
+            nxt = ctx.match_submit(idx, db, do, n_topics, exact=True) if i + 1 < a.steps else None
+            r = cur.wait()
+            kern_ms.append(ctx.stats()["match_kernel_ms"])
+            if last is not None:
+                last.free()
+            last, cur = r, nxt
     ctx.synchronize()
     barrier(pg)
     elapsed = time.perf_counter() - t0
@@ -391,7 +406,8 @@ def main():
         "detail": {"nnz_per_step": nnz, "matches_per_topic": nnz / n_topics, "probes_per_topic": st["probes"] /
                    n_topics, "overflow_rows": st["n_overflow"], "topic_bytes": tbytes,
                    "index_device_bytes": int(idx.info.device_bytes), "index_nodes": int(idx.info.n_nodes),
-                   "index_build_s": t_build, "device_ms_per_call": st["total_device_ms"]},
+                   "index_build_s": t_build, "device_ms_per_call": st["total_device_ms"],
+                   "calls_in_flight": 1 if a.no_pipeline else 2},
     }
     if not a.no_host_io and rank == 0:
         # PCIe-inclusive, outside the timed region: the same batch handed over in host

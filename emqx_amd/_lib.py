@@ -68,6 +68,8 @@ SIGNATURES = {
     "emqx_gm_index_filter": (_i32, [_vp, _u32, C.POINTER(_vp), C.POINTER(_u64)]),
     "emqx_gm_index_subscriber_count": (_i32, [_vp, _u32, C.POINTER(_u64)]),
     "emqx_gm_match": (_i32, [_vp, _vp, _vp, _vp, _u64, _u32, C.POINTER(Csr)]),
+    "emqx_gm_match_submit": (_i32, [_vp, _vp, _vp, _vp, _u64, _u32, C.POINTER(_vp)]),
+    "emqx_gm_match_wait": (_i32, [_vp, _vp, C.POINTER(Csr)]),
     "emqx_gm_fanout": (_i32, [_vp, _vp, C.POINTER(Csr), _u32, C.POINTER(Csr)]),
     "emqx_gm_csr_free": (_i32, [_vp, C.POINTER(Csr)]),
     "emqx_gm_last_stats": (_i32, [_vp, C.POINTER(MatchStats)]),

@@ -29,8 +29,43 @@ int set_err(emqx_gm_ctx* ctx, int code, const std::string& msg) {
 
 DevPool::~DevPool() {
   hipSetDevice(device_);
+  reclaim(true);
   for (auto& kv : free_) hipFree(kv.second);
   for (auto& kv : live_) hipFree(kv.first);
+  for (hipEvent_t e : ev_idle_) hipEventDestroy(e);
+}
+
+void DevPool::release_after(void* p, hipStream_t s) {
+  if (!p || !live_.count(p)) return;
+  hipEvent_t e = nullptr;
+  if (!ev_idle_.empty()) {
+    e = ev_idle_.back();
+    ev_idle_.pop_back();
+  } else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+    e = nullptr;
+  }
+  if (!e || hipEventRecord(e, s) != hipSuccess) {  // no event: the old way, wait for the stream
+    if (e) ev_idle_.push_back(e);
+    hipStreamSynchronize(s);
+    release(p);
+    return;
+  }
+  deferred_.emplace_back(p, e);
+}
+
+void DevPool::reclaim(bool wait) {
+  size_t keep = 0;
+  for (size_t i = 0; i < deferred_.size(); ++i) {
+    auto& d = deferred_[i];
+    const bool done = wait ? (hipEventSynchronize(d.second), true) : hipEventQuery(d.second) == hipSuccess;
+    if (done) {
+      ev_idle_.push_back(d.second);
+      release(d.first);
+    } else {
+      deferred_[keep++] = d;
+    }
+  }
+  deferred_.resize(keep);
 }
 
 // Buffers still handed out (live_) are NOT freed: a caller may hold a host CSR
@@ -90,6 +125,7 @@ static size_t round_size(size_t b) {
 }
 
 void* DevPool::alloc(size_t bytes) {
+  if (!deferred_.empty()) reclaim(false);
   size_t r = round_size(bytes);
   auto it = free_.lower_bound(r);
   if (it != free_.end() && it->first <= r + r / 4) {
@@ -103,6 +139,14 @@ void* DevPool::alloc(size_t bytes) {
   hipSetDevice(device_);
   if (hipMalloc(&p, r) != hipSuccess) {
     trim();
+    if (!deferred_.empty()) {  // memory is short: wait for the deferred frees, then try once more
+      reclaim(true);
+      trim();
+      if (hipMalloc(&p, r) == hipSuccess) {
+        live_[p] = r;
+        return p;
+      }
+    }
     if (hipMalloc(&p, r) != hipSuccess) return nullptr;
   }
   live_[p] = r;
@@ -120,6 +164,7 @@ void DevPool::release(void* p) {
 void DevPool::trim() {
   hipSetDevice(device_);
   hipDeviceSynchronize();
+  reclaim(false);  // (every event has passed now)
   for (auto& kv : free_) hipFree(kv.second);
   free_.clear();
   cached_ = 0;
@@ -194,7 +239,8 @@ int emqx_gm_close(emqx_gm_ctx* ctx) {
     }
     for (auto& e : ctx->ov_ev)
       if (e) hipEventDestroy(e);
-    if (ctx->pin) hipHostFree(ctx->pin);
+    for (hipEvent_t e : ctx->ev_free) hipEventDestroy(e);
+    for (void* p : ctx->pin_all) hipHostFree(p);
   }
   delete ctx;
   return EMQX_GM_OK;
@@ -306,7 +352,7 @@ int emqx_gm_index_subscriber_count(const emqx_gm_index* idx, uint32_t id, uint64
 int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to,
                   uint64_t n, uint32_t flags, emqx_gm_csr* out) {
   if (!ctx) return EMQX_GM_EINVAL;
-  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  std::unique_lock<std::recursive_mutex> lk(ctx->mu);
   if (!idx || !out || (n && (!tb || !to))) return gm::set_err(ctx, EMQX_GM_EINVAL, "match: NULL argument");
   if (flags & ~(EMQX_GM_WITH_EXACT | EMQX_GM_DEVICE_IO)) return gm::set_err(ctx, EMQX_GM_EINVAL, "match: flags");
   if (n >= 0xFFFFFFF0ull) return gm::set_err(ctx, EMQX_GM_EINVAL, "match: batch too large (>= 2^32 topics)");
@@ -317,7 +363,46 @@ int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb,
   if (idx->ov) return gm::run_match_overlay(ctx, idx, tb, to, n, flags, out);
   if (!(flags & EMQX_GM_DEVICE_IO) && !getenv("GM_HOST_SIMPLE"))  // host buffers: chunked, pipelined
     return gm::run_match_host(ctx, idx, tb, to, n, flags, out);
-  return gm::run_match(ctx, idx, tb, to, n, flags, out);
+  if (!(flags & EMQX_GM_DEVICE_IO)) return gm::run_match(ctx, idx, tb, to, n, flags, out);
+  // device buffers: the call is queued under the lock and waited for outside
+  // it, so concurrent callers' batches queue behind this one meanwhile
+  void* t = nullptr;
+  const int rc = gm::match_submit(ctx, idx, tb, to, n, flags, &t);
+  if (rc) return rc;
+  lk.unlock();
+  return gm::match_wait(ctx, t, out);
+  GM_GUARD_END(ctx)
+}
+
+int emqx_gm_match_submit(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to,
+                         uint64_t n, uint32_t flags, emqx_gm_call** call) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  if (!call) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: NULL call");
+  *call = nullptr;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (!idx || (n && (!tb || !to))) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: NULL argument");
+  if (flags & ~(EMQX_GM_WITH_EXACT | EMQX_GM_DEVICE_IO)) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: flags");
+  if (!(flags & EMQX_GM_DEVICE_IO))
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: device buffers only (EMQX_GM_DEVICE_IO)");
+  if (n >= 0xFFFFFFF0ull) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: batch too large (>= 2^32 topics)");
+  if (idx->device != ctx->device) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: index lives on another device");
+  if (idx->ov) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "match_submit: overlay snapshot (use emqx_gm_match)");
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  void* t = nullptr;
+  const int rc = gm::match_submit(ctx, idx, tb, to, n, flags, &t);
+  if (rc == EMQX_GM_OK) *call = static_cast<emqx_gm_call*>(t);
+  return rc;
+  GM_GUARD_END(ctx)
+}
+
+int emqx_gm_match_wait(emqx_gm_ctx* ctx, emqx_gm_call* call, emqx_gm_csr* out) {
+  if (!ctx || !call) return EMQX_GM_EINVAL;
+  if (!out) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_wait: NULL out");
+  std::memset(out, 0, sizeof(*out));
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  return gm::match_wait(ctx, call, out);
   GM_GUARD_END(ctx)
 }
 
@@ -363,10 +448,12 @@ int emqx_gm_csr_free(emqx_gm_ctx* ctx, emqx_gm_csr* csr) {
   if (csr->priv && csr->priv != static_cast<void*>(ctx))
     return gm::set_err(ctx, EMQX_GM_EINVAL, "csr_free: the CSR belongs to another context");
   if (csr->on_device) {
+    // back to the pool once the work queued so far (which may still read the
+    // rows: a fan-out, a later call's inputs) is done -- no wait here, so a
+    // caller with the next call in flight keeps it in flight
     hipSetDevice(ctx->device);
-    hipStreamSynchronize(ctx->stream);
-    if (csr->row_off) ctx->pool->release(csr->row_off);
-    if (csr->ids) ctx->pool->release(csr->ids);
+    if (csr->row_off) ctx->pool->release_after(csr->row_off, ctx->stream);
+    if (csr->ids) ctx->pool->release_after(csr->ids, ctx->stream);
   } else {
     ctx->hpool->release(csr->row_off);
     ctx->hpool->release(csr->ids);

@@ -26,6 +26,11 @@ class DevPool {
   ~DevPool();
   void* alloc(size_t bytes);           // nullptr on failure
   void release(void* p);
+  // Release once the work queued on `s` so far is done (a result CSR the
+  // caller frees while later calls may still be queued behind its readers):
+  // an event marks the point, alloc() reclaims the buffer once it has passed,
+  // and nothing waits.
+  void release_after(void* p, hipStream_t s);
   void trim();
   size_t cached_bytes() const { return cached_; }
 
@@ -33,7 +38,10 @@ class DevPool {
   int device_;
   std::multimap<size_t, void*> free_;  // rounded size -> ptr
   std::map<void*, size_t> live_;       // ptr -> rounded size
+  std::vector<std::pair<void*, hipEvent_t>> deferred_;
+  std::vector<hipEvent_t> ev_idle_;
   size_t cached_ = 0;
+  void reclaim(bool wait);
 };
 
 // Host result buffers (the CSRs emqx_gm_match / emqx_gm_fanout return in host
@@ -109,7 +117,10 @@ struct emqx_gm_ctx {
   gm::HostPool* hpool = nullptr;
   emqx_gm_match_stats stats{};
   hipEvent_t ev[6]{};
-  void* pin = nullptr;  // pinned host words for a call's small read-backs (calls are serialized by mu)
+  // per match call (gm_match.hip MatchCall, under mu): reusable events and
+  // 64-B pinned read-back slots, so several calls can be in flight
+  std::vector<hipEvent_t> ev_free;
+  std::vector<void*> pin_free, pin_all;
   double ids_per_topic = 4.0;  // speculative ids capacity of a match call (run_match), from recent calls
 };
 
@@ -214,6 +225,11 @@ struct MatchTail {
 };
 int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
               uint32_t flags, emqx_gm_csr* out, MatchTail* tail = nullptr);
+// the two halves of run_match (emqx_gm_match_submit / _wait): submit under
+// ctx->mu; wait without it (it takes the lock after the device wait)
+int match_submit(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                 uint32_t flags, void** ticket);
+int match_wait(emqx_gm_ctx* ctx, void* ticket, emqx_gm_csr* out);
 int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
                emqx_gm_csr* out, uint32_t part = 0, uint32_t n_parts = 1, uint64_t* first_out = nullptr);
 int run_merge_rows(emqx_gm_ctx* ctx, uint64_t n_rows, uint64_t stride, uint32_t n_pieces, const uint32_t* d_lens,

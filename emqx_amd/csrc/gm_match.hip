@@ -2720,18 +2720,81 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
 
 }  // namespace
 
-int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, const uint64_t* to_in, uint64_t n,
-              uint32_t flags, emqx_gm_csr* out, MatchTail* tail) {
-  const bool dev_io = flags & EMQX_GM_DEVICE_IO;
-  const bool exact = flags & EMQX_GM_WITH_EXACT;
+// One match call in two phases (emqx_gm_match = submit then finish at once;
+// emqx_gm_match_submit / emqx_gm_match_wait split them, so the next batch's
+// launches queue behind this one's before the host has read its total):
+//   submit(): every kernel of the call, the speculative assembly and the
+//     40-B read-back of the match total + pass counters into the call's own
+//     pinned words, then an event -- no host wait;
+//   finish(): waits on that event (without the context lock when it was
+//     submitted alone), then either hands out the speculative rows or runs
+//     the slow path / exact-size assembly and waits again.
+// A call owns its workspaces (PoolBufs), events and pinned words until
+// finish(), so several can be in flight on one context stream.
+struct MatchCall {
+  emqx_gm_ctx* ctx;
+  const emqx_gm_index* idx = nullptr;
+  uint64_t n = 0, n_tiles = 0, nblk = 0, cap_spec = 0;
+  bool dev_io = false, exact = false, cmp = false, spec = false, split = false, submitted = false;
+  const uint8_t* tb = nullptr;
+  const uint64_t* to = nullptr;
+  PoolBuf d_tb_own, d_to_own, row_off, cnt, stage, list1, list2, tsum, toff, probe_tile, hdr, wids;
+  PoolBuf c_tlen, c_lstage, c_lcnt, c_cnt8, scan_blk, ids;
+  CmpBufs cmpb{};
+  uint64_t* toff_p = nullptr;
+  uint8_t* ctrs_p = nullptr;
+  uint64_t* pin = nullptr;  // [0] match total, [1..4] the pass counters
+  hipEvent_t ev[3] = {};    // start, after the main pass, done
+  explicit MatchCall(emqx_gm_ctx* c) : ctx(c) {}
+  MatchCall(const MatchCall&) = delete;
+  MatchCall& operator=(const MatchCall&) = delete;
+  ~MatchCall() {
+    // (caller holds ctx->mu: the pools are not thread safe)
+    if (submitted) hipStreamSynchronize(ctx->stream);  // an abandoned call: its kernels may still use the buffers
+    for (hipEvent_t& e : ev)
+      if (e) ctx->ev_free.push_back(e);
+    if (pin) ctx->pin_free.push_back(pin);
+    if (idx) const_cast<emqx_gm_index*>(idx)->refs.fetch_sub(1) == 1 ? free_index(const_cast<emqx_gm_index*>(idx))
+                                                                     : void();
+  }
+  int take_event(hipEvent_t* e) {
+    if (!ctx->ev_free.empty()) {
+      *e = ctx->ev_free.back();
+      ctx->ev_free.pop_back();
+      return 0;
+    }
+    GM_HIP(ctx, hipEventCreate(e));
+    return 0;
+  }
+  int submit(const emqx_gm_index* index, const uint8_t* tb_in, const uint64_t* to_in, uint64_t n_topics,
+             uint32_t flags, MatchTail* tail);
+  int finish(emqx_gm_csr* out, MatchTail* tail, bool locked);
+};
+
+int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const uint64_t* to_in, uint64_t n_topics,
+                      uint32_t flags, MatchTail* tail) {
+  dev_io = flags & EMQX_GM_DEVICE_IO;
+  exact = flags & EMQX_GM_WITH_EXACT;
+  n = n_topics;
+  const_cast<emqx_gm_index*>(index)->refs.fetch_add(1);  // the snapshot stays alive until finish (RCU)
+  idx = index;
   hipStream_t st = ctx->stream;
-  ctx->stats = emqx_gm_match_stats{};
-  ctx->stats.n_topics = n;
+  for (hipEvent_t& e : ev)
+    if (int rc = take_event(&e)) return rc;
+  if (!ctx->pin_free.empty()) {
+    pin = static_cast<uint64_t*>(ctx->pin_free.back());
+    ctx->pin_free.pop_back();
+  } else {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocDefault) != hipSuccess)
+      return set_err(ctx, EMQX_GM_ENOMEM, "match: pinned read-back words");
+    ctx->pin_all.push_back(p);
+    pin = static_cast<uint64_t*>(p);
+  }
 
   // ---- inputs on the device
-  PoolBuf d_tb_own, d_to_own;
-  const uint8_t* tb = tb_in;
-  const uint64_t* to = to_in;
+  tb = tb_in;
+  to = to_in;
   if (!dev_io) {
     const uint64_t bytes = n ? to_in[n] : 0;
     for (uint64_t i = 0; i < n; ++i)
@@ -2739,6 +2802,7 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
     d_tb_own = PoolBuf(ctx->pool, bytes + 64);
     d_to_own = PoolBuf(ctx->pool, (n + 1) * 8);
     if (!d_tb_own.p || !d_to_own.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: input workspace");
+    submitted = true;
     if (bytes) GM_HIP(ctx, hipMemcpyAsync(d_tb_own.p, tb_in, bytes, hipMemcpyHostToDevice, st));
     GM_HIP(ctx, hipMemsetAsync(static_cast<uint8_t*>(d_tb_own.p) + bytes, 0, 64, st));
     GM_HIP(ctx, hipMemcpyAsync(d_to_own.p, to_in, (n + 1) * 8, hipMemcpyHostToDevice, st));
@@ -2746,37 +2810,39 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
     to = d_to_own.as<uint64_t>();
   }
 
-  PoolBuf row_off(ctx->pool, (n + 1) * 8);
+  row_off = PoolBuf(ctx->pool, (n + 1) * 8);
   if (!row_off.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: row_off");
+  submitted = true;
   if (n == 0) {
     GM_HIP(ctx, hipMemsetAsync(row_off.p, 0, 8, st));
-    PoolBuf ids(ctx->pool, 16);
-    return finish_csr(ctx, 0, 0, row_off, ids, dev_io, out);
+    ids = PoolBuf(ctx->pool, 16);
+    GM_HIP(ctx, hipEventRecord(ev[0], st));
+    GM_HIP(ctx, hipEventRecord(ev[1], st));
+    GM_HIP(ctx, hipEventRecord(ev[2], st));
+    pin[0] = pin[1] = pin[2] = pin[3] = pin[4] = 0;
+    return 0;
   }
 
-  const uint64_t n_tiles = (n + 63) / 64;
-  const uint64_t nblk = (n + 255) / 256;
-  PoolBuf cnt(ctx->pool, n * 4 + 16);
-  PoolBuf stage(ctx->pool, n_tiles * 64ull * FAST_MC * 4);
-  PoolBuf list1(ctx->pool, n * 4 + 16), list2(ctx->pool, n * 4 + 16);
-  PoolBuf tsum(ctx->pool, n_tiles * 8 + 8);
+  n_tiles = (n + 63) / 64;
+  nblk = (n + 255) / 256;
+  cnt = PoolBuf(ctx->pool, n * 4 + 16);
+  stage = PoolBuf(ctx->pool, n_tiles * 64ull * FAST_MC * 4);
+  list1 = PoolBuf(ctx->pool, n * 4 + 16);
+  list2 = PoolBuf(ctx->pool, n * 4 + 16);
+  tsum = PoolBuf(ctx->pool, n_tiles * 8 + 8);
   // tile offsets [n_tiles + 1] and, right behind the total, the pass counters:
   // one read-back brings the match total and the counters together
-  PoolBuf toff(ctx->pool, (n_tiles + 1) * 8 + 128);
+  toff = PoolBuf(ctx->pool, (n_tiles + 1) * 8 + 128);
   if (!cnt.p || !stage.p || !list1.p || !list2.p || !tsum.p || !toff.p)
     return set_err(ctx, EMQX_GM_ENOMEM, "match: workspace");
-  if (!ctx->pin && hipHostMalloc(&ctx->pin, 256, hipHostMallocDefault) != hipSuccess) {
-    ctx->pin = nullptr;
-    return set_err(ctx, EMQX_GM_ENOMEM, "match: pinned read-back words");
-  }
   // the counters start 64-B aligned, so zeroing them is one fill launch (an
   // unaligned 64-B memset is split into three)
   const uintptr_t ctrs_a = (reinterpret_cast<uintptr_t>(toff.p) + (n_tiles + 1) * 8 + 63) & ~uintptr_t(63);
-  uint8_t* const ctrs_p = reinterpret_cast<uint8_t*>(ctrs_a);
-  uint64_t* const toff_p = reinterpret_cast<uint64_t*>(ctrs_p) - (n_tiles + 1);
-  PoolBuf probe_tile(ctx->pool, n_tiles * 8 + 8);
+  ctrs_p = reinterpret_cast<uint8_t*>(ctrs_a);
+  toff_p = reinterpret_cast<uint64_t*>(ctrs_p) - (n_tiles + 1);
+  probe_tile = PoolBuf(ctx->pool, n_tiles * 8 + 8);
   if (!probe_tile.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: probe workspace");
-  PoolBuf hdr, wids;  // split forms: per-topic header and word ids [level][topic] (the fused kernel keeps them in registers)
+  // split forms: per-topic header and word ids [level][topic] (the fused kernel keeps them in registers)
   if (main_kind() != MAIN_FUSED) {
     hdr = PoolBuf(ctx->pool, n * 4 + 16);
     wids = PoolBuf(ctx->pool, uint64_t(TOK_LMAX) * n * 4 + 16);
@@ -2792,9 +2858,7 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   // before the main pass can be queued, a launch ~6)
   hipLaunchKernelGGL(k_zero16, dim3(1), dim3(64), 0, st, reinterpret_cast<uint32_t*>(ctrs_p));
 
-  PoolBuf c_tlen, c_lstage, c_lcnt, c_cnt8;
-  CmpBufs cmpb{};
-  const bool cmp = main_kind() == MAIN_FUSED && stage_compact() && uint64_t(idx->view.n_filters) < (1ull << CMP_SHIFT);
+  cmp = main_kind() == MAIN_FUSED && stage_compact() && uint64_t(idx->view.n_filters) < (1ull << CMP_SHIFT);
   if (cmp) {
     const char* le = getenv("GM_LISTED_CAP");  // (tests: listed rows past it go to the slow path)
     cmpb.lcap = std::min<uint64_t>(n, le ? strtoull(le, nullptr, 10) : (1u << 20));
@@ -2808,15 +2872,15 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
     cmpb.lstage = c_lstage.as<uint32_t>();
     cmpb.lcnt = c_lcnt.as<uint32_t>();
   }
-  GM_HIP(ctx, hipEventRecord(ctx->ev[1], st));  // (also the call's start: total_device_ms)
+  GM_HIP(ctx, hipEventRecord(ev[0], st));  // (also the call's start: total_device_ms)
   if (exact)
     launch_match<true>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
                        list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
-                       probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ctx->ev[2], cmp ? &cmpb : nullptr);
+                       probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ev[1], cmp ? &cmpb : nullptr);
   else
     launch_match<false>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(),
                         n1, list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
-                        probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ctx->ev[2], cmp ? &cmpb : nullptr);
+                        probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ev[1], cmp ? &cmpb : nullptr);
   GM_HIP(ctx, hipGetLastError());
 
   // count -> scan, then ONE host round trip reads the pass counters and the
@@ -2824,58 +2888,73 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
   // (tsum: per-tile match counts, written by the main pass and topped up by the listed and slow passes)
   // (compact staging: a two-level scan is left split, k_assemble_c adds the
   // block offsets -- one launch fewer; GM_SCAN_SPLIT=0 turns it off)
-  PoolBuf scan_blk;
   const char* se = getenv("GM_SCAN_SPLIT");
-  const bool split = cmp && (!se || atoi(se) != 0);
+  split = cmp && (!se || atoi(se) != 0);
   int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p,
                      SideSum{probe_tile.as<unsigned long long>(), n_tiles, probe_ctr}, split ? &scan_blk : nullptr);
   if (rc) return rc;
-  const uint64_t* const blk = scan_blk.as<uint64_t>();
   // Speculative assembly: the rows are written before the host has read the
   // match total, into an ids buffer sized from this context's recent matches
   // per topic (x1.25), so a call makes ONE host round trip.  The total, the
   // pass counters and the assembly come back together; a batch with a listed-
   // pass overflow (slow-path rows) or more matches than the buffer holds is
-  // assembled again below, once the host knows the total.
+  // assembled again in finish(), once the host knows the total.
   // (at most FAST_MC per topic: a longer row is a slow-path row, assembled again anyway)
-  const uint64_t cap_spec = 1024 + uint64_t(double(n) * std::min(ctx->ids_per_topic, double(FAST_MC)));
+  cap_spec = 1024 + uint64_t(double(n) * std::min(ctx->ids_per_topic, double(FAST_MC)));
   // (no room for the speculative buffer: skip speculation, the rows are
-  // assembled below at their exact size once the total is known)
-  PoolBuf ids(ctx->pool, cap_spec * 4 + 16);
-  const bool spec = ids.p != nullptr;
+  // assembled at their exact size once the total is known)
+  ids = PoolBuf(ctx->pool, cap_spec * 4 + 16);
+  spec = ids.p != nullptr;
   if (spec) {
     launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
-                    row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec, blk);
+                    row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec, scan_blk.as<uint64_t>());
     GM_HIP(ctx, hipGetLastError());
     if (tail && tail->enqueue) {
       rc = tail->enqueue(row_off.as<uint64_t>(), ids.as<uint32_t>(), cap_spec);
       if (rc) return rc;
     }
   }
-  uint64_t* const pin = static_cast<uint64_t*>(ctx->pin);  // [0] match total, [1..4] the counters
   GM_HIP(ctx, hipMemcpyAsync(pin, toff_p + n_tiles, 40, hipMemcpyDeviceToHost, st));
-  GM_HIP(ctx, hipEventRecord(ctx->ev[3], st));
-  GM_HIP(ctx, hipStreamSynchronize(st));
+  GM_HIP(ctx, hipEventRecord(ev[2], st));
+  return 0;
+}
+
+int MatchCall::finish(emqx_gm_csr* out, MatchTail* tail, bool locked) {
+  // wait for the read-back; a call submitted alone waits without the context
+  // lock, so other threads can queue their calls meanwhile
+  if (locked) {
+    GM_HIP(ctx, hipEventSynchronize(ev[2]));
+  } else {
+    const hipError_t e = hipEventSynchronize(ev[2]);
+    if (e != hipSuccess) return set_err(ctx, EMQX_GM_EDEVICE, std::string("match_wait: ") + hipGetErrorString(e));
+  }
+  std::unique_lock<std::recursive_mutex> lk(ctx->mu, std::defer_lock);
+  if (!locked) lk.lock();
+  hipStream_t st = ctx->stream;
+  emqx_gm_match_stats& S = ctx->stats;
+  S = emqx_gm_match_stats{};
+  S.n_topics = n;
+  if (n == 0) {
+    submitted = false;
+    return finish_csr(ctx, 0, 0, row_off, ids, dev_io, out);
+  }
   uint64_t nnz = pin[0];
   const uint64_t h_ctr[4] = {pin[1], pin[2], pin[3], pin[4]};
+  S.probes = h_ctr[2];
+  S.n_wildcard_topics = h_ctr[3];
+  S.n_overflow = uint32_t(h_ctr[0]);
   if (spec && uint32_t(h_ctr[0] >> 32) == 0 && nnz <= cap_spec) {  // no slow-path row, and the rows fit: done
-    ctx->stats.probes = h_ctr[2];
-    ctx->stats.n_wildcard_topics = h_ctr[3];
-    ctx->stats.n_overflow = uint32_t(h_ctr[0]);
     ctx->ids_per_topic = std::max(1.0, 1.25 * double(nnz) / double(n));
-    ctx->stats.nnz = nnz;
-    ctx->stats.match_kernel_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
-    ctx->stats.total_device_ms = ev_ms(ctx->ev[1], ctx->ev[3]);
+    S.nnz = nnz;
+    S.match_kernel_ms = ev_ms(ev[0], ev[1]);
+    S.total_device_ms = ev_ms(ev[0], ev[2]);
     if (tail) tail->used = true;
+    submitted = false;
     return finish_csr(ctx, n, nnz, row_off, ids, dev_io, out);
   }
   ids.reset();
   if (nnz > cap_spec) ctx->ids_per_topic = std::max(ctx->ids_per_topic, 1.25 * double(nnz) / double(n));
-  const uint64_t n_listed = uint32_t(h_ctr[0]);
   const uint64_t n_ovf = uint32_t(h_ctr[0] >> 32);
-  ctx->stats.probes = h_ctr[2];
-  ctx->stats.n_wildcard_topics = h_ctr[3];
-  ctx->stats.n_overflow = n_listed;
 
   // ---- slow path for rows the listed pass could not hold
   PoolBuf slow_off, slow_ids;
@@ -2928,30 +3007,59 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
       GM_HIP(ctx, hipGetLastError());
     }
     // the slow path added its rows' counts to tsum: scan again
-    rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p);
+    int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p);
     if (rc) return rc;
     GM_HIP(ctx, hipMemcpyAsync(&nnz, toff_p + n_tiles, 8, hipMemcpyDeviceToHost, st));
     GM_HIP(ctx, hipStreamSynchronize(st));
   }
 
-  // ---- write the rows (again: the speculative pass above did not fit or missed slow-path rows)
+  // ---- write the rows (again: the speculative pass did not fit or missed slow-path rows)
   ids = PoolBuf(ctx->pool, nnz * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: ids");
   // (after a slow-path rescan toff is whole; otherwise it is still the split first scan)
   launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
-                  row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, nnz, n_ovf ? nullptr : blk);
+                  row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, nnz,
+                  n_ovf ? nullptr : scan_blk.as<uint64_t>());
   GM_HIP(ctx, hipGetLastError());
   if (n_ovf) {
     hipLaunchKernelGGL(k_copy_slow, dim3(n_ovf), dim3(256), 0, st, ovf_list, n_ovf, row_off.as<uint64_t>(),
                        slow_off.as<uint64_t>(), slow_ids.as<uint32_t>(), ids.as<uint32_t>(), idx->view.gmap);
     GM_HIP(ctx, hipGetLastError());
   }
-  GM_HIP(ctx, hipEventRecord(ctx->ev[3], st));
-  GM_HIP(ctx, hipEventSynchronize(ctx->ev[3]));
-  ctx->stats.nnz = nnz;
-  ctx->stats.match_kernel_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
-  ctx->stats.total_device_ms = ev_ms(ctx->ev[1], ctx->ev[3]);
+  GM_HIP(ctx, hipEventRecord(ev[2], st));
+  GM_HIP(ctx, hipEventSynchronize(ev[2]));
+  S.nnz = nnz;
+  S.match_kernel_ms = ev_ms(ev[0], ev[1]);
+  S.total_device_ms = ev_ms(ev[0], ev[2]);
+  submitted = false;
   return finish_csr(ctx, n, nnz, row_off, ids, dev_io, out);
+}
+
+int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, const uint64_t* to_in, uint64_t n,
+              uint32_t flags, emqx_gm_csr* out, MatchTail* tail) {
+  MatchCall c(ctx);
+  if (int rc = c.submit(idx, tb_in, to_in, n, flags, tail)) return rc;
+  return c.finish(out, tail, true);
+}
+
+int match_submit(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                 uint32_t flags, void** ticket) {
+  auto* c = new MatchCall(ctx);
+  if (int rc = c->submit(idx, tb, to, n, flags, nullptr)) {
+    delete c;
+    return rc;
+  }
+  *ticket = c;
+  return 0;
+}
+
+// (called without ctx->mu; takes it after the wait)
+int match_wait(emqx_gm_ctx* ctx, void* ticket, emqx_gm_csr* out) {
+  auto* c = static_cast<MatchCall*>(ticket);
+  const int rc = c->finish(out, nullptr, false);
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  delete c;
+  return rc;
 }
 
 int scan_lengths(emqx_gm_ctx* ctx, const uint64_t* len, uint64_t n, uint64_t* out) {

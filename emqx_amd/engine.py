@@ -88,6 +88,28 @@ class DeviceCsr:
             pass
 
 
+class PendingMatch:
+    """A submitted match call (emqx_gm_match_submit); wait() exactly once."""
+
+    def __init__(self, ctx: "Context", call):
+        self.ctx, self.call = ctx, call
+
+    def wait(self) -> "DeviceCsr":
+        if not self.call:
+            raise GpuMatchError(_lib.EINVAL, "match_wait: already waited")
+        csr = Csr()
+        call, self.call = self.call, None
+        check(lib().emqx_gm_match_wait(self.ctx.h, call, C.byref(csr)), self.ctx.h, "match_wait")
+        return DeviceCsr(self.ctx, csr)
+
+    def __del__(self):
+        try:
+            if self.call and self.ctx.h:
+                self.wait().free()
+        except Exception:
+            pass
+
+
 class HostCsr:
     """A result CSR in host memory owned by the library (emqx_gm_match without
     DEVICE_IO); ``row_off`` / ``ids`` are views valid until ``free()``."""
@@ -277,6 +299,15 @@ class Context:
         check(lib().emqx_gm_match(self.h, index.h, C.c_void_p(d_bytes), C.c_void_p(d_off), n, flags,
                                   C.byref(csr)), self.h, "match")
         return DeviceCsr(self, csr)
+
+    def match_submit(self, index: Index, d_bytes: int, d_off: int, n: int, exact: bool = True) -> "PendingMatch":
+        """emqx_gm_match_submit: the call's kernels queued on the device, no wait;
+        ``wait()`` on the result gives the DeviceCsr.  Inputs stay the caller's until then."""
+        call = C.c_void_p()
+        flags = _lib.DEVICE_IO | (_lib.WITH_EXACT if exact else 0)
+        check(lib().emqx_gm_match_submit(self.h, index.h, C.c_void_p(d_bytes), C.c_void_p(d_off), n, flags,
+                                         C.byref(call)), self.h, "match_submit")
+        return PendingMatch(self, call)
 
     def fanout(self, index: Index, row_off: np.ndarray, ids: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
         """emqx_broker:dispatch/2 over each row's matched filters -> subscriber CSR (multiset rows)."""

@@ -73,6 +73,7 @@ extern "C" {
 
 typedef struct emqx_gm_ctx emqx_gm_ctx;
 typedef struct emqx_gm_index emqx_gm_index;
+typedef struct emqx_gm_call emqx_gm_call;
 
 typedef struct {
   int32_t device;        /* HIP device ordinal; one process per GPU            */
@@ -193,6 +194,21 @@ int emqx_gm_index_subscriber_count(const emqx_gm_index *idx, uint32_t id, uint64
 /* ---- hot path ---- */
 int emqx_gm_match(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const uint8_t *topic_bytes,
                   const uint64_t *topic_off, uint64_t n_topics, uint32_t flags, emqx_gm_csr *out);
+/* emqx_gm_match in two halves, for device buffers (EMQX_GM_DEVICE_IO
+ * required): submit queues the call's kernels on the context stream and
+ * returns at once; wait blocks until that call is done, hands out its rows
+ * (exactly what emqx_gm_match returns) and frees the call.  Several calls may
+ * be in flight on one context, from one thread or many (the reference matches
+ * in every publisher's own process, lock-free: emqx_trie.erl:68-70,
+ * emqx_router.erl:128-145): a batch's launches queue behind the previous
+ * one's while the host still finishes that one, so the device does not idle
+ * between small batches.  The inputs (and the index, which the call retains)
+ * must stay valid until wait returns.  Overlay snapshots: EMQX_GM_EUNSUPPORTED
+ * (use emqx_gm_match).  emqx_gm_match itself waits without the context lock
+ * for device buffers. */
+int emqx_gm_match_submit(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const uint8_t *topic_bytes,
+                         const uint64_t *topic_off, uint64_t n_topics, uint32_t flags, emqx_gm_call **call);
+int emqx_gm_match_wait(emqx_gm_ctx *ctx, emqx_gm_call *call, emqx_gm_csr *out);
 int emqx_gm_fanout(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const emqx_gm_csr *matches,
                    uint32_t flags, emqx_gm_csr *out_subs);
 int emqx_gm_csr_free(emqx_gm_ctx *ctx, emqx_gm_csr *csr);

@@ -21,13 +21,14 @@ ab() {  # ab <config> <spec...>
   for spec in "$@"; do
     i=$((i + 1))
     envs=(); [ "$spec" != "-" ] && IFS=',' read -r -a envs <<< "$spec"
-    env "${envs[@]}" timeout -k 10 400 python3 -u bench.py --config $cfg --steps ${STEPS:-5} --warmup 2 --no-cpu --no-parity \
+    env "${envs[@]}" timeout -k 10 400 python3 -u bench.py --config $cfg --steps ${STEPS:-5} --warmup ${WARM:-2} --no-cpu --no-parity \
       --no-host-io --no-update > $OUT/ab_${cfg}_$i.log 2>&1
     rc=$?
     echo "[$cfg $spec] rc=$rc $(tail -n 1 $OUT/ab_${cfg}_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value']/1e9, 3), 'Gtopics/s ms/step', round(d['ms_per_step'], 3), 'kernel_ms', round(d['roofline']['kernel_ms'], 3), 'listed', d['detail']['overflow_rows'])" 2>&1)"
     [ $rc -ne 0 ] && { tail -n 5 $OUT/ab_${cfg}_$i.log; exit $rc; }
   done
 }
+[ -n "${AB1:-}" ] && STEPS=200 ab c1 $AB1
 [ -n "${AB:-}" ] && ab c2 $AB
 [ -n "${AB3:-}" ] && ab c3 $AB3
 if [ -n "${PMC:-}" ]; then

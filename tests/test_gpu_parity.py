@@ -619,6 +619,7 @@ def test_concurrent_calls_one_context(ctx, orc):
     each failing call's message its own (emqx_gm_last_error is per thread)."""
     import threading
     from emqx_amd import GpuMatchError
+    from emqx_amd.engine import pack
     rng = random.Random(99)
     filters = sorted({_rand_filter(rng).encode() for _ in range(400)})
     subs = [rng.sample(range(10_000), rng.randint(0, 5)) for _ in filters]
@@ -627,6 +628,10 @@ def test_concurrent_calls_one_context(ctx, orc):
     plain = ctx.build_index(filters)
     want_ro, want_ids = ctx.match(idx, topics, exact=True)
     want_fro, want_fids = ctx.fanout(idx, want_ro, want_ids)
+    tb, to = pack(topics)
+    d_tb, d_to = ctx.dev_alloc(len(tb)), ctx.dev_alloc(len(to) * 8)
+    ctx.memcpy_h2d(d_tb, tb, len(tb))
+    ctx.memcpy_h2d(d_to, to, len(to) * 8)
     errors, done = [], []
 
     def worker(k):
@@ -640,6 +645,13 @@ def test_concurrent_calls_one_context(ctx, orc):
                 elif kind == 1:
                     fro, fids = ctx.fanout(idx, want_ro, want_ids)
                     assert np.array_equal(fro, want_fro) and np.array_equal(fids, want_fids)
+                    # and overlapping submits of device-buffer calls from this thread
+                    pend = [ctx.match_submit(idx, d_tb, d_to, len(topics)) for _ in range(3)]
+                    for pm in pend:
+                        res = pm.wait()
+                        ro, ids = res.to_host()
+                        res.free()
+                        assert np.array_equal(ro, want_ro) and np.array_equal(ids, want_ids)
                 elif kind == 2:  # an update of the shared plain index (overlay or patch) and a match on it
                     new_f = b"k%d/%d/+" % (k, it)
                     t = b"k%d/%d/x" % (k, it)
@@ -664,8 +676,51 @@ def test_concurrent_calls_one_context(ctx, orc):
         t.join()
     assert not errors, errors[:3]
     assert sorted(done) == list(range(8))
+    ctx.dev_free(d_tb)
+    ctx.dev_free(d_to)
     idx.release()
     plain.release()
+
+
+def test_submit_wait_pipelined_vs_oracle(ctx, orc):
+    """emqx_gm_match_submit / _wait: four batches of different sizes (one with
+    listed- and slow-path rows, one empty) in flight at once on one context,
+    waited for out of order; every result equals its own single emqx_gm_match
+    and the oracle; the index may be released while calls are in flight (a call
+    retains its snapshot)."""
+    from emqx_amd.engine import pack
+    lv = ["a", "b", "c", "d", "e", "f"]
+    heavy = set()
+    for m in range(1 << 6):  # slow-path rows: every '+'/word mix over 6 levels
+        ws = ["+" if (m >> i) & 1 else lv[i] for i in range(6)]
+        heavy.add("/".join(ws))
+        heavy.add("/".join(ws[:3]) + "/#")
+    rng = random.Random(5)
+    filters = sorted({f.encode() for f in heavy} | {_rand_filter(rng).encode() for _ in range(500)})
+    batches = [[_rand_topic(rng).encode() for _ in range(n)] for n in (1, 5000, 70_000)]
+    batches.append([b"a/b/c/d/e/f"] * 300 + [b"a/x/c/d/e/f"] * 300)
+    batches.append([])
+    idx = ctx.build_index(filters)
+    bufs, pend = [], []
+    for topics in batches:
+        tb, to = pack(topics) if topics else (np.zeros(64, np.uint8), np.zeros(1, np.uint64))
+        d_tb, d_to = ctx.dev_alloc(len(tb)), ctx.dev_alloc(len(to) * 8)
+        ctx.memcpy_h2d(d_tb, tb, len(tb))
+        ctx.memcpy_h2d(d_to, to, len(to) * 8)
+        bufs += [d_tb, d_to]
+        pend.append(ctx.match_submit(idx, d_tb, d_to, len(topics)))
+    want = [ctx.match(idx, t, exact=True) if t else (np.zeros(1, np.uint64), np.zeros(0, np.uint32)) for t in batches]
+    idx.release()  # the calls in flight keep the snapshot
+    for k in (3, 0, 4, 2, 1):  # out of submission order
+        res = pend[k].wait()
+        ro, ids = res.to_host()
+        res.free()
+        assert np.array_equal(ro, want[k][0]) and np.array_equal(ids, want[k][1]), k
+        if batches[k]:
+            oro, oids = _oracle_rows(orc, filters, batches[k], 1)
+            assert np.array_equal(ro, oro) and np.array_equal(ids, oids), k
+    for b in bufs:
+        ctx.dev_free(b)
 
 
 def test_fused_priority_knob_same_rows(ctx, orc, monkeypatch):
