@@ -43,10 +43,11 @@ def parse():
                    help="timed steps (default 5; C1's 0.13-ms step: 200, so the timed region is not noise)")
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2; C1: 20)")
     p.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
-    p.add_argument("--plan", default="replicated", choices=["replicated", "hash"],
+    p.add_argument("--plan", default="replicated", choices=["replicated", "prefix", "hash"],
                    help="C5: the unsharded index replicated on every GPU with the batch partitioned (north_star: "
-                        "replicate while the index fits 288 GB; 100M filters = 38 GB), or filters hash-sharded "
-                        "with the rows exchanged (all-to-all) and merged")
+                        "replicate while the index fits 288 GB; 100M filters = 38 GB); filters prefix-sharded "
+                        "(first word) with each topic routed to its one shard (all-to-all of topics, rows back); "
+                        "or filters hash-sharded, every rank walking every topic, rows exchanged and merged")
     p.add_argument("--filters", type=int, default=None)
     p.add_argument("--topics", type=int, default=None, help="topics per GPU per step")
     p.add_argument("--seed", type=int, default=1)
@@ -313,6 +314,8 @@ def main():
         return bench_c4(a, world, rank, local, pg)
     if cfg == "c5" and a.plan == "hash":
         return bench_c5(a, world, rank, local, pg)
+    if cfg == "c5" and a.plan == "prefix":
+        return bench_c5_prefix(a, world, rank, local, pg)
     n_filters = a.filters or {"c1": 10_000, "c2": 1_000_000, "c3": 10_000_000, "c5": 100_000_000}[cfg]
     n_topics = a.topics or {"c1": 1_000_000, "c2": 100_000_000, "c3": 100_000_000, "c5": 100_000_000}[cfg]
     wildcard_only = cfg == "c2"
@@ -531,6 +534,85 @@ def bench_c5(a, world, rank, local, pg):
     ctx.dev_free(db)
     ctx.dev_free(do)
     idx.release()
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def bench_c5_prefix(a, world, rank, local, pg):
+    """C5 prefix-sharded (gm_route.hip): filters partitioned by first word
+    over the ranks (root wildcards on every shard), each rank publishes its own
+    batch, every topic is routed to the one shard that holds all the filters it
+    can match and walked there (all-to-all of topics, rows back in batch order):
+    a rank walks ~1/N of the job, so topic throughput grows with N ("weak":
+    each rank publishes n topics per step)."""
+    import numpy as np
+    from emqx_amd import Context
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    from emqx_amd.sharded import PrefixShardedMatcher, plan_prefix_shard
+    n_filters = a.filters or 100_000_000
+    n_topics = a.topics or 100_000_000
+    ctx = Context(local)
+    t0 = time.perf_counter()
+    codes = gen_filter_codes(a.seed, n_filters)
+    fb, fo = render_codes(codes)
+    sfb, sfo, gids, n_unique, route = plan_prefix_shard(fb, fo, world, rank)
+    del fb, fo
+    idx = ctx.build_index_shard((sfb, sfo), gids)
+    t_build = time.perf_counter() - t0
+    db, do, tbytes = ctx.gen_topics_device(codes, a.seed, rank * n_topics, n_topics)
+    dev = BACKEND == "nccl"
+    if dev:
+        m = PrefixShardedMatcher(ctx, idx, route, world, rank, dist=pg)
+        step = lambda: m.match_device(db, do, n_topics)  # noqa: E731
+    else:  # rehearsal (gloo, ranks sharing a device): the exchange on host tensors, the match on the device
+        hb = np.zeros(tbytes + 64, np.uint8)
+        ho = np.zeros(n_topics + 1, np.uint64)
+        ctx.memcpy_d2h(hb, db, tbytes)
+        ctx.memcpy_d2h(ho, do, (n_topics + 1) * 8)
+        m = PrefixShardedMatcher(ctx, idx, route, world, rank, dist=pg, device_tensors=False,
+                                 match_fn=lambda tb, to: ctx.match(idx, (tb, to), exact=True))
+        step = lambda: m.match_host(hb, ho)  # noqa: E731
+    for _ in range(max(a.warmup, 1)):
+        r = step()
+        if dev:
+            r.free()
+    barrier(pg)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    nnz = 0
+    for _ in range(a.steps):
+        r = step()
+        nnz = r.nnz if dev else int(r[0][-1])
+        if dev:
+            r.free()
+    ctx.synchronize()
+    barrier(pg)
+    elapsed = barrier_max(pg, local, time.perf_counter() - t0)
+    walked = [m.last_topics_walked]
+    if pg is not None:
+        import torch
+        t = torch.zeros(world + 1, dtype=torch.float64, device=f"cuda:{local}" if dev else "cpu")
+        t[rank] = float(m.last_topics_walked)
+        t[world] = float(nnz)
+        pg.all_reduce(t)
+        walked = [int(x) for x in t[:world].tolist()]
+        nnz = int(t[world].item())
+    out = {"metric": "publish topics matched/sec, filters prefix-sharded over GPUs (C5)",
+           "value": world * n_topics * a.steps / elapsed, "unit": "topics/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic (seeded §8d generator, mixed filters; topics generated on device)",
+           "config": {"workload": f"C5: {n_unique} filters prefix-sharded over {world} GPU(s) (first word; root "
+                                  f"wildcards on every shard), {n_topics} topics per GPU routed to their shard",
+                      "filters": n_unique, "topics_per_gpu": n_topics, "parallelism": f"prefix shards x{world}"},
+           "matches_per_sec": nnz * a.steps / elapsed,
+           "detail": {"index_build_s": t_build, "shard_filters": int(len(gids)), "topics_walked_per_rank": walked,
+                      "exchange_bytes_per_step_rank0": m.last_exchange_bytes}}
+    ctx.dev_free(db)
+    ctx.dev_free(do)
+    idx.release()
+    route.release()
     ctx.close()
     if rank == 0:
         print(json.dumps(out), flush=True)

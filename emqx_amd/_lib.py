@@ -78,6 +78,12 @@ SIGNATURES = {
     "emqx_gm_index_build_shard": (_i32, [_vp, _vp, _vp, _u64, _vp, _vp, _vp, _vp, C.POINTER(_vp)]),
     "emqx_gm_csr_row_lengths": (_i32, [_vp, C.POINTER(Csr), _vp]),
     "emqx_gm_merge_rows": (_i32, [_vp, _u64, _u64, _u32, _vp, _vp, _u32, C.POINTER(Csr)]),
+    "emqx_gm_prefix_plan": (_i32, [_vp, _vp, _u64, _u32, _vp, C.POINTER(_vp)]),
+    "emqx_gm_route_topics_host": (_i32, [_vp, _vp, _vp, _u64, _vp]),
+    "emqx_gm_route_topics": (_i32, [_vp, _vp, _vp, _vp, _u64, _vp]),
+    "emqx_gm_route_release": (_i32, [_vp]),
+    "emqx_gm_permute_topics": (_i32, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "emqx_gm_unpermute_rows": (_i32, [_vp, _u64, _vp, _vp, _vp, _u32, C.POINTER(Csr)]),
     # emqx_gm_ext.h
     "emqx_gm_gen_filter_codes": (_i32, [_u64, _u64, _i32, _vp]),
     "emqx_gm_render_codes": (_u64, [_vp, _u64, _vp, _vp]),

@@ -574,6 +574,65 @@ int emqx_gm_merge_rows(emqx_gm_ctx* ctx, uint64_t n_rows, uint64_t stride, uint3
   GM_GUARD_END(ctx)
 }
 
+// ---- prefix sharding ----
+int emqx_gm_prefix_plan(const uint8_t* fb, const uint64_t* fo, uint64_t n, uint32_t n_shards, uint32_t* shard_out,
+                        emqx_gm_route** route) {
+  if (!route || !n_shards || (n && (!fb || !fo || !shard_out))) return EMQX_GM_EINVAL;
+  *route = nullptr;
+  GM_GUARD_BEGIN
+  return gm::route_plan(fb, fo, n, n_shards, shard_out, route);
+  GM_GUARD_END(nullptr)
+}
+
+int emqx_gm_route_topics_host(const emqx_gm_route* route, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                              uint32_t* dest) {
+  if (!route || (n && (!tb || !to || !dest))) return EMQX_GM_EINVAL;
+  return gm::route_topics_host(route, tb, to, n, dest);
+}
+
+int emqx_gm_route_topics(emqx_gm_ctx* ctx, emqx_gm_route* route, const uint8_t* d_tb, const uint64_t* d_to, uint64_t n,
+                         uint32_t* d_dest) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (!route || (n && (!d_tb || !d_to || !d_dest))) return gm::set_err(ctx, EMQX_GM_EINVAL, "route_topics: NULL argument");
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  return gm::route_topics_device(ctx, route, d_tb, d_to, n, d_dest);
+  GM_GUARD_END(ctx)
+}
+
+int emqx_gm_route_release(emqx_gm_route* route) {
+  if (!route) return EMQX_GM_EINVAL;
+  gm::free_route(route);
+  return EMQX_GM_OK;
+}
+
+int emqx_gm_permute_topics(emqx_gm_ctx* ctx, const uint8_t* d_tb, const uint64_t* d_to, uint64_t n,
+                           const uint32_t* d_perm, uint8_t* d_out, uint64_t* d_out_off) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (!d_out_off || (n && (!d_tb || !d_to || !d_perm || !d_out)))
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "permute_topics: NULL argument");
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  return gm::permute_topics(ctx, d_tb, d_to, n, d_perm, d_out, d_out_off);
+  GM_GUARD_END(ctx)
+}
+
+int emqx_gm_unpermute_rows(emqx_gm_ctx* ctx, uint64_t n, const uint32_t* d_perm, const uint32_t* d_lens,
+                           const uint32_t* d_ids, uint32_t flags, emqx_gm_csr* out) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (!out || (n && (!d_perm || !d_lens || !d_ids)))
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "unpermute_rows: NULL argument");
+  if (flags & ~EMQX_GM_DEVICE_IO) return gm::set_err(ctx, EMQX_GM_EINVAL, "unpermute_rows: flags");
+  std::memset(out, 0, sizeof(*out));
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  return gm::unpermute_rows(ctx, n, d_perm, d_lens, d_ids, flags, out);
+  GM_GUARD_END(ctx)
+}
+
 int emqx_gm_pool_trim(emqx_gm_ctx* ctx) {
   if (!ctx) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);

@@ -235,6 +235,18 @@ int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m,
 int run_merge_rows(emqx_gm_ctx* ctx, uint64_t n_rows, uint64_t stride, uint32_t n_pieces, const uint32_t* d_lens,
                    const uint32_t* d_ids, uint32_t flags, emqx_gm_csr* out);
 int run_row_lengths(emqx_gm_ctx* ctx, const emqx_gm_csr* csr, uint32_t* d_out);
+// prefix sharding (gm_route.hip) and the exchange's device steps
+int route_plan(const uint8_t* fb, const uint64_t* fo, uint64_t n, uint32_t n_shards, uint32_t* shard_out,
+               emqx_gm_route** out);
+int route_topics_host(const emqx_gm_route* r, const uint8_t* tb, const uint64_t* to, uint64_t n, uint32_t* dest);
+int route_topics_device(emqx_gm_ctx* ctx, emqx_gm_route* r, const uint8_t* d_tb, const uint64_t* d_to, uint64_t n,
+                        uint32_t* d_dest);
+void free_route(emqx_gm_route* r);
+int permute_topics(emqx_gm_ctx* ctx, const uint8_t* d_tb, const uint64_t* d_to, uint64_t n, const uint32_t* d_perm,
+                   uint8_t* d_out, uint64_t* d_out_off);
+int unpermute_rows(emqx_gm_ctx* ctx, uint64_t n, const uint32_t* d_perm, const uint32_t* d_lens, const uint32_t* d_ids,
+                   uint32_t flags, emqx_gm_csr* out);
+int scan_lengths(emqx_gm_ctx* ctx, const uint64_t* len, uint64_t n, uint64_t* out);
 
 // gm_overlay.cpp — incremental index maintenance.  An
 // overlay snapshot = an immutable base snapshot (shared, retained) minus

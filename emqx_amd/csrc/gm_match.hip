@@ -3150,6 +3150,54 @@ int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m,
   return finish_csr(ctx, n, cnt, row_off, ids, dev_out, out);
 }
 
+// Rows back in their batch order after a prefix-routed exchange (sharded.py,
+// gm_route.hip): out row perm[i] = input row i, the input rows packed in send
+// order with u32 lengths lens[i].
+__global__ __launch_bounds__(256) void k_unperm_lens(const uint32_t* __restrict__ lens, const uint32_t* __restrict__ perm,
+                                                     uint64_t n, uint64_t* __restrict__ lens_out,
+                                                     uint64_t* __restrict__ lens_in) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (i < n) {
+    lens_out[perm[i]] = lens[i];
+    lens_in[i] = lens[i];
+  }
+}
+__global__ __launch_bounds__(256) void k_unperm_rows(const uint32_t* __restrict__ ids, const uint64_t* __restrict__ in_off,
+                                                     const uint32_t* __restrict__ perm, uint64_t n,
+                                                     const uint64_t* __restrict__ row_off, uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t(blockIdx.x) * 256u + threadIdx.x) >> 6;  // a wave per row
+  const uint32_t lane = threadIdx.x & 63u;
+  if (i >= n) return;
+  const uint64_t a = in_off[i], len = in_off[i + 1] - a, d = row_off[perm[i]];
+  for (uint64_t k = lane; k < len; k += 64) out[d + k] = ids[a + k];
+}
+
+int unpermute_rows(emqx_gm_ctx* ctx, uint64_t n, const uint32_t* d_perm, const uint32_t* d_lens, const uint32_t* d_ids,
+                   uint32_t flags, emqx_gm_csr* out) {
+  hipStream_t st = ctx->stream;
+  PoolBuf row_off(ctx->pool, (n + 1) * 8), in_off(ctx->pool, (n + 1) * 8), l_out(ctx->pool, n * 8 + 8),
+      l_in(ctx->pool, n * 8 + 8);
+  if (!row_off.p || !in_off.p || !l_out.p || !l_in.p) return set_err(ctx, EMQX_GM_ENOMEM, "unpermute_rows: workspace");
+  if (n) {
+    hipLaunchKernelGGL(k_unperm_lens, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, st, d_lens, d_perm, n,
+                       l_out.as<uint64_t>(), l_in.as<uint64_t>());
+    GM_HIP(ctx, hipGetLastError());
+  }
+  if (int rc = scan_lengths(ctx, l_out.as<uint64_t>(), n, row_off.as<uint64_t>())) return rc;
+  if (int rc = scan_lengths(ctx, l_in.as<uint64_t>(), n, in_off.as<uint64_t>())) return rc;
+  uint64_t nnz = 0;
+  GM_HIP(ctx, hipMemcpyAsync(&nnz, row_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+  GM_HIP(ctx, hipStreamSynchronize(st));
+  PoolBuf ids(ctx->pool, nnz * 4 + 16);
+  if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "unpermute_rows: ids");
+  if (n) {
+    hipLaunchKernelGGL(k_unperm_rows, dim3(uint32_t((n * 64 + 255) / 256)), dim3(256), 0, st, d_ids,
+                       in_off.as<uint64_t>(), d_perm, n, row_off.as<uint64_t>(), ids.as<uint32_t>());
+    GM_HIP(ctx, hipGetLastError());
+  }
+  return finish_csr(ctx, n, nnz, row_off, ids, flags & EMQX_GM_DEVICE_IO, out);
+}
+
 int run_merge_rows(emqx_gm_ctx* ctx, uint64_t n, uint64_t stride, uint32_t pieces, const uint32_t* d_lens,
                    const uint32_t* d_ids, uint32_t flags, emqx_gm_csr* out) {
   hipStream_t st = ctx->stream;

@@ -1,0 +1,275 @@
+// gm_route.hip — prefix sharding of a filter set too large to replicate
+// (BASELINE.json configs[4]).
+//
+// Hash sharding (emqx_gm_shard_of) makes every rank walk EVERY topic against
+// its shard, so topic throughput cannot grow with the ranks.  Here filters are
+// partitioned by their FIRST WORD: a topic can only match filters whose first
+// word is its own first word, '+' or '#' (emqx_topic:match/2,
+// apps/emqx/src/emqx_topic.erl:65-87), so once the root-wildcard filters are
+// on every shard, each topic needs exactly ONE shard -- the one owning its
+// first word -- and a rank walks ~1/N of the topics.
+//   * first-word partitions are assigned greedily (largest first, to the
+//     least loaded shard);
+//   * a HOT first word (more than 1/(2N) of the non-root filters) is split by
+//     its second word; its filters whose second word is '+' / '#' or absent
+//     ('w', 'w/#', 'w/+/...') go to every shard, like the root wildcards;
+//   * a topic whose prefix owns no partition can only match replicated
+//     filters: any shard does (one picked by hash, for balance).
+// The route table (key bytes -> shard) is built on the host and used by the
+// host (tests) and by a device kernel (one thread per topic) with the same
+// logic; keys are verified byte for byte, so routing never aliases.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "gm_internal.h"
+#include "../../include/emqx_gm_ext.h"
+
+namespace gm {
+
+constexpr uint32_t RT_SPLIT = 0x80000000u;  // in RouteSlot::shard: a hot first word, split by its second word
+constexpr uint32_t RT_EMPTY = 0xFFFFFFFFu;
+
+struct RouteSlot {
+  uint32_t hash;   // dict_hash of the key bytes
+  uint32_t len;    // key length; RT_EMPTY marks an empty slot
+  uint32_t off;    // key bytes in the route arena
+  uint32_t shard;  // owning shard, or RT_SPLIT
+};
+
+}  // namespace gm
+
+struct emqx_gm_route {
+  uint32_t n_shards = 1;
+  std::vector<gm::RouteSlot> slots;  // open addressing, power-of-two capacity
+  std::vector<uint8_t> arena;        // key bytes ('w' or 'w/v')
+  // device copy per device (uploaded on first use)
+  std::mutex mu;
+  std::unordered_map<int, void*> dev;
+};
+
+namespace gm {
+namespace {
+
+GM_HD uint32_t rt_hash(const uint8_t* p, uint32_t len) {
+  uint32_t h = DICT_HASH_SEED;
+  for (uint32_t i = 0; i < len; i += 8) {
+    uint64_t c = 0;
+    for (uint32_t k = 0; k < 8 && i + k < len; ++k) c |= uint64_t(p[i + k]) << (8 * k);
+    h = dict_hash_step(h, c);
+  }
+  return dict_hash_final(h, len);
+}
+
+// the shard of a topic (host and device share it): its first word's
+// partition, or its two-word prefix's for a split first word, else by hash
+GM_HD uint32_t rt_route(const RouteSlot* slots, uint32_t mask, const uint8_t* arena, uint32_t n_shards,
+                        const uint8_t* t, uint32_t len) {
+  uint32_t e0 = 0;
+  while (e0 < len && t[e0] != '/') ++e0;
+  auto find = [&](uint32_t klen) -> uint32_t {
+    const uint32_t h = rt_hash(t, klen);
+    for (uint32_t s = h & mask;; s = (s + 1) & mask) {
+      const RouteSlot r = slots[s];
+      if (r.len == RT_EMPTY) return RT_EMPTY;
+      if (r.hash == h && r.len == klen) {
+        bool eq = true;
+        for (uint32_t i = 0; i < klen && eq; ++i) eq = arena[r.off + i] == t[i];
+        if (eq) return r.shard;
+      }
+    }
+  };
+  const uint32_t fallback = fmix32(rt_hash(t, e0) ^ 0x2545F491u) % n_shards;
+  uint32_t s = find(e0);
+  if (s == RT_EMPTY) return fallback;
+  if (!(s & RT_SPLIT)) return s;
+  if (e0 == len) return fallback;  // a one-word topic under a split word: only replicated filters match it
+  uint32_t e1 = e0 + 1;
+  while (e1 < len && t[e1] != '/') ++e1;
+  s = find(e1);
+  return s == RT_EMPTY || (s & RT_SPLIT) ? fallback : s;
+}
+
+__global__ __launch_bounds__(256) void k_route(const RouteSlot* __restrict__ slots, uint32_t mask,
+                                               const uint8_t* __restrict__ arena, uint32_t n_shards,
+                                               const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
+                                               uint64_t n, uint32_t* __restrict__ dest) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t a = to[i], b = to[i + 1];
+  dest[i] = rt_route(slots, mask, arena, n_shards, tb + a, uint32_t(b - a));
+}
+
+// out topic i = input topic perm[i]: lengths, then (after a scan) the bytes
+__global__ __launch_bounds__(256) void k_perm_lens(const uint64_t* __restrict__ to, const uint32_t* __restrict__ perm,
+                                                   uint64_t n, uint64_t* __restrict__ lens) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (i < n) lens[i] = to[perm[i] + 1] - to[perm[i]];
+}
+__global__ __launch_bounds__(256) void k_perm_bytes(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
+                                                    const uint32_t* __restrict__ perm, uint64_t n,
+                                                    const uint64_t* __restrict__ out_off, uint8_t* __restrict__ out) {
+  // a wave per topic: lanes copy its bytes
+  const uint64_t i = (uint64_t(blockIdx.x) * 256u + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63u;
+  if (i >= n) return;
+  const uint64_t a = to[perm[i]], len = to[perm[i] + 1] - a, d = out_off[i];
+  for (uint64_t k = lane; k < len; k += 64) out[d + k] = tb[a + k];
+}
+}  // namespace
+
+int route_plan(const uint8_t* fb, const uint64_t* fo, uint64_t n, uint32_t n_shards, uint32_t* shard_out,
+               emqx_gm_route** out) {
+  // ---- first words and their counts
+  std::vector<uint32_t> e0(n), e1(n);
+  std::unordered_map<std::string_view, uint64_t> cnt0;
+  uint64_t nonroot = 0;
+  auto sv = [&](uint64_t i, uint64_t len) {
+    return std::string_view(reinterpret_cast<const char*>(fb + fo[i]), len);
+  };
+  auto is_wild = [&](uint64_t i, uint64_t a, uint64_t b) {
+    return b - a == 1 && (fb[fo[i] + a] == '+' || fb[fo[i] + a] == '#');
+  };
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t len = fo[i + 1] - fo[i];
+    if (len >= (1ull << 31)) throw std::length_error("prefix_plan: filter too long");
+    uint64_t a = 0;
+    while (a < len && fb[fo[i] + a] != '/') ++a;
+    uint64_t b = a < len ? a + 1 : a;
+    while (b < len && fb[fo[i] + b] != '/') ++b;
+    e0[i] = uint32_t(a);
+    e1[i] = uint32_t(b);
+    if (is_wild(i, 0, a)) continue;
+    ++cnt0[sv(i, a)];
+    ++nonroot;
+  }
+  // ---- hot first words are split by their second word
+  std::unordered_map<std::string_view, uint64_t> parts;  // partition key -> filters
+  std::unordered_map<std::string_view, bool> hot;
+  for (const auto& kv : cnt0) hot[kv.first] = n_shards > 1 && kv.second * 2 * n_shards > nonroot;
+  std::vector<uint8_t> repl(n, 0);  // 1: every shard
+  std::vector<std::string_view> key(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t len = fo[i + 1] - fo[i];
+    if (is_wild(i, 0, e0[i])) {
+      repl[i] = 1;
+      continue;
+    }
+    std::string_view w0 = sv(i, e0[i]);
+    if (!hot[w0]) {
+      key[i] = w0;
+    } else if (e0[i] == len || is_wild(i, e0[i] + 1, e1[i])) {
+      repl[i] = 1;  // 'w', 'w/#', 'w/+/...': every topic under w may match it
+      continue;
+    } else {
+      key[i] = sv(i, e1[i]);
+    }
+    ++parts[key[i]];
+  }
+  // ---- greedy assignment: largest partition first, to the least loaded shard
+  std::vector<std::pair<uint64_t, std::string_view>> order;
+  order.reserve(parts.size());
+  for (const auto& kv : parts) order.emplace_back(kv.second, kv.first);
+  std::sort(order.begin(), order.end(), [](const auto& x, const auto& y) {
+    return x.first != y.first ? x.first > y.first : x.second < y.second;
+  });
+  std::vector<uint64_t> load(n_shards, 0);
+  std::unordered_map<std::string_view, uint32_t> owner;
+  for (const auto& p : order) {
+    const uint32_t s = uint32_t(std::min_element(load.begin(), load.end()) - load.begin());
+    owner[p.second] = s;
+    load[s] += p.first;
+  }
+  for (uint64_t i = 0; i < n; ++i) shard_out[i] = repl[i] ? EMQX_GM_ALL_SHARDS : owner[key[i]];
+  // ---- the route table: every partition key, plus each hot first word marked split
+  auto* r = new emqx_gm_route;
+  r->n_shards = n_shards;
+  std::vector<std::pair<std::string_view, uint32_t>> keys;
+  for (const auto& kv : owner) keys.emplace_back(kv.first, kv.second);
+  for (const auto& kv : hot)
+    if (kv.second) keys.emplace_back(kv.first, RT_SPLIT);
+  std::sort(keys.begin(), keys.end());  // deterministic layout
+  uint64_t cap = 16;
+  while (cap < keys.size() * 4) cap <<= 1;
+  r->slots.assign(cap, RouteSlot{0, RT_EMPTY, 0, 0});
+  for (const auto& k : keys) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(k.first.data());
+    const uint32_t len = uint32_t(k.first.size());
+    const uint32_t h = rt_hash(p, len);
+    uint64_t s = h & (cap - 1);
+    while (r->slots[s].len != RT_EMPTY) s = (s + 1) & (cap - 1);
+    r->slots[s] = RouteSlot{h, len, uint32_t(r->arena.size()), k.second};
+    r->arena.insert(r->arena.end(), p, p + len);
+    if (r->arena.size() >= 0xFFFFFFF0ull) throw std::length_error("prefix_plan: route keys exceed 4 GiB");
+  }
+  r->arena.resize(r->arena.size() + 8, 0);
+  *out = r;
+  return EMQX_GM_OK;
+}
+
+int route_topics_host(const emqx_gm_route* r, const uint8_t* tb, const uint64_t* to, uint64_t n, uint32_t* dest) {
+  const uint32_t mask = uint32_t(r->slots.size() - 1);
+  for (uint64_t i = 0; i < n; ++i)
+    dest[i] = rt_route(r->slots.data(), mask, r->arena.data(), r->n_shards, tb + to[i], uint32_t(to[i + 1] - to[i]));
+  return EMQX_GM_OK;
+}
+
+int route_topics_device(emqx_gm_ctx* ctx, emqx_gm_route* r, const uint8_t* d_tb, const uint64_t* d_to, uint64_t n,
+                        uint32_t* d_dest) {
+  void* dev = nullptr;
+  const size_t o_arena = (r->slots.size() * sizeof(RouteSlot) + 255) & ~size_t(255);
+  {
+    std::lock_guard<std::mutex> lk(r->mu);
+    auto it = r->dev.find(ctx->device);
+    if (it == r->dev.end()) {
+      GM_HIP(ctx, hipMalloc(&dev, o_arena + r->arena.size()));
+      GM_HIP(ctx, hipMemcpy(dev, r->slots.data(), r->slots.size() * sizeof(RouteSlot), hipMemcpyHostToDevice));
+      GM_HIP(ctx, hipMemcpy(static_cast<uint8_t*>(dev) + o_arena, r->arena.data(), r->arena.size(),
+                            hipMemcpyHostToDevice));
+      r->dev[ctx->device] = dev;
+    } else {
+      dev = it->second;
+    }
+  }
+  if (!n) return EMQX_GM_OK;
+  hipLaunchKernelGGL(k_route, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, ctx->stream,
+                     static_cast<const RouteSlot*>(dev), uint32_t(r->slots.size() - 1),
+                     static_cast<const uint8_t*>(dev) + o_arena, r->n_shards, d_tb, d_to, n, d_dest);
+  GM_HIP(ctx, hipGetLastError());
+  return EMQX_GM_OK;
+}
+
+void free_route(emqx_gm_route* r) {
+  for (auto& kv : r->dev) {
+    hipSetDevice(kv.first);
+    hipFree(kv.second);
+  }
+  delete r;
+}
+
+int scan_lengths(emqx_gm_ctx* ctx, const uint64_t* len, uint64_t n, uint64_t* out);
+
+int permute_topics(emqx_gm_ctx* ctx, const uint8_t* d_tb, const uint64_t* d_to, uint64_t n, const uint32_t* d_perm,
+                   uint8_t* d_out, uint64_t* d_out_off) {
+  if (!n) {
+    GM_HIP(ctx, hipMemsetAsync(d_out_off, 0, 8, ctx->stream));
+    return EMQX_GM_OK;
+  }
+  PoolBuf lens(ctx->pool, n * 8 + 8);
+  if (!lens.p) return set_err(ctx, EMQX_GM_ENOMEM, "permute_topics: workspace");
+  hipLaunchKernelGGL(k_perm_lens, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, ctx->stream, d_to, d_perm, n,
+                     lens.as<uint64_t>());
+  GM_HIP(ctx, hipGetLastError());
+  if (int rc = scan_lengths(ctx, lens.as<uint64_t>(), n, d_out_off)) return rc;
+  hipLaunchKernelGGL(k_perm_bytes, dim3(uint32_t((n * 64 + 255) / 256)), dim3(256), 0, ctx->stream, d_tb, d_to,
+                     d_perm, n, d_out_off, d_out);
+  GM_HIP(ctx, hipGetLastError());
+  GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return EMQX_GM_OK;
+}
+
+}  // namespace gm

@@ -356,6 +356,21 @@ class Context:
                                        _lib.DEVICE_IO, C.byref(out)), self.h, "merge_rows")
         return DeviceCsr(self, out)
 
+    def route_topics(self, route: "Route", d_tb: int, d_to: int, n: int, d_dest: int):
+        """emqx_gm_route_topics: the shard of each device topic into d_dest (u32)."""
+        check(lib().emqx_gm_route_topics(self.h, route.h, C.c_void_p(d_tb), C.c_void_p(d_to), n,
+                                         C.c_void_p(d_dest)), self.h, "route_topics")
+
+    def permute_topics(self, d_tb: int, d_to: int, n: int, d_perm: int, d_out: int, d_out_off: int):
+        check(lib().emqx_gm_permute_topics(self.h, C.c_void_p(d_tb), C.c_void_p(d_to), n, C.c_void_p(d_perm),
+                                           C.c_void_p(d_out), C.c_void_p(d_out_off)), self.h, "permute_topics")
+
+    def unpermute_rows(self, n: int, d_perm: int, d_lens: int, d_ids: int) -> DeviceCsr:
+        out = Csr()
+        check(lib().emqx_gm_unpermute_rows(self.h, n, C.c_void_p(d_perm), C.c_void_p(d_lens), C.c_void_p(d_ids),
+                                           _lib.DEVICE_IO, C.byref(out)), self.h, "unpermute_rows")
+        return DeviceCsr(self, out)
+
     def memcpy_d2d(self, dst_ptr: int, src_ptr: int, nbytes: int):
         if nbytes:
             check(lib().emqx_gm_memcpy(self.h, C.c_void_p(dst_ptr), C.c_void_p(src_ptr), nbytes, 2), self.h, "memcpy")
@@ -434,6 +449,43 @@ def select_filters(fb: np.ndarray, fo: np.ndarray, shard: np.ndarray, want: int)
     check(lib().emqx_gm_select_filters(_ptr(fb), _ptr(fo), n, _ptr(sh), want, _ptr(ob), _ptr(oo), C.byref(k),
                                        C.byref(nb)), None, "select_filters")
     return ob, oo
+
+
+ALL_SHARDS = 0xFFFFFFFF
+
+
+class Route:
+    """The topic -> shard map of a prefix-sharded filter set (emqx_gm_prefix_plan)."""
+
+    def __init__(self, h, n_shards: int):
+        self.h, self.n_shards = h, n_shards
+
+    def route_host(self, tb: np.ndarray, to: np.ndarray) -> np.ndarray:
+        n = len(to) - 1
+        out = np.zeros(max(n, 1), np.uint32)
+        check(lib().emqx_gm_route_topics_host(self.h, _ptr(tb), _ptr(to), n, _ptr(out)), None, "route_topics_host")
+        return out[:n]
+
+    def release(self):
+        if self.h:
+            lib().emqx_gm_route_release(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+def prefix_plan(fb: np.ndarray, fo: np.ndarray, n_shards: int) -> Tuple[np.ndarray, "Route"]:
+    """Prefix sharding (emqx_gm_prefix_plan): each filter's shard (ALL_SHARDS:
+    every shard) and the topic route."""
+    n = len(fo) - 1
+    out = np.zeros(max(n, 1), np.uint32)
+    h = C.c_void_p()
+    check(lib().emqx_gm_prefix_plan(_ptr(fb), _ptr(fo), n, n_shards, _ptr(out), C.byref(h)), None, "prefix_plan")
+    return out[:n], Route(h, n_shards)
 
 
 # ---------------------------------------------------------------------- workload

@@ -134,3 +134,162 @@ class ShardedMatcher:
                 ctx.dev_free(d_l)
                 ctx.dev_free(d_i)
         return out, b[r], b[r + 1] - b[r]
+
+
+# ---------------------------------------------------------------------------
+# Prefix sharding (gm_route.hip): every topic needs exactly one shard
+# ---------------------------------------------------------------------------
+def plan_prefix_shard(fb: np.ndarray, fo: np.ndarray, world: int, rank: int):
+    """This rank's filters under prefix sharding (its first-word partitions plus
+    the filters every shard holds), their global ids, the global filter count
+    and the route (emqx_gm_prefix_plan)."""
+    from .engine import ALL_SHARDS, prefix_plan
+    gids, n_unique = filter_ranks(fb, fo)
+    sh, route = prefix_plan(fb, fo, world)
+    mine = (sh == rank) | (sh == ALL_SHARDS)
+    sfb, sfo = select_filters(fb, fo, np.where(mine, 0, 1).astype(np.uint32), 0)
+    return sfb, sfo, gids[mine], n_unique, route
+
+
+class PrefixShardedMatcher:
+    """match_routes over a prefix-sharded filter set (one process per GPU).
+
+    Each rank holds its own publish batch.  A step routes every topic to the
+    one shard holding all the filters it can match (emqx_gm_route_topics),
+    sends the topics there (all-to-all-v of the topic bytes and lengths; RCCL
+    over xGMI on the device path), each rank walks only the topics it received
+    -- ~1/N of the job, against its shard -- and the rows go back to the
+    topics' ranks (all-to-all-v of row lengths and ids), where
+    emqx_gm_unpermute_rows puts them in batch order.  Per rank and step the
+    exchange moves the batch's topic bytes + 4 B per topic out, and 4 B per
+    topic + 4 B per match back; nothing is merged (each row comes from one
+    shard whole).
+
+    ``device_tensors`` False runs the same exchange on host tensors (gloo),
+    with ``match_fn(tb, to) -> (row_off, ids)`` standing in for the device
+    match (tests: the oracle over the rank's shard)."""
+
+    def __init__(self, ctx: Optional[Context], index: Optional[Index], route, world: int, rank: int, dist=None,
+                 group=None, device_tensors: bool = True, match_fn=None):
+        self.ctx, self.index, self.route, self.world, self.rank = ctx, index, route, world, rank
+        self.dist, self.group, self.device_tensors, self.match_fn = dist, group, device_tensors, match_fn
+        self.last_exchange_bytes = 0
+        self.last_topics_walked = 0
+        if device_tensors and ctx is not None and world > 1:
+            import torch
+            ctx.set_stream(torch.cuda.current_stream(torch.device("cuda", ctx.device)).cuda_stream)
+
+    def _a2a(self, out, inp, out_splits=None, in_splits=None):
+        if self.world == 1:
+            out.copy_(inp)
+            return
+        self.dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits,
+                                    group=self.group)
+
+    def match_host(self, tb: np.ndarray, to: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """The exchange on host tensors (gloo): rows of this rank's batch, in order."""
+        import torch
+        W = self.world
+        n = len(to) - 1
+        dest = self.route.route_host(tb, to).astype(np.int64)
+        perm = np.argsort(dest, kind="stable")
+        counts = np.bincount(dest, minlength=W).astype(np.int64)
+        lens = np.diff(to.astype(np.int64))[perm]
+        pb = np.concatenate([tb[int(to[i]):int(to[i + 1])] for i in perm]) if n else np.zeros(0, np.uint8)
+        cum = np.r_[0, np.cumsum(lens)]
+        bnd = np.r_[0, np.cumsum(counts)]
+        bsplit = [int(x) for x in cum[bnd[1:]] - cum[bnd[:-1]]]
+        sizes = torch.tensor(np.stack([counts, np.array(bsplit, np.int64)], 1).reshape(-1))
+        rsizes = torch.empty_like(sizes)
+        self._a2a(rsizes, sizes)
+        rc = rsizes.view(W, 2)[:, 0].tolist()
+        rb = rsizes.view(W, 2)[:, 1].tolist()
+        rbytes = torch.empty(sum(rb), dtype=torch.uint8)
+        self._a2a(rbytes, torch.from_numpy(pb.copy()), rb, bsplit)
+        rlens = torch.empty(sum(rc), dtype=torch.int64)
+        self._a2a(rlens, torch.from_numpy(lens.copy()), rc, [int(c) for c in counts])
+        roff = np.zeros(sum(rc) + 1, np.uint64)
+        roff[1:] = np.cumsum(rlens.numpy())
+        rtb = np.concatenate([rbytes.numpy(), np.zeros(64, np.uint8)])
+        ro, ids = self.match_fn(rtb, roff)
+        self.last_topics_walked = sum(rc)
+        rowlen = np.diff(ro.astype(np.int64))
+        # back to the topics' ranks: lengths (per source: the topics it sent) and ids
+        rbnd = np.r_[0, np.cumsum(rc)].astype(np.int64)
+        idsplit = [int(rowlen[a:b].sum()) for a, b in zip(rbnd[:-1], rbnd[1:])]
+        bsz = torch.tensor(idsplit, dtype=torch.int64)
+        rbsz = torch.empty_like(bsz)
+        self._a2a(rbsz, bsz)
+        back_lens = torch.empty(n, dtype=torch.int64)
+        self._a2a(back_lens, torch.from_numpy(rowlen), [int(c) for c in counts], rc)
+        back_ids = torch.empty(int(rbsz.sum()), dtype=torch.int32)
+        self._a2a(back_ids, torch.from_numpy(ids.astype(np.int32)), rbsz.tolist(), idsplit)
+        self.last_exchange_bytes = int(len(pb) + 8 * n + 8 * sum(rc) + 4 * int(ro[-1]))
+        # unpermute: row perm[k] <- received row k
+        bl = back_lens.numpy()
+        out_len = np.zeros(n, np.int64)
+        out_len[perm] = bl
+        out_off = np.zeros(n + 1, np.uint64)
+        out_off[1:] = np.cumsum(out_len)
+        in_off = np.r_[0, np.cumsum(bl)]
+        out_ids = np.zeros(int(out_off[-1]), np.uint32)
+        bi = back_ids.numpy().view(np.uint32)
+        for k in range(n):
+            o = int(out_off[perm[k]])
+            out_ids[o:o + int(bl[k])] = bi[in_off[k]:in_off[k + 1]]
+        return out_off, out_ids
+
+    def match_device(self, d_tb: int, d_to: int, n: int, exact: bool = True) -> DeviceCsr:
+        """The exchange on device tensors: rows of this rank's batch (device
+        topics d_tb / d_to, n of them), in batch order, as a DeviceCsr."""
+        import torch
+        ctx, W = self.ctx, self.world
+        dev = torch.device("cuda", ctx.device)
+        dest = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+        ctx.route_topics(self.route, d_tb, d_to, n, dest.data_ptr())
+        perm64 = torch.sort(dest, stable=True).indices
+        perm = perm64.to(torch.int32)
+        counts = torch.bincount(dest, minlength=W).to(torch.int64)
+        tot = np.zeros(1, np.uint64)
+        ctx.memcpy_d2h(tot, d_to + 8 * n, 8)
+        pbytes = torch.empty(int(tot[0]) + 64, dtype=torch.uint8, device=dev)
+        poff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        ctx.permute_topics(d_tb, d_to, n, perm.data_ptr(), pbytes.data_ptr(), poff.data_ptr())
+        bounds = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), counts.cumsum(0)])
+        bsplit_t = poff[bounds[1:]] - poff[bounds[:-1]]
+        sizes = torch.stack([counts, bsplit_t], 1).reshape(-1)
+        rsizes = torch.empty_like(sizes)
+        self._a2a(rsizes, sizes)
+        both = torch.cat([sizes, rsizes]).cpu().tolist()  # one D2H for the split sizes of the step
+        cs, bs = both[0:2 * W:2], both[1:2 * W:2]
+        rc, rb = both[2 * W::2], both[2 * W + 1::2]
+        rbytes = torch.empty(sum(rb) + 64, dtype=torch.uint8, device=dev)
+        self._a2a(rbytes[:sum(rb)], pbytes[:int(tot[0])], rb, bs)
+        rbytes[sum(rb):].zero_()
+        plens = (poff[1:] - poff[:-1]).to(torch.int32)
+        rlens = torch.empty(sum(rc), dtype=torch.int32, device=dev)
+        self._a2a(rlens, plens, rc, cs)
+        m = sum(rc)
+        roff = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+        roff[1:] = rlens.to(torch.int64).cumsum(0)
+        res = ctx.match_device(self.index, rbytes.data_ptr(), roff.data_ptr(), m, exact)
+        self.last_topics_walked = m
+        rowlen = torch.empty(max(m, 1), dtype=torch.int32, device=dev)[:m]
+        ctx.csr_row_lengths(res, rowlen.data_ptr())
+        nnz = res.nnz
+        ids = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
+        ctx.memcpy_d2d(ids.data_ptr(), _ptr(res.csr.ids), nnz * 4)
+        res.free()
+        rcb = torch.tensor([0] + rc, device=dev).cumsum(0)
+        csum = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), rowlen.to(torch.int64).cumsum(0)])
+        idsplit_t = csum[rcb[1:]] - csum[rcb[:-1]]
+        rbsz = torch.empty_like(idsplit_t)
+        self._a2a(rbsz, idsplit_t)
+        both = torch.cat([idsplit_t, rbsz]).cpu().tolist()
+        idsplit, backsplit = both[:W], both[W:]
+        back_lens = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+        self._a2a(back_lens, rowlen, cs, rc)
+        back_ids = torch.empty(max(sum(backsplit), 1), dtype=torch.int32, device=dev)
+        self._a2a(back_ids[:sum(backsplit)], ids, backsplit, idsplit)
+        self.last_exchange_bytes = int(tot[0]) + 4 * n + 4 * m + 4 * nnz
+        return ctx.unpermute_rows(n, perm.data_ptr(), back_lens.data_ptr(), back_ids.untyped_storage().data_ptr())

@@ -245,6 +245,35 @@ int emqx_gm_csr_row_lengths(emqx_gm_ctx *ctx, const emqx_gm_csr *csr, uint32_t *
 int emqx_gm_merge_rows(emqx_gm_ctx *ctx, uint64_t n_rows, uint64_t stride, uint32_t n_pieces,
                        const uint32_t *d_lens, const uint32_t *d_ids, uint32_t flags, emqx_gm_csr *out);
 
+/* ---- prefix sharding (gm_route.hip): each topic needs ONE shard ----
+ * A topic can only match filters whose first word is its own first word, '+'
+ * or '#' (emqx_topic:match/2, emqx_topic.erl:65-87).  emqx_gm_prefix_plan
+ * partitions filters by first word (a hot first word -- over 1/(2N) of the
+ * filters -- by its first two words) over n_shards, greedily by size; filters
+ * whose first word is '+' / '#' (and a hot word's 'w', 'w/#', 'w/+/...') go to
+ * every shard (shard_out = EMQX_GM_ALL_SHARDS).  The returned route maps each
+ * topic to the one shard that holds every filter it can match, so a batch is
+ * routed (all-to-all of topic bytes), each rank walks only its share, and the
+ * rows go back to the topics' ranks (emqx_gm_unpermute_rows) -- no merge. */
+#define EMQX_GM_ALL_SHARDS 0xFFFFFFFFu
+typedef struct emqx_gm_route emqx_gm_route;
+int emqx_gm_prefix_plan(const uint8_t *filter_bytes, const uint64_t *filter_off, uint64_t n_filters,
+                        uint32_t n_shards, uint32_t *shard_out, emqx_gm_route **route);
+/* dest[i] = the shard of topic i (host buffers / device buffers, n_topics entries) */
+int emqx_gm_route_topics_host(const emqx_gm_route *route, const uint8_t *topic_bytes, const uint64_t *topic_off,
+                              uint64_t n_topics, uint32_t *dest);
+int emqx_gm_route_topics(emqx_gm_ctx *ctx, emqx_gm_route *route, const uint8_t *d_topic_bytes,
+                         const uint64_t *d_topic_off, uint64_t n_topics, uint32_t *d_dest);
+int emqx_gm_route_release(emqx_gm_route *route);
+/* The exchange's device steps.  permute: out topic i = topic perm[i] (d_out
+ * holds as many bytes as the input, d_out_off n+1 entries).  unpermute: row
+ * perm[i] of the result = input row i, the input rows packed with u32 lengths
+ * d_lens[i] (flags: EMQX_GM_DEVICE_IO keeps the CSR on the device). */
+int emqx_gm_permute_topics(emqx_gm_ctx *ctx, const uint8_t *d_topic_bytes, const uint64_t *d_topic_off,
+                           uint64_t n_topics, const uint32_t *d_perm, uint8_t *d_out, uint64_t *d_out_off);
+int emqx_gm_unpermute_rows(emqx_gm_ctx *ctx, uint64_t n_rows, const uint32_t *d_perm, const uint32_t *d_lens,
+                           const uint32_t *d_ids, uint32_t flags, emqx_gm_csr *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,17 @@ def test_bench_two_ranks_c5_replicated():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(400)
+def test_bench_two_ranks_c5_prefix():
+    """C5 prefix-sharded: each rank walks about half of the two ranks' topics."""
+    out = _run_ranks(["--config", "c5", "--plan", "prefix", "--filters", "200000", "--topics", "200000"], world=2)
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
+    walked = out["detail"]["topics_walked_per_rank"]
+    assert sum(walked) == 400_000 and min(walked) > 0.35 * 400_000
+    assert out["detail"]["exchange_bytes_per_step_rank0"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
 def test_bench_two_ranks_c4():
     out = _run_ranks(["--config", "c4"], world=2)
     assert out["n_gpus"] == 2 and out["config"]["pairs"] == 10**9

@@ -181,3 +181,91 @@ def test_device_tensor_path_with_replayed_exchange():
                        capture_output=True, text=True, timeout=280)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     assert "SHARDED_DEVICE_PATH_OK" in p.stdout
+
+
+# ---------------------------------------------------------------------------
+# prefix sharding (gm_route.hip)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("kind", ["random", "c1"])
+def test_device_route_equals_host_route(ctx, kind):
+    """emqx_gm_route_topics (one thread per topic) == emqx_gm_route_topics_host."""
+    from emqx_amd.engine import pack, prefix_plan
+    fs, ts = _sets(kind)
+    fb, fo = pack(fs)
+    tb, to = pack(ts)
+    for world in (2, 3, 8):
+        _, route = prefix_plan(fb, fo, world)
+        d_tb, d_to = _to_device(ctx, tb, to)
+        n = len(to) - 1
+        d_dest = ctx.dev_alloc(max(n, 1) * 4)
+        ctx.route_topics(route, d_tb, d_to, n, d_dest)
+        got = np.zeros(max(n, 1), np.uint32)
+        ctx.memcpy_d2h(got, d_dest, n * 4)
+        assert np.array_equal(got[:n], route.route_host(tb, to))
+        for p in (d_tb, d_to, d_dest):
+            ctx.dev_free(p)
+        route.release()
+
+
+@pytest.mark.timeout(600)
+def test_prefix_shards_each_walk_their_routed_topics(ctx, orc):
+    """C5-shaped set (4M mixed filters) in 8 prefix shards built one after
+    another on one device: the batch is routed on the device, permuted so each
+    shard's topics are one range (emqx_gm_permute_topics), each shard walks
+    ONLY its range, and the rows put back in batch order
+    (emqx_gm_unpermute_rows) equal the unsharded index's rows, row for row;
+    a window is checked against the oracle."""
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    from emqx_amd.sharded import plan_prefix_shard
+    n_f, n, W = 4_000_000, 1_000_000, 8
+    codes = gen_filter_codes(1, n_f)
+    fb, fo = render_codes(codes)
+    db, do, tot = ctx.gen_topics_device(codes, 1, 0, n)
+    _, _, _, _, route = plan_prefix_shard(fb, fo, W, 0)
+    d_dest = ctx.dev_alloc(n * 4)
+    ctx.route_topics(route, db, do, n, d_dest)
+    dest = np.zeros(n, np.uint32)
+    ctx.memcpy_d2h(dest, d_dest, n * 4)
+    perm = np.argsort(dest, kind="stable").astype(np.uint32)
+    bnd = np.r_[0, np.cumsum(np.bincount(dest, minlength=W))].astype(np.int64)
+    d_perm = ctx.dev_alloc(n * 4)
+    ctx.memcpy_h2d(d_perm, perm, n * 4)
+    d_pb, d_po = ctx.dev_alloc(tot + 64), ctx.dev_alloc((n + 1) * 8)
+    ctx.permute_topics(db, do, n, d_perm, d_pb, d_po)
+    lens, ids = [], []
+    for q in range(W):
+        sfb, sfo, gids, _, r_q = plan_prefix_shard(fb, fo, W, q)
+        r_q.release()
+        sidx = ctx.build_index_shard((sfb, sfo), gids)
+        m = int(bnd[q + 1] - bnd[q])
+        res = ctx.match_device(sidx, d_pb, d_po + 8 * int(bnd[q]), m, exact=True)  # only its own range
+        ro, rid = res.rows(0, m)
+        lens.append(np.diff(ro.astype(np.int64)).astype(np.uint32))
+        ids.append(rid)
+        res.free()
+        sidx.release()
+    lens, ids = np.concatenate(lens), np.concatenate(ids).astype(np.uint32)
+    d_l, d_i = ctx.dev_alloc(n * 4), ctx.dev_alloc(max(len(ids), 1) * 4)
+    ctx.memcpy_h2d(d_l, lens, n * 4)
+    if len(ids):
+        ctx.memcpy_h2d(d_i, ids, len(ids) * 4)
+    back = ctx.unpermute_rows(n, d_perm, d_l, d_i)
+    bro, bids = back.to_host()
+    back.free()
+    idx = ctx.build_index((fb, fo))
+    full = ctx.match_device(idx, db, do, n, exact=True)
+    fro, fids = full.to_host()
+    full.free()
+    assert np.array_equal(bro, fro) and np.array_equal(bids, fids)
+    # each shard walked only its share: no shard more than twice its fair share
+    assert int(np.diff(bnd).max()) < 2 * n // W
+    tb, to = orc.render_codes(orc.gen_topic_codes(1, 0, 20_000, codes))
+    r = orc.Router(True)
+    r.add_routes((fb, fo))
+    import bench
+    oro, oids, _ = r.match_batch((tb, to), orc.Ranker(bench.sorted_unique(fb, fo)), mode=1, nthreads=8)
+    assert np.array_equal(bro[:20_001], oro) and np.array_equal(bids[:int(oro[-1])], oids)
+    for p in (db, do, d_dest, d_perm, d_pb, d_po, d_l, d_i):
+        ctx.dev_free(p)
+    idx.release()
+    route.release()

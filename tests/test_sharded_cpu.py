@@ -112,3 +112,102 @@ def test_exchange_rows_gloo(world, tmp_path, orc):
     import torch.multiprocessing as mp
     mp.spawn(_worker, args=(world, _free_port(), 7 + world, str(tmp_path)), nprocs=world, join=True)
     assert sorted(os.listdir(tmp_path)) == [f"ok{r}" for r in range(world)]
+
+
+# ---------------------------------------------------------------------------
+# prefix sharding (gm_route.hip): every filter a topic can match is on the
+# topic's one shard; the topic-routing exchange over gloo
+# ---------------------------------------------------------------------------
+def _skewed_set(seed, n_f=400, n_t=500):
+    """Mixed filters with one HOT first word (about half the set), so the plan
+    splits it by its second word; plus its 'w', 'w/#', 'w/+/..' filters, root
+    wildcards and $SYS."""
+    from tests.test_gpu_parity import _rand_filter, _rand_topic
+    rng = random.Random(seed)
+    filters = [_rand_filter(rng).encode() for _ in range(n_f // 2)]
+    hot = [b"hot/" + _rand_filter(rng).encode() for _ in range(n_f // 2)]
+    filters += hot + [b"hot", b"hot/#", b"hot/+", b"hot/+/x", b"#", b"+/+", b"+", b"$SYS/#", b"", b"/"]
+    topics = [_rand_topic(rng).encode() for _ in range(n_t // 2)]
+    topics += [b"hot/" + _rand_topic(rng).encode() for _ in range(n_t // 2)]
+    topics += [b"hot", b"hot/", b"hot/x", b"/", b"", b"$SYS/a", b"+/x", b"hot/+"]
+    return filters, topics
+
+
+@pytest.mark.parametrize("skew", [False, True], ids=["uniform", "hot_word_split"])
+def test_prefix_plan_every_match_on_the_topics_shard(skew, orc):
+    """For every topic and every filter emqx_topic:match/2 pairs it with
+    (oracle brute force, match_routes semantics: the literal route too), the
+    filter is on the topic's routed shard or on every shard."""
+    from emqx_amd.engine import ALL_SHARDS, pack, prefix_plan
+    filters, topics = _skewed_set(5) if skew else _rand_set(5)
+    fb, fo = pack(filters)
+    uniq = sorted(set(filters))
+    fro, fids = orc.bruteforce(topics, uniq, mode=1)
+    tb, to = pack(topics)
+    for world in (1, 2, 3, 8):
+        sh, route = prefix_plan(fb, fo, world)
+        shard_of_f = {}
+        for f, s in zip(filters, sh):
+            assert shard_of_f.setdefault(f, int(s)) == int(s)  # equal filters, one shard
+            assert s == ALL_SHARDS or s < world
+        dest = route.route_host(tb, to)
+        assert (dest < world).all()
+        for t in range(len(topics)):
+            for i in fids[fro[t]:fro[t + 1]]:
+                s = shard_of_f[uniq[i]]
+                assert s == ALL_SHARDS or s == dest[t], (world, topics[t], uniq[i], s, int(dest[t]))
+        if skew and world > 1:  # the hot word is split: its filters spread over shards
+            hot_sh = {shard_of_f[f] for f in filters if f.startswith(b"hot/") and f not in
+                      (b"hot/#", b"hot/+", b"hot/+/x")}
+            assert len(hot_sh) > 1
+            assert shard_of_f[b"hot/#"] == shard_of_f[b"hot"] == shard_of_f[b"hot/+/x"] == ALL_SHARDS
+        route.release()
+
+
+def _prefix_worker(rank, world, port, seed, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from emqx_amd.engine import pack
+    from emqx_amd.sharded import PrefixShardedMatcher, plan_prefix_shard
+    from oracle import oracle as orc
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        filters, topics = _skewed_set(seed)
+        fb, fo = pack(filters)
+        sfb, sfo, gids, _, route = plan_prefix_shard(fb, fo, world, rank)
+        part = [bytes(sfb[int(sfo[i]):int(sfo[i + 1])]) for i in range(len(sfo) - 1)]
+        local = sorted(set(part))
+        gid_of = {f: int(g) for f, g in zip(part, gids)}
+
+        def match_fn(rtb, roff):  # this rank's shard, global ids (the device match in production)
+            mine = orc.unpack(rtb, roff)
+            if not local:
+                return np.zeros(len(mine) + 1, np.uint64), np.zeros(0, np.uint32)
+            ro, ids = orc.bruteforce(mine, local, mode=1)
+            return ro, np.array([gid_of[local[i]] for i in ids], np.uint32)
+
+        # each rank publishes its own batch: a different slice of the topics
+        mine = topics[rank::world]
+        m = PrefixShardedMatcher(None, None, route, world, rank, dist=dist, device_tensors=False, match_fn=match_fn)
+        tb, to = pack(mine)
+        ro, ids = m.match_host(tb, to)
+        uniq = sorted(set(filters))
+        fro, fids = orc.bruteforce(mine, uniq, mode=1)
+        assert np.array_equal(ro, fro) and np.array_equal(ids, fids)
+        open(os.path.join(out_dir, f"ok{rank}"), "w").write(f"{len(mine)} {m.last_topics_walked}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world", [2, 3])
+def test_prefix_exchange_gloo(world, tmp_path, orc):
+    """The topic-routing exchange of PrefixShardedMatcher over gloo, world 2
+    and 3: every rank's rows (its own batch, in order) equal the unsharded
+    oracle's; each rank walked only the topics routed to it."""
+    import torch.multiprocessing as mp
+    mp.spawn(_prefix_worker, args=(world, _free_port(), 11 + world, str(tmp_path)), nprocs=world, join=True)
+    assert sorted(os.listdir(tmp_path)) == [f"ok{r}" for r in range(world)]
+    walked = [int(open(os.path.join(tmp_path, f"ok{r}")).read().split()[1]) for r in range(world)]
+    sent = [int(open(os.path.join(tmp_path, f"ok{r}")).read().split()[0]) for r in range(world)]
+    assert sum(walked) == sum(sent)  # every topic walked exactly once, on one rank
