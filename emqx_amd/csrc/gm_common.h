@@ -78,7 +78,9 @@ constexpr uint32_t HOT_INLINE = 0x40000000u;  // in a hot id: the '+' child held
 constexpr uint32_t SLOT_MASK = 0x3FFFFFFFu;
 constexpr uint32_t END_WILD = 0x80000000u;  // in end_filter: the filter is a wildcard one
 constexpr uint32_t HOT_PLUS = 0x80000000u;  // in HotSlot::hf: the node has a '+' child
-constexpr uint32_t HF_NONE = 0x7FFFFFFFu;   // HotSlot::hf without a '#' filter
+constexpr uint32_t HOT_CHAIN = 0x40000000u; // in HotSlot::hf: a chain node (below)
+constexpr uint32_t HF_MASK = 0x3FFFFFFFu;   // the filter id in HotSlot::hf
+constexpr uint32_t HF_NONE = 0x3FFFFFFFu;   // HotSlot::hf without a '#' filter (filter ids stay below it)
 constexpr uint32_t FR_PLUS = 0x80000000u;   // in a frontier entry: the node has a '+' child
 constexpr uint64_t HOT_KEY_MARK = 1ull << 63;  // parent lives in table HOT_TABLES-2, child in the shared last
 
@@ -95,6 +97,20 @@ struct alignas(32) HotSlot {
 // last level (one dwordx4); end_filter is read on the last level, and the
 // second 16 bytes {end_filter, p_sig, p_hf, p_end} (one dwordx4) are the
 // inline '+' child's record.
+//
+// Chain nodes (path compression of single-filter tails; HOT_CHAIN in hf): a
+// slot-owning node N with no '+' child whose only child c1 is an exact edge
+// that ends a chain of Lc = 1 or 2 exact words with no other branch -- c1 (and
+// c2) with no '+' or '#' child, only the last one holding a filter F and no
+// children at all.  Its slot then holds sig = s1 (c1's word id, not a
+// signature: hot_sig() gives the signature back), p_sig = s2 (c2's word id, or
+// NONE when Lc = 1), p_hf = HF_NONE and p_end = F | END_WILD flag.  The walk
+// of k_match_fused checks the topic's next one or two words against s1/s2 at
+// N's visit and emits F there, so c1 and c2 (still in the tables, for the
+// listed pass and the in-place update) are never probed by the main pass.
+// An in-place update clears HOT_CHAIN on every chain node of a path it writes
+// (Patcher::unchain), so chains only need to be right at build time.
+GM_HD uint32_t hot_sig(uint32_t hf, uint32_t sig);
 // Read-only view of one index resident in HBM (passed by value to kernels).
 constexpr uint32_t IX_HOT_FLAT = 1u;  // a hot table reaches 2 GiB: flat loads instead of buffer loads
 struct IndexView {
@@ -136,6 +152,7 @@ struct IndexView {
   uint32_t mph_nb[HOT_TABLES];       // buckets of each MPH table
   uint32_t mph_cap[HOT_TABLES];      // perfect-hash slots of each table; 0 = not an MPH table
   uint32_t mph_ovf;                  // bit t: table t's overflow region holds keys
+  uint32_t l1_bypass;                // bit t: table t's probes skip the CU's L1 (sc1 loads; GM_L1_BYPASS A/B knob)
 };
 
 GM_HD uint64_t fmix64(uint64_t k) {
@@ -220,6 +237,9 @@ GM_HD uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
+GM_HD uint32_t sig_bit(uint32_t word_id);
+// a slot's exact-child signature (a chain node holds its one child's word id)
+GM_HD uint32_t hot_sig(uint32_t hf, uint32_t sig) { return (hf & HOT_CHAIN) ? sig_bit(sig) : sig; }
 GM_HD uint32_t dict_hash_final(uint32_t h, uint32_t len) {
   h ^= len;
   h ^= h >> 16;
@@ -335,8 +355,9 @@ GM_HD uint32_t edge_filter_word(uint32_t h, uint32_t mask) { return (h >> 10) & 
 
 // In-place update (gm_overlay.cpp, patch_update): a filter-id field under the
 // renumbering rmap[old id] -> new id (NONE: deleted).  `none` is the field's
-// empty value (NONE or HF_NONE) and `flag` the flag bit it carries (END_WILD,
-// HOT_PLUS, or 0 for the level-trie fields).
+// empty value (NONE or HF_NONE) and `flag` the flag bits it carries (END_WILD,
+// HF_FLAGS, or 0 for the level-trie fields).
+constexpr uint32_t HF_FLAGS = HOT_PLUS | HOT_CHAIN;
 GM_HD uint32_t renum_field(uint32_t f, uint32_t none, uint32_t flag, const uint32_t* rmap) {
   if (f == none) return f;
   const uint32_t fl = f & flag, id = f & ~flag;

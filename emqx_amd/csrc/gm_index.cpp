@@ -214,6 +214,10 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       }
   }
 
+  if (nf >= HF_NONE) {  // filter ids share HotSlot::hf with two flag bits
+    delete idx;
+    return set_err(ctx, EMQX_GM_EINVAL, "index_build: more than 2^30 - 2 distinct filters");
+  }
   phase("sort+ids");
   // ---- 2. intern words, build the level trie
   std::unordered_map<std::string_view, uint32_t, ViewHash> wid;  // word -> arena offset
@@ -452,7 +456,9 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     return h.end_filter | ((h.flags & NF_END_WILD) ? END_WILD : 0u);
   };
   auto hf_of = [&](const HNode& h) -> uint32_t {
-    return (h.hash_child == NONE ? HF_NONE : nodes[h.hash_child].end_filter) | (h.plus_child != NONE ? HOT_PLUS : 0u);
+    // (a '#' node holding no filter -- "a/#/b" without "a/#" -- is no 'match_#')
+    const uint32_t hf = h.hash_child == NONE ? NONE : nodes[h.hash_child].end_filter;
+    return (hf == NONE ? HF_NONE : hf) | (h.plus_child != NONE ? HOT_PLUS : 0u);
   };
   // Tables of one depth (t < HOT_TABLES-1) are Robin Hood ordered: a key is
   // placed so that no key between its home slot and its slot is closer to its
@@ -602,7 +608,51 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
         }
   }
 
+  // ---- 3b'. chain nodes (gm_common.h): path compression of single-filter
+  // tails.  tcl[i] = the length of the chain that starts at exact node i (1: i
+  // is a leaf holding a filter; 2: i holds nothing but one exact child that is
+  // such a leaf), 0 if none.  A parent is created before its children, so one
+  // pass in reverse index order sees every child first.
+  // A chain trades one L2-hit read of the chain node's second half for the
+  // probes of c1 and c2; those are Infinity-Cache hits while the hot tables fit
+  // it (256 MiB), and there the trade does not pay (C2, 240 MB of tables: +0.9 %
+  // kernel time; C3, 2.4 GB: -3 %, profiles/r03_ab/chain_ab.txt).  So chains are
+  // built for larger tables only; GM_CHAIN=0/1 forces (A/B knob).
+  uint64_t n_chain = 0;
+  bool chains = hot_total * sizeof(HotSlot) > (256ull << 20);
+  if (const char* e = getenv("GM_CHAIN")) chains = atoi(e) != 0;
+  if (getenv("GM_NO_CHAIN")) chains = false;
+  if (chains) {
+    std::vector<uint32_t> nex(NN, 0), exch(NN, NONE);
+    for (uint64_t i = 1; i < NN; ++i)
+      if (nodes[i].kind == 0) {
+        nex[nodes[i].parent]++;
+        exch[nodes[i].parent] = uint32_t(i);
+      }
+    std::vector<uint8_t> tcl(NN, 0);
+    for (uint64_t i = NN; i-- > 1;) {
+      const HNode& h = nodes[i];
+      if (h.kind != 0 || h.plus_child != NONE || h.hash_child != NONE) continue;
+      if (nex[i] == 0) tcl[i] = h.end_filter != NONE ? 1 : 0;
+      else if (nex[i] == 1 && h.end_filter == NONE && tcl[exch[i]] == 1) tcl[i] = 2;
+    }
+    for (uint64_t i = 1; i < NN; ++i) {
+      const HNode& h = nodes[i];
+      if (h.kind == 2 || h.plus_child != NONE || nex[i] != 1 || hid[i] == NONE || (hid[i] & HOT_INLINE)) continue;
+      const uint32_t c1 = exch[i];
+      if (!tcl[c1]) continue;
+      HotSlot& o = hot[hot_off[hot_table(h.depth)] + hid[i]];
+      const HNode& leaf = tcl[c1] == 1 ? nodes[c1] : nodes[exch[c1]];
+      o.sig = nodes[c1].word;
+      o.hf |= HOT_CHAIN;
+      o.p_sig = tcl[c1] == 1 ? NONE : nodes[exch[c1]].word;
+      o.p_hf = HF_NONE;
+      o.p_end = end_of(leaf);
+      ++n_chain;
+    }
+  }
   if (getenv("GM_INDEX_STATS")) {  // diagnostics: the hot tables' sizes (stderr)
+    fprintf(stderr, "[gm_index] chain nodes %llu\n", (unsigned long long)n_chain);
     uint64_t inl_n = 0;
     for (uint64_t i = 1; i < NN; ++i) inl_n += inl[i];
     fprintf(stderr, "[gm_index] nodes %llu, inline '+' nodes %llu\n", (unsigned long long)NN,
@@ -821,6 +871,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.efilt = reinterpret_cast<const uint32_t*>(B + o_efilt);
   v.mph_word = reinterpret_cast<const uint64_t*>(B + o_mph);
   v.mph_ovf = mph_ovf;
+  v.l1_bypass = 0;
+  if (const char* e = getenv("GM_L1_BYPASS")) v.l1_bypass = uint32_t(strtoul(e, nullptr, 0));
   for (int t = 0; t < HOT_TABLES; ++t) {
     v.mph_off[t] = mph_off[t];
     v.mph_nb[t] = mph_nb[t];

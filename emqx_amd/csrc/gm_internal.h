@@ -298,9 +298,13 @@ int rebuild_subs_device(emqx_gm_ctx* ctx, const emqx_gm_index* prev, emqx_gm_ind
                         const std::vector<uint32_t>& aff_buf);
 int overlay_filter(const emqx_gm_index* idx, uint32_t id, const uint8_t** bytes, uint64_t* len);
 void free_overlay(emqx_gm_index* idx);
+// An op of Patcher::orops whose offset carries PATCH_AND clears its bits
+// instead of setting them (an op never sets a bit another op clears, so the
+// device applies them in any order).
+constexpr uint64_t PATCH_AND = 1ull << 63;
 // gm_match.hip: the device side of an in-place update (patch_update): dst =
 // src (bytes), then the host-patched byte ranges (offset, length) of `host`
-// written over it, the OR ops (offset of a word, bits) applied, then every
+// written over it, the OR / AND ops (offset of a word, bits) applied, then every
 // filter-id field of the hot slots and of nodes [0, n_nodes) renumbered by
 // the shift (its table built on the device)
 int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t bytes,

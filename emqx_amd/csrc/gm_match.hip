@@ -218,11 +218,13 @@ struct HotRec {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t hot_rsrc(const HotSlot* tab) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<HotSlot*>(tab), (short)0, 0x7FFFFFFF, 0x00020000);
 }
-__device__ __forceinline__ HotRec hot_load(const HotSlot* tab, uint32_t s, bool with_end, bool flat) {
+__device__ __forceinline__ HotRec hot_load(const HotSlot* tab, uint32_t s, bool with_end, bool flat, bool nol1 = false) {
   HotRec r;
   if (!flat) {
     const __amdgpu_buffer_rsrc_t rs = hot_rsrc(tab);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, s * 32u, 0, 0);
+    // nol1 (wave-uniform): an sc1 load, served by L2 without filling the L1
+    const auto v = nol1 ? __builtin_amdgcn_raw_buffer_load_b128(rs, s * 32u, 0, 16)
+                        : __builtin_amdgcn_raw_buffer_load_b128(rs, s * 32u, 0, 0);
     r.a = make_uint4(v[0], v[1], v[2], v[3]);
     r.ef = with_end ? __builtin_amdgcn_raw_buffer_load_b32(rs, s * 32u + 16u, 0, 0) : NONE;
   } else {
@@ -306,13 +308,13 @@ __device__ __forceinline__ uint32_t hot_resolve_x(const IndexView& ix, int ht, c
 // the next frontier (GM_PUSH is defined per kernel).
 #define GM_VISIT(hs, r)                                                                 \
   do {                                                                                  \
-    if (((r).a.w & ID_MASK) != HF_NONE) GM_EMIT((r).a.w & ID_MASK);                     \
+    if (((r).a.w & HF_MASK) != HF_NONE) GM_EMIT((r).a.w & HF_MASK);                     \
     if (last) {                                                                         \
       if ((r).ef != NONE && (EXACT || ((r).ef & END_WILD) || (dollar && level == 0)))   \
         GM_EMIT((r).ef & ID_MASK);                                                      \
       ++nfinal;                                                                         \
     } else {                                                                            \
-      GM_PUSH((hs) | ((r).a.w & FR_PLUS), (r).a.z);                                     \
+      GM_PUSH((hs) | ((r).a.w & FR_PLUS), hot_sig((r).a.w, (r).a.z));                   \
     }                                                                                   \
   } while (0)
 
@@ -355,6 +357,15 @@ __device__ __forceinline__ HotRec plus_inline_load(const HotSlot* ptab, uint32_t
   r.a = make_uint4(0u, 0u, q.y, q.z);
   r.ef = q.w;
   return r;
+}
+// The second 16 bytes of slot s: {end_filter, p_sig, p_hf, p_end} (a chain
+// node's tail: {end_filter, s2, HF_NONE, F}).
+__device__ __forceinline__ uint4 hot_tail_load(const HotSlot* tab, uint32_t s, bool flat) {
+  if (!flat) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(hot_rsrc(tab), s * 32u + 16u, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  return *reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(tab + s) + 4);
 }
 // Whether the '+' child of frontier entry `id` (a node at depth lvl) is inline.
 __device__ __forceinline__ bool plus_is_inline(uint32_t lvl, uint32_t id) { return plus_inline(lvl, !(id & HOT_INLINE)); }
@@ -1057,6 +1068,42 @@ constexpr uint32_t CMP_SHIFT = 22, CMP_RANK = 28;
 // '+' children taken inline.  Printed by run_match after each call.
 __device__ unsigned long long g_pstats[8][8];
 #endif
+#ifdef GM_PHASE_STATS
+// Diagnostic build only (-DGM_PHASE_STATS): per wave of k_match_fused, one
+// record of 16 words in g_phase_rec[tile], accumulated in registers and
+// written once at the wave's end (no atomics, no read-modify-write in the
+// walk): [0] staging, [1] tokenizer, [2+l] walk level l (l < 8) in s_memtime
+// ticks, [10] epilogue, [11] rounds of levels 0-3 (8 bits each), [12] rounds of
+// levels 4-7, [13] rounds with a chain tail load, [14..15] the wave's start
+// tick.  run_match reduces them after each call.
+__device__ uint32_t* g_phase_rec;
+struct PhaseRec {
+  uint32_t v[16];
+};
+#define GM_PHASE_ADD(k, x) (PH.v[k] += uint32_t(x))
+// level-indexed adds with constant indices (a dynamic index would put the
+// record in scratch memory)
+__device__ __forceinline__ void phase_level(PhaseRec& PH, uint32_t level, uint32_t ticks, uint32_t rounds) {
+  switch (level) {
+#define GM_PH_CASE(L)                                          \
+  case L:                                                      \
+    PH.v[2 + L] += ticks;                                      \
+    PH.v[L < 4 ? 11 : 12] += rounds << (8 * (L & 3));          \
+    break;
+    GM_PH_CASE(0) GM_PH_CASE(1) GM_PH_CASE(2) GM_PH_CASE(3) GM_PH_CASE(4) GM_PH_CASE(5) GM_PH_CASE(6)
+    default:
+      PH.v[9] += ticks;
+      PH.v[12] += rounds << 24;
+      break;
+#undef GM_PH_CASE
+  }
+}
+#else
+struct PhaseRec {};
+#define GM_PHASE_ADD(k, x) \
+  do {                     \
+  } while (0)
+#endif
 
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1092,9 +1139,13 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
                                                unsigned long long* __restrict__ probe_tile,
                                                unsigned long long* __restrict__ wild_ctr,
                                                uint64_t* __restrict__ tsum, uint32_t* __restrict__ tlen = nullptr,
-                                               uint8_t* __restrict__ cnt8 = nullptr) {
+                                               uint8_t* __restrict__ cnt8 = nullptr, PhaseRec* php = nullptr) {
+  PhaseRec ph_dummy{};
+  PhaseRec& PH = php ? *php : ph_dummy;
+  (void)PH;
   constexpr uint32_t MC = FAST_MC;
   constexpr uint32_t TCAP = 64u * FAST_MC;  // a tile's staging entries
+  constexpr bool KC = WORDS::kChain;        // the topic's future words are in its lane's registers
   const uint64_t tile = t >> 6;
   uint32_t* const MCNT = L.mc;
   uint2* const LW = L.lw;
@@ -1121,18 +1172,26 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
   uint32_t probes = walk ? 1u : 0u;  // + the exact-route probe
   // level 0: one root entry per walking topic
   const unsigned long long bw = __ballot(walk);
+  uint32_t wnext = walk ? words.first() : NONE;
   if (walk) {
     const uint32_t p = lane_prefix(bw);
     L.e[0][p] = make_uint2((!dollar && (ix.root_flags & HOT_PLUS)) ? FR_PLUS : 0u, ix.root_sig);
     L.ln[0][p] = uint8_t(lane);
   }
   uint32_t cur_total = uint32_t(__popcll(bw));
-  uint32_t wnext = walk ? words.first() : NONE;
   const bool hflat = (ix.flags & IX_HOT_FLAT) != 0;
   int cur = 0;
+#ifdef GM_PHASE_STATS
+  uint64_t tph = __builtin_amdgcn_s_memtime();
+#endif
   for (uint32_t level = 0; cur_total; ++level) {
+#ifdef GM_PHASE_STATS
+    const uint32_t ph_rounds = (cur_total + 63) / 64;
+#endif
     LW[lane] = make_uint2(wnext, nlev | (dollar ? TOK_DOLLAR : 0u));
     if (walk && level + 1 < nlev) wnext = words.next(level);  // next level's word, in flight
+    uint32_t wnext2 = NONE;  // KC: the word after it (chain nodes of two words)
+    if constexpr (KC) wnext2 = words.peek1();
     wave_lds_sync();
     const uint32_t lvl = __builtin_amdgcn_readfirstlane(level);
     const int ht = hot_table(lvl + 1);
@@ -1182,14 +1241,20 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
       }
       // issue both probes, then resolve
       HotRec rx{}, rp{};
-      if (dx) rx = hot_load(tab, sx, last, hflat);
+      const bool nol1 = (ix.l1_bypass >> ht) & 1u;
+      if (dx) rx = hot_load(tab, sx, last, hflat, nol1);
       if (pin) {
         rp = plus_inline_load(ptab, id, hflat);
       } else if (dp) {
-        rp = hot_load(tab, sp, last, hflat);
+        rp = hot_load(tab, sp, last, hflat, nol1);
       }
       const uint32_t hx = dx ? hot_resolve_x(ix, ht, tab, capu, kx, sx, rx, last, hflat, hrh) : NONE;
       const uint32_t hp = pin ? (id | HOT_INLINE) : dp ? hot_resolve_x(ix, ht, tab, capu, kp, sp, rp, last, hflat, hrh) : NONE;
+      // The topic's next word (its own lane holds it: wnext), for the push
+      // filter and the chain nodes below; the kernel forms without future words
+      // in registers (KC false) push every node with children.
+      uint32_t w1 = NONE;
+      if constexpr (KC) w1 = uint32_t(__builtin_amdgcn_ds_bpermute(int(tl) << 2, int(wnext)));
 #ifdef GM_PROBE_STATS
       {
         const unsigned long long c[8] = {__ballot(act), __ballot(st_cand), __ballot(st_sig), __ballot(dx),
@@ -1200,16 +1265,56 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
             if (c[k]) atomicAdd(&g_pstats[lvl < 7 ? lvl : 7][k], (unsigned long long)__popcll(c[k]));
       }
 #endif
+      const bool ex = hx != NONE, ep = hp != NONE;
+      // Chain nodes (gm_common.h): the topic must continue with s1 (the head's
+      // sig field) and end after the chain's Lc words; the tail {end, s2, -, F}
+      // is read (an L2 hit: the head's line was just fetched) only when s1 agrees.
+      const bool chx = KC && ex && !last && (rx.a.w & HOT_CHAIN);
+      const bool chp = KC && ep && !last && (rp.a.w & HOT_CHAIN);
+      const bool tx = chx && w1 == rx.a.z, tp = chp && w1 == rp.a.z;
+      const uint32_t rem = (lw.y & 0xFFu) - (level + 1);  // the topic's words after this level (>= 1 when !last)
+      uint32_t fx = NONE, fp = NONE, vx = 0, vp = 0;  // the chain's filter on a match; virtual probes
+      if constexpr (KC) {
+        if (__ballot(tx || tp)) {
+          GM_PHASE_ADD(13, 1);
+          const uint32_t w2 = uint32_t(__builtin_amdgcn_ds_bpermute(int(tl) << 2, int(wnext2)));
+          uint4 qx{}, qp{};
+          if (tx) qx = hot_tail_load(tab, hx, hflat);
+          if (tp) qp = hot_tail_load(tab, hp, hflat);
+          // the probes the reference NFA makes along the chain (SURVEY §8d's P):
+          // c1 found at level+1 (+2 there if it is the topic's last level,
+          // else +3 for c1's own frontier entry), c2 found at level+2 alike
+          auto chain = [&](const uint4& q, uint32_t& f, uint32_t& vpr) {
+            const uint32_t lc = q.y == NONE ? 1u : 2u;
+            const bool two = lc == 2u && w2 == q.y;
+            if (rem == lc && (lc == 1u || two)) f = q.w;
+            vpr = rem == 1u ? 2u : 3u + (two ? (rem == 2u ? 2u : 3u) : 0u);
+          };
+          if (tx) chain(qx, fx, vx);
+          if (tp) chain(qp, fp, vp);
+        }
+      }
+      const bool e5 = fx != NONE && (EXACT || (fx & END_WILD));
+      const bool e6 = fp != NONE && (EXACT || (fp & END_WILD));
+      // a node goes on to the next level only if one of its probes there can
+      // find something: a '+' child, or an exact child the next word's
+      // signature bit admits (KC; otherwise any exact child).  A node that
+      // stays behind (and a chain node) is counted with the probes the
+      // reference NFA would make for it there.
+      const uint32_t b1 = KC ? (w1 != NONE ? sig_bit(w1) : 0u) : 0xFFFFFFFFu;
+      const uint32_t yx = ex ? hot_sig(rx.a.w, rx.a.z) : 0u, yp = ep ? hot_sig(rp.a.w, rp.a.z) : 0u;
+      const bool cx = ex && !last && !chx && ((rx.a.w & FR_PLUS) || (yx & b1));
+      const bool cp = ep && !last && !chp && ((rp.a.w & FR_PLUS) || (yp & b1));
+      probes += (ex && !last && !cx ? 3u + vx : 0u) + (ep && !last && !cp ? 3u + vp : 0u);
       // visits: 'match_#', the end filter on the last level, else the next frontier
       if constexpr (CMP) {
-        const bool ex = hx != NONE, ep = hp != NONE;
-        const bool e1 = ex && (rx.a.w & ID_MASK) != HF_NONE;
+        const bool e1 = ex && (rx.a.w & HF_MASK) != HF_NONE;
         const bool e2 = ex && last && rx.ef != NONE && (EXACT || (rx.ef & END_WILD) || (ldollar && level == 0));
-        const bool e3 = ep && (rp.a.w & ID_MASK) != HF_NONE;
+        const bool e3 = ep && (rp.a.w & HF_MASK) != HF_NONE;
         const bool e4 = ep && last && rp.ef != NONE && (EXACT || (rp.ef & END_WILD) || (ldollar && level == 0));
         probes += last ? 2u * (uint32_t(ex) + uint32_t(ep)) : 0u;
         // the row's counter hands this lane's matches their ranks in the row
-        const uint32_t ne = uint32_t(e1) + uint32_t(e2) + uint32_t(e3) + uint32_t(e4);
+        const uint32_t ne = uint32_t(e1) + uint32_t(e2) + uint32_t(e3) + uint32_t(e4) + uint32_t(e5) + uint32_t(e6);
         uint32_t rk = ne ? atomicAdd(&MCNT[tl], ne) : 0u;
         const uint32_t tag = uint32_t(tl) << CMP_SHIFT;
 #define GM_CW_PUT(c, f)                                                                         \
@@ -1222,10 +1327,14 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
     }                                                                                           \
     wbase += uint32_t(__popcll(b_));                                                            \
   } while (0)
-        GM_CW_PUT(e1, rx.a.w & ID_MASK);
+        GM_CW_PUT(e1, rx.a.w & HF_MASK);
         GM_CW_PUT(e2, rx.ef & ID_MASK);
-        GM_CW_PUT(e3, rp.a.w & ID_MASK);
+        GM_CW_PUT(e3, rp.a.w & HF_MASK);
         GM_CW_PUT(e4, rp.ef & ID_MASK);
+        if (__ballot(e5 || e6)) {
+          GM_CW_PUT(e5, fx & ID_MASK);
+          GM_CW_PUT(e6, fp & ID_MASK);
+        }
 #undef GM_CW_PUT
       } else {
 #define GM_CW_EMIT(f)                                   \
@@ -1235,25 +1344,26 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
   } while (0)
 #define GM_CW_VISIT(r)                                                                          \
   do {                                                                                          \
-    if (((r).a.w & ID_MASK) != HF_NONE) GM_CW_EMIT((r).a.w & ID_MASK);                          \
+    if (((r).a.w & HF_MASK) != HF_NONE) GM_CW_EMIT((r).a.w & HF_MASK);                          \
     if (last) {                                                                                 \
       if ((r).ef != NONE && (EXACT || ((r).ef & END_WILD) || (ldollar && level == 0)))          \
         GM_CW_EMIT((r).ef & ID_MASK);                                                           \
       probes += 2u;                                                                             \
     }                                                                                           \
   } while (0)
-        if (hx != NONE) GM_CW_VISIT(rx);
-        if (hp != NONE) GM_CW_VISIT(rp);
+        if (ex) GM_CW_VISIT(rx);
+        if (ep) GM_CW_VISIT(rp);
+        if (e5) GM_CW_EMIT(fx & ID_MASK);
+        if (e6) GM_CW_EMIT(fp & ID_MASK);
 #undef GM_CW_VISIT
 #undef GM_CW_EMIT
       }
-      const bool cx = hx != NONE && !last, cp = hp != NONE && !last;
       const unsigned long long bx = __ballot(cx), bp = __ballot(cp);
       const uint32_t nx = uint32_t(__popcll(bx));
       if (cx) {
         const uint32_t q = nxt_total + lane_prefix(bx);
         if (q < uint32_t(CW_CAP)) {
-          EN[q] = make_uint2(hx | (rx.a.w & FR_PLUS), rx.a.z);
+          EN[q] = make_uint2(hx | (rx.a.w & FR_PLUS), yx);
           LNn[q] = uint8_t(tl);
         } else {
           atomicOr(&MCNT[tl], CW_OVF);
@@ -1262,7 +1372,7 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
       if (cp) {
         const uint32_t q = nxt_total + nx + lane_prefix(bp);
         if (q < uint32_t(CW_CAP)) {
-          EN[q] = make_uint2(hp | (rp.a.w & FR_PLUS), rp.a.z);
+          EN[q] = make_uint2(hp | (rp.a.w & FR_PLUS), yp);
           LNn[q] = uint8_t(tl);
         } else {
           atomicOr(&MCNT[tl], CW_OVF);
@@ -1273,6 +1383,13 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
     cur ^= 1;
     cur_total = nxt_total < uint32_t(CW_CAP) ? nxt_total : uint32_t(CW_CAP);
     wave_lds_sync();
+#ifdef GM_PHASE_STATS
+    {
+      const uint64_t tn = __builtin_amdgcn_s_memtime();
+      phase_level(PH, level, uint32_t(tn - tph), ph_rounds);
+      tph = tn;
+    }
+#endif
   }
   wave_lds_sync();
   const uint32_t m_n = MCNT[lane];
@@ -1294,10 +1411,17 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
     tsum[tile] = mtot;
     if (wb) atomicAdd(wild_ctr, (unsigned long long)__popcll(wb));
   }
+#ifdef GM_PHASE_STATS
+  GM_PHASE_ADD(10, __builtin_amdgcn_s_memtime() - tph);
+  if (lane == 0 && g_phase_rec)
+    for (int k = 0; k < 16; ++k) g_phase_rec[tile * 16 + k] = PH.v[k];
+#endif
 }
 
 
 struct WordsFromHbm {  // k_walk_coop: the tokenizer's level-major word ids
+  static constexpr bool kChain = false;
+  __device__ __forceinline__ uint32_t peek1() { return NONE; }
   const uint32_t* wp;  // wids + t
   uint64_t n;
   bool nt;
@@ -1337,7 +1461,9 @@ __global__ __launch_bounds__(256, 8) void k_walk_coop(const uint8_t* __restrict_
 // back ~48 B per C2 topic of them), and the tokenizer's ALU work of one wave
 // overlaps the walk's gathers of the others.
 struct WordsFromRegs {
+  static constexpr bool kChain = true;
   uint32_t (&w)[TOK_LMAX];
+  __device__ __forceinline__ uint32_t peek1() { return w[1]; }  // after next(level): the word of level + 2
   __device__ __forceinline__ uint32_t first() { return w[0]; }
   __device__ __forceinline__ uint32_t next(uint32_t) {  // shift the levels down: w[0] = the next level's word
 #pragma unroll
@@ -1367,6 +1493,9 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
   // ms, C3 13.68 -> 13.54; raising late walk levels instead was slower:
   // profiles/r02_ab/prio*_c*.txt)
   if constexpr (TOKPRIO) __builtin_amdgcn_s_setprio(1);
+#ifdef GM_PHASE_STATS
+  const uint64_t tp0 = __builtin_amdgcn_s_memtime();
+#endif
   const uint64_t t0 = uint64_t(blockIdx.x) * 256u;
   const uint64_t t = t0 + threadIdx.x;
   const uint64_t tl = t0 + 256 < n ? t0 + 256 : n;
@@ -1377,6 +1506,13 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
     for (uint64_t i = threadIdx.x; i < nw; i += 256) s_txt[i] = ld_s<NT>(reinterpret_cast<const uint64_t*>(tb + lo + 8 * i));
   }
   __syncthreads();
+  PhaseRec PH{};
+#ifdef GM_PHASE_STATS
+  const uint64_t tp1 = __builtin_amdgcn_s_memtime();
+  PH.v[0] = uint32_t(tp1 - tp0);
+  PH.v[14] = uint32_t(tp0);
+  PH.v[15] = uint32_t(tp0 >> 32);
+#endif
   const bool valid = t < n;
   uint32_t w[TOK_LMAX];
 #pragma unroll
@@ -1392,12 +1528,15 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
     }
   }
   __syncthreads();  // every lane is done with the staged text: the walk reuses the LDS
+#ifdef GM_PHASE_STATS
+  PH.v[1] = uint32_t(__builtin_amdgcn_s_memtime() - tp1);
+#endif
   if constexpr (TOKPRIO) __builtin_amdgcn_s_setprio(0);
   if ((t >> 6) * 64 >= n) return;  // wave-uniform, after the last workgroup barrier
   WordsFromRegs words{w};
   coop_walk_tile<EXACT, NT, WordsFromRegs, CMP>(reinterpret_cast<CoopLds*>(s_raw)[wv], h, words, valid, t, lane, tb,
                                                 toff, ix, cnt, stage, ovf_list, ovf_n, probe_tile, wild_ctr, tsum, tlen,
-                                                cnt8);
+                                                cnt8, &PH);
 }
 
 // ---------------------------------------------------------------------------
@@ -2251,7 +2390,10 @@ __global__ __launch_bounds__(256) void k_shift_table(uint32_t* __restrict__ rmap
 __global__ __launch_bounds__(256) void k_patch_or(uint32_t* __restrict__ dst, const uint64_t* __restrict__ ops,
                                                   uint64_t n) {
   const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
-  if (i < n) atomicOr(dst + (ops[2 * i] >> 2), uint32_t(ops[2 * i + 1]));
+  if (i >= n) return;
+  const uint64_t off = ops[2 * i];
+  if (off & PATCH_AND) atomicAnd(dst + ((off & ~PATCH_AND) >> 2), ~uint32_t(ops[2 * i + 1]));
+  else atomicOr(dst + (off >> 2), uint32_t(ops[2 * i + 1]));
 }
 // Every filter-id field renumbered (renum_field, the device twin of
 // gm_overlay.cpp's renumber_host): hot slots [0, n_hot), nodes [0, n_nodes).
@@ -2261,9 +2403,9 @@ __global__ __launch_bounds__(256) void k_renumber(HotSlot* __restrict__ hot, uin
   for (uint64_t s = uint64_t(blockIdx.x) * 256u + threadIdx.x; s < n_hot; s += stride) {
     HotSlot h = hot[s];
     if (h.key == EDGE_EMPTY) continue;
-    h.hf = renum_field(h.hf, HF_NONE, HOT_PLUS, rmap);
+    h.hf = renum_field(h.hf, HF_NONE, HF_FLAGS, rmap);
     h.end_filter = renum_field(h.end_filter, NONE, END_WILD, rmap);
-    h.p_hf = renum_field(h.p_hf, HF_NONE, HOT_PLUS, rmap);
+    h.p_hf = renum_field(h.p_hf, HF_NONE, HF_FLAGS, rmap);
     h.p_end = renum_field(h.p_end, NONE, END_WILD, rmap);
     hot[s] = h;
   }
@@ -2294,7 +2436,8 @@ int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t byte
     }
   }
   for (const auto& o : orops)
-    if ((o.first & 3) || o.first + 4 > bytes) return set_err(ctx, EMQX_GM_EINVAL, "index_update: OR op outside the blob");
+    if ((o.first & 3) || (o.first & ~PATCH_AND) + 4 > bytes)
+      return set_err(ctx, EMQX_GM_EINVAL, "index_update: OR/AND op outside the blob");
   std::vector<uint64_t> desc;
   uint64_t pay_n = 0;
   for (const auto& g : seg) {
@@ -2653,6 +2796,14 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
   }
   for (int i = 0; K > 1 && i <= K; ++i)
     if (!ctx->ov_ev[i] && hipEventCreateWithFlags(&ctx->ov_ev[i], hipEventDisableTiming) != hipSuccess) K = 1;
+#ifdef GM_PHASE_STATS
+  uint32_t* phase_rec = nullptr;
+  if (main_kind() == MAIN_FUSED && n && hipStreamSynchronize(st) == hipSuccess &&
+      hipMalloc(&phase_rec, (n + 63) / 64 * 64) == hipSuccess) {
+    (void)hipMemset(phase_rec, 0, (n + 63) / 64 * 64);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase_rec), &phase_rec, sizeof phase_rec);
+  }
+#endif
   if (main_kind() == MAIN_FUSED) {
     const char* pe = getenv("GM_FUSED_PRIO");  // A/B knob (read per call): 0 = every phase at priority 0
     const bool tp = !pe || atoi(pe) != 0;
@@ -2705,6 +2856,37 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
                   "plus_found %llu plus_inline %llu\n", l, h[l][0], h[l][1], h[l][2], h[l][3], h[l][4], h[l][5], h[l][6],
                   h[l][7]);
     }
+  }
+#endif
+#ifdef GM_PHASE_STATS
+  if (phase_rec) {
+    const uint64_t nt = (n + 63) / 64;
+    std::vector<uint32_t> h(nt * 16);
+    uint32_t* null_rec = nullptr;
+    if (hipStreamSynchronize(st) == hipSuccess &&
+        hipMemcpy(h.data(), phase_rec, h.size() * 4, hipMemcpyDeviceToHost) == hipSuccess) {
+      double sum[16] = {0}, rounds[8] = {0};
+      uint64_t t_min = ~0ull, t_max = 0;
+      for (uint64_t i = 0; i < nt; ++i) {
+        const uint32_t* r = &h[i * 16];
+        for (int k = 0; k < 11; ++k) sum[k] += r[k];
+        sum[13] += r[13];
+        for (int l = 0; l < 8; ++l) rounds[l] += (r[l < 4 ? 11 : 12] >> (8 * (l & 3))) & 0xFFu;
+        const uint64_t t0 = uint64_t(r[14]) | (uint64_t(r[15]) << 32);
+        uint64_t len = 0;
+        for (int k = 0; k < 11; ++k) len += r[k];
+        t_min = std::min(t_min, t0);
+        t_max = std::max(t_max, t0 + len);
+      }
+      const double w = double(nt);
+      fprintf(stderr, "[phase_stats] waves %llu span %llu ticks; ticks/wave: stage %.0f tok %.0f", (unsigned long long)nt,
+              (unsigned long long)(t_max - t_min), sum[0] / w, sum[1] / w);
+      for (int l = 0; l < 8; ++l)
+        if (rounds[l] > 0) fprintf(stderr, " L%d %.0f (%.2f rounds)", l, sum[2 + l] / w, rounds[l] / w);
+      fprintf(stderr, " epi %.0f; chain-tail rounds/wave %.2f\n", sum[10] / w, sum[13] / w);
+    }
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase_rec), &null_rec, sizeof null_rec);
+    (void)hipFree(phase_rec);
   }
 #endif
   hipEventRecord(after_main, st);

@@ -143,6 +143,14 @@ struct Patcher {
     orops.emplace_back(off, bits);
     w |= bits;
   }
+  // clear `bits` in such a word (an AND op on the device: offset | PATCH_AND)
+  void andw(uint32_t& w, uint32_t bits) {
+    if (!(w & bits)) return;
+    const uint64_t off = uint64_t(reinterpret_cast<const uint8_t*>(&w) - B());
+    save(off, 4);
+    orops.emplace_back(off | PATCH_AND, bits);
+    w &= ~bits;
+  }
   template <class T> T& W(T& r) {
     touch(&r, sizeof(T));
     return r;
@@ -285,7 +293,20 @@ struct Patcher {
       return;
     }
     uint32_t& f = F(c, f_hf(c));
-    f = (f & HOT_PLUS) | id;
+    f = (f & HF_FLAGS) | id;
+  }
+  // A chain node on the path of a filter this update writes goes back to a
+  // plain node (gm_common.h): its signature again, its tail free for an
+  // inline '+' record; the walk then probes c1 / c2 in the tables, where they
+  // still are.  Chains are only built by a rebuild.
+  void unchain(const Cur& c) {
+    if (c.kind != CUR_SLOT) return;
+    HotSlot& S = htab(c.table)[c.slot];
+    if (!(S.hf & HOT_CHAIN)) return;
+    W(S.sig) = sig_bit(S.sig);
+    W(S.p_sig) = 0;
+    W(S.p_end) = NONE;
+    andw(S.hf, HOT_CHAIN);
   }
   // a node's first exact child: set NF_HAS_EXACT and the REF_X bit of the
   // references to it (its parent's edge, and plus_child when it is a '+' child)
@@ -383,6 +404,7 @@ struct Patcher {
         n.table = t;
       }
       c = n;
+      unchain(c);
     }
     if (c.kind != CUR_ROOT) F(c, f_end(c)) = fid | (wild ? END_WILD : 0u);
     Node& en = nodes()[c.v1];
@@ -426,6 +448,7 @@ struct Patcher {
           n.table = t;
         }
         c = n;
+        unchain(c);
       }
       v1 = ch & REF_MASK;
     }
@@ -447,9 +470,9 @@ void renumber_host(Mirror& M, const IndexView& v, const std::vector<uint32_t>& r
     for (uint64_t s = slots * part / parts, e = slots * (part + 1) / parts; s < e; ++s) {
       HotSlot& h = hot[s];
       if (h.key == EDGE_EMPTY) continue;
-      h.hf = renum_field(h.hf, HF_NONE, HOT_PLUS, r);
+      h.hf = renum_field(h.hf, HF_NONE, HF_FLAGS, r);
       h.end_filter = renum_field(h.end_filter, NONE, END_WILD, r);
-      h.p_hf = renum_field(h.p_hf, HF_NONE, HOT_PLUS, r);
+      h.p_hf = renum_field(h.p_hf, HF_NONE, HF_FLAGS, r);
       h.p_end = renum_field(h.p_end, NONE, END_WILD, r);
     }
     for (uint64_t i = n_nodes * part / parts, e = n_nodes * (part + 1) / parts; i < e; ++i) {
@@ -477,6 +500,7 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
                  bool trie_only) {
   Mirror& M = *prev->mirror;
   const uint64_t nb = prev->info.n_filters, K = dset.size();
+  if (nb + K >= HF_NONE) return 1;  // temporary ids must stay below HF_NONE: the rebuild reports it
   const uint64_t nf_new = nb - tomb.size() + K;
   if (nf_new > M.flen_cap) return 1;  // the other tables are checked per insert (NoRoom)
   // GM_UPDATE_TIMING: phase times on stderr (diagnostics)

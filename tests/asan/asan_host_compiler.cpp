@@ -148,9 +148,17 @@ int verify(const emqx_gm_index* idx, const std::set<std::string>& cur, const cha
     for (size_t i = 0; i < ws.size(); ++i) {
       const HotSlot* P = kind ? &v.hot[v.hot_off[table] + slot] : nullptr;
       const uint32_t hf = kind == 1 ? P->hf : kind == 2 ? P->p_hf : 0u;
-      const uint32_t sig = kind == 0 ? v.root_sig : kind == 1 ? P->sig : P->p_sig;
+      const uint32_t sig = kind == 0 ? v.root_sig : kind == 1 ? hot_sig(P->hf, P->sig) : P->p_sig;
+      if (kind == 1 && (hf & HOT_CHAIN) && !(i + 1 == ws.size() && ws[i] == "#")) {
+        // a chain node: a filter through it is its own '#' filter or its one tail (s1 [s2] then F)
+        const uint32_t lc = P->p_sig == NONE ? 1u : 2u;
+        if (ws.size() - i != lc || v_dict_find(v, ws[i]) != P->sig ||
+            (lc == 2 && v_dict_find(v, ws[i + 1]) != P->p_sig) || P->p_end != (f | (wild ? END_WILD : 0u)) ||
+            (P->hf & HOT_PLUS))
+          fail("chain node on the path of " + flt);
+      }
       if (i + 1 == ws.size() && ws[i] == "#") {
-        const uint32_t id = kind == 0 ? v.root_hash : (hf & ID_MASK);
+        const uint32_t id = kind == 0 ? v.root_hash : (hf & HF_MASK);
         if (id != f) fail("hot '#' of " + flt);
         kind = 9;
         break;
@@ -212,7 +220,9 @@ int verify(const emqx_gm_index* idx, const std::set<std::string>& cur, const cha
       for (uint32_t x : {h.end_filter, h.p_end})
         if (x != NONE && (x & ID_MASK) >= cur.size()) fail("stale hot end id");
       for (uint32_t x : {h.hf, h.p_hf})
-        if ((x & ID_MASK) != HF_NONE && (x & ID_MASK) >= cur.size()) fail("stale hot hf id");
+        if ((x & HF_MASK) != HF_NONE && (x & HF_MASK) >= cur.size()) fail("stale hot hf id");
+      if ((h.p_hf & HOT_CHAIN) || ((h.hf & HOT_CHAIN) && (h.p_hf != HF_NONE || (h.hf & HOT_PLUS))))
+        fail("chain fields");
     }
   return bad;
 }

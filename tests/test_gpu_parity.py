@@ -130,6 +130,7 @@ def _rand_topic(rng):
 def test_random_small_sets(ctx, orc, exact, mph, monkeypatch):
     if mph:  # every per-depth hot table placed by hash-and-displace (default: 4k..128k-key tables)
         monkeypatch.setenv("GM_MPH_MIN_KEYS", "1")
+        monkeypatch.setenv("GM_CHAIN", "1")  # and chain nodes (default: past 256 MiB of hot tables)
     rng = random.Random(11)
     for _ in range(40):
         filters = [_rand_filter(rng) for _ in range(rng.randint(1, 60))]
@@ -141,12 +142,70 @@ def test_random_small_sets(ctx, orc, exact, mph, monkeypatch):
 def test_edge_cases(ctx, orc, mph, monkeypatch):
     if mph:
         monkeypatch.setenv("GM_MPH_MIN_KEYS", "1")
+        monkeypatch.setenv("GM_CHAIN", "1")
     filters = ["#", "+", "+/+", "/#", "/+", "$SYS/#", "$SYS/+", "$SYS", "sport/", "sport/+", "sport/#", "a/+/#",
                "", "+/#", "a//b", "a/+/b", "x/y", "a/+", "a/#/b", "é/+"]
     topics = ["", "/", "//", "sport", "sport/", "sport/x", "$SYS", "$SYS/", "$SYS/a", "$SYS/a/b", "a", "a/b",
               "a//b", "a/x/b", "x/y", "+", "#", "a/+", "a/#", "a/#/b", "sport/+", "$x", "é/1", "a/b/c/d/e/f"]
     for exact in (True, False):
         _check(ctx, orc, filters, topics, exact)
+
+
+# ------------------------------------------------------------------ chain nodes (path compression)
+CHAIN_FILTERS = [
+    "a/b/c/d", "a/b/c/e/f", "a/b/x/y/z",        # chains of 1 and 2 words under a/b/c and a/b/x
+    "a/b/c/#", "a/b/x/y", "a/b/x",              # a chain node's own '#' and end filters
+    "p/+/q/r/s", "p/+/q/t",                     # under an inline '+' node (no chain there) and a slot '+'
+    "+/k/l/m", "$SYS/s/t/u", "m/n/o/p/q/r/s",   # root '+' child, '$' words, a longer tail (chain at its last two)
+    "w/1", "w/2/3", "w/2/4",                    # a depth-1 chain, a branching node
+]
+CHAIN_TOPICS = [
+    "a/b/c/d", "a/b/c/d/e", "a/b/c", "a/b/c/e", "a/b/c/e/f", "a/b/c/e/g", "a/b/c/f/f", "a/b/x/y/z", "a/b/x/y",
+    "a/b/x", "a/b/x/y/z/w", "a/b/x/q/z", "p/1/q/r/s", "p/1/q/t", "p/1/q/r", "z/k/l/m", "$SYS/k/l/m",
+    "$SYS/s/t/u", "$SYS/s/t", "m/n/o/p/q/r/s", "m/n/o/p/q/r", "m/n/o/p/q/r/t", "w/1", "w/1/2", "w/2/3", "w/2",
+    "w/2/4/5", "a/b/c/#", "a/b/+/d",
+]
+
+
+def test_chain_nodes_vs_oracle_and_no_chain(ctx, orc, monkeypatch):
+    """Chain nodes (gm_common.h) take a filter's single-word or two-word tail
+    out of the walk: the main pass checks the topic's next words at the chain
+    node and emits the tail's filter there.  Rows equal the oracle and an
+    index built without chains (GM_CHAIN=0), in both modes, for every topic
+    length around each chain, '#' / end filters on the chain node, '+' paths
+    and '$' topics."""
+    topics = CHAIN_TOPICS + [t + "/x" for t in CHAIN_TOPICS]
+    for exact in (True, False):
+        monkeypatch.setenv("GM_CHAIN", "1")  # (by default only indexes past 256 MiB of hot tables get chains)
+        ro, ids = _check(ctx, orc, CHAIN_FILTERS, topics, exact)
+        monkeypatch.setenv("GM_CHAIN", "0")
+        ro2, ids2 = _check(ctx, orc, CHAIN_FILTERS, topics, exact)
+        assert np.array_equal(ro, ro2) and np.array_equal(ids, ids2)
+
+
+def test_chain_nodes_random_deep(ctx, orc, monkeypatch):
+    """Random filter sets with long unique tails (most deep nodes are chain
+    nodes) against the oracle."""
+    monkeypatch.setenv("GM_CHAIN", "1")
+    rng = random.Random(7)
+    words = ["a", "b", "c", "dd", "", "$e", "f1"]
+    for _ in range(20):
+        filters = set()
+        for _ in range(rng.randint(5, 80)):
+            n = rng.randint(1, 7)
+            ws = [rng.choice(words) for _ in range(n)]
+            if rng.random() < 0.3:
+                ws[rng.randrange(n)] = "+"
+            if rng.random() < 0.15:
+                ws.append("#")
+            filters.add("/".join(ws))
+        topics = []
+        for f in sorted(filters):  # every filter's path with its words (+ -> a word), cut and extended
+            ws = [rng.choice(words) if w == "+" else w for w in f.split("/") if w != "#"]
+            for cut in range(max(0, len(ws) - 3), len(ws) + 3):
+                topics.append("/".join((ws + [rng.choice(words) for _ in range(3)])[:max(cut, 1)]))
+        for exact in (True, False):
+            _check(ctx, orc, sorted(filters), topics, exact)
 
 
 def test_deep_and_long_topics(ctx, orc):

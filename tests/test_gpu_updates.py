@@ -27,6 +27,7 @@ def form(request, monkeypatch):
         monkeypatch.delenv("GM_UPDATE_OVERLAY", raising=False)
     if request.param == "patch_mph":  # every per-depth table hash-and-displace placed: inserts take the overflow region
         monkeypatch.setenv("GM_MPH_MIN_KEYS", "1")
+        monkeypatch.setenv("GM_CHAIN", "1")  # and chain nodes, which the patch turns back into plain nodes
     return "patch" if request.param == "patch_mph" else request.param
 
 
@@ -96,6 +97,35 @@ def test_update_sequences_vs_oracle(ctx, orc, form):
             assert _is_flat(ctx, new)
         if rnd % 4 == 0:  # RCU: the previous snapshot still answers for the previous set
             _check(ctx, orc, idx, before, topics)
+        idx.release()
+        idx = new
+    idx.release()
+
+
+def test_update_breaks_chain_nodes(ctx, orc, form, monkeypatch):
+    """In-place updates through chain nodes (gm_common.h): a new branch below a
+    chain node, its tail's filter deleted or re-inserted, a '+' child (whose
+    inline record takes the chain's tail fields), a '#' child, a filter ending
+    on the chain's middle node -- each patch must leave rows equal to the
+    oracle (the patcher turns the chain node back into a plain node)."""
+    from tests.test_gpu_parity import CHAIN_FILTERS, CHAIN_TOPICS
+    monkeypatch.setenv("GM_CHAIN", "1")
+    topics = [t.encode() for t in CHAIN_TOPICS] + [t.encode() + b"/x" for t in CHAIN_TOPICS] + [b"a/b/c/q", b"a/b/c/e"]
+    current = {f.encode() for f in CHAIN_FILTERS}
+    idx = ctx.build_index(sorted(current))
+    steps = [
+        [(b"a/b/c/e/g", True)],                      # a second leaf under the two-word chain's middle node
+        [(b"a/b/x/y/z", False)],                     # the chain's own filter deleted
+        [(b"a/b/x/y/z", True), (b"a/b/x/+", True)],  # re-inserted, and a '+' child of the chain node
+        [(b"m/n/o/p/q/r", True)],                    # a filter on a chain's middle node
+        [(b"w/1/#", True), (b"a/b/c/d", False)],
+        [(b"a/b/c/q", True), (b"a/b/c/e/f", False)],
+    ]
+    for ops in steps:
+        for f, ins in ops:
+            (current.add if ins else current.discard)(f)
+        new = ctx.update_index(idx, ops)
+        _check(ctx, orc, new, current, topics)
         idx.release()
         idx = new
     idx.release()
