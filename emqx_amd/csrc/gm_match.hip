@@ -37,6 +37,7 @@
 // Everything here is integer/byte work bound by HBM/L2 latency and bandwidth;
 // there is no MFMA.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -1078,22 +1079,27 @@ __device__ unsigned long long g_pstats[8][8];
 // tick.  run_match reduces them after each call.
 __device__ uint32_t* g_phase_rec;
 struct PhaseRec {
-  uint32_t v[16];
+  uint32_t v[32];  // [16 + l] ticks of level l's rounds up to the probes' data, [24 + l] the rest of them
 };
 #define GM_PHASE_ADD(k, x) (PH.v[k] += uint32_t(x))
 // level-indexed adds with constant indices (a dynamic index would put the
 // record in scratch memory)
-__device__ __forceinline__ void phase_level(PhaseRec& PH, uint32_t level, uint32_t ticks, uint32_t rounds) {
+__device__ __forceinline__ void phase_level(PhaseRec& PH, uint32_t level, uint32_t ticks, uint32_t rounds, uint32_t t_data,
+                                            uint32_t t_rest) {
   switch (level) {
 #define GM_PH_CASE(L)                                          \
   case L:                                                      \
     PH.v[2 + L] += ticks;                                      \
     PH.v[L < 4 ? 11 : 12] += rounds << (8 * (L & 3));          \
+    PH.v[16 + L] += t_data;                                    \
+    PH.v[24 + L] += t_rest;                                    \
     break;
     GM_PH_CASE(0) GM_PH_CASE(1) GM_PH_CASE(2) GM_PH_CASE(3) GM_PH_CASE(4) GM_PH_CASE(5) GM_PH_CASE(6)
     default:
       PH.v[9] += ticks;
       PH.v[12] += rounds << 24;
+      PH.v[23] += t_data;
+      PH.v[31] += t_rest;
       break;
 #undef GM_PH_CASE
   }
@@ -1187,6 +1193,7 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
   for (uint32_t level = 0; cur_total; ++level) {
 #ifdef GM_PHASE_STATS
     const uint32_t ph_rounds = (cur_total + 63) / 64;
+    uint32_t ph_data = 0, ph_rest = 0;
 #endif
     LW[lane] = make_uint2(wnext, nlev | (dollar ? TOK_DOLLAR : 0u));
     if (walk && level + 1 < nlev) wnext = words.next(level);  // next level's word, in flight
@@ -1208,6 +1215,9 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
     uint8_t* LNn = L.ln[cur ^ 1];
     uint32_t nxt_total = 0;
     for (uint32_t base = 0; base < cur_total; base += 64) {
+#ifdef GM_PHASE_STATS
+      const uint64_t tr0 = __builtin_amdgcn_s_memtime();
+#endif
       const uint32_t e = base + uint32_t(lane);
       const bool act = e < cur_total;
       const uint2 en = act ? E[e] : make_uint2(0u, 0u);
@@ -1250,6 +1260,11 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
       }
       const uint32_t hx = dx ? hot_resolve_x(ix, ht, tab, capu, kx, sx, rx, last, hflat, hrh) : NONE;
       const uint32_t hp = pin ? (id | HOT_INLINE) : dp ? hot_resolve_x(ix, ht, tab, capu, kp, sp, rp, last, hflat, hrh) : NONE;
+#ifdef GM_PHASE_STATS
+      __builtin_amdgcn_s_waitcnt(0);  // (diagnostic build: the probes' data is in)
+      const uint64_t tr1 = __builtin_amdgcn_s_memtime();
+      ph_data += uint32_t(tr1 - tr0);
+#endif
       // The topic's next word (its own lane holds it: wnext), for the push
       // filter and the chain nodes below; the kernel forms without future words
       // in registers (KC false) push every node with children.
@@ -1379,6 +1394,9 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
         }
       }
       nxt_total += nx + uint32_t(__popcll(bp));
+#ifdef GM_PHASE_STATS
+      ph_rest += uint32_t(__builtin_amdgcn_s_memtime() - tr1);
+#endif
     }
     cur ^= 1;
     cur_total = nxt_total < uint32_t(CW_CAP) ? nxt_total : uint32_t(CW_CAP);
@@ -1386,7 +1404,7 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
 #ifdef GM_PHASE_STATS
     {
       const uint64_t tn = __builtin_amdgcn_s_memtime();
-      phase_level(PH, level, uint32_t(tn - tph), ph_rounds);
+      phase_level(PH, level, uint32_t(tn - tph), ph_rounds, ph_data, ph_rest);
       tph = tn;
     }
 #endif
@@ -1397,8 +1415,15 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
   const bool ovf = valid && (m_n > MC || (CMP && wbase > TCAP));
   if (valid) {
     // CMP: one byte per row (0xFF: the listed and slow passes write the row's cnt word)
-    if constexpr (CMP) st_s<NT>(cnt8 + t, uint8_t(ovf ? 0xFFu : m_n));
-    else st_s<NT>(cnt + t, ovf ? OVF_BIT : m_n);
+    if constexpr (CMP) {
+      st_s<NT>(cnt8 + t, uint8_t(ovf ? 0xFFu : m_n));
+      // (the listed pass writes its rows' cnt words; until it has run -- it is
+      // deferred to the host's read-back, MatchCall::finish -- the row reads
+      // as a slow row with no ids, so an assembly before it stays in bounds)
+      if (ovf) cnt[t] = OVF_BIT;
+    } else {
+      st_s<NT>(cnt + t, ovf ? OVF_BIT : m_n);
+    }
     if (ovf) ovf_list[atomicAdd(ovf_n, 1u)] = uint32_t(t);
   }
   if (CMP && lane == 0) st_s<NT>(tlen + tile, wbase < TCAP ? wbase : TCAP);
@@ -1414,7 +1439,7 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
 #ifdef GM_PHASE_STATS
   GM_PHASE_ADD(10, __builtin_amdgcn_s_memtime() - tph);
   if (lane == 0 && g_phase_rec)
-    for (int k = 0; k < 16; ++k) g_phase_rec[tile * 16 + k] = PH.v[k];
+    for (int k = 0; k < 32; ++k) g_phase_rec[tile * 32 + k] = PH.v[k];
 #endif
 }
 
@@ -1510,8 +1535,6 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
 #ifdef GM_PHASE_STATS
   const uint64_t tp1 = __builtin_amdgcn_s_memtime();
   PH.v[0] = uint32_t(tp1 - tp0);
-  PH.v[14] = uint32_t(tp0);
-  PH.v[15] = uint32_t(tp0 >> 32);
 #endif
   const bool valid = t < n;
   uint32_t w[TOK_LMAX];
@@ -1913,10 +1936,19 @@ __global__ __launch_bounds__(256) void k_assemble_c(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ lcnt,
                                                     uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids,
                                                     const uint32_t* __restrict__ gmap, uint64_t cap,
-                                                    const uint64_t* __restrict__ blk) {
+                                                    const uint64_t* __restrict__ blk,
+                                                    const uint32_t* __restrict__ rb_src, uint32_t* __restrict__ rb_dst) {
   __shared__ uint32_t s_out[4][64 * FAST_MC];
   __shared__ uint32_t s_pa[4][64];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // rb_dst (the call's pinned host words): the 40-B read-back -- the match
+  // total and the pass counters, final before this kernel -- written by the
+  // first wave's lanes (vector stores), so the call needs no copy packet; the
+  // host reads it once this launch's stop event has completed
+  if (rb_dst && blockIdx.x == 0 && wv == 0) {
+    if (lane < 10) rb_dst[lane] = rb_src[lane];
+    __threadfence_system();  // (out to host memory before the kernel's end is signalled)
+  }
   const uint64_t n_tiles = (n + 63) / 64;
   const uint64_t tile0 = (uint64_t(blockIdx.x) * 4 + wv) * ASM_TPW;
   if (tile0 >= n_tiles) return;  // wave-uniform; no block barrier below
@@ -2722,11 +2754,15 @@ struct CmpBufs {
 };
 void launch_assemble(hipStream_t st, uint64_t nblk, const CmpBufs* cb, const uint32_t* cnt, uint64_t n,
                      const uint64_t* toff, const uint32_t* stage, uint64_t* row_off, uint32_t* ids,
-                     const uint32_t* gmap, uint64_t cap, const uint64_t* blk = nullptr) {
+                     const uint32_t* gmap, uint64_t cap, const uint64_t* blk = nullptr, uint32_t* rb_dst = nullptr,
+                     hipEvent_t done = nullptr) {
   // blk (compact staging only): toff is a split scan's block-local part, blk its block offsets
+  // rb_dst (compact staging only): the read-back words written by the kernel, `done` its stop event
+  const uint32_t* rb_src = reinterpret_cast<const uint32_t*>(toff + (n + 63) / 64);
   if (cb)
-    hipLaunchKernelGGL(k_assemble_c, dim3((nblk + ASM_TPW - 1) / ASM_TPW), dim3(256), 0, st, cb->cnt8, cnt, n, toff,
-                       stage, cb->tlen, cb->lstage, cb->lcnt, row_off, ids, gmap, cap, blk);
+    hipExtLaunchKernelGGL(k_assemble_c, dim3((nblk + ASM_TPW - 1) / ASM_TPW), dim3(256), 0, st, nullptr, done, 0,
+                          cb->cnt8, cnt, n, toff, stage, cb->tlen, cb->lstage, cb->lcnt, row_off, ids, gmap, cap, blk,
+                          rb_src, rb_dst);
   else
     hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt, n, toff, stage, row_off, ids, gmap, cap);
 }
@@ -2763,12 +2799,18 @@ int overlap_chunks() {
 // device).  `after_main` is recorded between the two: the roofline times the
 // main pass alone, the same kernel rocprofv3 reports.
 template <bool EXACT>
+void launch_listed(hipStream_t st, const IndexView& v, const uint8_t* tb, const uint64_t* to, uint64_t n, uint32_t* cnt,
+                   uint32_t* stage, uint32_t* list1, uint32_t* n1, uint32_t* list2, uint32_t* n2,
+                   unsigned long long* probe_ctr, unsigned long long* wild_ctr, uint64_t* tsum, const CmpBufs* cb);
+template <bool EXACT>
 void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const uint64_t* to, uint64_t n,
                   uint32_t* cnt, uint32_t* stage, uint32_t* list1, uint32_t* n1, uint32_t* list2, uint32_t* n2,
                   unsigned long long* probe_ctr, unsigned long long* wild_ctr, uint32_t* hdr, uint32_t* wids,
-                  unsigned long long* probe_tile, uint64_t* tsum, hipEvent_t after_main, const CmpBufs* cb) {
+                  unsigned long long* probe_tile, uint64_t* tsum, hipEvent_t before_main, hipEvent_t after_main,
+                  const CmpBufs* cb, bool* listed_deferred) {
   hipStream_t st = ctx->stream;
   const uint64_t nblk = (n + 255) / 256;
+  *listed_deferred = false;
 #define GM_LAUNCH_WALK(W, P, sw, g, base)                                                                        \
   hipLaunchKernelGGL((k_walk<EXACT, W, P>), dim3(g), dim3(256), 0, sw, tb, to, n, v, hdr, wids, cnt, stage, list1, n1, \
                      probe_tile, wild_ctr, tsum, base)
@@ -2799,8 +2841,8 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
 #ifdef GM_PHASE_STATS
   uint32_t* phase_rec = nullptr;
   if (main_kind() == MAIN_FUSED && n && hipStreamSynchronize(st) == hipSuccess &&
-      hipMalloc(&phase_rec, (n + 63) / 64 * 64) == hipSuccess) {
-    (void)hipMemset(phase_rec, 0, (n + 63) / 64 * 64);
+      hipMalloc(&phase_rec, (n + 63) / 64 * 128) == hipSuccess) {
+    (void)hipMemset(phase_rec, 0, (n + 63) / 64 * 128);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase_rec), &phase_rec, sizeof phase_rec);
   }
 #endif
@@ -2809,9 +2851,12 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
     const bool tp = !pe || atoi(pe) != 0;
     uint32_t* const tl = cb ? cb->tlen : nullptr;
     uint8_t* const c8 = cb ? cb->cnt8 : nullptr;
-#define GM_FUSED(NT, P, C)                                                                                            \
-  hipLaunchKernelGGL((k_match_fused<3, EXACT, NT, P, C>), dim3(nblk), dim3(256), 0, st, tb, to, n, v, cnt, stage, list1, \
-                     n1, probe_tile, wild_ctr, tsum, tl, c8)
+    // the kernel's own start / stop timestamps (hipExtLaunchKernel) instead of
+    // two event records around it: each record is a barrier packet that costs
+    // the stream ~5.5 us of idle GPU (C1 per-call trace, profiles/r03_c1_trace.txt)
+#define GM_FUSED(NT, P, C)                                                                                          \
+  hipExtLaunchKernelGGL((k_match_fused<3, EXACT, NT, P, C>), dim3(nblk), dim3(256), 0, st, before_main, after_main, 0, \
+                        tb, to, n, v, cnt, stage, list1, n1, probe_tile, wild_ctr, tsum, tl, c8)
     if (cb) {
       if (nt_streams() && tp) GM_FUSED(true, true, true);
       else if (nt_streams()) GM_FUSED(true, false, true);
@@ -2826,9 +2871,11 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
     }
 #undef GM_FUSED
   } else if (K == 1) {
+    hipEventRecord(before_main, st);
     launch_tokenize(st, nblk, tb, to, n, v, hdr, wids, 0);
     GM_WALK(st, nblk, 0ull);
   } else {
+    hipEventRecord(before_main, st);
     hipStream_t st2 = ctx->stream2;
     hipEventRecord(ctx->ov_ev[0], st);  // the tokenizer stream starts after the work queued so far
     hipStreamWaitEvent(st2, ctx->ov_ev[0], 0);
@@ -2861,36 +2908,51 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
 #ifdef GM_PHASE_STATS
   if (phase_rec) {
     const uint64_t nt = (n + 63) / 64;
-    std::vector<uint32_t> h(nt * 16);
+    std::vector<uint32_t> h(nt * 32);
     uint32_t* null_rec = nullptr;
     if (hipStreamSynchronize(st) == hipSuccess &&
         hipMemcpy(h.data(), phase_rec, h.size() * 4, hipMemcpyDeviceToHost) == hipSuccess) {
-      double sum[16] = {0}, rounds[8] = {0};
-      uint64_t t_min = ~0ull, t_max = 0;
+      double sum[32] = {0}, rounds[8] = {0};
       for (uint64_t i = 0; i < nt; ++i) {
-        const uint32_t* r = &h[i * 16];
-        for (int k = 0; k < 11; ++k) sum[k] += r[k];
-        sum[13] += r[13];
+        const uint32_t* r = &h[i * 32];
+        for (int k = 0; k < 32; ++k) sum[k] += r[k];
         for (int l = 0; l < 8; ++l) rounds[l] += (r[l < 4 ? 11 : 12] >> (8 * (l & 3))) & 0xFFu;
-        const uint64_t t0 = uint64_t(r[14]) | (uint64_t(r[15]) << 32);
-        uint64_t len = 0;
-        for (int k = 0; k < 11; ++k) len += r[k];
-        t_min = std::min(t_min, t0);
-        t_max = std::max(t_max, t0 + len);
       }
       const double w = double(nt);
-      fprintf(stderr, "[phase_stats] waves %llu span %llu ticks; ticks/wave: stage %.0f tok %.0f", (unsigned long long)nt,
-              (unsigned long long)(t_max - t_min), sum[0] / w, sum[1] / w);
+      fprintf(stderr, "[phase_stats] waves %llu; ticks/wave: stage %.0f tok %.0f", (unsigned long long)nt, sum[0] / w,
+              sum[1] / w);
       for (int l = 0; l < 8; ++l)
-        if (rounds[l] > 0) fprintf(stderr, " L%d %.0f (%.2f rounds)", l, sum[2 + l] / w, rounds[l] / w);
+        if (rounds[l] > 0)
+          fprintf(stderr, " L%d %.0f (%.2f rounds: to data %.0f, rest %.0f)", l, sum[2 + l] / w, rounds[l] / w,
+                  sum[16 + l] / w, sum[24 + l] / w);
       fprintf(stderr, " epi %.0f; chain-tail rounds/wave %.2f\n", sum[10] / w, sum[13] / w);
     }
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase_rec), &null_rec, sizeof null_rec);
     (void)hipFree(phase_rec);
   }
 #endif
-  hipEventRecord(after_main, st);
+  if (main_kind() != MAIN_FUSED) hipEventRecord(after_main, st);
   (void)probe_tile;  // summed into the probe counter by the tile scan (run_match)
+  // The fused main pass with compact staging leaves the listed pass to the
+  // host's read-back (MatchCall::finish): it launches it only when the main
+  // pass queued rows, instead of an (almost always idle) launch per call.
+  // GM_LISTED_DEFER=0: launch it here (A/B knob).
+  if (cb && main_kind() == MAIN_FUSED) {
+    const char* le = getenv("GM_LISTED_DEFER");
+    if (!le || atoi(le) != 0) {
+      *listed_deferred = true;
+      return;
+    }
+  }
+  launch_listed<EXACT>(st, v, tb, to, n, cnt, stage, list1, n1, list2, n2, probe_ctr, wild_ctr, tsum, cb);
+}
+
+// The listed pass over the main pass's overflow queue (list1, its count n1 on the device)
+template <bool EXACT>
+void launch_listed(hipStream_t st, const IndexView& v, const uint8_t* tb, const uint64_t* to, uint64_t n, uint32_t* cnt,
+                   uint32_t* stage, uint32_t* list1, uint32_t* n1, uint32_t* list2, uint32_t* n2,
+                   unsigned long long* probe_ctr, unsigned long long* wild_ctr, uint64_t* tsum, const CmpBufs* cb) {
+  const uint64_t nblk = (n + 255) / 256;
   const uint64_t lblk = std::min<uint64_t>(nblk, 512);
   if (cb)
     hipLaunchKernelGGL((k_match_lds<EXACT, LISTED_FC, true, true>), dim3(lblk), dim3(256), 0, st, tb, to, n, v, cnt,
@@ -2918,6 +2980,7 @@ struct MatchCall {
   const emqx_gm_index* idx = nullptr;
   uint64_t n = 0, n_tiles = 0, nblk = 0, cap_spec = 0;
   bool dev_io = false, exact = false, cmp = false, spec = false, split = false, submitted = false;
+  bool listed_deferred = false;  // the listed pass is left to finish() (launched only for queued rows)
   const uint8_t* tb = nullptr;
   const uint64_t* to = nullptr;
   PoolBuf d_tb_own, d_to_own, row_off, cnt, stage, list1, list2, tsum, toff, probe_tile, hdr, wids;
@@ -3054,15 +3117,17 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
     cmpb.lstage = c_lstage.as<uint32_t>();
     cmpb.lcnt = c_lcnt.as<uint32_t>();
   }
-  GM_HIP(ctx, hipEventRecord(ev[0], st));  // (also the call's start: total_device_ms)
+  // ev[0] / ev[1]: the main pass's start and end (also the call's start: total_device_ms)
   if (exact)
     launch_match<true>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
                        list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
-                       probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ev[1], cmp ? &cmpb : nullptr);
+                       probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ev[0], ev[1], cmp ? &cmpb : nullptr,
+                       &listed_deferred);
   else
     launch_match<false>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(),
                         n1, list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
-                        probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ev[1], cmp ? &cmpb : nullptr);
+                        probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ev[0], ev[1],
+                        cmp ? &cmpb : nullptr, &listed_deferred);
   GM_HIP(ctx, hipGetLastError());
 
   // count -> scan, then ONE host round trip reads the pass counters and the
@@ -3087,17 +3152,26 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   // assembled at their exact size once the total is known)
   ids = PoolBuf(ctx->pool, cap_spec * 4 + 16);
   spec = ids.p != nullptr;
+  // (compact staging with no host copy-out queued behind: the assembly kernel
+  // writes the read-back words itself and its stop event is the call's end --
+  // a copy and an event record fewer, ~10 us of idle stream per call at C1)
+  uint32_t* pin_dev = nullptr;  // the pinned words as the device addresses them
+  const bool rb_kernel = spec && cmp && !(tail && tail->enqueue) &&
+                         hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_dev), pin, 0) == hipSuccess && pin_dev;
   if (spec) {
     launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
-                    row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec, scan_blk.as<uint64_t>());
+                    row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec, scan_blk.as<uint64_t>(),
+                    rb_kernel ? pin_dev : nullptr, rb_kernel ? ev[2] : nullptr);
     GM_HIP(ctx, hipGetLastError());
     if (tail && tail->enqueue) {
       rc = tail->enqueue(row_off.as<uint64_t>(), ids.as<uint32_t>(), cap_spec);
       if (rc) return rc;
     }
   }
-  GM_HIP(ctx, hipMemcpyAsync(pin, toff_p + n_tiles, 40, hipMemcpyDeviceToHost, st));
-  GM_HIP(ctx, hipEventRecord(ev[2], st));
+  if (!rb_kernel) {
+    GM_HIP(ctx, hipMemcpyAsync(pin, toff_p + n_tiles, 40, hipMemcpyDeviceToHost, st));
+    GM_HIP(ctx, hipEventRecord(ev[2], st));
+  }
   return 0;
 }
 
@@ -3121,15 +3195,39 @@ int MatchCall::finish(emqx_gm_csr* out, MatchTail* tail, bool locked) {
     return finish_csr(ctx, 0, 0, row_off, ids, dev_io, out);
   }
   uint64_t nnz = pin[0];
-  const uint64_t h_ctr[4] = {pin[1], pin[2], pin[3], pin[4]};
+  uint64_t h_ctr[4] = {pin[1], pin[2], pin[3], pin[4]};
+  const float main_ms = ev_ms(ev[0], ev[1]), call_ms = ev_ms(ev[0], ev[2]);
+  if (listed_deferred && uint32_t(h_ctr[0])) {
+    // the main pass queued rows: the listed pass now, a full scan of the
+    // topped-up tile sums, the read-back again; the rows are assembled below
+    uint32_t* n1 = reinterpret_cast<uint32_t*>(ctrs_p);
+    unsigned long long* probe_ctr = reinterpret_cast<unsigned long long*>(ctrs_p + 16);
+    unsigned long long* wild_ctr = reinterpret_cast<unsigned long long*>(ctrs_p + 24);
+    if (exact)
+      launch_listed<true>(st, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
+                          list2.as<uint32_t>(), n1 + 1, probe_ctr, wild_ctr, tsum.as<uint64_t>(), &cmpb);
+    else
+      launch_listed<false>(st, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(),
+                           n1, list2.as<uint32_t>(), n1 + 1, probe_ctr, wild_ctr, tsum.as<uint64_t>(), &cmpb);
+    GM_HIP(ctx, hipGetLastError());
+    // (the probe counter already holds the main pass's tiles: the side sum is not repeated)
+    int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p);
+    if (rc) return rc;
+    GM_HIP(ctx, hipMemcpyAsync(pin, toff_p + n_tiles, 40, hipMemcpyDeviceToHost, st));
+    GM_HIP(ctx, hipStreamSynchronize(st));
+    nnz = pin[0];
+    for (int k = 0; k < 4; ++k) h_ctr[k] = pin[k + 1];
+    spec = false;  // the speculative rows lacked the listed rows
+    split = false;  // toff is whole now
+  }
   S.probes = h_ctr[2];
   S.n_wildcard_topics = h_ctr[3];
   S.n_overflow = uint32_t(h_ctr[0]);
   if (spec && uint32_t(h_ctr[0] >> 32) == 0 && nnz <= cap_spec) {  // no slow-path row, and the rows fit: done
     ctx->ids_per_topic = std::max(1.0, 1.25 * double(nnz) / double(n));
     S.nnz = nnz;
-    S.match_kernel_ms = ev_ms(ev[0], ev[1]);
-    S.total_device_ms = ev_ms(ev[0], ev[2]);
+    S.match_kernel_ms = main_ms;
+    S.total_device_ms = call_ms;
     if (tail) tail->used = true;
     submitted = false;
     return finish_csr(ctx, n, nnz, row_off, ids, dev_io, out);
@@ -3201,7 +3299,7 @@ int MatchCall::finish(emqx_gm_csr* out, MatchTail* tail, bool locked) {
   // (after a slow-path rescan toff is whole; otherwise it is still the split first scan)
   launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
                   row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, nnz,
-                  n_ovf ? nullptr : scan_blk.as<uint64_t>());
+                  (n_ovf || !split) ? nullptr : scan_blk.as<uint64_t>());
   GM_HIP(ctx, hipGetLastError());
   if (n_ovf) {
     hipLaunchKernelGGL(k_copy_slow, dim3(n_ovf), dim3(256), 0, st, ovf_list, n_ovf, row_off.as<uint64_t>(),

@@ -889,10 +889,16 @@ def test_compact_staging_vs_columns(ctx, orc, monkeypatch, listed_cap):
     assert len(r.match_routes(b"m/a/b")) == 16 and len(r.match_routes(b"n/3/x/y")) == 33
     oro, oids, _ = r.match_batch(topics, filters, mode=1, nthreads=8)
     idx = ctx.build_index(filters)
-    for mode in ("1", "0"):
+    # compact staging with the listed pass deferred to the read-back (default)
+    # or launched with the main pass (GM_LISTED_DEFER=0), and the columns
+    for mode, defer in (("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("GM_STAGE_COMPACT", mode)
+        monkeypatch.setenv("GM_LISTED_DEFER", defer)
         ro, ids = ctx.match(idx, topics, exact=True)
-        assert np.array_equal(ro, oro) and np.array_equal(ids, oids), mode
+        assert np.array_equal(ro, oro) and np.array_equal(ids, oids), (mode, defer)
+        # a batch with no listed rows right after one with them (the fast path again)
+        ro2, ids2 = ctx.match(idx, topics[:40_000], exact=True)
+        assert np.array_equal(ro2, oro[:40_001]) and np.array_equal(ids2, oids[:oro[40_000]]), (mode, defer)
     idx.release()
 
 
