@@ -349,7 +349,7 @@ def main():
             if last is not None:
                 last.free()
             last = ctx.match_device(idx, db, do, n_topics, exact=True)
-            kern_ms.append(ctx.stats()["match_kernel_ms"])
+            kern_ms.append(ctx.last_kernel_ms())
     else:
         # two calls in flight (emqx_gm_match_submit / _wait): step i+1's kernels
         # are queued before the host finishes step i, as a serving loop does
@@ -357,7 +357,7 @@ def main():
         for i in range(a.steps):
             nxt = ctx.match_submit(idx, db, do, n_topics, exact=True) if i + 1 < a.steps else None
             r = cur.wait()
-            kern_ms.append(ctx.stats()["match_kernel_ms"])
+            kern_ms.append(ctx.last_kernel_ms())
             if last is not None:
                 last.free()
             last, cur = r, nxt

@@ -35,8 +35,15 @@ DevPool::~DevPool() {
   for (hipEvent_t e : ev_idle_) hipEventDestroy(e);
 }
 
-void DevPool::release_after(void* p, hipStream_t s) {
-  if (!p || !live_.count(p)) return;
+void DevPool::release_after(void* p, hipStream_t s) { release_after(&p, 1, s); }
+// (one event for all the buffers: each event record is a marker packet on the
+// stream, ~5 us of idle GPU between the kernels around it)
+void DevPool::release_after(void* const* ps, int np, hipStream_t s) {
+  void* q[4];
+  int nq = 0;
+  for (int i = 0; i < np && nq < 4; ++i)
+    if (ps[i] && live_.count(ps[i])) q[nq++] = ps[i];
+  if (!nq) return;
   hipEvent_t e = nullptr;
   if (!ev_idle_.empty()) {
     e = ev_idle_.back();
@@ -47,23 +54,31 @@ void DevPool::release_after(void* p, hipStream_t s) {
   if (!e || hipEventRecord(e, s) != hipSuccess) {  // no event: the old way, wait for the stream
     if (e) ev_idle_.push_back(e);
     hipStreamSynchronize(s);
-    release(p);
+    for (int i = 0; i < nq; ++i) release(q[i]);
     return;
   }
-  deferred_.emplace_back(p, e);
+  for (int i = 0; i < nq; ++i) deferred_.emplace_back(q[i], i + 1 == nq ? e : nullptr);
 }
 
 void DevPool::reclaim(bool wait) {
+  // a group of buffers freed together is consecutive, the event on its last
   size_t keep = 0;
-  for (size_t i = 0; i < deferred_.size(); ++i) {
-    auto& d = deferred_[i];
-    const bool done = wait ? (hipEventSynchronize(d.second), true) : hipEventQuery(d.second) == hipSuccess;
-    if (done) {
-      ev_idle_.push_back(d.second);
-      release(d.first);
-    } else {
-      deferred_[keep++] = d;
+  for (size_t i = 0; i < deferred_.size();) {
+    size_t j = i;
+    while (j < deferred_.size() && !deferred_[j].second) ++j;  // the group's event entry
+    if (j == deferred_.size()) {  // (not expected: an unterminated group stays)
+      while (i < j) deferred_[keep++] = deferred_[i++];
+      break;
     }
+    hipEvent_t e = deferred_[j].second;
+    const bool done = wait ? (hipEventSynchronize(e), true) : hipEventQuery(e) == hipSuccess;
+    if (done) {
+      ev_idle_.push_back(e);
+      for (size_t k = i; k <= j; ++k) release(deferred_[k].first);
+    } else {
+      for (size_t k = i; k <= j; ++k) deferred_[keep++] = deferred_[k];
+    }
+    i = j + 1;
   }
   deferred_.resize(keep);
 }
@@ -452,8 +467,8 @@ int emqx_gm_csr_free(emqx_gm_ctx* ctx, emqx_gm_csr* csr) {
     // rows: a fan-out, a later call's inputs) is done -- no wait here, so a
     // caller with the next call in flight keeps it in flight
     hipSetDevice(ctx->device);
-    if (csr->row_off) ctx->pool->release_after(csr->row_off, ctx->stream);
-    if (csr->ids) ctx->pool->release_after(csr->ids, ctx->stream);
+    void* const bufs[2] = {csr->row_off, csr->ids};
+    ctx->pool->release_after(bufs, 2, ctx->stream);
   } else {
     ctx->hpool->release(csr->row_off);
     ctx->hpool->release(csr->ids);

@@ -31,6 +31,7 @@ class DevPool {
   // an event marks the point, alloc() reclaims the buffer once it has passed,
   // and nothing waits.
   void release_after(void* p, hipStream_t s);
+  void release_after(void* const* ps, int np, hipStream_t s);  // one event for up to 4 buffers
   void trim();
   size_t cached_bytes() const { return cached_; }
 

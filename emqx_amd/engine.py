@@ -190,6 +190,7 @@ class Context:
             raise GpuMatchError(rc, f"emqx_gm_open(device={device}) failed (no MI355X visible?)")
         self.h = h
         self.device = device
+        self._stats_buf = MatchStats()
 
     def close(self):
         if self.h:
@@ -380,6 +381,12 @@ class Context:
         s = MatchStats()
         check(lib().emqx_gm_last_stats(self.h, C.byref(s)), self.h, "last_stats")
         return {k: getattr(s, k) for k, _ in MatchStats._fields_}
+
+    def last_kernel_ms(self) -> float:
+        """stats()["match_kernel_ms"] without building the dict (a serving loop's per-call read)."""
+        s = self._stats_buf
+        check(lib().emqx_gm_last_stats(self.h, C.byref(s)), self.h, "last_stats")
+        return s.match_kernel_ms
 
     def synchronize(self):
         check(lib().emqx_gm_synchronize(self.h), self.h, "synchronize")
