@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("EMQX_GM_LIB") or os.path.join(_HERE, "libemqx_gpu_mat
 OK, EINVAL, ENOMEM, EDEVICE, EOVERFLOW, EUNSUPPORTED = 0, -1, -2, -3, -4, -5
 WITH_EXACT = 0x1
 DEVICE_IO = 0x2
+NO_TIMING = 0x4
 
 ERRNAMES = {EINVAL: "EINVAL", ENOMEM: "ENOMEM", EDEVICE: "EDEVICE", EOVERFLOW: "EOVERFLOW",
             EUNSUPPORTED: "EUNSUPPORTED"}

@@ -369,7 +369,10 @@ int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb,
   if (!ctx) return EMQX_GM_EINVAL;
   std::unique_lock<std::recursive_mutex> lk(ctx->mu);
   if (!idx || !out || (n && (!tb || !to))) return gm::set_err(ctx, EMQX_GM_EINVAL, "match: NULL argument");
-  if (flags & ~(EMQX_GM_WITH_EXACT | EMQX_GM_DEVICE_IO)) return gm::set_err(ctx, EMQX_GM_EINVAL, "match: flags");
+  if (flags & ~(EMQX_GM_WITH_EXACT | EMQX_GM_DEVICE_IO | EMQX_GM_NO_TIMING))
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "match: flags");
+  if ((flags & EMQX_GM_NO_TIMING) && !(flags & EMQX_GM_DEVICE_IO))
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "match: EMQX_GM_NO_TIMING needs EMQX_GM_DEVICE_IO");
   if (n >= 0xFFFFFFF0ull) return gm::set_err(ctx, EMQX_GM_EINVAL, "match: batch too large (>= 2^32 topics)");
   if (idx->device != ctx->device) return gm::set_err(ctx, EMQX_GM_EINVAL, "match: index lives on another device");
   std::memset(out, 0, sizeof(*out));
@@ -396,7 +399,8 @@ int emqx_gm_match_submit(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8
   *call = nullptr;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   if (!idx || (n && (!tb || !to))) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: NULL argument");
-  if (flags & ~(EMQX_GM_WITH_EXACT | EMQX_GM_DEVICE_IO)) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: flags");
+  if (flags & ~(EMQX_GM_WITH_EXACT | EMQX_GM_DEVICE_IO | EMQX_GM_NO_TIMING))
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: flags");
   if (!(flags & EMQX_GM_DEVICE_IO))
     return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: device buffers only (EMQX_GM_DEVICE_IO)");
   if (n >= 0xFFFFFFF0ull) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: batch too large (>= 2^32 topics)");

@@ -2695,7 +2695,10 @@ int finish_csr(emqx_gm_ctx* ctx, uint64_t n, uint64_t nnz, PoolBuf& row_off, Poo
 
 float ev_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0.f;
-  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+    (void)hipGetLastError();  // (an event not recorded for this call: no timing, and no sticky error)
+    return 0.f;
+  }
   return ms;
 }
 
@@ -2855,8 +2858,10 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
     // two event records around it: each record is a barrier packet that costs
     // the stream ~5.5 us of idle GPU (C1 per-call trace, profiles/r03_c1_trace.txt)
 #define GM_FUSED(NT, P, C)                                                                                          \
-  hipExtLaunchKernelGGL((k_match_fused<3, EXACT, NT, P, C>), dim3(nblk), dim3(256), 0, st, before_main, after_main, 0, \
+  hipExtLaunchKernelGGL((k_match_fused<3, EXACT, NT, P, C>), dim3(nblk), dim3(256), 0, st, kt ? before_main : nullptr,   \
+                        kt ? after_main : nullptr, 0,                                                                     \
                         tb, to, n, v, cnt, stage, list1, n1, probe_tile, wild_ctr, tsum, tl, c8)
+    const bool kt = before_main != nullptr;  // (an untimed call: EMQX_GM_NO_TIMING)
     if (cb) {
       if (nt_streams() && tp) GM_FUSED(true, true, true);
       else if (nt_streams()) GM_FUSED(true, false, true);
@@ -2981,6 +2986,7 @@ struct MatchCall {
   uint64_t n = 0, n_tiles = 0, nblk = 0, cap_spec = 0;
   bool dev_io = false, exact = false, cmp = false, spec = false, split = false, submitted = false;
   bool listed_deferred = false;  // the listed pass is left to finish() (launched only for queued rows)
+  bool timed = true;             // the main pass's start / stop events (EMQX_GM_NO_TIMING: none)
   const uint8_t* tb = nullptr;
   const uint64_t* to = nullptr;
   PoolBuf d_tb_own, d_to_own, row_off, cnt, stage, list1, list2, tsum, toff, probe_tile, hdr, wids;
@@ -3020,6 +3026,7 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
                       uint32_t flags, MatchTail* tail) {
   dev_io = flags & EMQX_GM_DEVICE_IO;
   exact = flags & EMQX_GM_WITH_EXACT;
+  timed = !(flags & EMQX_GM_NO_TIMING);
   n = n_topics;
   const_cast<emqx_gm_index*>(index)->refs.fetch_add(1);  // the snapshot stays alive until finish (RCU)
   idx = index;
@@ -3117,16 +3124,20 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
     cmpb.lstage = c_lstage.as<uint32_t>();
     cmpb.lcnt = c_lcnt.as<uint32_t>();
   }
-  // ev[0] / ev[1]: the main pass's start and end (also the call's start: total_device_ms)
+  // ev[0] / ev[1]: the main pass's start and end (also the call's start: total_device_ms);
+  // an untimed call of the fused pass launches it without them
+  if (main_kind() != MAIN_FUSED) timed = true;  // (the other forms record their events around the launches)
+  hipEvent_t main_ev0 = ev[0], main_ev1 = ev[1];
+  if (!timed) main_ev0 = main_ev1 = nullptr;
   if (exact)
     launch_match<true>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
                        list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
-                       probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ev[0], ev[1], cmp ? &cmpb : nullptr,
-                       &listed_deferred);
+                       probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), main_ev0, main_ev1,
+                       cmp ? &cmpb : nullptr, &listed_deferred);
   else
     launch_match<false>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(),
                         n1, list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
-                        probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), ev[0], ev[1],
+                        probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), main_ev0, main_ev1,
                         cmp ? &cmpb : nullptr, &listed_deferred);
   GM_HIP(ctx, hipGetLastError());
 
@@ -3196,7 +3207,8 @@ int MatchCall::finish(emqx_gm_csr* out, MatchTail* tail, bool locked) {
   }
   uint64_t nnz = pin[0];
   uint64_t h_ctr[4] = {pin[1], pin[2], pin[3], pin[4]};
-  const float main_ms = ev_ms(ev[0], ev[1]), call_ms = ev_ms(ev[0], ev[2]);
+  // (an untimed call's events hold an older call's stamps: no figures)
+  const float main_ms = timed ? ev_ms(ev[0], ev[1]) : 0.f, call_ms = timed ? ev_ms(ev[0], ev[2]) : 0.f;
   if (listed_deferred && uint32_t(h_ctr[0])) {
     // the main pass queued rows: the listed pass now, a full scan of the
     // topped-up tile sums, the read-back again; the rows are assembled below
@@ -3309,8 +3321,8 @@ int MatchCall::finish(emqx_gm_csr* out, MatchTail* tail, bool locked) {
   GM_HIP(ctx, hipEventRecord(ev[2], st));
   GM_HIP(ctx, hipEventSynchronize(ev[2]));
   S.nnz = nnz;
-  S.match_kernel_ms = ev_ms(ev[0], ev[1]);
-  S.total_device_ms = ev_ms(ev[0], ev[2]);
+  S.match_kernel_ms = main_ms;
+  S.total_device_ms = timed ? ev_ms(ev[0], ev[2]) : 0.f;
   submitted = false;
   return finish_csr(ctx, n, nnz, row_off, ids, dev_io, out);
 }

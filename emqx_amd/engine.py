@@ -301,11 +301,13 @@ class Context:
                                   C.byref(csr)), self.h, "match")
         return DeviceCsr(self, csr)
 
-    def match_submit(self, index: Index, d_bytes: int, d_off: int, n: int, exact: bool = True) -> "PendingMatch":
+    def match_submit(self, index: Index, d_bytes: int, d_off: int, n: int, exact: bool = True,
+                     timed: bool = True) -> "PendingMatch":
         """emqx_gm_match_submit: the call's kernels queued on the device, no wait;
-        ``wait()`` on the result gives the DeviceCsr.  Inputs stay the caller's until then."""
+        ``wait()`` on the result gives the DeviceCsr.  Inputs stay the caller's until then.
+        ``timed`` False: EMQX_GM_NO_TIMING (no main-pass timestamps on the stream)."""
         call = C.c_void_p()
-        flags = _lib.DEVICE_IO | (_lib.WITH_EXACT if exact else 0)
+        flags = _lib.DEVICE_IO | (_lib.WITH_EXACT if exact else 0) | (0 if timed else _lib.NO_TIMING)
         check(lib().emqx_gm_match_submit(self.h, index.h, C.c_void_p(d_bytes), C.c_void_p(d_off), n, flags,
                                          C.byref(call)), self.h, "match_submit")
         return PendingMatch(self, call)

@@ -70,6 +70,13 @@ extern "C" {
 #define EMQX_GM_WITH_EXACT 0x1u /* emqx_router:match_routes/1 semantics        */
 #define EMQX_GM_DEVICE_IO  0x2u /* inputs are device pointers; result stays on
                                    the device (bench / multi-GPU path)         */
+#define EMQX_GM_NO_TIMING  0x4u /* emqx_gm_match / _submit on device buffers:
+                                   do not time this call's main pass
+                                   (stats.match_kernel_ms and total_device_ms
+                                   read 0).  A timed call puts the kernel's
+                                   start/stop timestamps on the stream, which
+                                   costs the device ~5 us of idle each; a
+                                   serving loop times one call in a few      */
 
 typedef struct emqx_gm_ctx emqx_gm_ctx;
 typedef struct emqx_gm_index emqx_gm_index;

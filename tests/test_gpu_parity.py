@@ -902,6 +902,30 @@ def test_compact_staging_vs_columns(ctx, orc, monkeypatch, listed_cap):
     idx.release()
 
 
+def test_untimed_submits_same_rows(ctx, orc):
+    """EMQX_GM_NO_TIMING: calls without the main pass's timestamps return the
+    same rows; their stats read 0 (not an older call's stamps); a timed call
+    after them is timed again."""
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    codes = gen_filter_codes(3, 10_000)
+    idx = ctx.build_index(render_codes(codes))
+    n = 200_000
+    db, do, _ = ctx.gen_topics_device(codes, 3, 0, n)
+    ref = ctx.match_device(idx, db, do, n)
+    assert ctx.stats()["match_kernel_ms"] > 0
+    ro0, ids0 = ref.to_host()
+    ref.free()
+    pend = [ctx.match_submit(idx, db, do, n, timed=(k == 3)) for k in range(4)]
+    for k, p in enumerate(pend):
+        r = p.wait()
+        st = ctx.stats()
+        assert (st["match_kernel_ms"] > 0) == (k == 3), (k, st["match_kernel_ms"])
+        ro, ids = r.to_host()
+        assert np.array_equal(ro, ro0) and np.array_equal(ids, ids0)
+        r.free()
+    idx.release()
+
+
 def test_host_csr_ownership_across_contexts(ctx, orc):
     """A result CSR records its context: freeing it through another context is
     refused (its buffers belong to the first context's pool), and host rows
