@@ -256,6 +256,7 @@ int emqx_gm_close(emqx_gm_ctx* ctx) {
       if (e) hipEventDestroy(e);
     for (hipEvent_t e : ctx->ev_free) hipEventDestroy(e);
     for (void* p : ctx->pin_all) hipHostFree(p);
+    if (ctx->ctr_ring) hipFree(ctx->ctr_ring);
   }
   delete ctx;
   return EMQX_GM_OK;

@@ -123,6 +123,15 @@ struct emqx_gm_ctx {
   std::vector<hipEvent_t> ev_free;
   std::vector<void*> pin_free, pin_all;
   double ids_per_topic = 4.0;  // speculative ids capacity of a match call (run_match), from recent calls
+  // A ring of 64-B pass-counter blocks (gm_match.hip MatchCall): a call takes
+  // the next block, already zeroed -- the previous call's assembly kernel zeroes
+  // it -- so a call needs no zeroing launch of its own.  State per block: 0 ready
+  // (zero, or zeroed by a kernel queued before any later use), 1 held by a call,
+  // 2 dirty (its call is done).
+  static constexpr int CTR_RING = 16;
+  void* ctr_ring = nullptr;
+  uint8_t ctr_state[CTR_RING] = {};
+  int ctr_next = 0;
 };
 
 namespace gm {

@@ -1937,7 +1937,9 @@ __global__ __launch_bounds__(256) void k_assemble_c(const uint8_t* __restrict__ 
                                                     uint64_t* __restrict__ row_off, uint32_t* __restrict__ ids,
                                                     const uint32_t* __restrict__ gmap, uint64_t cap,
                                                     const uint64_t* __restrict__ blk,
-                                                    const uint32_t* __restrict__ rb_src, uint32_t* __restrict__ rb_dst) {
+                                                    const uint32_t* __restrict__ rb_total,
+                                                    const uint32_t* __restrict__ rb_ctr, uint32_t* __restrict__ rb_dst,
+                                                    uint32_t* __restrict__ zero16) {
   __shared__ uint32_t s_out[4][64 * FAST_MC];
   __shared__ uint32_t s_pa[4][64];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1946,9 +1948,12 @@ __global__ __launch_bounds__(256) void k_assemble_c(const uint8_t* __restrict__ 
   // first wave's lanes (vector stores), so the call needs no copy packet; the
   // host reads it once this launch's stop event has completed
   if (rb_dst && blockIdx.x == 0 && wv == 0) {
-    if (lane < 10) rb_dst[lane] = rb_src[lane];
+    if (lane < 10) rb_dst[lane] = lane < 2 ? rb_total[lane] : rb_ctr[lane - 2];
     __threadfence_system();  // (out to host memory before the kernel's end is signalled)
   }
+  // zero16: the next call's pass-counter block (the context's ring), zeroed
+  // for it here so that call needs no zeroing launch
+  if (zero16 && blockIdx.x == 0 && wv == 1 && lane < 16) zero16[lane] = 0u;
   const uint64_t n_tiles = (n + 63) / 64;
   const uint64_t tile0 = (uint64_t(blockIdx.x) * 4 + wv) * ASM_TPW;
   if (tile0 >= n_tiles) return;  // wave-uniform; no block barrier below
@@ -2758,14 +2763,16 @@ struct CmpBufs {
 void launch_assemble(hipStream_t st, uint64_t nblk, const CmpBufs* cb, const uint32_t* cnt, uint64_t n,
                      const uint64_t* toff, const uint32_t* stage, uint64_t* row_off, uint32_t* ids,
                      const uint32_t* gmap, uint64_t cap, const uint64_t* blk = nullptr, uint32_t* rb_dst = nullptr,
-                     hipEvent_t done = nullptr) {
+                     const uint32_t* rb_ctr = nullptr, hipEvent_t done = nullptr, uint32_t* zero16 = nullptr) {
   // blk (compact staging only): toff is a split scan's block-local part, blk its block offsets
-  // rb_dst (compact staging only): the read-back words written by the kernel, `done` its stop event
-  const uint32_t* rb_src = reinterpret_cast<const uint32_t*>(toff + (n + 63) / 64);
+  // rb_dst (compact staging only): the read-back words (the total behind toff, the
+  // counters at rb_ctr) written by the kernel, `done` its stop event
+  // zero16 (compact staging only): a 64-B counter block the kernel zeroes
+  const uint32_t* rb_total = reinterpret_cast<const uint32_t*>(toff + (n + 63) / 64);
   if (cb)
     hipExtLaunchKernelGGL(k_assemble_c, dim3((nblk + ASM_TPW - 1) / ASM_TPW), dim3(256), 0, st, nullptr, done, 0,
                           cb->cnt8, cnt, n, toff, stage, cb->tlen, cb->lstage, cb->lcnt, row_off, ids, gmap, cap, blk,
-                          rb_src, rb_dst);
+                          rb_total, rb_ctr, rb_dst, zero16);
   else
     hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt, n, toff, stage, row_off, ids, gmap, cap);
 }
@@ -2987,6 +2994,7 @@ struct MatchCall {
   bool dev_io = false, exact = false, cmp = false, spec = false, split = false, submitted = false;
   bool listed_deferred = false;  // the listed pass is left to finish() (launched only for queued rows)
   bool timed = true;             // the main pass's start / stop events (EMQX_GM_NO_TIMING: none)
+  int ctr_slot = -1;             // the pass-counter block of the context's ring, or -1 (counters behind toff)
   const uint8_t* tb = nullptr;
   const uint64_t* to = nullptr;
   PoolBuf d_tb_own, d_to_own, row_off, cnt, stage, list1, list2, tsum, toff, probe_tile, hdr, wids;
@@ -3005,8 +3013,19 @@ struct MatchCall {
     for (hipEvent_t& e : ev)
       if (e) ctx->ev_free.push_back(e);
     if (pin) ctx->pin_free.push_back(pin);
+    if (ctr_slot >= 0) ctx->ctr_state[ctr_slot] = 2;  // dirty: zeroed before its next use
     if (idx) const_cast<emqx_gm_index*>(idx)->refs.fetch_sub(1) == 1 ? free_index(const_cast<emqx_gm_index*>(idx))
                                                                      : void();
+  }
+  // the 40-B read-back (match total + pass counters) into the pinned words
+  int readback(hipStream_t st) {
+    if (ctr_slot < 0) {
+      GM_HIP(ctx, hipMemcpyAsync(pin, toff_p + n_tiles, 40, hipMemcpyDeviceToHost, st));
+    } else {
+      GM_HIP(ctx, hipMemcpyAsync(pin, toff_p + n_tiles, 8, hipMemcpyDeviceToHost, st));
+      GM_HIP(ctx, hipMemcpyAsync(pin + 1, ctrs_p, 32, hipMemcpyDeviceToHost, st));
+    }
+    return 0;
   }
   int take_event(hipEvent_t* e) {
     if (!ctx->ev_free.empty()) {
@@ -3092,6 +3111,24 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   const uintptr_t ctrs_a = (reinterpret_cast<uintptr_t>(toff.p) + (n_tiles + 1) * 8 + 63) & ~uintptr_t(63);
   ctrs_p = reinterpret_cast<uint8_t*>(ctrs_a);
   toff_p = reinterpret_cast<uint64_t*>(ctrs_p) - (n_tiles + 1);
+  // the pass counters: the next block of the context's ring when it is free
+  // (zeroed by the previous call's assembly, or here if it is dirty), else the
+  // 64-B block behind toff, zeroed here
+  bool zero_ctrs = true;
+  if (!ctx->ctr_ring) {
+    void* r = nullptr;
+    if (hipMalloc(&r, emqx_gm_ctx::CTR_RING * 64) == hipSuccess) {
+      if (hipMemset(r, 0, emqx_gm_ctx::CTR_RING * 64) == hipSuccess) ctx->ctr_ring = r;
+      else hipFree(r);
+    }
+  }
+  if (ctx->ctr_ring && ctx->ctr_state[ctx->ctr_next] != 1) {
+    ctr_slot = ctx->ctr_next;
+    ctx->ctr_next = (ctx->ctr_next + 1) % emqx_gm_ctx::CTR_RING;
+    zero_ctrs = ctx->ctr_state[ctr_slot] == 2;
+    ctx->ctr_state[ctr_slot] = 1;
+    ctrs_p = static_cast<uint8_t*>(ctx->ctr_ring) + 64 * ctr_slot;
+  }
   probe_tile = PoolBuf(ctx->pool, n_tiles * 8 + 8);
   if (!probe_tile.p) return set_err(ctx, EMQX_GM_ENOMEM, "match: probe workspace");
   // split forms: per-topic header and word ids [level][topic] (the fused kernel keeps them in registers)
@@ -3108,7 +3145,7 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   unsigned long long* wild_ctr = reinterpret_cast<unsigned long long*>(ctrs_p + 24);
   // (a one-wave kernel: a 64-B hipMemsetAsync costs 11-26 us of host time
   // before the main pass can be queued, a launch ~6)
-  hipLaunchKernelGGL(k_zero16, dim3(1), dim3(64), 0, st, reinterpret_cast<uint32_t*>(ctrs_p));
+  if (zero_ctrs) hipLaunchKernelGGL(k_zero16, dim3(1), dim3(64), 0, st, reinterpret_cast<uint32_t*>(ctrs_p));
 
   cmp = main_kind() == MAIN_FUSED && stage_compact() && uint64_t(idx->view.n_filters) < (1ull << CMP_SHIFT);
   if (cmp) {
@@ -3169,10 +3206,20 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   uint32_t* pin_dev = nullptr;  // the pinned words as the device addresses them
   const bool rb_kernel = spec && cmp && !(tail && tail->enqueue) &&
                          hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_dev), pin, 0) == hipSuccess && pin_dev;
+  // (compact staging: the assembly also zeroes the ring's next block for the next call, if it is dirty)
+  uint32_t* zero_next = nullptr;
+  if (spec && cmp && ctr_slot >= 0) {
+    const int z = (ctr_slot + 1) % emqx_gm_ctx::CTR_RING;
+    if (ctx->ctr_state[z] == 2) {
+      zero_next = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->ctr_ring) + 64 * z);
+      ctx->ctr_state[z] = 0;  // (a kernel queued before any later call zeroes it)
+    }
+  }
   if (spec) {
     launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
                     row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec, scan_blk.as<uint64_t>(),
-                    rb_kernel ? pin_dev : nullptr, rb_kernel ? ev[2] : nullptr);
+                    rb_kernel ? pin_dev : nullptr, reinterpret_cast<const uint32_t*>(ctrs_p),
+                    rb_kernel ? ev[2] : nullptr, zero_next);
     GM_HIP(ctx, hipGetLastError());
     if (tail && tail->enqueue) {
       rc = tail->enqueue(row_off.as<uint64_t>(), ids.as<uint32_t>(), cap_spec);
@@ -3180,7 +3227,7 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
     }
   }
   if (!rb_kernel) {
-    GM_HIP(ctx, hipMemcpyAsync(pin, toff_p + n_tiles, 40, hipMemcpyDeviceToHost, st));
+    if (int rc2 = readback(st)) return rc2;
     GM_HIP(ctx, hipEventRecord(ev[2], st));
   }
   return 0;
@@ -3225,7 +3272,7 @@ int MatchCall::finish(emqx_gm_csr* out, MatchTail* tail, bool locked) {
     // (the probe counter already holds the main pass's tiles: the side sum is not repeated)
     int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p);
     if (rc) return rc;
-    GM_HIP(ctx, hipMemcpyAsync(pin, toff_p + n_tiles, 40, hipMemcpyDeviceToHost, st));
+    if (int rc2 = readback(st)) return rc2;
     GM_HIP(ctx, hipStreamSynchronize(st));
     nnz = pin[0];
     for (int k = 0; k < 4; ++k) h_ctr[k] = pin[k + 1];
