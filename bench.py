@@ -305,8 +305,23 @@ def ctypes_ptr(p) -> int:
     return ctypes.cast(p, ctypes.c_void_p).value or 0
 
 
+def heartbeat(every_s: float = 60.0):
+    """A line on stderr every minute while the bench runs (the 100M-filter C5
+    index alone builds for ~2.5 min in one library call)."""
+    import threading
+    t0 = time.perf_counter()
+
+    def beat():
+        while True:
+            time.sleep(every_s)
+            print(f"[bench] running, {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     a = parse()
+    heartbeat()
     world, rank, local, pg = dist_setup(a.gpus)
     import numpy as np
     from emqx_amd import Context
