@@ -41,28 +41,36 @@ def plan_shard(fb: np.ndarray, fo: np.ndarray, world: int, rank: int):
     return sfb, sfo, gids[sh == rank], n_unique
 
 
-def exchange_rows(dist, lens, ids, id_bounds: Sequence[int], world: int, group=None):
+def exchange_rows(dist, lens, ids, id_bounds: Optional[Sequence[int]], world: int, group=None):
     """All-to-all of per-slice rows.
 
     lens: int32 tensor [world * S], this rank's row lengths for the whole batch
     (zero-padded past the last row); ids: int32 tensor, this rank's ids with
     rows in topic order; id_bounds: world + 1 offsets into ids where each slice
-    starts.  Returns (recv_lens [world * S]: piece p = rank p's lengths for this
-    rank's slice, recv_ids: the pieces' ids concatenated in rank order).
+    starts, or None (derived from lens).  Returns (recv_lens [world * S]: piece
+    p = rank p's lengths for this rank's slice, recv_ids: the pieces' ids
+    concatenated in rank order).
+
+    The row lengths go first (fixed sizes); both the counts this rank sends and
+    the counts it receives are then sums over them, so ONE device-to-host copy
+    of 2 x world values gives the all-to-all-v its split sizes.
     """
     import torch
+    recv_lens = torch.empty_like(lens)
+    dist.all_to_all_single(recv_lens, lens, group=group)
+    recv_per = recv_lens.view(world, -1).to(torch.int64).sum(1)
+    if id_bounds is None:
+        send_per = lens.view(world, -1).to(torch.int64).sum(1)
+        both = torch.cat([send_per, recv_per]).cpu().tolist()
+        send_counts, recv_counts = [int(x) for x in both[:world]], [int(x) for x in both[world:]]
+    else:
+        send_counts = [int(id_bounds[q + 1] - id_bounds[q]) for q in range(world)]
+        recv_counts = [int(x) for x in recv_per.cpu().tolist()]
     dev = lens.device
-    send_counts = [int(id_bounds[q + 1] - id_bounds[q]) for q in range(world)]
-    sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
-    rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = [int(x) for x in rc.tolist()]
     # never a NULL buffer, also when nothing is received (the merge takes a device pointer)
     recv_ids = torch.empty(max(sum(recv_counts), 1), dtype=torch.int32, device=dev)[:sum(recv_counts)]
     dist.all_to_all_single(recv_ids, ids, output_split_sizes=recv_counts, input_split_sizes=send_counts,
                            group=group)
-    recv_lens = torch.empty_like(lens)
-    dist.all_to_all_single(recv_lens, lens, group=group)
     return recv_lens, recv_ids
 
 
@@ -107,9 +115,7 @@ class ShardedMatcher:
             ctx.csr_row_lengths(res, lens.data_ptr())
             ids = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
             ctx.memcpy_d2d(ids.data_ptr(), ids_ptr, nnz * 4)
-            # where each peer's slice starts in ids: one device reduction, one D2H of W values
-            per = lens.view(W, S).to(torch.int64).sum(1).cumsum(0).cpu().tolist()
-            bounds = [0] + [int(x) for x in per]
+            bounds = None  # (the exchange derives the send and receive counts from the lengths: one D2H)
         else:
             ro_h, ids_h = res.to_host()
             lens = torch.zeros(W * S, dtype=torch.int32)

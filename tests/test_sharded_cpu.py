@@ -96,6 +96,9 @@ def _worker(rank, world, port, seed, out_dir):
         lens[:n] = torch.from_numpy(np.diff(ro.astype(np.int64)).astype(np.int32))
         bounds = [int(ro[x]) for x in b]
         rl, ri = exchange_rows(dist, lens, torch.from_numpy(gl), bounds, world)
+        # the same exchange with the counts derived from the lengths (the device path: one D2H)
+        rl2, ri2 = exchange_rows(dist, lens, torch.from_numpy(gl), None, world)
+        assert torch.equal(rl, rl2) and torch.equal(ri, ri2)
         rows = _merge_np(rl.numpy(), ri.numpy(), world, S, b[rank + 1] - b[rank])
         uniq = sorted(set(filters))
         fro, fids = orc.bruteforce(topics, uniq, mode=1)
