@@ -926,6 +926,42 @@ def test_untimed_submits_same_rows(ctx, orc):
     idx.release()
 
 
+def test_many_calls_in_flight_counter_ring(ctx, orc):
+    """More calls in flight than the context's ring of pre-zeroed pass-counter
+    blocks (16): the calls past it take counters behind their own workspace;
+    every call's rows equal a lone call's, also for a batch whose rows go
+    through the listed pass (its counters are read after the ring moved on)."""
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    codes = gen_filter_codes(4, 10_000)
+    filters = sorted(set(orc.unpack(*render_codes(codes))) | {("/".join(["d"] + ["x"] * 9)).encode()})
+    idx = ctx.build_index(filters)
+    n = 50_000
+    db, do, _ = ctx.gen_topics_device(codes, 4, 0, n)
+    ref = ctx.match_device(idx, db, do, n)
+    ro0, ids0 = ref.to_host()
+    ref.free()
+    pend = [ctx.match_submit(idx, db, do, n, timed=(k % 5 == 0)) for k in range(24)]
+    for p in pend:
+        r = p.wait()
+        ro, ids = r.to_host()
+        assert np.array_equal(ro, ro0) and np.array_equal(ids, ids0)
+        r.free()
+    # listed-pass rows (10-level topics) between fast-path calls
+    deep = [("/".join(["d"] + ["x"] * 9)).encode()] * 300 + [b"z"] * 100
+    r = orc.Router(True)
+    for f in filters:
+        r.add_route(f)
+    oro, oids, _ = r.match_batch(deep, filters, mode=1)
+    for _ in range(3):
+        g_ro, g_ids = ctx.match(idx, deep, exact=True)
+        assert np.array_equal(g_ro, oro) and np.array_equal(g_ids, oids)
+        rr = ctx.match_device(idx, db, do, n)
+        ro, ids = rr.to_host()
+        assert np.array_equal(ro, ro0) and np.array_equal(ids, ids0)
+        rr.free()
+    idx.release()
+
+
 def test_host_csr_ownership_across_contexts(ctx, orc):
     """A result CSR records its context: freeing it through another context is
     refused (its buffers belong to the first context's pool), and host rows
