@@ -408,19 +408,38 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (uint64_t i = 1; i < NN; ++i)
     if (nodes[i].kind != 2 && !inl[i]) hot_n[hot_table(nodes[i].depth)]++;
   uint64_t hot_off[HOT_TABLES], hot_cap[HOT_TABLES], hot_total = 0;
-  // Minimal-perfect-hash tables (gm_common.h, mph_*): a per-depth table of
-  // [GM_MPH_MIN_KEYS, GM_MPH_MAX_KEYS] keys is placed by hash-and-displace at
-  // load ~0.97 (C2/C3: the depth-2 table, 66.5k keys, 8.5 MB at 0.25 load ->
-  // 2.2 MB, which one XCD's 4 MB L2 keeps); smaller tables stay in L2 anyway and
-  // larger ones do not fit it either way.  GM_NO_MPH / the two bounds: A/B knobs.
+  // Minimal-perfect-hash tables (gm_common.h, mph_*), placed by hash-and-displace
+  // at load ~0.97:
+  //  * a per-depth table of [GM_MPH_MIN_KEYS, GM_MPH_MAX_KEYS] keys (C2/C3: the
+  //    depth-2 table, 66.5k keys, 8.5 MB at 0.25 load -> 2.2 MB, which one XCD's
+  //    4 MB L2 keeps); smaller tables stay in L2 anyway;
+  //  * a table whose parents average >= 4 exact children -- the ones that get an
+  //    exact-edge filter, a dependent L2 read in front of every exact probe --
+  //    when its bucket words (2 B per key) fit 2 MB: the bucket word is that
+  //    read, filters better (12 Bloom bits per key) and the table shrinks 4x
+  //    (C2's depth-3 table, 600k keys: 77 -> 20 MB, kernel 8.76 -> 8.56 ms;
+  //    placing the depth-4/5 tables too, which have no filter read to replace,
+  //    was slower: profiles/r03_ab/mph_tables.txt).
+  // GM_NO_MPH / the two bounds / GM_MPH_TABLES (a table bit mask): A/B knobs.
   uint32_t mph_cap[HOT_TABLES] = {0}, mph_nb[HOT_TABLES] = {0};
   uint64_t mph_off[HOT_TABLES] = {0}, mph_total = 0;
+  uint64_t x_keys[HOT_TABLES] = {0}, x_parents[HOT_TABLES] = {0};  // exact edges into table t, their parents
+  for (uint64_t i = 1; i < NN; ++i)
+    if (nodes[i].kind == 0) x_keys[hot_table(nodes[i].depth)]++;
+  for (uint64_t i = 0; i < NN; ++i)
+    if ((nodes[i].flags & NF_HAS_EXACT) && nodes[i].kind != 2) x_parents[hot_table(nodes[i].depth + 1)]++;
   {
     uint64_t lo = 4096, hi = 131072;
     if (const char* e = getenv("GM_MPH_MIN_KEYS")) lo = strtoull(e, nullptr, 10);
     if (const char* e = getenv("GM_MPH_MAX_KEYS")) hi = strtoull(e, nullptr, 10);
+    // GM_MPH_TABLES: A/B knob, a bit mask of the tables to place this way (overrides the bounds)
+    const char* mt = getenv("GM_MPH_TABLES");
+    const uint32_t mask = mt ? uint32_t(strtoul(mt, nullptr, 0)) : 0u;
     for (int t = 1; t < HOT_TABLES - 1; ++t) {  // (the shared last table mixes depths: open addressing)
-      if (getenv("GM_NO_MPH") || hot_n[t] < lo || hot_n[t] > hi) continue;
+      if (getenv("GM_NO_MPH") || !hot_n[t]) continue;
+      const bool small = hot_n[t] >= lo && hot_n[t] <= hi;
+      const bool filtered = x_keys[t] >= 4 * x_parents[t] && hot_n[t] <= (1u << 20) && !getenv("GM_MPH_NO_FILTERED");
+      if (mt ? !((mask >> t) & 1u) : !(small || filtered)) continue;
       mph_cap[t] = uint32_t(hot_n[t] + hot_n[t] / 32 + 16);
       mph_nb[t] = uint32_t((hot_n[t] + MPH_LAMBDA - 1) / MPH_LAMBDA);
       mph_off[t] = mph_total;
