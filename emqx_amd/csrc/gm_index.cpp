@@ -727,7 +727,17 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   phase("edge filter");
   // ---- 4. word dictionary (open addressing by hash, verified by bytes)
   uint64_t nw = word_ids.size();
-  uint64_t dcap = next_pow2(nw * 4 + 4);  // load <= 0.25: a second (dependent) slot read is rare
+  // Load <= 0.25, and a small vocabulary spread over up to 2 MB (32 slots per
+  // word): a word off its home slot costs its wave a dependent L2 round trip
+  // whenever any of the 64 lanes holds it, and the few words of the upper
+  // levels are in nearly every wave (C2's 2,192 words: 4 -> 32 slots per word
+  // took k_match_fused 8.72 -> 8.48 ms, profiles/r03_ab/dict_load.txt).  Only
+  // the slots holding words are ever read, so the sparse table's cache
+  // footprint stays ~one line per word.  GM_DICT_MUL (A/B knob): slots per word.
+  uint64_t dslots = std::max<uint64_t>(nw * 4 + 4, std::min<uint64_t>(nw * 32, 1ull << 17));
+  if (const char* e = getenv("GM_DICT_MUL"))
+    dslots = nw * std::min<uint64_t>(64, std::max<uint64_t>(1, strtoull(e, nullptr, 10))) + 4;
+  uint64_t dcap = next_pow2(dslots);
   std::vector<DictSlot> dict(dcap, DictSlot{0, DICT_EMPTY_LEN, 0});
   for (uint64_t k = 0; k < nw; ++k) {
     uint64_t s = dict_slot(word_hash[k], dcap - 1);

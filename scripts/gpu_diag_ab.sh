@@ -16,7 +16,7 @@ for cfg in ${CFGS:-c2}; do
       rc=$?; echo "[$cfg $kind phase] rc=$rc"; grep phase_stats $OUT/phase_${cfg}_$kind.log | tail -n 1
       [ $rc -ne 0 ] && { tail -n 5 $OUT/phase_${cfg}_$kind.log; exit $rc; }
     fi
-    EMQX_GM_LIB=$lib timeout -k 10 400 python3 -u bench.py --config $cfg --steps 5 --warmup 2 --no-cpu --no-parity --no-host-io \
+    EMQX_GM_LIB=$lib timeout -k 10 400 python3 -u bench.py --config $cfg --steps ${STEPS:-5} --warmup ${WARM:-2} --no-cpu --no-parity --no-host-io \
       --no-update > $OUT/bench_${cfg}_$kind.log 2>&1
     rc=$?
     echo "[$cfg $kind bench] rc=$rc $(tail -n 1 $OUT/bench_${cfg}_$kind.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value']/1e9, 3), 'Gtopics/s kernel_ms', round(d['roofline']['kernel_ms'], 3))" 2>&1)"
