@@ -395,6 +395,9 @@ def main():
     # algorithmic bytes of one match call's main pass, k_match_fused:
     #   B = Σ len(topic) + 8·n (offsets) + 16·P + Σ_matches (4 + len f) + 8·n (row offsets)
     algo = tbytes + 8 * n_topics + 16 * st["probes"] + 4 * nnz + fbytes_matched + 8 * n_topics
+    kern_ms = [k for k in kern_ms if k > 0]  # (an untimed call reports 0)
+    if not kern_ms:
+        raise SystemExit("bench: no timed k_match_fused launch in the timed region (--time-every > --steps?)")
     kavg = sum(kern_ms) / len(kern_ms)
     achieved = algo / (kavg / 1e3) / 1e9
     # roofline.traffic: the PMC bytes of this very build (scripts/profile.sh ->

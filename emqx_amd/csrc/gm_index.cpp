@@ -449,6 +449,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   uint32_t mph_ovf = 0;
   uint64_t mph_ovf_n[HOT_TABLES] = {0};
   std::vector<uint64_t> mph_word(mph_total + 1, 0);
+  uint64_t hot_sparse = 0;
+  if (const char* e = getenv("GM_HOT_SPARSE")) hot_sparse = std::min<uint64_t>(1u << 22, strtoull(e, nullptr, 10));
   uint64_t hot_load_pct = 25;  // load factor (%); GM_HOT_LOAD_PCT: A/B knob (10..90)
   if (const char* e = getenv("GM_HOT_LOAD_PCT")) hot_load_pct = std::min<uint64_t>(90, std::max<uint64_t>(10, strtoull(e, nullptr, 10)));
   for (int t = 0; t < HOT_TABLES; ++t) {
@@ -460,6 +462,13 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     if (const char* e = getenv("GM_HOT_LOAD_PCT_UPPER"))  // A/B knob: load of the depth 1-2 tables
       if (t <= 2) pct = std::min<uint64_t>(90, std::max<uint64_t>(10, strtoull(e, nullptr, 10)));
     hot_cap[t] = hot_n[t] ? std::max<uint64_t>(8, hot_n[t] * 100 / pct + 1) : 0;
+    // GM_HOT_SPARSE=65536 (A/B knob, off by default until measured): a small
+    // table (<= 1,024 keys: the depth-1 table of every config) is spread over
+    // 65,536 slots (2 MB, of which only its ~n lines are ever read), so
+    // almost every key sits at its home slot and a lookup decides in one read:
+    // at load 0.25 one key in eight is off home, and any lane that probes one
+    // makes its whole wave wait a dependent round (as with the dictionary).
+    if (hot_n[t] && hot_n[t] * 64 <= hot_sparse) hot_cap[t] = std::max<uint64_t>(hot_cap[t], hot_sparse);
     // an MPH table: its perfect-hash region plus an overflow region for in-place
     // inserts (load <= 0.5 there, Patcher::hot_add)
     if (mph_cap[t]) hot_cap[t] = mph_cap[t] + std::max<uint64_t>(64, hot_n[t] / 16);

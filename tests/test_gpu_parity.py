@@ -125,12 +125,26 @@ def _rand_topic(rng):
     return "/".join(ws)
 
 
-@pytest.mark.parametrize("mph", [False, True], ids=["open_addressing", "mph_all_tables"])
-@pytest.mark.parametrize("exact", [True, False], ids=["match_routes", "trie_match"])
-def test_random_small_sets(ctx, orc, exact, mph, monkeypatch):
-    if mph:  # every per-depth hot table placed by hash-and-displace (default: 4k..128k-key tables)
+def _layout_env(monkeypatch, layout):
+    if layout == "mph_all_tables":  # every per-depth hot table placed by hash-and-displace (default: 4k..128k keys)
         monkeypatch.setenv("GM_MPH_MIN_KEYS", "1")
         monkeypatch.setenv("GM_CHAIN", "1")  # and chain nodes (default: past 256 MiB of hot tables)
+    elif layout == "dense":
+        # the dictionary at one slot per word and the hot tables at load 0.9, not
+        # spread out: words and keys off their home slots, the probe loops the
+        # sparse defaults make rare
+        monkeypatch.setenv("GM_DICT_MUL", "1")
+        monkeypatch.setenv("GM_HOT_SPARSE", "0")
+        monkeypatch.setenv("GM_HOT_LOAD_PCT", "90")
+
+
+LAYOUTS = ["open_addressing", "mph_all_tables", "dense"]
+
+
+@pytest.mark.parametrize("mph", LAYOUTS)
+@pytest.mark.parametrize("exact", [True, False], ids=["match_routes", "trie_match"])
+def test_random_small_sets(ctx, orc, exact, mph, monkeypatch):
+    _layout_env(monkeypatch, mph)
     rng = random.Random(11)
     for _ in range(40):
         filters = [_rand_filter(rng) for _ in range(rng.randint(1, 60))]
@@ -138,11 +152,9 @@ def test_random_small_sets(ctx, orc, exact, mph, monkeypatch):
         _check(ctx, orc, filters, topics, exact)
 
 
-@pytest.mark.parametrize("mph", [False, True], ids=["open_addressing", "mph_all_tables"])
+@pytest.mark.parametrize("mph", LAYOUTS)
 def test_edge_cases(ctx, orc, mph, monkeypatch):
-    if mph:
-        monkeypatch.setenv("GM_MPH_MIN_KEYS", "1")
-        monkeypatch.setenv("GM_CHAIN", "1")
+    _layout_env(monkeypatch, mph)
     filters = ["#", "+", "+/+", "/#", "/+", "$SYS/#", "$SYS/+", "$SYS", "sport/", "sport/+", "sport/#", "a/+/#",
                "", "+/#", "a//b", "a/+/b", "x/y", "a/+", "a/#/b", "é/+"]
     topics = ["", "/", "//", "sport", "sport/", "sport/x", "$SYS", "$SYS/", "$SYS/a", "$SYS/a/b", "a", "a/b",
