@@ -64,6 +64,8 @@ class GpuRoutes:
         self.index = ctx.build_index([], subs=[])  # load_index([], []) at init
         self.ops: List[Tuple[bytes, int, str]] = []  # since the snapshot, oldest first
         self.ids: Dict[object, int] = {}       # subscriber -> id
+        self._next_id = 0                      # monotonic, as next_id in the Erlang server: a
+                                               # subscriber that went down never lends its id
         self.subs: Dict[int, object] = {}      # id -> subscriber (the ?SUBS table)
         self.filters_of: Dict[object, set] = {}
         self.other: Dict[bytes, int] = {}      # filter -> destinations other than node (?OTHER)
@@ -79,7 +81,8 @@ class GpuRoutes:
         with self._lock:
             sid = self.ids.get(sub)
             if sid is None:
-                sid = self.ids[sub] = len(self.ids)
+                sid = self.ids[sub] = self._next_id
+                self._next_id += 1
                 self.subs[sid] = sub
             self.filters_of.setdefault(sub, set()).add(f)
             self.ops.append((f, sid, "subscribe"))
@@ -110,7 +113,7 @@ class GpuRoutes:
         self._route(_b(filt), dest, -1)
 
     def _route(self, f: bytes, dest, d: int) -> None:
-        if dest == self.node:  # the local route follows the local subscribers
+        if not isinstance(dest, tuple) and _b(dest) == self.node:  # the local route follows the local subscribers
             return
         with self._lock:
             old = self.other.get(f, 0)
@@ -178,9 +181,16 @@ class PublishBatcher:
     dest)]`` (match_routes/1) with ``fallback_dispatch(filter, msg)``;
     ``on_dropped(msg)`` (the 'message.dropped' hook); ``persist(topic, msg)``;
     ``metrics`` counts messages.publish / dropped / dropped.no_subscribers.
-    A dest is the node name (bytes) or a (group, node) tuple."""
+    A dest is the node name (bytes or str) or a (group, node) tuple.
 
-    def __init__(self, groups_fn: Callable[[Sequence[bytes]], List[Row]], max_batch: int = 4096,
+    ``routes`` (a GpuRoutes) wires the server's own index in one argument:
+    ``groups_fn`` defaults to ``routes.groups``, ``others`` to ``routes.other``
+    (the ?OTHER table the Erlang caller reads directly) and ``subscribers`` to
+    ``routes.subs``.  A ``groups_fn`` that is a bound ``GpuRoutes.groups`` gets
+    its ``others`` the same way, so remote and shared routes cannot be dropped
+    by forgetting the second argument."""
+
+    def __init__(self, groups_fn: Optional[Callable[[Sequence[bytes]], List[Row]]] = None, max_batch: int = 4096,
                  window_s: float = 0.001, subscribers: Optional[Dict[int, object]] = None,
                  deliver: Optional[Callable[[object, bytes, object], bool]] = None,
                  clock: Callable[[], float] = time.monotonic, timer: bool = True, node: bytes = b"node",
@@ -190,7 +200,19 @@ class PublishBatcher:
                  fallback: Optional[Callable[[bytes], List[Tuple[bytes, object]]]] = None,
                  fallback_dispatch: Optional[Callable[[bytes, object], object]] = None,
                  on_dropped: Optional[Callable[[object], None]] = None,
-                 persist: Optional[Callable[[bytes, object], None]] = None):
+                 persist: Optional[Callable[[bytes, object], None]] = None,
+                 routes: Optional[GpuRoutes] = None):
+        if routes is None and isinstance(getattr(groups_fn, "__self__", None), GpuRoutes):
+            routes = groups_fn.__self__
+        if groups_fn is None:
+            if routes is None:
+                raise TypeError("PublishBatcher needs groups_fn or routes")
+            groups_fn = routes.groups
+        if routes is not None:
+            if others is None:
+                others = routes.other
+            if subscribers is None:
+                subscribers = routes.subs
         self.groups_fn = groups_fn
         self.max_batch = max_batch
         self.window_s = window_s
@@ -325,7 +347,8 @@ class PublishBatcher:
         """route(aggre(Routes)) over a matched row (emqx_broker.erl:245-273)."""
         if row[0] == "ok":
             routes: List[tuple] = [(f, self.node, ids) for f, ids in row[1] if len(ids)]
-            other = [(f, d) for f, _ in row[1] if f in self.others for d in self.lookup_routes(f) if d != self.node]
+            other = [(f, d) for f, _ in row[1] if f in self.others for d in self.lookup_routes(f)
+                     if isinstance(d, tuple) or _b(d) != self.node]
         else:  # the reference path
             routes, other = [], list(self.fallback(topic)) if self.fallback else []
         routes += self.aggre(other)
@@ -340,7 +363,7 @@ class PublishBatcher:
     @staticmethod
     def aggre(routes: Sequence[Tuple[bytes, object]]) -> List[tuple]:
         """aggre/1: (filter, node) per node route, one (filter, group) per shared group."""
-        nodes = [(f, d) for f, d in routes if not isinstance(d, tuple)]
+        nodes = [(f, _b(d)) for f, d in routes if not isinstance(d, tuple)]
         groups = sorted({(f, ("group", d[0])) for f, d in routes if isinstance(d, tuple)})
         return nodes + groups
 
@@ -351,7 +374,7 @@ class PublishBatcher:
         f, d = r
         if isinstance(d, tuple):  # ("group", G): emqx_shared_sub:dispatch/3
             return ("share", f, self.shared_dispatch(d[1], f, msg))
-        if d == self.node:
+        if _b(d) == self.node:
             return (d, f, self.fallback_dispatch(f, msg))
         return (d, f, self.forward(d, f, msg))
 

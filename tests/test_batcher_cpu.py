@@ -179,3 +179,93 @@ def test_concurrent_publishers():
     assert b.messages == 1600 and sum(len(c) for c in calls) == 1600
     assert max(len(c) for c in calls) <= 64
     assert b.metrics["messages.dropped"] == 1600
+
+
+# ---------------------------------------------------------------------------
+# GpuRoutes bookkeeping on the CPU: a dict-backed stand-in for the context
+# (the real emqx_gm_index_update_subs path is tests/test_gpu_mirror.py)
+# ---------------------------------------------------------------------------
+class _FakeIndex:
+    def __init__(self, lists, marks):
+        self.lists, self.marks = lists, marks
+        self.names = sorted(f for f in set(lists) | marks if lists.get(f) or f in marks)
+
+    def subscriber_count(self, fid):
+        return len(self.lists.get(self.names[fid], []))
+
+    def filter(self, fid):
+        return self.names[fid]
+
+
+class _FakeCtx:
+    """build_index / update_subs / match / fanout over Python dicts, ids = rank of
+    the filter bytes (the library's id rule), matching by emqx_amd.topic.match."""
+
+    def build_index(self, filters, subs=None):
+        return _FakeIndex({}, set())
+
+    def update_subs(self, idx, ops):
+        lists = {f: list(v) for f, v in idx.lists.items()}
+        marks = set(idx.marks)
+        for f, sid, op in ops:
+            cur = lists.setdefault(f, [])
+            if op == "subscribe" and sid not in cur:
+                cur.append(sid)
+            elif op == "unsubscribe" and sid in cur:
+                cur.remove(sid)
+            elif op == "route_add":
+                marks.add(f)
+            elif op == "route_delete":
+                marks.discard(f)
+        return _FakeIndex(lists, marks)
+
+    def match(self, idx, topics, exact=True):
+        from emqx_amd.topic import match
+        rows = [[i for i, f in enumerate(idx.names) if match(t, f)] for t in topics]
+        ro = np.zeros(len(rows) + 1, np.uint64)
+        ro[1:] = np.cumsum([len(r) for r in rows])
+        return ro, np.array([i for r in rows for i in r], np.uint32)
+
+    def fanout(self, idx, ro, ids):
+        segs = [idx.lists.get(idx.names[int(i)], []) for i in ids]
+        out = np.zeros(len(ro), np.uint64)
+        for k in range(len(ro) - 1):
+            out[k + 1] = out[k] + sum(len(segs[j]) for j in range(int(ro[k]), int(ro[k + 1])))
+        return out, np.array([s for seg in segs for s in seg], np.uint32)
+
+
+def test_subscriber_ids_are_never_reused_after_down():
+    """a subscriber that goes down must not lend its id to the next
+    new subscriber (next_id in nif/emqx_gpu_match_batcher.erl is monotonic)."""
+    from emqx_amd.batcher import GpuRoutes
+    routes = GpuRoutes(_FakeCtx())
+    ia, ib = [], []
+    routes.subscribe("t/+", "a")
+    routes.subscribe("t/#", "b")
+    routes.subscriber_down("a")
+    routes.subscribe("t/1", "c")
+    assert routes.ids["c"] not in (0, 1) and routes.ids["b"] == 1
+    inbox = {"b": ib, "c": ia}
+    b = PublishBatcher(routes=routes, timer=False,
+                       deliver=lambda sub, f, m: inbox[sub].append((f, m)) or True)
+    (res,) = b.publish_batch([(b"t/1", "m")])
+    assert ib == [(b"t/#", "m")] and ia == [(b"t/1", "m")]
+    assert sorted(res) == sorted([(b"node", b"t/#", ("ok", 1)), (b"node", b"t/1", ("ok", 1))])
+
+
+def test_batcher_takes_the_routes_other_table():
+    """groups_fn=routes.groups alone wires routes.other, so a remote
+    route is forwarded; a str node name is the local node, not a remote one."""
+    from emqx_amd.batcher import GpuRoutes
+    routes = GpuRoutes(_FakeCtx(), node="n1")
+    routes.subscribe("r/+", "s")
+    routes.route_add("r/+", "n1")      # the local node as str: no ?OTHER entry
+    routes.route_add("r/+", b"n2")
+    assert routes.other == {b"r/+": 1}
+    fwd = []
+    b = PublishBatcher(routes.groups, timer=False, node="n1", subscribers={0: []},
+                       lookup_routes=lambda f: ["n1", b"n2"],
+                       forward=lambda n, f, m: fwd.append((n, f)) or ("ok", 1))
+    (res,) = b.publish_batch([(b"r/x", "m")])
+    assert fwd == [(b"n2", b"r/+")]
+    assert sorted(res) == sorted([(b"n1", b"r/+", ("ok", 1)), (b"n2", b"r/+", ("ok", 1))])

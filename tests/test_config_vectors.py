@@ -54,3 +54,21 @@ def test_oracles_reproduce_fixture_rows(orc, name):
     assert rows_as_strings(filters, nro, nids) == fx["matches"]
     # every derived-looking topic has a match; a fixture of empty rows would prove nothing
     assert sum(len(m) for m in fx["matches"]) > len(topics)
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3"])
+def test_c5_fixture_method_reproduces_faithful_fixtures(orc, name):
+    """The C5 fixture's third method (tests/golden/make_config_c5.py: the 63
+    candidate filters of each topic looked up in the filter set) must give the
+    faithful restatement's committed rows for C1, C2 and C3 -- so a drift in
+    candidates() or keys_of() fails here, not only in a manual --check."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_config_c5", os.path.join(GOLDEN, "make_config_c5.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    fx = load(name)
+    ids, topics, rows = mk.rows_for(name, log=lambda *a: None)
+    assert ids == fx["topic_index"] and topics == fx["topics"]
+    assert rows == fx["matches"]
+    c5 = load("c5")
+    assert c5["generated_by"].startswith("tests/golden/make_config_c5.py") and len(c5["matches"]) == 2000
