@@ -62,6 +62,9 @@ def parse():
                         "(default: every call; C1, whose step is ~0.1 ms: every 8th)")
     p.add_argument("--no-pipeline", action="store_true",
                    help="one call at a time (emqx_gm_match) instead of two in flight (submit / wait)")
+    p.add_argument("--build-each", action="store_true",
+                   help="replicated configs at N>1: every rank compiles the index itself (the default: rank 0 "
+                        "compiles it once and the others import its image, the device tables broadcast over RCCL)")
     p.add_argument("--no-host-io", action="store_true",
                    help="skip the host-buffer call (PCIe-inclusive rate, reported in detail, never `value`)")
     a = p.parse_args()
@@ -97,6 +100,15 @@ def dist_setup(n_gpus):
             dist.init_process_group(BACKEND)
         pg = dist
     return world, rank, local, pg
+
+
+def torch_first(local):
+    """The device-tensor exchange paths use torch on the GPU: its device runtime
+    must be initialised before the library's (DESIGN.md §7 "Process order with
+    torch"; at N>1 dist_setup has done it, at N=1 this does)."""
+    if BACKEND == "nccl":
+        import torch
+        torch.zeros(1, device=f"cuda:{local}")
 
 
 def _reduce_tensor(local, x: float):
@@ -259,26 +271,38 @@ def optimized_cpu(codes, seed, target_s, threads):
 
 
 def parity_sample(ctx, r, res, codes, fpack_sorted, seed, first_topic, n_topics, threads, windows=20, width=50_000):
-    """A strided sample of one step's CSR (still in HBM) against the oracle: `windows`
-    windows of `width` topics spread over the batch, the last window included."""
+    """A strided sample of one step's CSR (still in HBM: a DeviceCsr; or a host
+    (row_off, ids) pair) against the oracle: `windows` windows of `width`
+    topics spread over the batch, the last window included."""
     import numpy as np
     from oracle import oracle as orc
     ranker = orc.Ranker(fpack_sorted)
     width = min(width, n_topics)
     starts = sorted({int(x) for x in np.linspace(0, n_topics - width, windows)})
-    ro_ptr = ctypes_ptr(res.csr.row_off)
-    ids_ptr = ctypes_ptr(res.csr.ids)
+    if isinstance(res, tuple):
+        hro, hids = res
+
+        def rows(s):
+            ro = hro[s:s + width + 1].astype(np.uint64)
+            return ro, hids[int(ro[0]):int(ro[-1])]
+    else:
+        ro_ptr = ctypes_ptr(res.csr.row_off)
+        ids_ptr = ctypes_ptr(res.csr.ids)
+
+        def rows(s):
+            ro = np.zeros(width + 1, np.uint64)
+            ctx.memcpy_d2h(ro, ro_ptr + 8 * s, (width + 1) * 8)
+            nnz = int(ro[-1] - ro[0])
+            ids = np.zeros(max(nnz, 1), np.uint32)
+            if nnz:
+                ctx.memcpy_d2h(ids, ids_ptr + 4 * int(ro[0]), nnz * 4)
+            return ro, ids[:nnz]
     checked, ok, bad = 0, True, []
     for s in starts:
-        ro = np.zeros(width + 1, np.uint64)
-        ctx.memcpy_d2h(ro, ro_ptr + 8 * s, (width + 1) * 8)
-        nnz = int(ro[-1] - ro[0])
-        ids = np.zeros(max(nnz, 1), np.uint32)
-        if nnz:
-            ctx.memcpy_d2h(ids, ids_ptr + 4 * int(ro[0]), nnz * 4)
+        ro, ids = rows(s)
         tb, to = orc.render_codes(orc.gen_topic_codes(seed, first_topic + s, width, codes))
         oro, oids, _ = r.match_batch((tb, to), ranker, mode=1, nthreads=threads)
-        good = np.array_equal(ro - ro[0], oro) and np.array_equal(ids[:nnz], oids)
+        good = np.array_equal(ro - ro[0], oro) and np.array_equal(ids, oids)
         checked += width
         if not good:
             ok = False
@@ -298,6 +322,75 @@ def fixture_check(ctx, idx, name):
     bad = [i for i, (g, w) in enumerate(zip(got, fx["matches"])) if g != w]
     return {"topics": len(got), "fixture": f"tests/golden/config_{name}.json", "ok": not bad,
             "mismatched_topics": bad[:8]}
+
+
+def host_peak_rss_gb() -> float:
+    """This process's peak resident host memory (ru_maxrss, KiB) in GB."""
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024 / 1e9
+
+
+def replicated_index(a, ctx, world, rank, local, pg, fpack):
+    """The replicated configs' index ("the index is broadcast once
+    at build time"; the reference replicates one routing table to every node,
+    emqx_router.erl:75-84): rank 0 compiles the filter set, the other ranks
+    import its image (emqx_gm_index_export / _import).  Over RCCL the host part
+    of the image (filter table, layout) and the device tables are broadcast as
+    device tensors -- the tables GPU to GPU over xGMI, never through the host;
+    over gloo (rehearsals) the whole image goes as one host tensor.  Returns
+    (index, "built" | "imported")."""
+    if world == 1 or a.build_each:
+        return ctx.build_index(fpack), "built"
+    import numpy as np
+    import torch
+    dev = BACKEND == "nccl"
+    tdev = torch.device("cuda", local) if dev else torch.device("cpu")
+    idx = img = None
+    sizes = torch.zeros(2, dtype=torch.int64, device=tdev)
+    if rank == 0:
+        idx = ctx.build_index(fpack)
+        img = idx.export(with_blob=not dev)
+        sizes[0], sizes[1] = img.nbytes, (idx.device_blob()[1] if dev else 0)
+    pg.broadcast(sizes, 0)
+    n_img, n_blob = (int(x) for x in sizes.tolist())
+    timg = torch.from_numpy(img).to(tdev) if rank == 0 else torch.empty(n_img, dtype=torch.uint8, device=tdev)
+    pg.broadcast(timg, 0)
+    if not dev:
+        out = idx if rank == 0 else ctx.import_index(timg.numpy())
+        return out, "built" if rank == 0 else "imported"
+    blob = torch.empty(n_blob, dtype=torch.uint8, device=tdev)
+    if rank == 0:
+        ptr, nb = idx.device_blob()
+        ctx.memcpy_d2d(blob.data_ptr(), ptr, nb)  # (synchronous on the library's stream)
+    pg.broadcast(blob, 0)
+    torch.cuda.synchronize(tdev)
+    if rank == 0:
+        return idx, "built"
+    out = ctx.import_index(timg.cpu().numpy(), d_blob=blob.data_ptr())
+    del blob, timg
+    torch.cuda.empty_cache()
+    return out, "imported"
+
+
+def replicas_agree(ctx, idx, codes, seed, pg, local, n=65_536) -> bool:
+    """Every rank matches the same probe batch (the stream's first n topics) on
+    its replica and the rows' digest must be the same on all ranks (min == max
+    over the ranks): an imported replica answers exactly as rank 0's build."""
+    import numpy as np
+    db, do, _ = ctx.gen_topics_device(codes, seed, 0, n)
+    r = ctx.match_device(idx, db, do, n, exact=True)
+    ro, ids = r.to_host()
+    r.free()
+    ctx.dev_free(db)
+    ctx.dev_free(do)
+    h = np.uint64(1469598103934665603)
+    for part in (ro.astype(np.uint64), ids.astype(np.uint64)):
+        w = np.arange(1, len(part) + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        h = np.uint64((int(h) * 1099511628211 + int(np.bitwise_xor.reduce(part * w ^ (part >> np.uint64(7)))))
+                      % (1 << 64))
+    d = float(int(h) % (1 << 52))
+    lo = -barrier_max(pg, local, -d)
+    return lo == barrier_max(pg, local, d)
 
 
 def ctypes_ptr(p) -> int:
@@ -342,8 +435,15 @@ def main():
     t_build0 = time.perf_counter()
     codes = gen_filter_codes(a.seed, n_filters, wildcard_only=wildcard_only)
     fpack = render_codes(codes)
-    idx = ctx.build_index(fpack)
+    idx, source = replicated_index(a, ctx, world, rank, local, pg, fpack)
     t_build = time.perf_counter() - t_build0
+    build_info = {"index_source": source, "index_build_s": t_build}
+    if pg is not None:  # how many ranks compiled, the slowest rank's build, the largest host RSS
+        n_built = _reduce_tensor(local, float(source == "built"))
+        pg.all_reduce(n_built)
+        build_info.update(ranks_compiled=int(n_built.item()), index_build_s_max=barrier_max(pg, local, t_build),
+                          host_peak_rss_gb_max=barrier_max(pg, local, host_peak_rss_gb()),
+                          replicas_agree=replicas_agree(ctx, idx, codes, a.seed, pg, local))
     db, do, tbytes = ctx.gen_topics_device(codes, a.seed, rank * n_topics, n_topics)
 
     # warmup (also yields the per-batch constants for the roofline)
@@ -437,7 +537,8 @@ def main():
         "detail": {"nnz_per_step": nnz, "matches_per_topic": nnz / n_topics, "probes_per_topic": st["probes"] /
                    n_topics, "overflow_rows": st["n_overflow"], "topic_bytes": tbytes,
                    "index_device_bytes": int(idx.info.device_bytes), "index_nodes": int(idx.info.n_nodes),
-                   "index_build_s": t_build, "device_ms_per_call": st["total_device_ms"],
+                   **build_info, "host_peak_rss_gb": host_peak_rss_gb(),
+                   "device_ms_per_call": st["total_device_ms"],
                    "calls_in_flight": 1 if a.no_pipeline else 2},
     }
     if not a.no_host_io and rank == 0:
@@ -520,6 +621,7 @@ def bench_c5(a, world, rank, local, pg):
     from emqx_amd.sharded import ShardedMatcher, plan_shard
     n_filters = a.filters or 100_000_000
     n_topics = a.topics or 100_000_000
+    torch_first(local)
     ctx = Context(local)
     t0 = time.perf_counter()
     codes = gen_filter_codes(a.seed, n_filters)
@@ -580,6 +682,7 @@ def bench_c5_prefix(a, world, rank, local, pg):
     from emqx_amd.sharded import PrefixShardedMatcher, plan_prefix_shard
     n_filters = a.filters or 100_000_000
     n_topics = a.topics or 100_000_000
+    torch_first(local)
     ctx = Context(local)
     t0 = time.perf_counter()
     codes = gen_filter_codes(a.seed, n_filters)
@@ -608,12 +711,12 @@ def bench_c5_prefix(a, world, rank, local, pg):
     barrier(pg)
     ctx.synchronize()
     t0 = time.perf_counter()
-    nnz = 0
+    nnz, last = 0, None
     for _ in range(a.steps):
-        r = step()
-        nnz = r.nnz if dev else int(r[0][-1])
-        if dev:
-            r.free()
+        if dev and last is not None:
+            last.free()
+        last = step()
+        nnz = last.nnz if dev else int(last[0][-1])
     ctx.synchronize()
     barrier(pg)
     elapsed = barrier_max(pg, local, time.perf_counter() - t0)
@@ -636,7 +739,17 @@ def bench_c5_prefix(a, world, rank, local, pg):
                       "filters": n_unique, "topics_per_gpu": n_topics, "parallelism": f"prefix shards x{world}"},
            "matches_per_sec": nnz * a.steps / elapsed,
            "detail": {"index_build_s": t_build, "shard_filters": int(len(gids)), "topics_walked_per_rank": walked,
-                      "exchange_bytes_per_step_rank0": m.last_exchange_bytes}}
+                      "exchange_bytes_per_step_rank0": m.last_exchange_bytes,
+                      "device_exchange": dev}}
+    if rank == 0 and not a.no_parity and n_filters < 50_000_000:
+        # rank 0's rows of its own batch (walked on every shard they were routed to,
+        # back in batch order) against the oracle over the whole filter set
+        threads = a.cpu_threads or len(os.sched_getaffinity(0))
+        fpack = render_codes(codes)
+        out["parity_sample"] = parity_sample(ctx, oracle_router(fpack), last, codes, sorted_unique(*fpack), a.seed,
+                                             0, n_topics, threads, width=min(50_000, n_topics // 4 or 1))
+    if dev:
+        last.free()
     ctx.dev_free(db)
     ctx.dev_free(do)
     idx.release()

@@ -17,6 +17,9 @@ OK, EINVAL, ENOMEM, EDEVICE, EOVERFLOW, EUNSUPPORTED = 0, -1, -2, -3, -4, -5
 WITH_EXACT = 0x1
 DEVICE_IO = 0x2
 NO_TIMING = 0x4
+OPEN_MIRROR_EAGER = 0x1
+OPEN_MIRROR_LAZY = 0x2
+IMAGE_NO_BLOB = 0x1
 
 ERRNAMES = {EINVAL: "EINVAL", ENOMEM: "ENOMEM", EDEVICE: "EDEVICE", EOVERFLOW: "EOVERFLOW",
             EUNSUPPORTED: "EUNSUPPORTED"}
@@ -29,7 +32,7 @@ class GpuMatchError(RuntimeError):
 
 
 class Opts(C.Structure):
-    _fields_ = [("device", C.c_int32), ("reserved0", C.c_uint32), ("reserved", C.c_uint64 * 7)]
+    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("reserved", C.c_uint64 * 7)]
 
 
 class Csr(C.Structure):
@@ -63,6 +66,9 @@ SIGNATURES = {
     "emqx_gm_index_build": (_i32, [_vp, _vp, _vp, _u64, _vp, _vp, _vp, C.POINTER(_vp)]),
     "emqx_gm_index_update": (_i32, [_vp, _vp, _vp, _vp, _vp, _u64, C.POINTER(_vp)]),
     "emqx_gm_index_update_subs": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _u64, C.POINTER(_vp)]),
+    "emqx_gm_index_export": (_i32, [_vp, _vp, _u32, _vp, C.POINTER(_u64)]),
+    "emqx_gm_index_device_blob": (_i32, [_vp, C.POINTER(_vp), C.POINTER(_u64)]),
+    "emqx_gm_index_import": (_i32, [_vp, _vp, _u64, _vp, C.POINTER(_vp)]),
     "emqx_gm_index_retain": (_i32, [_vp]),
     "emqx_gm_index_release": (_i32, [_vp]),
     "emqx_gm_index_info": (_i32, [_vp, C.POINTER(IndexInfo)]),

@@ -216,8 +216,12 @@ int emqx_gm_open(const emqx_gm_opts* opts, emqx_gm_ctx** out) {
   if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return EMQX_GM_EDEVICE;
   if (dev < 0 || dev >= count) return EMQX_GM_EINVAL;
   if (hipSetDevice(dev) != hipSuccess) return EMQX_GM_EDEVICE;
+  if (opts && (opts->flags & ~(EMQX_GM_OPEN_MIRROR_EAGER | EMQX_GM_OPEN_MIRROR_LAZY))) return EMQX_GM_EINVAL;
+  if (opts && (opts->flags & EMQX_GM_OPEN_MIRROR_EAGER) && (opts->flags & EMQX_GM_OPEN_MIRROR_LAZY))
+    return EMQX_GM_EINVAL;
   auto* ctx = new emqx_gm_ctx;
   ctx->device = dev;
+  ctx->open_flags = opts ? opts->flags : 0;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return EMQX_GM_EDEVICE;
@@ -252,6 +256,10 @@ int emqx_gm_close(emqx_gm_ctx* ctx) {
       hipStreamSynchronize(ctx->stream2);
       hipStreamDestroy(ctx->stream2);
     }
+    if (ctx->stream_asm) {
+      hipStreamSynchronize(ctx->stream_asm);
+      hipStreamDestroy(ctx->stream_asm);
+    }
     for (auto& e : ctx->ov_ev)
       if (e) hipEventDestroy(e);
     for (hipEvent_t e : ctx->ev_free) hipEventDestroy(e);
@@ -272,6 +280,7 @@ int emqx_gm_set_stream(emqx_gm_ctx* ctx, void* s) {
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
+  if (ctx->stream_asm) hipStreamSynchronize(ctx->stream_asm);
   if (s) {
     if (ctx->own_stream) hipStreamDestroy(ctx->stream);
     ctx->stream = static_cast<hipStream_t>(s);
@@ -289,6 +298,7 @@ int emqx_gm_synchronize(emqx_gm_ctx* ctx) {
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   hipSetDevice(ctx->device);
   GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->stream_asm) GM_HIP(ctx, hipStreamSynchronize(ctx->stream_asm));
   return EMQX_GM_OK;
 }
 
@@ -324,6 +334,31 @@ int emqx_gm_index_update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
   return gm::update_subs(ctx, prev, fb, fo, subs, ops, n_ops, out);
+  GM_GUARD_END(ctx)
+}
+
+int emqx_gm_index_export(emqx_gm_ctx* ctx, const emqx_gm_index* idx, uint32_t flags, uint8_t* buf, uint64_t* size) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  GM_GUARD_BEGIN
+  return gm::index_export(ctx, idx, flags, buf, size);
+  GM_GUARD_END(ctx)
+}
+
+int emqx_gm_index_device_blob(const emqx_gm_index* idx, const void** d_blob, uint64_t* bytes) {
+  if (!idx || !d_blob || !bytes) return EMQX_GM_EINVAL;
+  if (idx->ov || idx->dev_subs || !idx->dev_base) return EMQX_GM_EUNSUPPORTED;
+  *d_blob = idx->dev_base;
+  *bytes = idx->dev_bytes;
+  return EMQX_GM_OK;
+}
+
+int emqx_gm_index_import(emqx_gm_ctx* ctx, const uint8_t* image, uint64_t size, const void* d_blob,
+                         emqx_gm_index** out) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  GM_GUARD_BEGIN
+  return gm::index_import(ctx, image, size, d_blob, out);
   GM_GUARD_END(ctx)
 }
 

@@ -792,6 +792,9 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     delete idx;
     return set_err(ctx, EMQX_GM_EINVAL, "index_build: host-only index without subscribers or shard ids only");
   }
+  // keep_mirror: the layout reserves update headroom and the index carries a
+  // Mirror; its host copy of the blob is kept from here (eager) or downloaded
+  // on the line's first update (load_mirror_blob), see EMQX_GM_OPEN_MIRROR_*
   const bool keep_mirror = host_mirror || (ctx && !gids && !getenv("GM_NO_MIRROR"));
   const uint64_t nodes_cap = keep_mirror ? NN + NN / 4 + 1024 : NN;
   const uint64_t arena_cap = keep_mirror ? arena.size() + arena.size() / 4 + 65536 : arena.size();
@@ -859,10 +862,19 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     return set_err(ctx, EMQX_GM_EDEVICE, std::string("index_build: upload: ") + hipGetErrorString(e));
   }
   if (keep_mirror) {
+    bool eager = host_mirror || o_soff <= kEagerMirrorBytes;
+    if (!host_mirror) {
+      if (const char* pol = getenv("GM_MIRROR")) eager = !strcmp(pol, "eager");  // A/B and test knob
+      if (ctx->open_flags & EMQX_GM_OPEN_MIRROR_EAGER) eager = true;
+      if (ctx->open_flags & EMQX_GM_OPEN_MIRROR_LAZY) eager = false;
+    }
     auto* m = new Mirror;
-    hb.resize(o_soff);  // the mirror stops at the subscriber CSR
-    hb.shrink_to_fit();
-    m->blob = std::move(hb);
+    m->blob_size = o_soff;  // the mirror stops at the subscriber CSR
+    if (eager) {
+      hb.resize(o_soff);
+      hb.shrink_to_fit();
+      m->blob = std::move(hb);
+    }
     m->o_nodes = o_nodes;
     m->o_dict = o_dict;
     m->o_edges = o_edges;
@@ -884,6 +896,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   }
   // the view's base: the device blob, or (host-only index) the mirror
   uint8_t* B = host_mirror ? idx->mirror->blob.data() : static_cast<uint8_t*>(idx->dev_base);
+  std::vector<uint8_t>().swap(hb);  // (a lazy mirror: no host copy of the tables stays)
 
   phase("upload");
   IndexView& v = idx->view;

@@ -108,10 +108,15 @@ struct HostPipe;  // gm_host.cpp: pinned staging + copy streams + worker threads
 
 struct emqx_gm_ctx {
   int device = 0;
+  uint32_t open_flags = 0;  // emqx_gm_opts.flags (EMQX_GM_OPEN_*)
   gm::HostPipe* host = nullptr;
   hipStream_t stream = nullptr;
   bool own_stream = false;
   hipStream_t stream2 = nullptr;  // tokenizer stream of the overlapped match (GM_OVERLAP)
+  // assembly stream (gm_match.hip MatchCall): a large device-buffer call's
+  // scan + assembly run here behind its main pass, so the next call's main
+  // pass (context stream) overlaps them
+  hipStream_t stream_asm = nullptr;
   hipEvent_t ov_ev[9] = {};
   std::recursive_mutex mu;
   gm::DevPool* pool = nullptr;
@@ -180,7 +185,8 @@ struct IdShift {
 // an update moves it from the old snapshot (which stays valid for its readers)
 // to the new one.
 struct Mirror {
-  std::vector<uint8_t> blob;
+  std::vector<uint8_t> blob;             // empty until the first update when built lazily (load_mirror_blob)
+  size_t blob_size = 0;                  // bytes of the blob: the device tables up to the subscriber CSR
   size_t o_nodes = 0, o_dict = 0, o_edges = 0, o_hot = 0, o_arena = 0, o_flen = 0, o_efilt = 0, o_mph = 0;
   uint64_t nodes_n = 0, nodes_cap = 0;   // v1 level-trie nodes used / capacity
   uint64_t arena_n = 0, arena_cap = 0;   // word bytes used / capacity
@@ -290,6 +296,12 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
                  const std::set<std::string>& dset, emqx_gm_index** out, std::vector<uint32_t>* rmap_out = nullptr,
                  bool trie_only = false);
 bool well_formed_filter(const uint8_t* p, uint64_t len);
+// gm_image.cpp: index images (emqx_gm_index_export / _import) and the lazy host mirror
+int index_export(emqx_gm_ctx* ctx, const emqx_gm_index* idx, uint32_t flags, uint8_t* buf, uint64_t* size);
+int index_import(emqx_gm_ctx* ctx, const uint8_t* img, uint64_t size, const void* d_blob, emqx_gm_index** out);
+int load_mirror_blob(emqx_gm_ctx* ctx, emqx_gm_index* idx);
+// a plain index's host mirror is kept from the build when its tables are at most this big
+constexpr size_t kEagerMirrorBytes = size_t(2) << 30;
 // rank of f among idx's filters; *found = exact hit
 uint64_t filter_rank(const emqx_gm_index* idx, const uint8_t* f, uint64_t len, bool* found);
 // gm_subs.cpp: emqx_gm_index_update_subs

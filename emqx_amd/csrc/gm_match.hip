@@ -1687,12 +1687,16 @@ struct LoadSegLen {  // subscriber count of the filter of match entry i
 // hand back the blocks' offsets in *split (out[i] + (*split)[i / SCAN_B] is the
 // scan; out[n_in] is the grand total) -- the consumer adds them, one launch
 // (k_scan_add) fewer.  split->p stays null when the scan was not split.
+// st: the stream (default: the context's).  On another stream the scan's
+// workspace goes back to the pool behind an event on that stream (the pool's
+// immediate reuse assumes the context stream's order).
 template <class LOAD>
 int scan_excl(emqx_gm_ctx* ctx, LOAD load, uint64_t n_in, uint64_t* out, SideSum side = SideSum{},
-              PoolBuf* split = nullptr) {
+              PoolBuf* split = nullptr, hipStream_t st = nullptr) {
+  if (!st) st = ctx->stream;
   const uint64_t n_out = n_in + 1;
   if (n_out <= uint64_t(SCAN1_B)) {  // one launch
-    hipLaunchKernelGGL(k_scan_one<LOAD>, dim3(1), dim3(SCAN1_T), 0, ctx->stream, load, n_in, n_out, out, side,
+    hipLaunchKernelGGL(k_scan_one<LOAD>, dim3(1), dim3(SCAN1_T), 0, st, load, n_in, n_out, out, side,
                        static_cast<uint64_t*>(nullptr));
     GM_HIP(ctx, hipGetLastError());
     return 0;
@@ -1700,19 +1704,29 @@ int scan_excl(emqx_gm_ctx* ctx, LOAD load, uint64_t n_in, uint64_t* out, SideSum
   const uint64_t nb = (n_out + SCAN_B - 1) / SCAN_B;
   PoolBuf sums(ctx->pool, nb * 8 + 8), offs(ctx->pool, (nb + 1) * 8 + 8);
   if (!sums.p || !offs.p) return set_err(ctx, EMQX_GM_ENOMEM, "scan: workspace");
-  hipLaunchKernelGGL(k_scan_local<LOAD>, dim3(nb), dim3(SCAN_T), 0, ctx->stream, load, n_in, n_out, out,
+  struct Later {  // (another stream: release the workspace behind that stream's work)
+    emqx_gm_ctx* c;
+    hipStream_t s;
+    PoolBuf* b[2];
+    ~Later() {
+      if (s == c->stream) return;
+      for (PoolBuf* x : b)
+        if (x->p) c->pool->release_after(x->release_ownership(), s);
+    }
+  } later{ctx, st, {&sums, &offs}};
+  hipLaunchKernelGGL(k_scan_local<LOAD>, dim3(nb), dim3(SCAN_T), 0, st, load, n_in, n_out, out,
                      sums.as<uint64_t>(), side);
   if (split && nb + 1 <= uint64_t(SCAN1_B)) {  // the blocks' offsets, and the total into out[n_in]
-    hipLaunchKernelGGL(k_scan_one<LoadU64>, dim3(1), dim3(SCAN1_T), 0, ctx->stream, LoadU64{sums.as<uint64_t>()}, nb,
+    hipLaunchKernelGGL(k_scan_one<LoadU64>, dim3(1), dim3(SCAN1_T), 0, st, LoadU64{sums.as<uint64_t>()}, nb,
                        nb + 1, offs.as<uint64_t>(), SideSum{}, out + n_in);
     GM_HIP(ctx, hipGetLastError());
     *split = std::move(offs);
     return 0;
   }
   if (nb > 1) {
-    int rc = scan_excl(ctx, LoadU64{sums.as<uint64_t>()}, nb, offs.as<uint64_t>());
+    int rc = scan_excl(ctx, LoadU64{sums.as<uint64_t>()}, nb, offs.as<uint64_t>(), SideSum{}, nullptr, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(SCAN_T), 0, ctx->stream, out, n_out, offs.as<uint64_t>());
+    hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(SCAN_T), 0, st, out, n_out, offs.as<uint64_t>());
   }
   GM_HIP(ctx, hipGetLastError());
   return 0;
@@ -2749,6 +2763,15 @@ bool nt_streams() {
 // Compact staging of the fused main pass (k_match_fused<CMP> + k_assemble_c).
 // GM_STAGE_COMPACT (A/B knob, read per call so tests cover both; default on):
 // used when the index's filter ids fit CMP_SHIFT bits.
+// The assembly stream (MatchCall::submit) for device-buffer calls of at least
+// this many topics; GM_ASM_STREAM (A/B knob, read per call): 0 = never, N =
+// from N topics.  Below it (C1's 1M-topic calls) the extra event and wait
+// packets cost more than the overlap gives.
+uint64_t asm_stream_min() {
+  const char* e = getenv("GM_ASM_STREAM");
+  return e ? strtoull(e, nullptr, 10) : (4ull << 20);
+}
+
 bool stage_compact() {
   const char* e = getenv("GM_STAGE_COMPACT");
   return !e || atoi(e) != 0;
@@ -2994,6 +3017,8 @@ struct MatchCall {
   bool dev_io = false, exact = false, cmp = false, spec = false, split = false, submitted = false;
   bool listed_deferred = false;  // the listed pass is left to finish() (launched only for queued rows)
   bool timed = true;             // the main pass's start / stop events (EMQX_GM_NO_TIMING: none)
+  bool asm_overlap = false;      // scan + speculative assembly on ctx->stream_asm (wanted)
+  bool on_asm = false;           // ... and queued there
   int ctr_slot = -1;             // the pass-counter block of the context's ring, or -1 (counters behind toff)
   const uint8_t* tb = nullptr;
   const uint64_t* to = nullptr;
@@ -3009,7 +3034,10 @@ struct MatchCall {
   MatchCall& operator=(const MatchCall&) = delete;
   ~MatchCall() {
     // (caller holds ctx->mu: the pools are not thread safe)
-    if (submitted) hipStreamSynchronize(ctx->stream);  // an abandoned call: its kernels may still use the buffers
+    if (submitted) {  // an abandoned call: its kernels may still use the buffers
+      hipStreamSynchronize(ctx->stream);
+      if (on_asm) hipStreamSynchronize(ctx->stream_asm);
+    }
     for (hipEvent_t& e : ev)
       if (e) ctx->ev_free.push_back(e);
     if (pin) ctx->pin_free.push_back(pin);
@@ -3047,6 +3075,7 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   exact = flags & EMQX_GM_WITH_EXACT;
   timed = !(flags & EMQX_GM_NO_TIMING);
   n = n_topics;
+  asm_overlap = dev_io && !tail && asm_stream_min() && n >= asm_stream_min();
   const_cast<emqx_gm_index*>(index)->refs.fetch_add(1);  // the snapshot stays alive until finish (RCU)
   idx = index;
   hipStream_t st = ctx->stream;
@@ -3178,6 +3207,24 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
                         cmp ? &cmpb : nullptr, &listed_deferred);
   GM_HIP(ctx, hipGetLastError());
 
+  // Assembly stream: a large device-buffer call's scan and speculative
+  // assembly go to ctx->stream_asm behind its main pass (an event), so the
+  // NEXT call's main pass, queued on the context stream, starts as soon as
+  // this one's ends and overlaps this call's latency-bound assembly and the
+  // walk's tail.  (Its pass counters were zeroed on the context stream; the
+  // assembly then zeroes no ring block for a later call.)
+  hipStream_t sa = st;
+  if (asm_overlap && main_kind() == MAIN_FUSED) {
+    if (!ctx->stream_asm && hipStreamCreateWithFlags(&ctx->stream_asm, hipStreamNonBlocking) != hipSuccess)
+      ctx->stream_asm = nullptr;
+    if (ctx->stream_asm) {
+      if (!timed) GM_HIP(ctx, hipEventRecord(ev[1], st));  // (a timed call's main pass records it itself)
+      GM_HIP(ctx, hipStreamWaitEvent(ctx->stream_asm, ev[1], 0));
+      sa = ctx->stream_asm;
+    }
+  }
+  on_asm = sa != st;
+
   // count -> scan, then ONE host round trip reads the pass counters and the
   // match total together (the slow path below is rare; it re-scans)
   // (tsum: per-tile match counts, written by the main pass and topped up by the listed and slow passes)
@@ -3186,7 +3233,7 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   const char* se = getenv("GM_SCAN_SPLIT");
   split = cmp && (!se || atoi(se) != 0);
   int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p,
-                     SideSum{probe_tile.as<unsigned long long>(), n_tiles, probe_ctr}, split ? &scan_blk : nullptr);
+                     SideSum{probe_tile.as<unsigned long long>(), n_tiles, probe_ctr}, split ? &scan_blk : nullptr, sa);
   if (rc) return rc;
   // Speculative assembly: the rows are written before the host has read the
   // match total, into an ids buffer sized from this context's recent matches
@@ -3208,7 +3255,7 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
                          hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_dev), pin, 0) == hipSuccess && pin_dev;
   // (compact staging: the assembly also zeroes the ring's next block for the next call, if it is dirty)
   uint32_t* zero_next = nullptr;
-  if (spec && cmp && ctr_slot >= 0) {
+  if (spec && cmp && ctr_slot >= 0 && !on_asm) {
     const int z = (ctr_slot + 1) % emqx_gm_ctx::CTR_RING;
     if (ctx->ctr_state[z] == 2) {
       zero_next = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->ctr_ring) + 64 * z);
@@ -3216,7 +3263,7 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
     }
   }
   if (spec) {
-    launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
+    launch_assemble(sa, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
                     row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec, scan_blk.as<uint64_t>(),
                     rb_kernel ? pin_dev : nullptr, reinterpret_cast<const uint32_t*>(ctrs_p),
                     rb_kernel ? ev[2] : nullptr, zero_next);
@@ -3227,8 +3274,8 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
     }
   }
   if (!rb_kernel) {
-    if (int rc2 = readback(st)) return rc2;
-    GM_HIP(ctx, hipEventRecord(ev[2], st));
+    if (int rc2 = readback(sa)) return rc2;
+    GM_HIP(ctx, hipEventRecord(ev[2], sa));
   }
   return 0;
 }

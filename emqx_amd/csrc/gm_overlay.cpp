@@ -498,6 +498,7 @@ uint64_t filter_rank(const emqx_gm_index* idx, const uint8_t* f, uint64_t len, b
 int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>& tomb,
                  const std::set<std::string>& dset, emqx_gm_index** out, std::vector<uint32_t>* rmap_out,
                  bool trie_only) {
+  if (const int rc = load_mirror_blob(ctx, prev)) return rc;  // (a lazy mirror: the first update loads it)
   Mirror& M = *prev->mirror;
   const uint64_t nb = prev->info.n_filters, K = dset.size();
   if (nb + K >= HF_NONE) return 1;  // temporary ids must stay below HF_NONE: the rebuild reports it

@@ -166,6 +166,24 @@ class Index:
     def filters(self) -> List[bytes]:
         return [self.filter(i) for i in range(self.n_filters)]
 
+    def export(self, with_blob: bool = True, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """The snapshot as a host image (emqx_gm_index_export): the host tables
+        and, with ``with_blob``, the device tables.  ``out`` (uint8, e.g. a
+        shared-memory map) receives it when given and large enough."""
+        flags = 0 if with_blob else _lib.IMAGE_NO_BLOB
+        n = C.c_uint64()
+        check(lib().emqx_gm_index_export(self.ctx.h, self.h, flags, None, C.byref(n)), self.ctx.h, "index_export")
+        buf = out if out is not None and out.nbytes >= n.value else np.empty(n.value, np.uint8)
+        check(lib().emqx_gm_index_export(self.ctx.h, self.h, flags, _ptr(buf), C.byref(n)), self.ctx.h,
+              "index_export")
+        return buf[:n.value]
+
+    def device_blob(self) -> Tuple[int, int]:
+        """(device pointer, bytes) of the snapshot's device tables (emqx_gm_index_device_blob)."""
+        p, n = C.c_void_p(), C.c_uint64()
+        check(lib().emqx_gm_index_device_blob(self.h, C.byref(p), C.byref(n)), None, "index_device_blob")
+        return p.value, int(n.value)
+
     def release(self):
         if self.h:
             lib().emqx_gm_index_release(self.h)
@@ -181,9 +199,13 @@ class Index:
 class Context:
     """One process per GPU: a context binds one HIP device and one stream."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, mirror: Optional[str] = None):
+        """``mirror``: None (library default: the host copy of a plain index's
+        tables is kept from the build up to 2 GiB, loaded on the first update
+        above), "eager" or "lazy" (EMQX_GM_OPEN_MIRROR_*)."""
         o = Opts()
         o.device = device
+        o.flags = {None: 0, "eager": _lib.OPEN_MIRROR_EAGER, "lazy": _lib.OPEN_MIRROR_LAZY}[mirror]
         h = C.c_void_p()
         rc = lib().emqx_gm_open(C.byref(o), C.byref(h))
         if rc != _lib.OK:
@@ -225,6 +247,15 @@ class Context:
         check(lib().emqx_gm_index_build(self.h, _ptr(fb), _ptr(fo), n, _ptr(so), _ptr(si), _ptr(perm),
                                         C.byref(h)), self.h, "index_build")
         return Index(self, h, perm[:n])
+
+    def import_index(self, image: np.ndarray, d_blob: Optional[int] = None) -> Index:
+        """A snapshot from an image (emqx_gm_index_import); its device tables from
+        the image or, with ``d_blob``, copied from that device pointer."""
+        img = np.ascontiguousarray(image, np.uint8)
+        h = C.c_void_p()
+        check(lib().emqx_gm_index_import(self.h, _ptr(img), img.nbytes, C.c_void_p(d_blob) if d_blob else None,
+                                         C.byref(h)), self.h, "index_import")
+        return Index(self, h, np.zeros(0, np.uint32))
 
     def build_index_shard(self, filters, global_ids: np.ndarray, subs=None) -> Index:
         """An index over one shard whose rows carry ``global_ids`` (emqx_gm_index_build_shard)."""
@@ -351,6 +382,16 @@ class Context:
     def csr_row_lengths(self, res: DeviceCsr, d_out: int):
         """Row lengths (u32) of a device CSR into device memory at ``d_out``."""
         check(lib().emqx_gm_csr_row_lengths(self.h, C.byref(res.csr), C.c_void_p(d_out)), self.h, "csr_row_lengths")
+
+    def offsets_lengths(self, d_off: int, n: int, d_out: int):
+        """Lengths (u32) of n device segments given by u64 offsets d_off[0..n] into
+        ``d_out`` (emqx_gm_csr_row_lengths over a CSR whose row offsets are d_off)."""
+        if not n:
+            return
+        c = Csr()
+        c.n_rows, c.nnz, c.on_device = n, 0, 1
+        c.row_off = C.cast(C.c_void_p(d_off), C.POINTER(C.c_uint64))
+        check(lib().emqx_gm_csr_row_lengths(self.h, C.byref(c), C.c_void_p(d_out)), self.h, "csr_row_lengths")
 
     def merge_rows(self, n_rows: int, stride: int, pieces: int, d_lens: int, d_ids: int) -> DeviceCsr:
         """Merge per-shard rows by global id (emqx_gm_merge_rows); result stays on the device."""

@@ -78,15 +78,44 @@ def _ptr(p) -> int:
     return C.cast(p, C.c_void_p).value or 0
 
 
+def _own_stream(ctx):
+    """A torch stream the library is switched to (emqx_gm_set_stream): the
+    library's kernels, torch's tensor ops and the collectives then share one
+    ordered stream.  torch's DEFAULT stream cannot serve: its handle is NULL,
+    which the library reads as "keep your own (non-blocking) stream", and
+    nothing would order the two."""
+    import torch
+    s = torch.cuda.Stream(device=torch.device("cuda", ctx.device))
+    ctx.set_stream(s.cuda_stream)
+    return s
+
+
+class _on:
+    """``with torch.cuda.stream(s)`` for a stream that may be None (host path)."""
+
+    def __init__(self, stream):
+        self.stream, self.cm = stream, None
+
+    def __enter__(self):
+        if self.stream is not None:
+            import torch
+            self.cm = torch.cuda.stream(self.stream)
+            self.cm.__enter__()
+
+    def __exit__(self, *a):
+        if self.cm is not None:
+            self.cm.__exit__(*a)
+
+
 class ShardedMatcher:
     """match_routes over a filter set sharded across ranks (one process per GPU).
 
     ``device_tensors`` True exchanges device buffers (RCCL, backend "nccl");
     False stages them through host memory (backend "gloo", e.g. several ranks
-    sharing one device in tests).  On the device path the library runs on
-    torch's current stream (emqx_gm_set_stream), so its kernels, torch's
-    tensor ops and the collectives are ordered by one stream: no cross-stream
-    race, no device-wide synchronisation between the steps.
+    sharing one device in tests).  On the device path the library and torch
+    run on the matcher's own stream (emqx_gm_set_stream), so its kernels,
+    torch's tensor ops and the collectives are ordered by one stream: no
+    cross-stream race, no device-wide synchronisation between the steps.
     """
 
     def __init__(self, ctx: Context, index: Index, world: int, rank: int, dist=None, group=None,
@@ -94,12 +123,14 @@ class ShardedMatcher:
         self.ctx, self.index, self.world, self.rank = ctx, index, world, rank
         self.dist, self.group, self.device_tensors = dist, group, device_tensors
         self.last_exchange_bytes = 0
-        if device_tensors and world > 1:
-            import torch
-            ctx.set_stream(torch.cuda.current_stream(torch.device("cuda", ctx.device)).cuda_stream)
+        self.stream = _own_stream(ctx) if device_tensors else None
 
     def match_device(self, d_tb: int, d_to: int, n: int, exact: bool = True) -> Tuple[DeviceCsr, int, int]:
         """Rows of this rank's topic slice; returns (csr, first_row, n_rows)."""
+        with _on(self.stream):
+            return self._match_device(d_tb, d_to, n, exact)
+
+    def _match_device(self, d_tb: int, d_to: int, n: int, exact: bool) -> Tuple[DeviceCsr, int, int]:
         ctx = self.ctx
         res = ctx.match_device(self.index, d_tb, d_to, n, exact)
         if self.world == 1:
@@ -181,9 +212,8 @@ class PrefixShardedMatcher:
         self.dist, self.group, self.device_tensors, self.match_fn = dist, group, device_tensors, match_fn
         self.last_exchange_bytes = 0
         self.last_topics_walked = 0
-        if device_tensors and ctx is not None and world > 1:
-            import torch
-            ctx.set_stream(torch.cuda.current_stream(torch.device("cuda", ctx.device)).cuda_stream)
+        # also at world 1: torch's sort / bincount read what the library's kernels write
+        self.stream = _own_stream(ctx) if device_tensors and ctx is not None else None
 
     def _a2a(self, out, inp, out_splits=None, in_splits=None):
         if self.world == 1:
@@ -247,55 +277,64 @@ class PrefixShardedMatcher:
 
     def match_device(self, d_tb: int, d_to: int, n: int, exact: bool = True) -> DeviceCsr:
         """The exchange on device tensors: rows of this rank's batch (device
-        topics d_tb / d_to, n of them), in batch order, as a DeviceCsr."""
+        topics d_tb / d_to, n of them), in batch order, as a DeviceCsr.
+
+        Host round trips per step: ONE device-to-host copy of the outbound
+        split sizes (topics and bytes per peer, both directions: the byte total
+        is their sum), the match's own read-back (its match total), and ONE
+        copy of the return split sizes (ids per peer, both directions).  The
+        library and torch's ops run on the matcher's own stream (set in
+        __init__), so route, sort, permute, the collectives and the walk are
+        ordered by one stream."""
+        with _on(self.stream):
+            return self._match_device(d_tb, d_to, n, exact)
+
+    def _match_device(self, d_tb: int, d_to: int, n: int, exact: bool) -> DeviceCsr:
         import torch
         ctx, W = self.ctx, self.world
         dev = torch.device("cuda", ctx.device)
         dest = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
         ctx.route_topics(self.route, d_tb, d_to, n, dest.data_ptr())
-        perm64 = torch.sort(dest, stable=True).indices
-        perm = perm64.to(torch.int32)
-        counts = torch.bincount(dest, minlength=W).to(torch.int64)
-        tot = np.zeros(1, np.uint64)
-        ctx.memcpy_d2h(tot, d_to + 8 * n, 8)
-        pbytes = torch.empty(int(tot[0]) + 64, dtype=torch.uint8, device=dev)
-        poff = torch.empty(n + 1, dtype=torch.int64, device=dev)
-        ctx.permute_topics(d_tb, d_to, n, perm.data_ptr(), pbytes.data_ptr(), poff.data_ptr())
-        bounds = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), counts.cumsum(0)])
-        bsplit_t = poff[bounds[1:]] - poff[bounds[:-1]]
-        sizes = torch.stack([counts, bsplit_t], 1).reshape(-1)
+        tlen = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+        ctx.offsets_lengths(d_to, n, tlen.data_ptr())
+        perm = torch.sort(dest, stable=True).indices.to(torch.int32)
+        d64 = dest.to(torch.int64)
+        counts = torch.bincount(d64, minlength=W)
+        bsplit = torch.zeros(W, dtype=torch.int64, device=dev).index_add_(0, d64, tlen.to(torch.int64))
+        sizes = torch.stack([counts, bsplit], 1).reshape(-1)
         rsizes = torch.empty_like(sizes)
         self._a2a(rsizes, sizes)
-        both = torch.cat([sizes, rsizes]).cpu().tolist()  # one D2H for the split sizes of the step
+        both = torch.cat([sizes, rsizes]).cpu().tolist()  # D2H 1: the outbound split sizes
         cs, bs = both[0:2 * W:2], both[1:2 * W:2]
         rc, rb = both[2 * W::2], both[2 * W + 1::2]
+        tot, m = sum(bs), sum(rc)
+        pbytes = torch.empty(tot + 64, dtype=torch.uint8, device=dev)
+        poff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        ctx.permute_topics(d_tb, d_to, n, perm.data_ptr(), pbytes.data_ptr(), poff.data_ptr())
         rbytes = torch.empty(sum(rb) + 64, dtype=torch.uint8, device=dev)
-        self._a2a(rbytes[:sum(rb)], pbytes[:int(tot[0])], rb, bs)
+        self._a2a(rbytes[:sum(rb)], pbytes[:tot], rb, bs)
         rbytes[sum(rb):].zero_()
-        plens = (poff[1:] - poff[:-1]).to(torch.int32)
-        rlens = torch.empty(sum(rc), dtype=torch.int32, device=dev)
-        self._a2a(rlens, plens, rc, cs)
-        m = sum(rc)
+        rlens = torch.empty(m, dtype=torch.int32, device=dev)
+        self._a2a(rlens, tlen[perm.to(torch.int64)], rc, cs)
         roff = torch.zeros(m + 1, dtype=torch.int64, device=dev)
         roff[1:] = rlens.to(torch.int64).cumsum(0)
-        res = ctx.match_device(self.index, rbytes.data_ptr(), roff.data_ptr(), m, exact)
+        res = ctx.match_device(self.index, rbytes.data_ptr(), roff.data_ptr(), m, exact)  # read-back: nnz
         self.last_topics_walked = m
+        nnz = res.nnz
         rowlen = torch.empty(max(m, 1), dtype=torch.int32, device=dev)[:m]
         ctx.csr_row_lengths(res, rowlen.data_ptr())
-        nnz = res.nnz
         ids = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
         ctx.memcpy_d2d(ids.data_ptr(), _ptr(res.csr.ids), nnz * 4)
         res.free()
-        rcb = torch.tensor([0] + rc, device=dev).cumsum(0)
-        csum = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), rowlen.to(torch.int64).cumsum(0)])
-        idsplit_t = csum[rcb[1:]] - csum[rcb[:-1]]
+        src = torch.repeat_interleave(torch.arange(W, device=dev), torch.tensor(rc, device=dev), output_size=m)
+        idsplit_t = torch.zeros(W, dtype=torch.int64, device=dev).index_add_(0, src, rowlen.to(torch.int64))
         rbsz = torch.empty_like(idsplit_t)
         self._a2a(rbsz, idsplit_t)
-        both = torch.cat([idsplit_t, rbsz]).cpu().tolist()
+        both = torch.cat([idsplit_t, rbsz]).cpu().tolist()  # D2H 2: the return split sizes
         idsplit, backsplit = both[:W], both[W:]
         back_lens = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
         self._a2a(back_lens, rowlen, cs, rc)
         back_ids = torch.empty(max(sum(backsplit), 1), dtype=torch.int32, device=dev)
         self._a2a(back_ids[:sum(backsplit)], ids, backsplit, idsplit)
-        self.last_exchange_bytes = int(tot[0]) + 4 * n + 4 * m + 4 * nnz
+        self.last_exchange_bytes = tot + 4 * n + 4 * m + 4 * nnz
         return ctx.unpermute_rows(n, perm.data_ptr(), back_lens.data_ptr(), back_ids.untyped_storage().data_ptr())

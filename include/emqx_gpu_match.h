@@ -84,9 +84,17 @@ typedef struct emqx_gm_call emqx_gm_call;
 
 typedef struct {
   int32_t device;        /* HIP device ordinal; one process per GPU            */
-  uint32_t reserved0;
+  uint32_t flags;        /* EMQX_GM_OPEN_* (0: defaults)                        */
   uint64_t reserved[7];
 } emqx_gm_opts;
+
+/* emqx_gm_opts.flags: the host copy of a plain index's device tables that an
+ * in-place emqx_gm_index_update patches (host RAM ~ the tables' size).  By
+ * default it is kept from the build for tables up to 2 GiB and downloaded from
+ * the device on a snapshot line's first update above that (a 100M-filter index
+ * holds no 38 GB host copy unless it is updated). */
+#define EMQX_GM_OPEN_MIRROR_EAGER 0x1u /* always keep it from the build            */
+#define EMQX_GM_OPEN_MIRROR_LAZY  0x2u /* never at build: on the first update      */
 
 /* CSR result: row i = ids[row_off[i] .. row_off[i+1]) */
 typedef struct {
@@ -186,6 +194,27 @@ int emqx_gm_index_update(emqx_gm_ctx *ctx, emqx_gm_index *prev, const uint8_t *f
 int emqx_gm_index_update_subs(emqx_gm_ctx *ctx, emqx_gm_index *prev, const uint8_t *filter_bytes,
                               const uint64_t *filter_off, const uint32_t *sub_ids, const uint8_t *ops,
                               uint64_t n_ops, emqx_gm_index **out);
+/* Index images: one snapshot compiled once and replicated (the reference's
+ * routing tables are ONE copy that mria replicates to every node, not a
+ * per-node recomputation: apps/emqx/src/emqx_router.erl:75-84, 136).
+ * export: the snapshot as a self-contained host image -- the host tables
+ * (layout, sorted filter table, shard ids, subscriber offsets, route marks)
+ * and, unless EMQX_GM_IMAGE_NO_BLOB, the device tables; two-call sizing (buf
+ * NULL sets *size).  device_blob: the device tables of a snapshot (read-only;
+ * e.g. the source of an RCCL broadcast to the other GPUs).  import: a new
+ * snapshot on ctx's device from an image, its device tables from the image or,
+ * when d_blob is not NULL, copied from d_blob (device memory of ctx's device,
+ * device_blob's bytes).  An imported plain index keeps its in-place update
+ * line: its host mirror loads on the first update.  Overlay snapshots and
+ * emqx_gm_index_update_subs results: EMQX_GM_EUNSUPPORTED (export a rebuilt
+ * or emqx_gm_index_update'd snapshot).  An image is accepted only by a library
+ * of the same table layout (EMQX_GM_EINVAL otherwise). */
+#define EMQX_GM_IMAGE_NO_BLOB 0x1u
+int emqx_gm_index_export(emqx_gm_ctx *ctx, const emqx_gm_index *idx, uint32_t flags, uint8_t *buf,
+                         uint64_t *size);
+int emqx_gm_index_device_blob(const emqx_gm_index *idx, const void **d_blob, uint64_t *bytes);
+int emqx_gm_index_import(emqx_gm_ctx *ctx, const uint8_t *image, uint64_t size, const void *d_blob,
+                         emqx_gm_index **out);
 int emqx_gm_index_retain(emqx_gm_index *idx);
 int emqx_gm_index_release(emqx_gm_index *idx);
 int emqx_gm_index_info(const emqx_gm_index *idx, emqx_gm_index_info_t *info);

@@ -66,6 +66,7 @@ def main():
     recs = [_RecordExchange() for _ in range(W)]
     for q in range(W):
         res, _, _ = ShardedMatcher(ctx, idxs[q], W, q, dist=recs[q], device_tensors=True).match_device(d_tb, d_to, n)
+        torch.cuda.synchronize()  # the recorded sends were written on that matcher's stream
         res.free()
     out, first, rows = ShardedMatcher(ctx, idxs[0], W, 0, dist=_ReplayExchange(recs, 0),
                                       device_tensors=True).match_device(d_tb, d_to, n)

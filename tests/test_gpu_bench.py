@@ -37,6 +37,7 @@ def test_bench_two_ranks_c2():
     one = _run_ranks(["--filters", "20000", "--topics", "1000000"], world=1)
     two = _run_ranks(["--filters", "20000", "--topics", "1000000"], world=2)
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["detail"]["ranks_compiled"] == 1 and two["detail"]["replicas_agree"] is True
     # weak scaling: each rank matches its own slice, same per-rank work
     assert two["config"]["topics_per_gpu"] == one["config"]["topics_per_gpu"] == 1_000_000
     assert two["value"] > 0 and two["roofline"]["frac"] > 0
@@ -62,6 +63,10 @@ def test_bench_two_ranks_c5_replicated():
     assert out["n_gpus"] == 2 and out["scaling"] == "weak"
     assert out["config"]["topics_per_gpu"] == 200_000 and "replicated" in out["config"]["workload"]
     assert out["parity_sample"]["ok"]
+    # the index is compiled ONCE (rank 0) and the other rank imports its image
+    d = out["detail"]
+    assert d["index_source"] == "built" and d["ranks_compiled"] == 1, d
+    assert d["replicas_agree"] is True and d["host_peak_rss_gb_max"] > 0
 
 
 @pytest.mark.gpu
@@ -80,3 +85,22 @@ def test_bench_two_ranks_c5_prefix():
 def test_bench_two_ranks_c4():
     out = _run_ranks(["--config", "c4"], world=2)
     assert out["n_gpus"] == 2 and out["config"]["pairs"] == 10**9
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_c5_prefix_one_gpu_device_path():
+    """bench.py --config c5 --plan prefix --gpus 1 on its default (nccl) path:
+    PrefixShardedMatcher on device tensors, the exchange's copy path at world 1,
+    and the oracle parity sample over rank 0's rows."""
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    env.pop("GM_BENCH_BACKEND", None)
+    env.pop("GM_BENCH_DEVICE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "c5", "--plan", "prefix", "--gpus", "1",
+           "--filters", "4000000", "--topics", "2000000", "--steps", "3", "--warmup", "1", "--no-cpu"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=380)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith('{"metric"')][-1])
+    assert out["detail"]["device_exchange"] is True
+    assert out["detail"]["topics_walked_per_rank"] == [2_000_000]
+    assert out["parity_sample"]["ok"], out["parity_sample"]

@@ -753,12 +753,16 @@ def test_concurrent_calls_one_context(ctx, orc):
     plain.release()
 
 
-def test_submit_wait_pipelined_vs_oracle(ctx, orc):
+@pytest.mark.parametrize("asm_stream", [None, "1"])
+def test_submit_wait_pipelined_vs_oracle(ctx, orc, monkeypatch, asm_stream):
     """emqx_gm_match_submit / _wait: four batches of different sizes (one with
     listed- and slow-path rows, one empty) in flight at once on one context,
     waited for out of order; every result equals its own single emqx_gm_match
     and the oracle; the index may be released while calls are in flight (a call
-    retains its snapshot)."""
+    retains its snapshot).  GM_ASM_STREAM=1: every device-buffer call's scan
+    and assembly on the assembly stream, overlapping the next call's walk."""
+    if asm_stream:
+        monkeypatch.setenv("GM_ASM_STREAM", asm_stream)
     from emqx_amd.engine import pack
     lv = ["a", "b", "c", "d", "e", "f"]
     heavy = set()
@@ -938,11 +942,16 @@ def test_untimed_submits_same_rows(ctx, orc):
     idx.release()
 
 
-def test_many_calls_in_flight_counter_ring(ctx, orc):
+@pytest.mark.parametrize("asm_stream", [None, "1"])
+def test_many_calls_in_flight_counter_ring(ctx, orc, monkeypatch, asm_stream):
     """More calls in flight than the context's ring of pre-zeroed pass-counter
     blocks (16): the calls past it take counters behind their own workspace;
     every call's rows equal a lone call's, also for a batch whose rows go
-    through the listed pass (its counters are read after the ring moved on)."""
+    through the listed pass (its counters are read after the ring moved on).
+    GM_ASM_STREAM=1: the assemblies on their own stream (no ring block is then
+    zeroed by an assembly), mixed with host-buffer calls on the context stream."""
+    if asm_stream:
+        monkeypatch.setenv("GM_ASM_STREAM", asm_stream)
     from emqx_amd.engine import gen_filter_codes, render_codes
     codes = gen_filter_codes(4, 10_000)
     filters = sorted(set(orc.unpack(*render_codes(codes))) | {("/".join(["d"] + ["x"] * 9)).encode()})

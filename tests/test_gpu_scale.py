@@ -342,3 +342,80 @@ def test_c5_100m_d_unsharded_equals_fixture_and_merged(ctx):
         idx.release()
         c2.close()
         _C5.clear()
+
+
+# ---------------------------------------------------------------------------
+# C4 at its stated size: 1k hot topics x 1M subscribers = 10^9 deliveries
+# ---------------------------------------------------------------------------
+def _c4_index(ctx):
+    """bench.py's C4 index: hot/# -> 0..599,999; hot/+/x/# -> 600,000..999,899;
+    each hot/K/x/y/z -> 999,900..999,999."""
+    K, S = 1000, 1_000_000
+    filters = [b"hot/#", b"hot/+/x/#"] + [b"hot/%d/x/y/z" % k for k in range(K)]
+    lists = [np.arange(0, 600_000), np.arange(600_000, 999_900)] + [np.arange(999_900, S)] * K
+    so = np.zeros(len(lists) + 1, np.uint64)
+    so[1:] = np.cumsum([len(x) for x in lists])
+    si = np.concatenate(lists).astype(np.uint32)
+    return ctx.build_index(filters, subs=(so, si)), [b"hot/%d/x/y/z" % k for k in range(K)]
+
+
+def _check_deliveries(ctx, d_ids, first, count, chunk=50_000_000):
+    """Deliveries [first, first+count) of the C4 fan-out, device buffer d_ids,
+    against the analytic expectation, in host chunks.  Every row's matched
+    filters in id order are hot/#, hot/+/x/#, hot/K/x/y/z (Erlang binary order:
+    '#' < '+' < digits), so its segments concatenate to 0..999,999: delivery g
+    is g mod 10^6 (emqx_broker.erl:506-530 dispatches each filter's
+    subscribers in turn; the rows are multisets in that order)."""
+    S = 1_000_000
+    tile = np.tile(np.arange(S, dtype=np.uint32), chunk // S + 2)
+    buf = np.zeros(chunk, np.uint32)
+    done = 0
+    while done < count:
+        L = min(chunk, count - done)
+        ctx.memcpy_d2h(buf, d_ids + 4 * done, 4 * L)
+        g0 = (first + done) % S
+        if not np.array_equal(buf[:L], tile[g0:g0 + L]):
+            bad = int(np.nonzero(buf[:L] != tile[g0:g0 + L])[0][0])
+            pytest.fail(f"delivery {first + done + bad}: {int(buf[bad])} != {int(tile[g0 + bad])}")
+        done += L
+    return done
+
+
+@pytest.mark.timeout(600)
+def test_c4_full_fanout_every_delivery(ctx):
+    """the whole 10^9-entry C4 fan-out (emqx_gm_fanout, device CSR)
+    checked entry by entry, its row offsets exactly k * 10^6, and the 8-way
+    delivery-range split (emqx_gm_fanout_part, the multi-GPU C4 path) checked
+    part by part against the same expectation."""
+    idx, topics = _c4_index(ctx)
+    from emqx_amd.engine import pack
+    tb, to = pack(topics)
+    d_tb, d_to = ctx.dev_alloc(len(tb)), ctx.dev_alloc(len(to) * 8)
+    ctx.memcpy_h2d(d_tb, tb, len(tb))
+    ctx.memcpy_h2d(d_to, to, len(to) * 8)
+    m = ctx.match_device(idx, d_tb, d_to, len(topics), exact=True)
+    mro, mids = m.to_host()
+    assert np.array_equal(mro, np.arange(0, 3001, 3, dtype=np.uint64))
+    assert [idx.filter(int(i)) for i in mids[:3]] == [b"hot/#", b"hot/+/x/#", b"hot/0/x/y/z"]
+    fan = ctx.fanout_device(idx, m)
+    assert fan.nnz == 10**9
+    ro = np.zeros(1001, np.uint64)
+    ctx.memcpy_d2h(ro, ctypes.cast(fan.csr.row_off, ctypes.c_void_p).value, 1001 * 8)
+    assert np.array_equal(ro, np.arange(0, 10**9 + 1, 10**6, dtype=np.uint64))
+    _log("C4 whole fan-out: checking 10^9 deliveries")
+    assert _check_deliveries(ctx, ctypes.cast(fan.csr.ids, ctypes.c_void_p).value, 0, 10**9) == 10**9
+    fan.free()
+    total = 0
+    for p in range(8):
+        part, first = ctx.fanout_part(idx, m, p, 8)
+        assert first == total and part.nnz == 10**9 * (p + 1) // 8 - 10**9 * p // 8
+        pro = np.zeros(1001, np.uint64)
+        ctx.memcpy_d2h(pro, ctypes.cast(part.csr.row_off, ctypes.c_void_p).value, 1001 * 8)
+        assert np.array_equal(pro, ro)  # global delivery offsets
+        total += _check_deliveries(ctx, ctypes.cast(part.csr.ids, ctypes.c_void_p).value, first, part.nnz)
+        part.free()
+    assert total == 10**9
+    m.free()
+    idx.release()
+    ctx.dev_free(d_tb)
+    ctx.dev_free(d_to)

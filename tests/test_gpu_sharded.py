@@ -269,3 +269,33 @@ def test_prefix_shards_each_walk_their_routed_topics(ctx, orc):
         ctx.dev_free(p)
     idx.release()
     route.release()
+
+
+def _run_worker(script, *args, timeout=560):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-u", os.path.join(root, "tests", script)] + [str(a) for a in args],
+                       cwd=root, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    return p.stdout
+
+
+@pytest.mark.timeout(300)
+def test_prefix_device_path_world1():
+    """PrefixShardedMatcher.match_device at world 1 (the nccl bench's 1-GPU
+    path): the library on the matcher's own stream, route -> torch.sort /
+    bincount -> permute -> walk -> unpermute, rows == the unsharded index and
+    the oracle (tests/_prefix_device_worker.py)."""
+    assert "PREFIX_DEVICE_PATH_OK world=1" in _run_worker("_prefix_device_worker.py", 1, 200_000, 300_000)
+
+
+@pytest.mark.timeout(600)
+def test_prefix_device_path_world8_lockstep():
+    """The 4M-filter set in 8 prefix shards, 8 ranks as threads on one device,
+    each with its own context, stream and 500k-topic batch; the six
+    all_to_all_single calls of a step run in lock step across the ranks.  Every
+    rank's rows == the unsharded index on its batch; rank 0's window == the
+    oracle; no rank walks twice its share."""
+    out = _run_worker("_prefix_device_worker.py", 8, 4_000_000, 500_000)
+    assert "PREFIX_DEVICE_PATH_OK world=8" in out
