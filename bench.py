@@ -55,7 +55,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-parity", action="store_true", help="skip the oracle check of the last step's sample")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--traffic-json", default=None,
+                   help="PMC traffic of this build (scripts/traffic.py); default profiles/traffic.json for C2, "
+                        "profiles/traffic_<config>.json for the others")
     p.add_argument("--no-update", action="store_true", help="skip the incremental-update detail")
     p.add_argument("--time-every", type=int, default=None,
                    help="time the main pass (HIP events) on every N-th call of the timed region "
@@ -65,10 +67,16 @@ def parse():
     p.add_argument("--build-each", action="store_true",
                    help="replicated configs at N>1: every rank compiles the index itself (the default: rank 0 "
                         "compiles it once and the others import its image, the device tables broadcast over RCCL)")
+    p.add_argument("--index-cache", default=None,
+                   help="replicated configs: an index image file (emqx_gm_index_export); imported when it exists, "
+                        "written after the build otherwise (profiling passes of C3/C5 skip the host build)")
     p.add_argument("--no-host-io", action="store_true",
                    help="skip the host-buffer call (PCIe-inclusive rate, reported in detail, never `value`)")
     a = p.parse_args()
     a.no_pipeline = a.no_pipeline or bool(os.environ.get("GM_BENCH_NO_PIPELINE"))  # (A/B scripts set env knobs)
+    if a.traffic_json is None:
+        a.traffic_json = os.path.join(ROOT, "profiles", "traffic.json" if a.config == "c2" else
+                                      f"traffic_{a.config}.json")
     if a.steps is None:
         a.steps = 200 if a.config == "c1" else 5
     if a.warmup is None:
@@ -339,6 +347,16 @@ def replicated_index(a, ctx, world, rank, local, pg, fpack):
     device tensors -- the tables GPU to GPU over xGMI, never through the host;
     over gloo (rehearsals) the whole image goes as one host tensor.  Returns
     (index, "built" | "imported")."""
+    if a.index_cache and world == 1:
+        import numpy as np
+        if os.path.exists(a.index_cache):
+            return ctx.import_index(np.memmap(a.index_cache, np.uint8, "r")), "imported (cache)"
+        idx = ctx.build_index(fpack)
+        img = np.memmap(a.index_cache, np.uint8, "w+", shape=(idx.export_size(),))
+        idx.export(out=img)
+        img.flush()
+        del img
+        return idx, "built"
     if world == 1 or a.build_each:
         return ctx.build_index(fpack), "built"
     import numpy as np

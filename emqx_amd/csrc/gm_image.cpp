@@ -33,8 +33,8 @@ namespace gm {
 namespace {
 
 constexpr char kMagic[8] = {'E', 'M', 'Q', 'X', 'G', 'M', 'I', '1'};
-constexpr uint32_t kVersion = 1;
-constexpr int kPtrs = 10;  // the view's device pointers, in ptr_fields() order
+constexpr uint32_t kVersion = 2;
+constexpr int kPtrs = 11;  // the view's device pointers, in ptr_fields() order
 
 uint64_t layout_signature() {
   uint64_t h = 0x9E3779B97F4A7C15ull;
@@ -51,7 +51,8 @@ template <class V> auto ptr_fields(V& v) {
       reinterpret_cast<const void**>(&v.edges),   reinterpret_cast<const void**>(&v.hot),
       reinterpret_cast<const void**>(&v.arena),   reinterpret_cast<const void**>(&v.sub_off),
       reinterpret_cast<const void**>(&v.sub_ids), reinterpret_cast<const void**>(&v.gmap),
-      reinterpret_cast<const void**>(&v.efilt),   reinterpret_cast<const void**>(&v.mph_word)};
+      reinterpret_cast<const void**>(&v.efilt),   reinterpret_cast<const void**>(&v.mph_word),
+      reinterpret_cast<const void**>(&v.d0_root)};
 }
 
 struct MirrorMeta {  // gm::Mirror without its blob (an imported index loads it lazily)

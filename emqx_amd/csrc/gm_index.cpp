@@ -809,7 +809,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   size_t o_gmap = o_flen + al(flen_cap * 2 + 2);
   size_t o_efilt = o_gmap + al(idx->gmap.size() * 4 + 4);
   size_t o_mph = o_efilt + al(efilt.size() * 4 + 4);
-  size_t o_soff = o_mph + al(mph_word.size() * 8);
+  size_t o_d0 = o_mph + al(mph_word.size() * 8);
+  size_t o_soff = o_d0 + al(16);
   // (a plain index's offsets stay zero past nf: appended filters have no subscribers)
   size_t o_sids = o_soff + al((keep_mirror && !sub_off ? flen_cap + 1 : soff.size()) * 8);
   size_t total = o_sids + al(sids.size() * 4 + 4);
@@ -846,6 +847,10 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   };
   put(o_nodes, dnodes.data(), NN * sizeof(Node));
   put(o_dict, dict.data(), dcap * sizeof(DictSlot));
+  {
+    const uint32_t d0[4] = {NONE, 0, HF_NONE, NONE};
+    put(o_d0, d0, sizeof d0);
+  }
   put(o_edges, dedges.data(), dedges.size() * sizeof(EdgeSlot));
   put(o_hot, hot.data(), hot.size() * sizeof(HotSlot));
   put(o_arena, arena.data(), arena.size());
@@ -902,6 +907,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   IndexView& v = idx->view;
   v.nodes = reinterpret_cast<const Node*>(B + o_nodes);
   v.dict = reinterpret_cast<const DictSlot*>(B + o_dict);
+  v.d0_root = reinterpret_cast<const uint32_t*>(B + o_d0);
   v.edges = reinterpret_cast<const EdgeSlot*>(B + o_edges);
   v.hot = reinterpret_cast<const HotSlot*>(B + o_hot);
   v.arena = B + o_arena;
@@ -943,6 +949,16 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.plus_word = plus_word;
   v.hash_word = hash_word;
   idx->dev_flen = reinterpret_cast<uint16_t*>(B + o_flen);
+  // the root's '+' record, from the depth-1 hot table on the device
+  // (gm_match.hip); IX_D0 once it is written
+  if (!host_mirror) {
+    const int rc = refresh_d0(ctx, v, static_cast<uint8_t*>(idx->dev_base) + o_d0);
+    if (rc < 0) {
+      free_index(idx);
+      return rc;
+    }
+    if (rc == 0) v.flags |= IX_D0;
+  }
 
   if (sub_off) idx->soff = std::move(soff);
   emqx_gm_index_info_t& in = idx->info;
@@ -958,6 +974,10 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   *out = idx;
   return EMQX_GM_OK;
 }
+
+// (the device build defines it in gm_match.hip; the host-only ASAN build of
+// this file links this stand-in, which reports "not written")
+__attribute__((weak)) int refresh_d0(emqx_gm_ctx*, const IndexView&, void*) { return 1; }
 
 void free_index(emqx_gm_index* idx) {
   if (!idx) return;

@@ -300,6 +300,11 @@ bool well_formed_filter(const uint8_t* p, uint64_t len);
 int index_export(emqx_gm_ctx* ctx, const emqx_gm_index* idx, uint32_t flags, uint8_t* buf, uint64_t* size);
 int index_import(emqx_gm_ctx* ctx, const uint8_t* img, uint64_t size, const void* d_blob, emqx_gm_index** out);
 int load_mirror_blob(emqx_gm_ctx* ctx, emqx_gm_index* idx);
+// gm_match.hip: write the root's '+' record (IndexView::d0_root) from view v's
+// depth-1 hot table on the device; d0 is the region's device address (v's own
+// pointer is const).  0: written (the caller sets IX_D0), 1: not wanted
+// (GM_D0=0), <0: error.
+int refresh_d0(emqx_gm_ctx* ctx, const IndexView& v, void* d0);
 // a plain index's host mirror is kept from the build when its tables are at most this big
 constexpr size_t kEagerMirrorBytes = size_t(2) << 30;
 // rank of f among idx's filters; *found = exact hit

@@ -43,6 +43,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "gm_internal.h"
@@ -129,6 +130,10 @@ __device__ __noinline__ bool tail_equal(const uint8_t* a, const uint8_t* b, uint
   return true;
 }
 
+__device__ __forceinline__ DictSlot dict_at(const IndexView& ix, uint64_t s) { return ix.dict[s]; }
+// a depth-1 node's record as the level-0 round takes it: {hot id, sig, hf, end_filter}
+constexpr uint4 D1_NONE = {NONE, 0u, HF_NONE, NONE};
+
 // Resolve a word in the dictionary starting from the (prefetched) first slot.
 // A hit is exact: length + first 8 bytes compared inline, the rest against
 // the arena (only for words longer than 8 bytes).
@@ -144,13 +149,14 @@ __device__ __forceinline__ uint32_t dict_resolve(const IndexView& ix, const Word
         (w.len <= 8 || tail_equal(ix.arena + d.word + 8, tb + w.start + 8, w.len - 8)))
       return d.word;
     s = (s + 1) & ix.dict_mask;
-    d = ix.dict[s];
+    d = dict_at(ix, s);
   }
 }
 
 __device__ __forceinline__ DictSlot dict_first(const IndexView& ix, const WordTok& w) {
-  return ix.dict[dict_slot(w.h, ix.dict_mask)];
+  return dict_at(ix, dict_slot(w.h, ix.dict_mask));
 }
+
 
 __device__ __forceinline__ uint32_t edge_lookup(const IndexView& ix, uint32_t depth, uint32_t parent,
                                                 uint32_t word) {
@@ -1136,7 +1142,37 @@ struct CoopLds {
 // ballot + mbcnt; tlen[tile] = the list's length.  k_assemble_c sorts them
 // into rows.  A tile whose list would pass 64 x FAST_MC entries sends every
 // topic to the listed pass.  Otherwise ([slot][lane]): one column per topic.
-template <bool EXACT, bool NT, class WORDS, bool CMP = false>
+// IX_D0: a topic's level-0 exact probe, issued by k_match_fused right after
+// its tokenizer (the home slot of (root, level-0 word) in the depth-1 table;
+// s = NONE: no probe) and resolved in the walk's level-0 round.
+struct D0Probe {
+  uint4 a;     // the home slot's head {key lo, key hi, sig, hf}
+  uint32_t s;  // its slot index, or NONE
+};
+__device__ __forceinline__ D0Probe d0_issue(const IndexView& ix, uint32_t w0, uint32_t h, bool valid) {
+  D0Probe p{make_uint4(0u, 0u, 0u, 0u), NONE};
+  const bool walk = valid && !(h & (TOK_WILD | TOK_DEEP));
+  if (!walk || w0 == NONE || !(ix.root_sig & sig_bit(w0))) return p;
+  const int ht = hot_table(1);
+  const uint64_t key = hot_key(0u, w0, 0u);
+  uint32_t s;
+  if (const uint32_t mc = ix.mph_cap[ht]) {
+    if (!mph_gate(ix, ht, key, mc, s)) return p;
+  } else {
+    s = uint32_t(hot_slot(key, ix.hot_cap[ht]));
+  }
+  p.a = hot_load(ix.hot + ix.hot_off[ht], s, false, (ix.flags & IX_HOT_FLAT) != 0).a;
+  p.s = s;
+  return p;
+}
+
+// D0 (k_match_fused with IX_D0): level 0 issues no probe of its own.  Each
+// walking lane takes its own topic's root entry, resolves the exact probe its
+// tokenizer issued (d1; parked in the level-0 list's LDS, which a level-0
+// round from registers does not use) and takes the root's '+' child from
+// ix.d0_root (one uniform load); the rest of the round -- visits, chains,
+// pushes, probe counts -- is the general round's.
+template <bool EXACT, bool NT, class WORDS, bool CMP = false, bool D0 = false>
 __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& words, bool valid, uint64_t t,
                                                int lane, const uint8_t* __restrict__ tb,
                                                const uint64_t* __restrict__ toff, const IndexView& ix,
@@ -1145,13 +1181,24 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
                                                unsigned long long* __restrict__ probe_tile,
                                                unsigned long long* __restrict__ wild_ctr,
                                                uint64_t* __restrict__ tsum, uint32_t* __restrict__ tlen = nullptr,
-                                               uint8_t* __restrict__ cnt8 = nullptr, PhaseRec* php = nullptr) {
+                                               uint8_t* __restrict__ cnt8 = nullptr, PhaseRec* php = nullptr,
+                                               D0Probe d1 = D0Probe{}) {
   PhaseRec ph_dummy{};
   PhaseRec& PH = php ? *php : ph_dummy;
   (void)PH;
   constexpr uint32_t MC = FAST_MC;
   constexpr uint32_t TCAP = 64u * FAST_MC;  // a tile's staging entries
   constexpr bool KC = WORDS::kChain;        // the topic's future words are in its lane's registers
+  // d0: the lanes' issued level-0 probes wait in the level-0 list's LDS (a
+  // level-0 round from registers reads no list), not in VGPRs: stored first
+  // thing, before the wildcard topics' literal lookup needs its registers
+  uint4* const D1L = reinterpret_cast<uint4*>(L.e[0]);
+  uint32_t* const D1S = reinterpret_cast<uint32_t*>(D1L + 64);
+  static_assert(sizeof(L.e[0]) >= 64 * (sizeof(uint4) + 4), "the level-0 list holds 64 probes");
+  if (D0 && (ix.flags & IX_D0)) {
+    D1L[lane] = d1.a;
+    D1S[lane] = d1.s;
+  }
   const uint64_t tile = t >> 6;
   uint32_t* const MCNT = L.mc;
   uint2* const LW = L.lw;
@@ -1179,18 +1226,25 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
   // level 0: one root entry per walking topic
   const unsigned long long bw = __ballot(walk);
   uint32_t wnext = walk ? words.first() : NONE;
-  if (walk) {
+  if (walk && !(D0 && (ix.flags & IX_D0))) {
     const uint32_t p = lane_prefix(bw);
     L.e[0][p] = make_uint2((!dollar && (ix.root_flags & HOT_PLUS)) ? FR_PLUS : 0u, ix.root_sig);
     L.ln[0][p] = uint8_t(lane);
   }
   uint32_t cur_total = uint32_t(__popcll(bw));
   const bool hflat = (ix.flags & IX_HOT_FLAT) != 0;
+  const bool d0 = D0 && (ix.flags & IX_D0);  // (wave-uniform)
+  uint4 rq = D1_NONE;                       // the root's '+' child {hot id, sig, hf, end}
+  if (d0) rq = *reinterpret_cast<const uint4*>(ix.d0_root);
   int cur = 0;
 #ifdef GM_PHASE_STATS
   uint64_t tph = __builtin_amdgcn_s_memtime();
 #endif
-  for (uint32_t level = 0; cur_total; ++level) {
+  // One level of the walk (a lambda, so that level 0 under D0 -- the round
+  // from registers -- is its own instance and its extra live values do not
+  // raise the general loop's register pressure)
+  auto walk_level = [&](uint32_t level, auto d0r_tag) {
+    constexpr bool D0R = decltype(d0r_tag)::value;
 #ifdef GM_PHASE_STATS
     const uint32_t ph_rounds = (cur_total + 63) / 64;
     uint32_t ph_data = 0, ph_rest = 0;
@@ -1214,14 +1268,17 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
     uint2* EN = L.e[cur ^ 1];
     uint8_t* LNn = L.ln[cur ^ 1];
     uint32_t nxt_total = 0;
-    for (uint32_t base = 0; base < cur_total; base += 64) {
+    for (uint32_t base = 0; base < (D0R ? 1u : cur_total); base += 64) {
 #ifdef GM_PHASE_STATS
       const uint64_t tr0 = __builtin_amdgcn_s_memtime();
 #endif
+      // (d0r: level 0 from registers; every walking lane takes its own root entry)
+      constexpr bool d0r = D0R;
       const uint32_t e = base + uint32_t(lane);
-      const bool act = e < cur_total;
-      const uint2 en = act ? E[e] : make_uint2(0u, 0u);
-      const uint32_t tl = act ? LNc[e] : 0u;
+      const bool act = d0r ? walk : e < cur_total;
+      const uint2 en = d0r ? make_uint2((!dollar && (ix.root_flags & HOT_PLUS)) ? FR_PLUS : 0u, ix.root_sig)
+                           : act ? E[e] : make_uint2(0u, 0u);
+      const uint32_t tl = d0r ? uint32_t(lane) : act ? LNc[e] : 0u;
       const uint2 lw = LW[tl];
       const uint32_t wid = lw.x, id = en.x & ID_MASK;
       const bool last = act && level + 1 == (lw.y & 0xFFu);
@@ -1235,6 +1292,23 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
       const bool pin = dp && plus_is_inline(lvl, id);
       const uint64_t kx = hot_key(id, wid, lvl), kp = hot_key(id, ix.plus_word, lvl);
       uint32_t sx = 0, sp = 0;
+      HotRec rx{}, rp{};
+      uint32_t hx = NONE, hp = NONE;
+      if (d0r) {
+        const uint32_t s1 = D1S[lane];
+        dx = dx && s1 != NONE;  // (NONE: the tokenizer's gates -- root sig, MPH Bloom bits -- ruled it out)
+        if (dx) {  // resolve the issued probe; the end filter (a one-level topic) from the found slot
+          rx.a = D1L[lane];
+          rx.ef = NONE;
+          hx = hot_resolve_x(ix, ht, tab, capu, kx, s1, rx, false, hflat, hrh);
+          if (last && hx != NONE) rx.ef = hot_load(tab, hx, true, hflat).ef;
+        }
+        if (dp) {
+          hp = rq.x;
+          rp.a = make_uint4(0u, 0u, rq.y, rq.z);
+          rp.ef = last ? rq.w : NONE;
+        }
+      } else {
       if (const uint32_t mc = ix.mph_cap[ht]) {
         // an MPH table (wave-uniform): one L2 read of the key's bucket word
         // filters the probe and gives its slot, in place of the exact-edge filter
@@ -1250,7 +1324,6 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
         if (dp && !pin) sp = uint32_t(hot_slot(kp, cap));
       }
       // issue both probes, then resolve
-      HotRec rx{}, rp{};
       const bool nol1 = (ix.l1_bypass >> ht) & 1u;
       if (dx) rx = hot_load(tab, sx, last, hflat, nol1);
       if (pin) {
@@ -1258,8 +1331,9 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
       } else if (dp) {
         rp = hot_load(tab, sp, last, hflat, nol1);
       }
-      const uint32_t hx = dx ? hot_resolve_x(ix, ht, tab, capu, kx, sx, rx, last, hflat, hrh) : NONE;
-      const uint32_t hp = pin ? (id | HOT_INLINE) : dp ? hot_resolve_x(ix, ht, tab, capu, kp, sp, rp, last, hflat, hrh) : NONE;
+      hx = dx ? hot_resolve_x(ix, ht, tab, capu, kx, sx, rx, last, hflat, hrh) : NONE;
+      hp = pin ? (id | HOT_INLINE) : dp ? hot_resolve_x(ix, ht, tab, capu, kp, sp, rp, last, hflat, hrh) : NONE;
+      }
 #ifdef GM_PHASE_STATS
       __builtin_amdgcn_s_waitcnt(0);  // (diagnostic build: the probes' data is in)
       const uint64_t tr1 = __builtin_amdgcn_s_memtime();
@@ -1408,7 +1482,14 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
       tph = tn;
     }
 #endif
+  };
+  uint32_t level0 = 0;
+  if (d0 && cur_total) {
+    walk_level(0u, std::true_type{});
+    level0 = 1;
   }
+  uint32_t level = level0;
+  while (cur_total != 0) walk_level(level++, std::false_type{});  // (each level updates cur_total)
   wave_lds_sync();
   const uint32_t m_n = MCNT[lane];
   // CW_OVF or a row past the staging capacity; CMP: the tile's list past its capacity
@@ -1499,7 +1580,7 @@ struct WordsFromRegs {
 
 constexpr size_t FUSED_LDS = sizeof(CoopLds) * 4 > (TOK_STAGE + 8) ? sizeof(CoopLds) * 4 : (TOK_STAGE + 8);
 
-template <int G, bool EXACT, bool NT, bool TOKPRIO, bool CMP>
+template <int G, bool EXACT, bool NT, bool TOKPRIO, bool CMP, bool D0 = true>
 __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restrict__ tb,
                                                         const uint64_t* __restrict__ toff, uint64_t n, IndexView ix,
                                                         uint32_t* __restrict__ cnt, uint32_t* __restrict__ stage,
@@ -1556,10 +1637,15 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
 #endif
   if constexpr (TOKPRIO) __builtin_amdgcn_s_setprio(0);
   if ((t >> 6) * 64 >= n) return;  // wave-uniform, after the last workgroup barrier
+  // IX_D0: the level-0 exact probe -- the depth-1 node (root, level-0 word) --
+  // issued before the walk's setup and resolved in its level-0 round (held
+  // across the block barrier it spilled)
+  D0Probe d1{make_uint4(0u, 0u, 0u, 0u), NONE};
+  if (D0 && (ix.flags & IX_D0)) d1 = d0_issue(ix, w[0], h, valid);
   WordsFromRegs words{w};
-  coop_walk_tile<EXACT, NT, WordsFromRegs, CMP>(reinterpret_cast<CoopLds*>(s_raw)[wv], h, words, valid, t, lane, tb,
-                                                toff, ix, cnt, stage, ovf_list, ovf_n, probe_tile, wild_ctr, tsum, tlen,
-                                                cnt8, &PH);
+  coop_walk_tile<EXACT, NT, WordsFromRegs, CMP, D0>(reinterpret_cast<CoopLds*>(s_raw)[wv], h, words, valid, t, lane,
+                                                    tb, toff, ix, cnt, stage, ovf_list, ovf_n, probe_tile, wild_ctr,
+                                                    tsum, tlen, cnt8, &PH, d1);
 }
 
 // ---------------------------------------------------------------------------
@@ -2765,11 +2851,12 @@ bool nt_streams() {
 // used when the index's filter ids fit CMP_SHIFT bits.
 // The assembly stream (MatchCall::submit) for device-buffer calls of at least
 // this many topics; GM_ASM_STREAM (A/B knob, read per call): 0 = never, N =
-// from N topics.  Below it (C1's 1M-topic calls) the extra event and wait
-// packets cost more than the overlap gives.
+// from N topics.
+// (Off by default: at C2 the overlapped assembly slowed the walk by what it
+// hid, 9.16 vs 9.16 ms per step, profiles/r04_ab/asm_stream_c2.txt.)
 uint64_t asm_stream_min() {
   const char* e = getenv("GM_ASM_STREAM");
-  return e ? strtoull(e, nullptr, 10) : (4ull << 20);
+  return e ? strtoull(e, nullptr, 10) : 0;
 }
 
 bool stage_compact() {
@@ -3195,13 +3282,17 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   if (main_kind() != MAIN_FUSED) timed = true;  // (the other forms record their events around the launches)
   hipEvent_t main_ev0 = ev[0], main_ev1 = ev[1];
   if (!timed) main_ev0 = main_ev1 = nullptr;
+  // GM_D0=0 (A/B knob, read per call): level 0 probed like any other level
+  IndexView vcall = idx->view;
+  if (const char* de = getenv("GM_D0"))
+    if (!atoi(de)) vcall.flags &= ~IX_D0;
   if (exact)
-    launch_match<true>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
+    launch_match<true>(ctx, vcall, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
                        list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
                        probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), main_ev0, main_ev1,
                        cmp ? &cmpb : nullptr, &listed_deferred);
   else
-    launch_match<false>(ctx, idx->view, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(),
+    launch_match<false>(ctx, vcall, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(),
                         n1, list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
                         probe_tile.as<unsigned long long>(), tsum.as<uint64_t>(), main_ev0, main_ev1,
                         cmp ? &cmpb : nullptr, &listed_deferred);
@@ -3446,6 +3537,50 @@ int match_wait(emqx_gm_ctx* ctx, void* ticket, emqx_gm_csr* out) {
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   delete c;
   return rc;
+}
+
+// ---- IX_D0: the root's '+' child's record (IndexView::d0_root), read from
+// the depth-1 hot table (the gm_common.h hot_lookup rules: MPH slot + overflow
+// region, or linear probing) by one thread, at build and after each in-place
+// update (the update renumbers filter ids and may change its sig / hf).
+__device__ __forceinline__ uint32_t hot_find(const IndexView& v, int t, uint64_t key) {
+  const uint64_t cap = v.hot_cap[t];
+  if (!cap) return NONE;
+  const HotSlot* tab = v.hot + v.hot_off[t];
+  if (const uint32_t mc = v.mph_cap[t]) {
+    const uint64_t w = v.mph_word[v.mph_off[t] + mph_bucket(key, v.mph_nb[t])];
+    if (!mph_may_hold(w, key)) return NONE;
+    const uint32_t s = mph_slot(key, uint32_t(w & 0xFFFFu), mc);
+    if (tab[s].key == key) return s;
+    if (!((v.mph_ovf >> t) & 1u)) return NONE;
+    for (uint64_t o = mph_ovf_home(key, mc, uint32_t(cap));; o = o + 1 == cap ? mc : o + 1) {
+      if (tab[o].key == key) return uint32_t(o);
+      if (tab[o].key == EDGE_EMPTY) return NONE;
+    }
+  }
+  for (uint64_t s = hot_slot(key, cap);; s = s + 1 == cap ? 0 : s + 1) {
+    if (tab[s].key == key) return uint32_t(s);
+    if (tab[s].key == EDGE_EMPTY) return NONE;
+  }
+}
+__global__ void k_d0_refresh(IndexView v, uint4* __restrict__ d0) {
+  const int t = hot_table(1);
+  const uint32_t s = v.plus_word == NONE ? NONE : hot_find(v, t, hot_key(0u, v.plus_word, 0u));
+  if (s == NONE) {
+    *d0 = D1_NONE;
+  } else {
+    const HotSlot& h = v.hot[v.hot_off[t] + s];
+    *d0 = make_uint4(s, h.sig, h.hf, h.end_filter);
+  }
+}
+
+int refresh_d0(emqx_gm_ctx* ctx, const IndexView& v, void* d0) {
+  if (const char* e = getenv("GM_D0"))  // A/B knob: 0 = the walk probes level 0 like any other
+    if (!atoi(e)) return 1;
+  hipLaunchKernelGGL(k_d0_refresh, dim3(1), dim3(1), 0, ctx->stream, v, static_cast<uint4*>(d0));
+  GM_HIP(ctx, hipGetLastError());
+  GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
 }
 
 int scan_lengths(emqx_gm_ctx* ctx, const uint64_t* len, uint64_t n, uint64_t* out) {

@@ -605,6 +605,7 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
   };
   v.nodes = rebase(v.nodes);
   v.dict = rebase(v.dict);
+  v.d0_root = rebase(v.d0_root);
   v.edges = rebase(v.edges);
   v.hot = rebase(v.hot);
   v.arena = rebase(v.arena);
@@ -613,6 +614,16 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
   v.efilt = rebase(v.efilt);
   v.mph_word = rebase(v.mph_word);
   idx->dev_flen = host ? nullptr : reinterpret_cast<uint16_t*>(NB + M.o_flen);
+  if (!host && (v.flags & IX_D0)) {  // the root's '+' record again, from the patched and renumbered tables
+    const int rc = refresh_d0(ctx, v, const_cast<uint32_t*>(v.d0_root));
+    if (rc < 0) {  // (the mirror is past prev's tables now: later updates of this line rebuild)
+      free_index(idx);
+      delete prev->mirror;
+      prev->mirror = nullptr;
+      return rc;
+    }
+    if (rc) v.flags &= ~IX_D0;
+  }
   emqx_gm_index_info_t& in = idx->info;
   in.n_filters = nf_new;
   in.n_wildcard = prev->info.n_wildcard - twild + dwild;

@@ -166,6 +166,12 @@ class Index:
     def filters(self) -> List[bytes]:
         return [self.filter(i) for i in range(self.n_filters)]
 
+    def export_size(self, with_blob: bool = True) -> int:
+        n = C.c_uint64()
+        check(lib().emqx_gm_index_export(self.ctx.h, self.h, 0 if with_blob else _lib.IMAGE_NO_BLOB, None,
+                                         C.byref(n)), self.ctx.h, "index_export")
+        return int(n.value)
+
     def export(self, with_blob: bool = True, out: Optional[np.ndarray] = None) -> np.ndarray:
         """The snapshot as a host image (emqx_gm_index_export): the host tables
         and, with ``with_blob``, the device tables.  ``out`` (uint8, e.g. a

@@ -1,13 +1,14 @@
 #!/bin/bash
-# rocprofv3 passes for the C2 bench (run on the GPU box).  Each PMC pass is its
+# rocprofv3 passes for a bench config (CONFIG, default c2; run on the GPU box).  Each PMC pass is its
 # own run (no counter splitting), bounded by timeout -s KILL.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
-mkdir -p $OUT
 TOPICS=${TOPICS:-100000000}
-ARGS="bench.py --topics $TOPICS --steps 2 --warmup 1 --no-cpu --no-parity --no-host-io"
+CONFIG=${CONFIG:-c2}
+OUT=gpurun_out/prof${PROF_TAG:-}
+mkdir -p $OUT
+ARGS="bench.py --config $CONFIG --topics $TOPICS --steps 2 --warmup 1 --no-cpu --no-parity --no-host-io --no-update ${BENCH_ARGS:-}"
 run() {  # run <name> <timeout> <rocprof args...>
   local name=$1 t=$2; shift 2
   echo "=== $name"
