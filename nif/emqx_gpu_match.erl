@@ -11,7 +11,7 @@
 -module(emqx_gpu_match).
 
 -export([load_index/1, load_index/2, update_index/2, update_subs/2, match_batch/2, match_routes_batch/2, fanout_batch/2,
-         empty/1]).
+         empty/1, export_index/1, import_index/1]).
 -export([match/2]).
 
 -on_load(init/0).
@@ -58,6 +58,17 @@ fanout_batch(_Index, _Topics) -> erlang:nif_error(nif_not_loaded).
 
 -spec empty(reference()) -> boolean().
 empty(_Index) -> erlang:nif_error(nif_not_loaded).
+
+%% The snapshot as one binary (emqx_gm_index_export): what a node joining the
+%% cluster imports instead of recompiling the route table -- the reference
+%% replicates its routing tables through mria (emqx_router.erl:75-84).
+-spec export_index(reference()) -> {ok, binary()} | {error, term()}.
+export_index(_Index) -> erlang:nif_error(nif_not_loaded).
+
+%% emqx_gm_index_import on this node's GPU; an image of another table layout
+%% (another library build) is {error, _}.
+-spec import_index(binary()) -> {ok, reference()} | {error, term()}.
+import_index(_Image) -> erlang:nif_error(nif_not_loaded).
 
 %% emqx_trie:match/1 drop-in with fallback.
 -spec match(reference(), binary()) -> [binary()].

@@ -370,6 +370,43 @@ static ERL_NIF_TERM empty(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
   return enif_make_atom(env, info.trie_empty ? "true" : "false");
 }
 
+/* export_index(Index) -> {ok, Image :: binary()} | {error, Reason}
+ * emqx_gm_index_export with the device tables: the snapshot as one binary a
+ * joining node imports instead of recompiling the route table (the reference
+ * replicates its routing tables through mria, emqx_router.erl:75-84). */
+static ERL_NIF_TERM export_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_index_res *r;
+  ErlNifBinary bin;
+  uint64_t size = 0;
+  int rc;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], INDEX_RT, (void **)&r)) return enif_make_badarg(env);
+  rc = emqx_gm_index_export(CTX, r->idx, 0, NULL, &size);
+  if (rc != EMQX_GM_OK) return error_tuple(env, rc);
+  if (!enif_alloc_binary((size_t)size, &bin))
+    return enif_make_tuple2(env, A_ERROR, enif_make_string(env, "enomem", ERL_NIF_LATIN1));
+  rc = emqx_gm_index_export(CTX, r->idx, 0, bin.data, &size);
+  if (rc != EMQX_GM_OK) {
+    enif_release_binary(&bin);
+    return error_tuple(env, rc);
+  }
+  return enif_make_tuple2(env, A_OK, enif_make_binary(env, &bin));
+}
+
+/* import_index(Image :: binary()) -> {ok, Index} | {error, Reason}
+ * emqx_gm_index_import on this node's device (an image of another layout or
+ * a truncated one: {error, _}). */
+static ERL_NIF_TERM import_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+  ErlNifBinary bin;
+  emqx_gm_index *idx = NULL;
+  int rc;
+  (void)argc;
+  if (!enif_inspect_binary(env, argv[0], &bin)) return enif_make_badarg(env);
+  rc = emqx_gm_index_import(CTX, bin.data, bin.size, NULL, &idx);
+  if (rc != EMQX_GM_OK) return error_tuple(env, rc);
+  return make_index_term(env, idx);
+}
+
 static ErlNifFunc funcs[] = {
     {"load_index", 1, load_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"load_index", 2, load_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
@@ -379,6 +416,8 @@ static ErlNifFunc funcs[] = {
     {"match_routes_batch", 2, match_routes_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"fanout_batch", 2, fanout_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"empty", 1, empty, 0},
+    {"export_index", 1, export_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"import_index", 1, import_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
 };
 
 ERL_NIF_INIT(emqx_gpu_match, funcs, load, NULL, NULL, unload)

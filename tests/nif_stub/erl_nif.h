@@ -37,6 +37,9 @@ ERL_NIF_TERM enif_make_string(ErlNifEnv *, const char *, ErlNifCharEncoding);
 int enif_get_list_length(ErlNifEnv *, ERL_NIF_TERM, unsigned *);
 int enif_get_list_cell(ErlNifEnv *, ERL_NIF_TERM, ERL_NIF_TERM *, ERL_NIF_TERM *);
 int enif_inspect_binary(ErlNifEnv *, ERL_NIF_TERM, ErlNifBinary *);
+int enif_alloc_binary(size_t, ErlNifBinary *);
+void enif_release_binary(ErlNifBinary *);
+ERL_NIF_TERM enif_make_binary(ErlNifEnv *, ErlNifBinary *);
 void *enif_alloc(size_t);
 void enif_free(void *);
 void *enif_alloc_resource(ErlNifResourceType *, size_t);
