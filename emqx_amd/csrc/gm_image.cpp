@@ -249,7 +249,10 @@ int load_mirror_blob(emqx_gm_ctx* ctx, emqx_gm_index* idx) {
   M.blob.resize(M.blob_size);
   hipSetDevice(idx->device);
   if (ctx) GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // pinned for the copy (several times the pageable rate), when the host allows it
+  const bool reg = hipHostRegister(M.blob.data(), M.blob_size, hipHostRegisterDefault) == hipSuccess;
   const hipError_t e = hipMemcpy(M.blob.data(), idx->dev_base, M.blob_size, hipMemcpyDeviceToHost);
+  if (reg) (void)hipHostUnregister(M.blob.data());
   if (e != hipSuccess) {
     std::vector<uint8_t>().swap(M.blob);
     return set_err(ctx, EMQX_GM_EDEVICE, std::string("index_update: mirror download: ") + hipGetErrorString(e));

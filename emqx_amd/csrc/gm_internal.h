@@ -306,7 +306,9 @@ int load_mirror_blob(emqx_gm_ctx* ctx, emqx_gm_index* idx);
 // (GM_D0=0), <0: error.
 int refresh_d0(emqx_gm_ctx* ctx, const IndexView& v, void* d0);
 // a plain index's host mirror is kept from the build when its tables are at most this big
-constexpr size_t kEagerMirrorBytes = size_t(2) << 30;
+// (C3's 4.6 GB tables keep theirs: a lazy first update downloads the tables,
+// 0.8 s at C3 over pageable copies; the 38 GB C5 index does not)
+constexpr size_t kEagerMirrorBytes = size_t(8) << 30;
 // rank of f among idx's filters; *found = exact hit
 uint64_t filter_rank(const emqx_gm_index* idx, const uint8_t* f, uint64_t len, bool* found);
 // gm_subs.cpp: emqx_gm_index_update_subs

@@ -207,7 +207,7 @@ class Context:
 
     def __init__(self, device: int = 0, mirror: Optional[str] = None):
         """``mirror``: None (library default: the host copy of a plain index's
-        tables is kept from the build up to 2 GiB, loaded on the first update
+        tables is kept from the build up to 8 GiB, loaded on the first update
         above), "eager" or "lazy" (EMQX_GM_OPEN_MIRROR_*)."""
         o = Opts()
         o.device = device

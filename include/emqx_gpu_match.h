@@ -90,7 +90,7 @@ typedef struct {
 
 /* emqx_gm_opts.flags: the host copy of a plain index's device tables that an
  * in-place emqx_gm_index_update patches (host RAM ~ the tables' size).  By
- * default it is kept from the build for tables up to 2 GiB and downloaded from
+ * default it is kept from the build for tables up to 8 GiB and downloaded from
  * the device on a snapshot line's first update above that (a 100M-filter index
  * holds no 38 GB host copy unless it is updated). */
 #define EMQX_GM_OPEN_MIRROR_EAGER 0x1u /* always keep it from the build            */

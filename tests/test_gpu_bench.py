@@ -104,3 +104,18 @@ def test_bench_c5_prefix_one_gpu_device_path():
     assert out["detail"]["device_exchange"] is True
     assert out["detail"]["topics_walked_per_rank"] == [2_000_000]
     assert out["parity_sample"]["ok"], out["parity_sample"]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_replicated_index_rccl_branch_lockstep():
+    """bench.replicated_index on its device-tensor (RCCL) branch, 3 ranks as
+    threads on one GPU with a lock-step broadcast: rank 0 compiles, ranks 1-2
+    import the broadcast image + device tables; every replica's rows equal rank
+    0's and the oracle's, and an imported replica takes an in-place update
+    (tests/_replicate_worker.py)."""
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "_replicate_worker.py"), "3", "200000",
+                        "100000"], cwd=ROOT, capture_output=True, text=True, timeout=380,
+                       env={k: v for k, v in os.environ.items() if k not in ("GM_BENCH_BACKEND", "GM_BENCH_DEVICE")})
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "REPLICATE_OK world=3" in p.stdout
