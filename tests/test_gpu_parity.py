@@ -4,6 +4,7 @@ Bit-exact for every row: filter ids are lexicographic ranks, rows sorted, so
 equality of (row_off, ids) is equality of lists:sort/1 of the reference result.
 """
 
+import os
 import ctypes
 import random
 
@@ -1010,3 +1011,20 @@ def test_host_csr_ownership_across_contexts(ctx, orc):
     assert np.array_equal(ro, ro2)
     oro, oids = _oracle_rows(orc, sorted(filters), topics, 1)
     assert np.array_equal(ro2, oro) and np.array_equal(ids, oids)
+
+
+def test_c_abi_smoke_program():
+    """The C ABI from a plain C program (tests/c_abi_smoke.c, built by
+    __graft_entry__.build()): emqx_router_SUITE's t_match_routes filters in both
+    match modes, fan-out with a duplicate filter's lists concatenated, a
+    snapshot replicated through an image, a corrupt image and bad arguments
+    refused with error codes."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "c_abi_smoke")
+    if not os.path.exists(exe):  # (normally prebuilt by __graft_entry__.build())
+        subprocess.run(["gcc", "-O2", "-std=c11", "-I", os.path.join(root, "include"), exe + ".c", "-L",
+                        os.path.join(root, "emqx_amd"), "-l:libemqx_gpu_match.so",
+                        "-Wl,-rpath," + os.path.join(root, "emqx_amd"), "-o", exe], check=True)
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "C_ABI_SMOKE_OK" in p.stdout, p.stdout + p.stderr

@@ -226,3 +226,17 @@ def test_host_compiler_under_asan(mph_min):
     p = subprocess.run([os.path.join(ROOT, "tests", "asan", "asan_host_compiler")], capture_output=True, text=True,
                        env=env, timeout=300)
     assert p.returncode == 0 and "ASAN_HOST_CHECK_OK" in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
+
+
+def test_c_abi_smoke_program_builds():
+    """tests/c_abi_smoke.c -- the boundary driven from plain C, as the NIF or any
+    native caller would -- compiles warning-free against include/ and links
+    against the library (it runs on the GPU box: test_gpu_parity.py)."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "c_abi_smoke")
+        p = subprocess.run(["gcc", "-O2", "-Wall", "-Wextra", "-Werror", "-std=c11", "-I", os.path.join(ROOT, "include"),
+                            os.path.join(ROOT, "tests", "c_abi_smoke.c"), "-L", os.path.join(ROOT, "emqx_amd"),
+                            "-l:libemqx_gpu_match.so", "-o", out], capture_output=True, text=True)
+        assert p.returncode == 0, p.stderr
