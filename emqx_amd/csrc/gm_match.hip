@@ -1776,9 +1776,13 @@ struct LoadSegLen {  // subscriber count of the filter of match entry i
 // st: the stream (default: the context's).  On another stream the scan's
 // workspace goes back to the pool behind an event on that stream (the pool's
 // immediate reuse assumes the context stream's order).
+// split_sums (optional, with split): a scan of at most 64 blocks may hand
+// back the blocks' SUMS instead (*split_sums = their count): no second launch;
+// the consumer (k_assemble_c) sums the prefixes and writes out[n_in] itself.
 template <class LOAD>
 int scan_excl(emqx_gm_ctx* ctx, LOAD load, uint64_t n_in, uint64_t* out, SideSum side = SideSum{},
-              PoolBuf* split = nullptr, hipStream_t st = nullptr) {
+              PoolBuf* split = nullptr, hipStream_t st = nullptr, uint32_t* split_sums = nullptr) {
+  if (split_sums) *split_sums = 0;
   if (!st) st = ctx->stream;
   const uint64_t n_out = n_in + 1;
   if (n_out <= uint64_t(SCAN1_B)) {  // one launch
@@ -1802,6 +1806,12 @@ int scan_excl(emqx_gm_ctx* ctx, LOAD load, uint64_t n_in, uint64_t* out, SideSum
   } later{ctx, st, {&sums, &offs}};
   hipLaunchKernelGGL(k_scan_local<LOAD>, dim3(nb), dim3(SCAN_T), 0, st, load, n_in, n_out, out,
                      sums.as<uint64_t>(), side);
+  if (split && split_sums && nb <= 64) {
+    GM_HIP(ctx, hipGetLastError());
+    *split = std::move(sums);
+    *split_sums = uint32_t(nb);
+    return 0;
+  }
   if (split && nb + 1 <= uint64_t(SCAN1_B)) {  // the blocks' offsets, and the total into out[n_in]
     hipLaunchKernelGGL(k_scan_one<LoadU64>, dim3(1), dim3(SCAN1_T), 0, st, LoadU64{sums.as<uint64_t>()}, nb,
                        nb + 1, offs.as<uint64_t>(), SideSum{}, out + n_in);
@@ -1957,17 +1967,27 @@ struct AsmCLoads {  // one tile's loads of k_assemble_c, issued before any is us
   uint32_t len, c;
   uint64_t tb0;
 };
+// blk_sums: blk holds the split scan's block SUMS (a scan of at most 64
+// blocks: the prefix is summed here by the wave, one scan launch fewer), not
+// their offsets.
+__device__ __forceinline__ uint64_t blk_prefix(const uint64_t* __restrict__ sums, uint32_t j, int lane) {
+  uint64_t v = uint32_t(lane) < j ? sums[lane] : 0ull;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
 __device__ __forceinline__ void asm_c_load(AsmCLoads& L, uint64_t tile, uint64_t n, int lane,
                                            const uint8_t* __restrict__ cnt8, const uint64_t* __restrict__ tile_off,
                                            const uint32_t* __restrict__ stage, const uint32_t* __restrict__ tlen,
-                                           const uint64_t* __restrict__ blk) {
+                                           const uint64_t* __restrict__ blk, bool blk_sums = false) {
   const uint32_t* const lst = stage + tile * (64ull * FAST_MC);
 #pragma unroll
   for (int q = 0; q < AsmCLoads::PRE; ++q) L.pre[q] = ld_s<true>(lst + q * 64 + lane);
   L.len = tlen[tile];
   const uint64_t t = tile * 64 + lane;
   L.c = t < n ? ld_s<true>(cnt8 + t) : 0u;  // 0xFF: the row's cnt word (asm_c_tile)
-  L.tb0 = tile_off[tile] + (blk ? blk[tile / SCAN_B] : 0);  // blk: a split scan's block offsets
+  L.tb0 = tile_off[tile] + (!blk ? 0ull : blk_sums ? blk_prefix(blk, uint32_t(tile / SCAN_B), lane)
+                                                   : blk[tile / SCAN_B]);  // blk: a split scan's block offsets
 }
 
 // One tile of k_assemble_c from its loads (out, s_pa: the wave's LDS).
@@ -2039,7 +2059,8 @@ __global__ __launch_bounds__(256) void k_assemble_c(const uint8_t* __restrict__ 
                                                     const uint64_t* __restrict__ blk,
                                                     const uint32_t* __restrict__ rb_total,
                                                     const uint32_t* __restrict__ rb_ctr, uint32_t* __restrict__ rb_dst,
-                                                    uint32_t* __restrict__ zero16) {
+                                                    uint32_t* __restrict__ zero16, uint32_t blk_sums,
+                                                    uint64_t* __restrict__ total_out) {
   __shared__ uint32_t s_out[4][64 * FAST_MC];
   __shared__ uint32_t s_pa[4][64];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -2047,8 +2068,16 @@ __global__ __launch_bounds__(256) void k_assemble_c(const uint8_t* __restrict__ 
   // total and the pass counters, final before this kernel -- written by the
   // first wave's lanes (vector stores), so the call needs no copy packet; the
   // host reads it once this launch's stop event has completed
+  // blk_sums (= the number of scan blocks): no launch wrote the grand total;
+  // the first wave sums the blocks and writes it behind the tile offsets
+  uint64_t gtot = 0;
+  if (blk_sums && blockIdx.x == 0 && wv == 0) {
+    gtot = blk_prefix(blk, blk_sums, lane);
+    if (lane == 0) *total_out = gtot;
+  }
   if (rb_dst && blockIdx.x == 0 && wv == 0) {
-    if (lane < 10) rb_dst[lane] = lane < 2 ? rb_total[lane] : rb_ctr[lane - 2];
+    if (lane < 10)
+      rb_dst[lane] = lane < 2 ? (blk_sums ? uint32_t(gtot >> (32 * lane)) : rb_total[lane]) : rb_ctr[lane - 2];
     __threadfence_system();  // (out to host memory before the kernel's end is signalled)
   }
   // zero16: the next call's pass-counter block (the context's ring), zeroed
@@ -2060,7 +2089,7 @@ __global__ __launch_bounds__(256) void k_assemble_c(const uint8_t* __restrict__ 
   AsmCLoads L[ASM_TPW];
 #pragma unroll
   for (int k = 0; k < ASM_TPW; ++k)
-    if (tile0 + k < n_tiles) asm_c_load(L[k], tile0 + k, n, lane, cnt8, tile_off, stage, tlen, blk);
+    if (tile0 + k < n_tiles) asm_c_load(L[k], tile0 + k, n, lane, cnt8, tile_off, stage, tlen, blk, blk_sums != 0);
 #pragma unroll
   for (int k = 0; k < ASM_TPW; ++k) {
     if (tile0 + k >= n_tiles) break;
@@ -2854,6 +2883,14 @@ bool nt_streams() {
 // from N topics.
 // (Off by default: at C2 the overlapped assembly slowed the walk by what it
 // hid, 9.16 vs 9.16 ms per step, profiles/r04_ab/asm_stream_c2.txt.)
+// GM_SCAN_SUMS (A/B knob, read per call; default on): a split tile scan of at
+// most 64 blocks (calls up to ~4M topics: C1) ends after its first launch and
+// k_assemble_c sums the block prefixes itself.
+bool sums_mode() {
+  const char* e = getenv("GM_SCAN_SUMS");
+  return !e || atoi(e) != 0;
+}
+
 uint64_t asm_stream_min() {
   const char* e = getenv("GM_ASM_STREAM");
   return e ? strtoull(e, nullptr, 10) : 0;
@@ -2873,8 +2910,10 @@ struct CmpBufs {
 void launch_assemble(hipStream_t st, uint64_t nblk, const CmpBufs* cb, const uint32_t* cnt, uint64_t n,
                      const uint64_t* toff, const uint32_t* stage, uint64_t* row_off, uint32_t* ids,
                      const uint32_t* gmap, uint64_t cap, const uint64_t* blk = nullptr, uint32_t* rb_dst = nullptr,
-                     const uint32_t* rb_ctr = nullptr, hipEvent_t done = nullptr, uint32_t* zero16 = nullptr) {
+                     const uint32_t* rb_ctr = nullptr, hipEvent_t done = nullptr, uint32_t* zero16 = nullptr,
+                     uint32_t blk_sums = 0) {
   // blk (compact staging only): toff is a split scan's block-local part, blk its block offsets
+  // (blk_sums != 0: blk holds that many block SUMS, and the kernel writes the grand total at toff[n_tiles])
   // rb_dst (compact staging only): the read-back words (the total behind toff, the
   // counters at rb_ctr) written by the kernel, `done` its stop event
   // zero16 (compact staging only): a 64-B counter block the kernel zeroes
@@ -2882,7 +2921,8 @@ void launch_assemble(hipStream_t st, uint64_t nblk, const CmpBufs* cb, const uin
   if (cb)
     hipExtLaunchKernelGGL(k_assemble_c, dim3((nblk + ASM_TPW - 1) / ASM_TPW), dim3(256), 0, st, nullptr, done, 0,
                           cb->cnt8, cnt, n, toff, stage, cb->tlen, cb->lstage, cb->lcnt, row_off, ids, gmap, cap, blk,
-                          rb_total, rb_ctr, rb_dst, zero16);
+                          rb_total, rb_ctr, rb_dst, zero16, blk_sums,
+                          const_cast<uint64_t*>(toff) + (n + 63) / 64);
   else
     hipLaunchKernelGGL(k_assemble, dim3(nblk), dim3(256), 0, st, cnt, n, toff, stage, row_off, ids, gmap, cap);
 }
@@ -3102,6 +3142,7 @@ struct MatchCall {
   const emqx_gm_index* idx = nullptr;
   uint64_t n = 0, n_tiles = 0, nblk = 0, cap_spec = 0;
   bool dev_io = false, exact = false, cmp = false, spec = false, split = false, submitted = false;
+  uint32_t split_sums = 0;       // the split scan handed back block sums (k_assemble_c sums them)
   bool listed_deferred = false;  // the listed pass is left to finish() (launched only for queued rows)
   bool timed = true;             // the main pass's start / stop events (EMQX_GM_NO_TIMING: none)
   bool asm_overlap = false;      // scan + speculative assembly on ctx->stream_asm (wanted)
@@ -3324,7 +3365,8 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   const char* se = getenv("GM_SCAN_SPLIT");
   split = cmp && (!se || atoi(se) != 0);
   int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p,
-                     SideSum{probe_tile.as<unsigned long long>(), n_tiles, probe_ctr}, split ? &scan_blk : nullptr, sa);
+                     SideSum{probe_tile.as<unsigned long long>(), n_tiles, probe_ctr}, split ? &scan_blk : nullptr, sa,
+                     split && sums_mode() ? &split_sums : nullptr);
   if (rc) return rc;
   // Speculative assembly: the rows are written before the host has read the
   // match total, into an ids buffer sized from this context's recent matches
@@ -3357,7 +3399,7 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
     launch_assemble(sa, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
                     row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec, scan_blk.as<uint64_t>(),
                     rb_kernel ? pin_dev : nullptr, reinterpret_cast<const uint32_t*>(ctrs_p),
-                    rb_kernel ? ev[2] : nullptr, zero_next);
+                    rb_kernel ? ev[2] : nullptr, zero_next, split_sums);
     GM_HIP(ctx, hipGetLastError());
     if (tail && tail->enqueue) {
       rc = tail->enqueue(row_off.as<uint64_t>(), ids.as<uint32_t>(), cap_spec);
@@ -3496,7 +3538,8 @@ int MatchCall::finish(emqx_gm_csr* out, MatchTail* tail, bool locked) {
   // (after a slow-path rescan toff is whole; otherwise it is still the split first scan)
   launch_assemble(st, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
                   row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, nnz,
-                  (n_ovf || !split) ? nullptr : scan_blk.as<uint64_t>());
+                  (n_ovf || !split) ? nullptr : scan_blk.as<uint64_t>(), nullptr, nullptr, nullptr, nullptr,
+                  (n_ovf || !split) ? 0u : split_sums);
   GM_HIP(ctx, hipGetLastError());
   if (n_ovf) {
     hipLaunchKernelGGL(k_copy_slow, dim3(n_ovf), dim3(256), 0, st, ovf_list, n_ovf, row_off.as<uint64_t>(),
