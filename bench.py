@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "publish topics matched/sec at 1M wildcard subs (1/2/4/8 GPU); achieved HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+RANDOM_LINE_CEILING = 52.9e9  # random 128-B line requests/s, 2 GiB table (scripts/randread.hip, profiles/r02_randread)
 
 
 def parse():
@@ -551,7 +552,13 @@ def main():
                      # the SURVEY §8d formula credits Σ len(f) of the matched filters, bytes no kernel reads
                      "frac_without_filter_bytes": (algo - fbytes_matched) / (kavg / 1e3) / 1e9 / HBM_PEAK_GBS,
                      "kernel": "k_match_fused", "kernel_ms": kavg, "timed_launches": len(kern_ms),
-                     "algo_bytes_per_launch": algo},
+                     "algo_bytes_per_launch": algo,
+                     # the walk's physical bound: random 128-B fabric line requests (PMC TCC_EA0_RDREQ per
+                     # topic) against the calibrated ceiling of this access pattern (scripts/randread.hip:
+                     # 52.9 G random lines/s beyond the Infinity Cache, profiles/r02_randread/)
+                     "fabric_lines_per_s": None if lines is None else lines * n_topics / (kavg / 1e3),
+                     "frac_of_random_line_ceiling": None if lines is None else
+                     lines * n_topics / (kavg / 1e3) / RANDOM_LINE_CEILING},
         "detail": {"nnz_per_step": nnz, "matches_per_topic": nnz / n_topics, "probes_per_topic": st["probes"] /
                    n_topics, "overflow_rows": st["n_overflow"], "topic_bytes": tbytes,
                    "index_device_bytes": int(idx.info.device_bytes), "index_nodes": int(idx.info.n_nodes),
