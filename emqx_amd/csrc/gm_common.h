@@ -113,6 +113,7 @@ struct alignas(32) HotSlot {
 GM_HD uint32_t hot_sig(uint32_t hf, uint32_t sig);
 // Read-only view of one index resident in HBM (passed by value to kernels).
 constexpr uint32_t IX_HOT_FLAT = 1u;  // a hot table reaches 2 GiB: flat loads instead of buffer loads
+constexpr uint32_t IX_STAGE_SC1 = 4u;  // A/B: the compact staging list stored sc1 (set per call, GM_STAGE_SC1)
 constexpr uint32_t IX_D0 = 2u;        // d0_root is current: k_match_fused's level 0 round without hot-table probes of its own
 struct IndexView {
   const Node* nodes;
@@ -153,7 +154,8 @@ struct IndexView {
   uint32_t mph_nb[HOT_TABLES];       // buckets of each MPH table
   uint32_t mph_cap[HOT_TABLES];      // perfect-hash slots of each table; 0 = not an MPH table
   uint32_t mph_ovf;                  // bit t: table t's overflow region holds keys
-  uint32_t l1_bypass;                // bit t: table t's probes skip the CU's L1 (sc1 loads; GM_L1_BYPASS A/B knob)
+  uint32_t l1_bypass;                // bit t: table t's probes use hot_policy (GM_L1_BYPASS A/B knob)
+  uint32_t hot_policy;               // their cache policy (gm_match.hip hot_load; 1 = sc1: no L1 fill)
   // IX_D0: the root's '+' child as the walk reads it at level 0 (one uniform
   // 16-B load per wave): {hot id (NONE: no '+' at the root), sig, hf,
   // end_filter}, written from the depth-1 hot table by k_d0_refresh

@@ -929,6 +929,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.mph_word = reinterpret_cast<const uint64_t*>(B + o_mph);
   v.mph_ovf = mph_ovf;
   v.l1_bypass = 0;
+  v.hot_policy = 1;  // (sc1, for the tables GM_L1_BYPASS selects; both A/B knobs, read per call too)
   if (const char* e = getenv("GM_L1_BYPASS")) v.l1_bypass = uint32_t(strtoul(e, nullptr, 0));
   for (int t = 0; t < HOT_TABLES; ++t) {
     v.mph_off[t] = mph_off[t];

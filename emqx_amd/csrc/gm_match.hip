@@ -225,13 +225,18 @@ struct HotRec {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t hot_rsrc(const HotSlot* tab) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<HotSlot*>(tab), (short)0, 0x7FFFFFFF, 0x00020000);
 }
-__device__ __forceinline__ HotRec hot_load(const HotSlot* tab, uint32_t s, bool with_end, bool flat, bool nol1 = false) {
+// pol (wave-uniform; 0 = default): the cache policy of a probe of a table
+// selected by IndexView::l1_bypass (A/B knobs GM_L1_BYPASS, GM_HOT_POLICY):
+// 1 sc1 (no L1 fill), 2 sc0 sc1 (system scope), 3 nt, 4 sc1 nt
+__device__ __forceinline__ HotRec hot_load(const HotSlot* tab, uint32_t s, bool with_end, bool flat, uint32_t pol = 0) {
   HotRec r;
   if (!flat) {
     const __amdgpu_buffer_rsrc_t rs = hot_rsrc(tab);
-    // nol1 (wave-uniform): an sc1 load, served by L2 without filling the L1
-    const auto v = nol1 ? __builtin_amdgcn_raw_buffer_load_b128(rs, s * 32u, 0, 16)
-                        : __builtin_amdgcn_raw_buffer_load_b128(rs, s * 32u, 0, 0);
+    const auto v = pol == 0 ? __builtin_amdgcn_raw_buffer_load_b128(rs, s * 32u, 0, 0)
+                   : pol == 1 ? __builtin_amdgcn_raw_buffer_load_b128(rs, s * 32u, 0, 16)
+                   : pol == 2 ? __builtin_amdgcn_raw_buffer_load_b128(rs, s * 32u, 0, 17)
+                   : pol == 3 ? __builtin_amdgcn_raw_buffer_load_b128(rs, s * 32u, 0, 2)
+                              : __builtin_amdgcn_raw_buffer_load_b128(rs, s * 32u, 0, 18);
     r.a = make_uint4(v[0], v[1], v[2], v[3]);
     r.ef = with_end ? __builtin_amdgcn_raw_buffer_load_b32(rs, s * 32u + 16u, 0, 0) : NONE;
   } else {
@@ -297,6 +302,19 @@ __device__ __forceinline__ uint32_t hot_resolve_x(const IndexView& ix, int ht, c
     }
   }
   return hot_resolve(tab, cap, key, s, r, with_end, flat, rh);
+}
+
+// A compact staging list entry (IX_STAGE_SC1, A/B knob GM_STAGE_SC1: an sc1
+// store, which leaves the line out of the XCD's L2 instead of keeping it there
+// until eviction; the list is read by the next kernel anyway)
+template <bool NT>
+__device__ __forceinline__ void stage_st(uint32_t* base, uint32_t k, uint32_t v, bool sc1) {
+  if (sc1) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7FFFFFFF, 0x00020000),
+                                          int(k * 4u), 0, 16);
+  } else {
+    st_s<NT>(base + k, v);
+  }
 }
 
 // Per-lane match staging: emit one filter id into the topic's row (slot m_n
@@ -1216,7 +1234,7 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
   if (f0 != NONE) m0 = 1;
   if constexpr (CMP) {  // (rank 0 of the lane's row)
     const unsigned long long b0 = __ballot(f0 != NONE);
-    if (f0 != NONE) st_s<NT>(stile + lane_prefix(b0), f0 | (uint32_t(lane) << CMP_SHIFT));
+    if (f0 != NONE) stage_st<NT>(stile, lane_prefix(b0), f0 | (uint32_t(lane) << CMP_SHIFT), ix.flags & IX_STAGE_SC1);
     wbase = uint32_t(__popcll(b0));
   } else {
     if (f0 != NONE) stile[lane] = f0;
@@ -1324,7 +1342,7 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
         if (dp && !pin) sp = uint32_t(hot_slot(kp, cap));
       }
       // issue both probes, then resolve
-      const bool nol1 = (ix.l1_bypass >> ht) & 1u;
+      const uint32_t nol1 = ((ix.l1_bypass >> ht) & 1u) ? ix.hot_policy : 0u;
       if (dx) rx = hot_load(tab, sx, last, hflat, nol1);
       if (pin) {
         rp = plus_inline_load(ptab, id, hflat);
@@ -1406,12 +1424,13 @@ __device__ __forceinline__ void coop_walk_tile(CoopLds& L, uint32_t h, WORDS& wo
         const uint32_t ne = uint32_t(e1) + uint32_t(e2) + uint32_t(e3) + uint32_t(e4) + uint32_t(e5) + uint32_t(e6);
         uint32_t rk = ne ? atomicAdd(&MCNT[tl], ne) : 0u;
         const uint32_t tag = uint32_t(tl) << CMP_SHIFT;
+        const bool sc1st = (ix.flags & IX_STAGE_SC1) != 0;
 #define GM_CW_PUT(c, f)                                                                         \
   do {                                                                                          \
     const unsigned long long b_ = __ballot(c);                                                  \
     if (c) {                                                                                    \
       const uint32_t k_ = wbase + lane_prefix(b_);                                              \
-      if (k_ < TCAP) st_s<NT>(stile + k_, (f) | tag | ((rk < MC ? rk : MC - 1) << CMP_RANK));   \
+      if (k_ < TCAP) stage_st<NT>(stile, k_, (f) | tag | ((rk < MC ? rk : MC - 1) << CMP_RANK), sc1st); \
       ++rk;                                                                                     \
     }                                                                                           \
     wbase += uint32_t(__popcll(b_));                                                            \
@@ -3327,6 +3346,10 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   IndexView vcall = idx->view;
   if (const char* de = getenv("GM_D0"))
     if (!atoi(de)) vcall.flags &= ~IX_D0;
+  if (const char* se = getenv("GM_STAGE_SC1"))  // A/B knobs (read per call)
+    if (atoi(se)) vcall.flags |= IX_STAGE_SC1;
+  if (const char* be = getenv("GM_L1_BYPASS")) vcall.l1_bypass = uint32_t(strtoul(be, nullptr, 0));
+  if (const char* pe = getenv("GM_HOT_POLICY")) vcall.hot_policy = uint32_t(strtoul(pe, nullptr, 0));
   if (exact)
     launch_match<true>(ctx, vcall, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
                        list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
