@@ -3752,11 +3752,11 @@ __global__ __launch_bounds__(256) void k_unperm_lens(const uint32_t* __restrict_
 __global__ __launch_bounds__(256) void k_unperm_rows(const uint32_t* __restrict__ ids, const uint64_t* __restrict__ in_off,
                                                      const uint32_t* __restrict__ perm, uint64_t n,
                                                      const uint64_t* __restrict__ row_off, uint32_t* __restrict__ out) {
-  const uint64_t i = (uint64_t(blockIdx.x) * 256u + threadIdx.x) >> 6;  // a wave per row
-  const uint32_t lane = threadIdx.x & 63u;
-  if (i >= n) return;
-  const uint64_t a = in_off[i], len = in_off[i + 1] - a, d = row_off[perm[i]];
-  for (uint64_t k = lane; k < len; k += 64) out[d + k] = ids[a + k];
+  const uint32_t sub = threadIdx.x & 15u;  // 16 lanes per row, grid-stride (see k_perm_bytes)
+  for (uint64_t i = (uint64_t(blockIdx.x) * 256u + threadIdx.x) >> 4; i < n; i += uint64_t(gridDim.x) * 16u) {
+    const uint64_t a = in_off[i], len = in_off[i + 1] - a, d = row_off[perm[i]];
+    for (uint64_t k = sub; k < len; k += 16) out[d + k] = ids[a + k];
+  }
 }
 
 int unpermute_rows(emqx_gm_ctx* ctx, uint64_t n, const uint32_t* d_perm, const uint32_t* d_lens, const uint32_t* d_ids,
@@ -3778,7 +3778,7 @@ int unpermute_rows(emqx_gm_ctx* ctx, uint64_t n, const uint32_t* d_perm, const u
   PoolBuf ids(ctx->pool, nnz * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "unpermute_rows: ids");
   if (n) {
-    hipLaunchKernelGGL(k_unperm_rows, dim3(uint32_t((n * 64 + 255) / 256)), dim3(256), 0, st, d_ids,
+    hipLaunchKernelGGL(k_unperm_rows, dim3(grid_groups16(n)), dim3(256), 0, st, d_ids,
                        in_off.as<uint64_t>(), d_perm, n, row_off.as<uint64_t>(), ids.as<uint32_t>());
     GM_HIP(ctx, hipGetLastError());
   }

@@ -113,12 +113,14 @@ __global__ __launch_bounds__(256) void k_perm_lens(const uint64_t* __restrict__ 
 __global__ __launch_bounds__(256) void k_perm_bytes(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
                                                     const uint32_t* __restrict__ perm, uint64_t n,
                                                     const uint64_t* __restrict__ out_off, uint8_t* __restrict__ out) {
-  // a wave per topic: lanes copy its bytes
-  const uint64_t i = (uint64_t(blockIdx.x) * 256u + threadIdx.x) >> 6;
-  const uint32_t lane = threadIdx.x & 63u;
-  if (i >= n) return;
-  const uint64_t a = to[perm[i]], len = to[perm[i] + 1] - a, d = out_off[i];
-  for (uint64_t k = lane; k < len; k += 64) out[d + k] = tb[a + k];
+  // 16 lanes per topic copy its bytes, grid-stride: one work-item per byte
+  // lane of every topic (the former wave per topic) passes the dispatch's
+  // 2^32 work-item limit at 67M topics
+  const uint32_t sub = threadIdx.x & 15u;
+  for (uint64_t i = (uint64_t(blockIdx.x) * 256u + threadIdx.x) >> 4; i < n; i += uint64_t(gridDim.x) * 16u) {
+    const uint64_t a = to[perm[i]], len = to[perm[i] + 1] - a, d = out_off[i];
+    for (uint64_t k = sub; k < len; k += 16) out[d + k] = tb[a + k];
+  }
 }
 }  // namespace
 
@@ -265,8 +267,8 @@ int permute_topics(emqx_gm_ctx* ctx, const uint8_t* d_tb, const uint64_t* d_to, 
                      lens.as<uint64_t>());
   GM_HIP(ctx, hipGetLastError());
   if (int rc = scan_lengths(ctx, lens.as<uint64_t>(), n, d_out_off)) return rc;
-  hipLaunchKernelGGL(k_perm_bytes, dim3(uint32_t((n * 64 + 255) / 256)), dim3(256), 0, ctx->stream, d_tb, d_to,
-                     d_perm, n, d_out_off, d_out);
+  hipLaunchKernelGGL(k_perm_bytes, dim3(grid_groups16(n)), dim3(256), 0, ctx->stream, d_tb, d_to, d_perm, n, d_out_off,
+                     d_out);
   GM_HIP(ctx, hipGetLastError());
   GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return EMQX_GM_OK;

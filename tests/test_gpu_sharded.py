@@ -271,6 +271,52 @@ def test_prefix_shards_each_walk_their_routed_topics(ctx, orc):
     route.release()
 
 
+@pytest.mark.timeout(300)
+def test_permute_and_unpermute_past_2_pow_26_rows(ctx):
+    """A C5 prefix rank permutes 100M topics: the permute/unpermute launches
+    once gave each item a 64-lane wave, 64 * n work-items, past the dispatch's
+    2^32 limit above 67,108,864 items, and silently copied only the first ones.
+    70M topics reversed twice give the batch back byte for byte; 70M one-id rows
+    unpermuted by the reversal give the ids reversed."""
+    from emqx_amd.engine import gen_filter_codes
+    n = 70_000_000
+    codes = gen_filter_codes(5, 1000)
+    db, do, tot = ctx.gen_topics_device(codes, 5, 0, n)
+    rev = np.arange(n - 1, -1, -1, dtype=np.uint32)
+    d_perm = ctx.dev_alloc(n * 4)
+    ctx.memcpy_h2d(d_perm, rev, n * 4)
+    d_pb, d_po = ctx.dev_alloc(tot + 64), ctx.dev_alloc((n + 1) * 8)
+    d_pb2, d_po2 = ctx.dev_alloc(tot + 64), ctx.dev_alloc((n + 1) * 8)
+    ctx.permute_topics(db, do, n, d_perm, d_pb, d_po)
+    tail = np.zeros(2, np.uint64)  # the last permuted topic = the first generated one
+    ctx.memcpy_d2h(tail, d_po + 8 * (n - 1), 16)
+    first = np.zeros(2, np.uint64)
+    ctx.memcpy_d2h(first, do, 16)
+    assert int(tail[1] - tail[0]) == int(first[1] - first[0]) and int(tail[1]) == tot
+    ctx.permute_topics(d_pb, d_po, n, d_perm, d_pb2, d_po2)
+    a, b = np.zeros(tot, np.uint8), np.zeros(tot, np.uint8)
+    ctx.memcpy_d2h(a, db, tot)
+    ctx.memcpy_d2h(b, d_pb2, tot)
+    assert np.array_equal(a, b)
+    del a, b
+    oa, ob = np.zeros(n + 1, np.uint64), np.zeros(n + 1, np.uint64)
+    ctx.memcpy_d2h(oa, do, 8 * (n + 1))
+    ctx.memcpy_d2h(ob, d_po2, 8 * (n + 1))
+    assert np.array_equal(oa, ob)
+    del oa, ob
+    for p in (db, do, d_pb, d_po, d_pb2, d_po2):
+        ctx.dev_free(p)
+    d_l, d_i = ctx.dev_alloc(n * 4), ctx.dev_alloc(n * 4)
+    ctx.memcpy_h2d(d_l, np.ones(n, np.uint32), n * 4)
+    ctx.memcpy_h2d(d_i, np.arange(n, dtype=np.uint32), n * 4)
+    back = ctx.unpermute_rows(n, d_perm, d_l, d_i)
+    ro, ids = back.to_host()
+    back.free()
+    assert np.array_equal(ro, np.arange(n + 1, dtype=np.uint64)) and np.array_equal(ids, rev)
+    for p in (d_perm, d_l, d_i):
+        ctx.dev_free(p)
+
+
 def _run_worker(script, *args, timeout=560):
     import subprocess
     import sys
