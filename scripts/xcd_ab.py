@@ -9,6 +9,9 @@ reordered on the device with emqx_gm_permute_topics):
   w1_xcd   class = level-1 word % 8, tile b <- class b % 8
   w0_ctrl  class = level-0 word % 8, tile b <- class (b // 8) % 8 (same tiles, every
            XCD sees every class: separates XCD locality from in-tile locality)
+  w0_seg8  stable sort by level-0 word % 8: 8 contiguous segments, no XCD mapping (all
+           XCDs walk one class at a time)
+  w0_seg   stable sort by level-0 word: 64 contiguous segments
   sorted   sorted by (w0, w1): the locality bound
 Prints the main pass's kernel time per variant (several rounds, interleaved).
 
@@ -126,6 +129,10 @@ def main():
         perms["w1_xcd"] = xcd_perm(w1 % 8)
     if "w0_ctrl" in vs:
         perms["w0_ctrl"] = xcd_perm(w0 % 8, ctrl=True)
+    if "w0_seg8" in vs:
+        perms["w0_seg8"] = torch.sort(w0 % 8, stable=True).indices
+    if "w0_seg" in vs:
+        perms["w0_seg"] = torch.sort(w0, stable=True).indices
     if "sorted" in vs:
         perms["sorted"] = torch.sort(w0 * 4096 + w1, stable=True).indices
     batches = {"base": (tb, off)} if "base" in vs else {}
