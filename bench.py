@@ -522,6 +522,7 @@ def main():
     # roofline.traffic: the PMC bytes of this very build (scripts/profile.sh ->
     # scripts/traffic.py stamps the library's hash); a stale file gives null
     traffic, lines, traffic_note = None, None, "no profile of this build (scripts/gpu_full.sh)"
+    pmc = {}  # the same profile's L2 hit rate and wave occupancy
     try:
         import hashlib
         with open(a.traffic_json) as f:
@@ -530,6 +531,8 @@ def main():
             sha = hashlib.sha256(f.read()).hexdigest()[:16]
         if tj.get("config") == cfg and tj.get("n_topics") == n_topics and tj.get("lib_sha16") == sha:
             traffic, lines = tj.get("hbm_bytes_per_launch"), tj.get("lines_per_topic")
+            pmc = {k: tj[k] for k in ("l2_hit_rate", "l2_requests_per_topic", "occupancy_waves_per_cu",
+                                      "occupancy_frac") if tj.get(k) is not None}
             traffic_note = f"PMC of this build ({os.path.relpath(a.traffic_json, ROOT)}, lib {sha})"
     except (OSError, ValueError):
         pass
@@ -548,7 +551,7 @@ def main():
         "matches_per_sec": world * nnz * a.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
-                     "lines_per_topic": lines,
+                     "lines_per_topic": lines, **pmc,
                      # the SURVEY §8d formula credits Σ len(f) of the matched filters, bytes no kernel reads
                      "frac_without_filter_bytes": (algo - fbytes_matched) / (kavg / 1e3) / 1e9 / HBM_PEAK_GBS,
                      "kernel": "k_match_fused", "kernel_ms": kavg, "timed_launches": len(kern_ms),
@@ -663,11 +666,12 @@ def bench_c5(a, world, rank, local, pg):
     barrier(pg)
     ctx.synchronize()
     t0 = time.perf_counter()
-    nnz = 0
+    nnz, res = 0, None
     for _ in range(a.steps):
+        if res is not None:
+            res.free()
         res, first, rows = m.match_device(db, do, n_topics)
         nnz = res.nnz
-        res.free()
     ctx.synchronize()
     barrier(pg)
     elapsed = barrier_max(pg, local, time.perf_counter() - t0)
@@ -686,6 +690,14 @@ def bench_c5(a, world, rank, local, pg):
            "matches_per_sec": nnz * a.steps / elapsed,
            "detail": {"index_build_s": t_build, "shard_filters": int(len(gids)),
                       "exchange_bytes_per_step_rank0": m.last_exchange_bytes}}
+    if rank == 0 and not a.no_parity and n_filters < 50_000_000:
+        # rank 0's merged rows (its slice of the batch: every shard's piece merged
+        # by global id) against the oracle over the whole filter set
+        threads = a.cpu_threads or len(os.sched_getaffinity(0))
+        fpack = render_codes(codes)
+        out["parity_sample"] = parity_sample(ctx, oracle_router(fpack), res, codes, sorted_unique(*fpack), a.seed,
+                                             first, rows, threads, width=min(50_000, rows // 4 or 1))
+    res.free()
     ctx.dev_free(db)
     ctx.dev_free(do)
     idx.release()

@@ -63,6 +63,20 @@ def main():
     fetch_b = fetch * 1024 * 2  # KB -> B, gfx950 x2 correction
     write_b = write * 1024
     rdreq, _ = per_launch_sum(os.path.join(a.prof, "pmc_ea", "run_counter_collection.csv"), ks, a.topics, "TCC_EA0_RDREQ_sum")
+    # L2 hit rate and requests (SURVEY §8d "L2 hit %"), from the pmc_l2 pass
+    l2 = os.path.join(a.prof, "pmc_l2", "run_counter_collection.csv")
+    hit, _ = per_launch_sum(l2, ks, a.topics, "TCC_HIT_sum")
+    miss, _ = per_launch_sum(l2, ks, a.topics, "TCC_MISS_sum")
+    # wave occupancy (§8d) from the pmc_sq pass: SQ_WAVE_CYCLES counts quad-cycles
+    # summed over waves (MI355X_MICROARCH.md, s_memtime vs SQ units); SQ_BUSY_CYCLES
+    # is summed over the 32 shader engines (8 XCDs x 4), so the kernel's cycles are
+    # SQ_BUSY_CYCLES / 32 and the mean resident waves per CU is
+    # 4 * SQ_WAVE_CYCLES / (256 CUs * kernel cycles) (of at most 32)
+    sq = os.path.join(a.prof, "pmc_sq", "run_counter_collection.csv")
+    wcyc, _ = per_launch_sum(sq, ks, a.topics, "SQ_WAVE_CYCLES")
+    busy, _ = per_launch_sum(sq, ks, a.topics, "SQ_BUSY_CYCLES")
+    waves, _ = per_launch_sum(sq, ks, a.topics, "SQ_WAVES")
+    occ = 4 * wcyc / (256 * busy / 32) if wcyc and busy else None
     import hashlib
     with open(os.path.join(ROOT, "emqx_amd", "libemqx_gpu_match.so"), "rb") as f:
         lib_sha = hashlib.sha256(f.read()).hexdigest()[:16]
@@ -70,6 +84,11 @@ def main():
            "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
            "hbm_bytes_per_launch": fetch_b + write_b, "launches": [nf, nw],
            "lines_per_topic": None if rdreq is None else rdreq / a.topics,
+           "l2_hit_rate": hit / (hit + miss) if hit is not None and miss is not None else None,
+           "l2_requests_per_topic": (hit + miss) / a.topics if hit is not None and miss is not None else None,
+           "occupancy_waves_per_cu": occ,
+           "occupancy_frac": None if occ is None else occ / 32,
+           "wave_lifetime_cycles": 4 * wcyc / waves if wcyc and waves else None,
            "lib_sha16": lib_sha,
            "note": "FETCH_SIZE x1024 x2 (gfx950 correction) + WRITE_SIZE x1024 per launch; L2 fabric side, "
                    "Infinity-Cache hits included"}

@@ -52,6 +52,8 @@ def test_bench_two_ranks_c5_exchange():
     assert out["n_gpus"] == 2 and out["scaling"] == "strong"
     assert out["detail"]["exchange_bytes_per_step_rank0"] > 0
     assert out["matches_per_sec"] > 0
+    # rank 0's merged rows (slice 0: the shards' pieces merged by global id) = the oracle
+    assert out["parity_sample"]["ok"] and out["parity_sample"]["topics"] > 0
 
 
 @pytest.mark.gpu
