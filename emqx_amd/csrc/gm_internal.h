@@ -263,12 +263,6 @@ int permute_topics(emqx_gm_ctx* ctx, const uint8_t* d_tb, const uint64_t* d_to, 
 int unpermute_rows(emqx_gm_ctx* ctx, uint64_t n, const uint32_t* d_perm, const uint32_t* d_lens, const uint32_t* d_ids,
                    uint32_t flags, emqx_gm_csr* out);
 int scan_lengths(emqx_gm_ctx* ctx, const uint64_t* len, uint64_t n, uint64_t* out);
-// Blocks of 256 for a grid-stride kernel that gives each of n items a group of
-// 16 lanes: all items in one pass up to 1M items, then 65,536 blocks.
-inline uint32_t grid_groups16(uint64_t n) {
-  const uint64_t b = (n + 15) / 16;
-  return uint32_t(b < 65536 ? (b ? b : 1) : 65536);
-}
 
 // gm_overlay.cpp — incremental index maintenance.  An
 // overlay snapshot = an immutable base snapshot (shared, retained) minus

@@ -46,6 +46,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "gm_gather.h"
 #include "gm_internal.h"
 
 namespace gm {
@@ -3742,32 +3743,33 @@ int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m,
 // order with u32 lengths lens[i].
 __global__ __launch_bounds__(256) void k_unperm_lens(const uint32_t* __restrict__ lens, const uint32_t* __restrict__ perm,
                                                      uint64_t n, uint64_t* __restrict__ lens_out,
-                                                     uint64_t* __restrict__ lens_in) {
+                                                     uint64_t* __restrict__ lens_in, uint32_t* __restrict__ inv) {
   const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
   if (i < n) {
     lens_out[perm[i]] = lens[i];
     lens_in[i] = lens[i];
+    inv[perm[i]] = uint32_t(i);
   }
 }
-__global__ __launch_bounds__(256) void k_unperm_rows(const uint32_t* __restrict__ ids, const uint64_t* __restrict__ in_off,
-                                                     const uint32_t* __restrict__ perm, uint64_t n,
-                                                     const uint64_t* __restrict__ row_off, uint32_t* __restrict__ out) {
-  const uint32_t sub = threadIdx.x & 15u;  // 16 lanes per row, grid-stride (see k_perm_bytes)
-  for (uint64_t i = (uint64_t(blockIdx.x) * 256u + threadIdx.x) >> 4; i < n; i += uint64_t(gridDim.x) * 16u) {
-    const uint64_t a = in_off[i], len = in_off[i + 1] - a, d = row_off[perm[i]];
-    for (uint64_t k = sub; k < len; k += 16) out[d + k] = ids[a + k];
+// output row j = input row inv[j] (k_gather_segs, output-driven: one coalesced write)
+struct UnpermSeg {
+  const uint64_t* in_off;
+  const uint32_t* inv;
+  __device__ __forceinline__ SegSpan at(uint64_t j) const {
+    const uint64_t a = in_off[inv[j]];
+    return {a, in_off[inv[j] + 1] - a};
   }
-}
-
+};
 int unpermute_rows(emqx_gm_ctx* ctx, uint64_t n, const uint32_t* d_perm, const uint32_t* d_lens, const uint32_t* d_ids,
                    uint32_t flags, emqx_gm_csr* out) {
   hipStream_t st = ctx->stream;
   PoolBuf row_off(ctx->pool, (n + 1) * 8), in_off(ctx->pool, (n + 1) * 8), l_out(ctx->pool, n * 8 + 8),
-      l_in(ctx->pool, n * 8 + 8);
-  if (!row_off.p || !in_off.p || !l_out.p || !l_in.p) return set_err(ctx, EMQX_GM_ENOMEM, "unpermute_rows: workspace");
+      l_in(ctx->pool, n * 8 + 8), inv(ctx->pool, n * 4 + 4);
+  if (!row_off.p || !in_off.p || !l_out.p || !l_in.p || !inv.p)
+    return set_err(ctx, EMQX_GM_ENOMEM, "unpermute_rows: workspace");
   if (n) {
     hipLaunchKernelGGL(k_unperm_lens, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, st, d_lens, d_perm, n,
-                       l_out.as<uint64_t>(), l_in.as<uint64_t>());
+                       l_out.as<uint64_t>(), l_in.as<uint64_t>(), inv.as<uint32_t>());
     GM_HIP(ctx, hipGetLastError());
   }
   if (int rc = scan_lengths(ctx, l_out.as<uint64_t>(), n, row_off.as<uint64_t>())) return rc;
@@ -3778,8 +3780,9 @@ int unpermute_rows(emqx_gm_ctx* ctx, uint64_t n, const uint32_t* d_perm, const u
   PoolBuf ids(ctx->pool, nnz * 4 + 16);
   if (!ids.p) return set_err(ctx, EMQX_GM_ENOMEM, "unpermute_rows: ids");
   if (n) {
-    hipLaunchKernelGGL(k_unperm_rows, dim3(grid_groups16(n)), dim3(256), 0, st, d_ids,
-                       in_off.as<uint64_t>(), d_perm, n, row_off.as<uint64_t>(), ids.as<uint32_t>());
+    hipLaunchKernelGGL((k_gather_segs<uint32_t, UnpermSeg>), dim3(gather_blocks(n)), dim3(256), 0, st, d_ids,
+                       UnpermSeg{in_off.as<uint64_t>(), inv.as<uint32_t>()}, n, row_off.as<uint64_t>(),
+                       ids.as<uint32_t>());
     GM_HIP(ctx, hipGetLastError());
   }
   return finish_csr(ctx, n, nnz, row_off, ids, flags & EMQX_GM_DEVICE_IO, out);

@@ -26,6 +26,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "gm_gather.h"
 #include "gm_internal.h"
 #include "../../include/emqx_gm_ext.h"
 
@@ -110,18 +111,15 @@ __global__ __launch_bounds__(256) void k_perm_lens(const uint64_t* __restrict__ 
   const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
   if (i < n) lens[i] = to[perm[i] + 1] - to[perm[i]];
 }
-__global__ __launch_bounds__(256) void k_perm_bytes(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
-                                                    const uint32_t* __restrict__ perm, uint64_t n,
-                                                    const uint64_t* __restrict__ out_off, uint8_t* __restrict__ out) {
-  // 16 lanes per topic copy its bytes, grid-stride: one work-item per byte
-  // lane of every topic (the former wave per topic) passes the dispatch's
-  // 2^32 work-item limit at 67M topics
-  const uint32_t sub = threadIdx.x & 15u;
-  for (uint64_t i = (uint64_t(blockIdx.x) * 256u + threadIdx.x) >> 4; i < n; i += uint64_t(gridDim.x) * 16u) {
-    const uint64_t a = to[perm[i]], len = to[perm[i] + 1] - a, d = out_off[i];
-    for (uint64_t k = sub; k < len; k += 16) out[d + k] = tb[a + k];
+// segment i of the permuted batch = topic perm[i] (k_gather_segs)
+struct PermSeg {
+  const uint64_t* to;
+  const uint32_t* perm;
+  __device__ __forceinline__ SegSpan at(uint64_t i) const {
+    const uint64_t a = to[perm[i]];
+    return {a, to[perm[i] + 1] - a};
   }
-}
+};
 }  // namespace
 
 int route_plan(const uint8_t* fb, const uint64_t* fo, uint64_t n, uint32_t n_shards, uint32_t* shard_out,
@@ -267,8 +265,8 @@ int permute_topics(emqx_gm_ctx* ctx, const uint8_t* d_tb, const uint64_t* d_to, 
                      lens.as<uint64_t>());
   GM_HIP(ctx, hipGetLastError());
   if (int rc = scan_lengths(ctx, lens.as<uint64_t>(), n, d_out_off)) return rc;
-  hipLaunchKernelGGL(k_perm_bytes, dim3(grid_groups16(n)), dim3(256), 0, ctx->stream, d_tb, d_to, d_perm, n, d_out_off,
-                     d_out);
+  hipLaunchKernelGGL((k_gather_segs<uint8_t, PermSeg>), dim3(gather_blocks(n)), dim3(256), 0, ctx->stream, d_tb,
+                     PermSeg{d_to, d_perm}, n, d_out_off, d_out);
   GM_HIP(ctx, hipGetLastError());
   GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return EMQX_GM_OK;

@@ -271,6 +271,51 @@ def test_prefix_shards_each_walk_their_routed_topics(ctx, orc):
     route.release()
 
 
+@pytest.mark.parametrize("shape", ["short", "mixed", "long"])
+def test_permute_and_unpermute_ragged_vs_numpy(ctx, shape):
+    """k_gather_segs (the permute / unpermute copy): random permutations of
+    ragged segments -- 1-byte topics, empty rows, segments at every byte
+    alignment, blocks whose 256 segments pass the 32 KB LDS image (the
+    element-by-element path) -- against numpy."""
+    rng = np.random.default_rng({"short": 1, "mixed": 2, "long": 3}[shape])
+    n = 50_000
+    lens = {"short": rng.integers(1, 12, n), "mixed": np.where(rng.random(n) < 0.02, rng.integers(200, 2000, n),
+                                                                 rng.integers(1, 60, n)),
+            "long": rng.integers(100, 400, n)}[shape].astype(np.uint64)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    tb = rng.integers(0, 256, int(off[-1]) + 64).astype(np.uint8)
+    perm = rng.permutation(n).astype(np.uint32)
+    d_tb, d_to = _to_device(ctx, tb, off)
+    d_perm = ctx.dev_alloc(n * 4)
+    ctx.memcpy_h2d(d_perm, perm, n * 4)
+    d_pb, d_po = ctx.dev_alloc(int(off[-1]) + 64), ctx.dev_alloc((n + 1) * 8)
+    ctx.permute_topics(d_tb, d_to, n, d_perm, d_pb, d_po)
+    pb, po = np.zeros(int(off[-1]), np.uint8), np.zeros(n + 1, np.uint64)
+    ctx.memcpy_d2h(pb, d_pb, len(pb))
+    ctx.memcpy_d2h(po, d_po, 8 * (n + 1))
+    want = np.concatenate([tb[int(off[p]):int(off[p + 1])] for p in perm])
+    assert np.array_equal(po[1:], np.cumsum(lens[perm])) and np.array_equal(pb, want)
+    # rows: input row i (ragged, empty rows included) goes to output row perm[i]
+    rlen = (rng.integers(0, 5, n) * (rng.random(n) < 0.7)).astype(np.uint32)
+    if shape == "long":
+        rlen = rng.integers(0, 300, n).astype(np.uint32)
+    ids = rng.integers(0, 2**32, int(rlen.sum()), dtype=np.uint64).astype(np.uint32)
+    d_l, d_i = ctx.dev_alloc(n * 4), ctx.dev_alloc(max(len(ids), 1) * 4)
+    ctx.memcpy_h2d(d_l, rlen, n * 4)
+    ctx.memcpy_h2d(d_i, ids, len(ids) * 4)
+    back = ctx.unpermute_rows(n, d_perm, d_l, d_i)
+    ro, got = back.to_host()
+    back.free()
+    rin = np.r_[0, np.cumsum(rlen.astype(np.uint64))].astype(np.uint64)
+    inv = np.empty(n, np.int64)
+    inv[perm] = np.arange(n)
+    want_ids = np.concatenate([ids[int(rin[i]):int(rin[i + 1])] for i in inv])
+    assert np.array_equal(np.diff(ro.astype(np.int64)), rlen[inv].astype(np.int64)) and np.array_equal(got, want_ids)
+    for p in (d_tb, d_to, d_perm, d_pb, d_po, d_l, d_i):
+        ctx.dev_free(p)
+
+
 @pytest.mark.timeout(300)
 def test_permute_and_unpermute_past_2_pow_26_rows(ctx):
     """A C5 prefix rank permutes 100M topics: the permute/unpermute launches
