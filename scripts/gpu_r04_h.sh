@@ -7,8 +7,8 @@ export PYTHONUNBUFFERED=1
 export TMPDIR=/tmp
 O=gpurun_out/r04_h
 mkdir -p $O
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --config c5 --plan prefix --filters 1000000 --topics 100000000 --steps 3 --warmup 1 --no-cpu --no-parity > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
-tail -n 1 $O/bench.log
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 -u bench.py --config c5 --plan prefix --filters 1000000 --topics 100000000 --steps 3 --warmup 1 --no-cpu --no-parity > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
+grep "^{" $O/bench.log | tail -n 1
 f=$(find $O/prof -name "*kernel_stats.csv" | head -1)
 cp "$f" $O/kernel_stats.csv
 python3 - <<'PY'
