@@ -89,6 +89,7 @@ SIGNATURES = {
     "emqx_gm_route_topics_host": (_i32, [_vp, _vp, _vp, _u64, _vp]),
     "emqx_gm_route_topics": (_i32, [_vp, _vp, _vp, _vp, _u64, _vp]),
     "emqx_gm_route_release": (_i32, [_vp]),
+    "emqx_gm_route_partition": (_i32, [_vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "emqx_gm_permute_topics": (_i32, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "emqx_gm_unpermute_rows": (_i32, [_vp, _u64, _vp, _vp, _vp, _u32, C.POINTER(Csr)]),
     # emqx_gm_ext.h

@@ -656,6 +656,18 @@ int emqx_gm_route_topics(emqx_gm_ctx* ctx, emqx_gm_route* route, const uint8_t* 
   GM_GUARD_END(ctx)
 }
 
+int emqx_gm_route_partition(emqx_gm_ctx* ctx, emqx_gm_route* route, const uint8_t* d_tb, const uint64_t* d_to,
+                            uint64_t n, uint32_t* d_perm, uint32_t* d_plen, uint64_t* d_split) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (!route || !d_split || (n && (!d_tb || !d_to || !d_perm || !d_plen)))
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "route_partition: NULL argument");
+  GM_GUARD_BEGIN
+  hipSetDevice(ctx->device);
+  return gm::route_partition(ctx, route, d_tb, d_to, n, d_perm, d_plen, d_split);
+  GM_GUARD_END(ctx)
+}
+
 int emqx_gm_route_release(emqx_gm_route* route) {
   if (!route) return EMQX_GM_EINVAL;
   gm::free_route(route);

@@ -257,6 +257,8 @@ int route_plan(const uint8_t* fb, const uint64_t* fo, uint64_t n, uint32_t n_sha
 int route_topics_host(const emqx_gm_route* r, const uint8_t* tb, const uint64_t* to, uint64_t n, uint32_t* dest);
 int route_topics_device(emqx_gm_ctx* ctx, emqx_gm_route* r, const uint8_t* d_tb, const uint64_t* d_to, uint64_t n,
                         uint32_t* d_dest);
+int route_partition(emqx_gm_ctx* ctx, emqx_gm_route* r, const uint8_t* d_tb, const uint64_t* d_to, uint64_t n,
+                    uint32_t* d_perm, uint32_t* d_plen, uint64_t* d_split);
 void free_route(emqx_gm_route* r);
 int permute_topics(emqx_gm_ctx* ctx, const uint8_t* d_tb, const uint64_t* d_to, uint64_t n, const uint32_t* d_perm,
                    uint8_t* d_out, uint64_t* d_out_off);

@@ -105,6 +105,98 @@ __global__ __launch_bounds__(256) void k_route(const RouteSlot* __restrict__ slo
   dest[i] = rt_route(slots, mask, arena, n_shards, tb + a, uint32_t(b - a));
 }
 
+// ---- the send order in one pass pair (emqx_gm_route_partition): a counting
+// sort of the batch by shard, stable in batch order.  A block takes RP_B
+// consecutive topics; pass 1 routes them (dest kept for pass 2) and writes the
+// block's topic and byte counts per shard, shard-major ([s][block]) so ONE
+// exclusive scan of each array gives every (shard, block) its first position;
+// pass 2 ranks each topic among the block's earlier topics of its shard (wave
+// ballots over the shard's 8 bits, then the 16 (round, wave) slots in order)
+// and writes perm / plen at its position.  Replaces a stable radix sort of
+// the shard numbers, a gather of the lengths and two prefix sums.
+constexpr int RP_B = 1024;  // topics per block: 4 rounds of 256
+__global__ __launch_bounds__(256) void k_part_count(const RouteSlot* __restrict__ slots, uint32_t mask,
+                                                    const uint8_t* __restrict__ arena, uint32_t n_shards,
+                                                    const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
+                                                    uint64_t n, uint64_t nblk, uint8_t* __restrict__ dest,
+                                                    uint64_t* __restrict__ cnt, uint64_t* __restrict__ bytes) {
+  __shared__ uint32_t s_c[256];
+  __shared__ unsigned long long s_b[256];
+  const int tid = threadIdx.x;
+  s_c[tid] = 0;
+  s_b[tid] = 0;
+  __syncthreads();
+  const uint64_t b = blockIdx.x;
+  for (int v = 0; v < RP_B / 256; ++v) {
+    const uint64_t i = b * RP_B + uint64_t(v) * 256 + tid;
+    if (i < n) {
+      const uint64_t a = to[i], e = to[i + 1];
+      uint32_t d = rt_route(slots, mask, arena, n_shards, tb + a, uint32_t(e - a));
+      d = d < n_shards ? d : d % n_shards;  // (rt_route returns a shard < n_shards; the LDS tables hold 256)
+      dest[i] = uint8_t(d);
+      atomicAdd(&s_c[d], 1u);
+      atomicAdd(&s_b[d], (unsigned long long)(e - a));
+    }
+  }
+  __syncthreads();
+  if (uint32_t(tid) < n_shards) {
+    cnt[uint64_t(tid) * nblk + b] = s_c[tid];
+    bytes[uint64_t(tid) * nblk + b] = s_b[tid];
+  }
+}
+__global__ __launch_bounds__(256) void k_part_scatter(const uint8_t* __restrict__ dest, const uint64_t* __restrict__ to,
+                                                      uint64_t n, uint64_t nblk, uint32_t n_shards,
+                                                      const uint64_t* __restrict__ pos, uint32_t* __restrict__ perm,
+                                                      uint32_t* __restrict__ plen) {
+  constexpr int SLOTS = RP_B / 64;  // (round, wave) in batch order
+  __shared__ uint32_t s_n[SLOTS][256];
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  for (int k = tid; k < SLOTS * 256; k += 256) (&s_n[0][0])[k] = 0;
+  __syncthreads();
+  const uint64_t b = blockIdx.x;
+  uint32_t d[RP_B / 256], r[RP_B / 256];
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int v = 0; v < RP_B / 256; ++v) {
+    const uint64_t i = b * RP_B + uint64_t(v) * 256 + tid;
+    const bool ok = i < n;
+    d[v] = ok ? dest[i] : 0xFFu;
+    uint64_t peers = __ballot(ok);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const uint64_t m = __ballot((d[v] >> bit) & 1u);
+      peers &= ((d[v] >> bit) & 1u) ? m : ~m;
+    }
+    r[v] = uint32_t(__popcll(peers & lt));
+    if (ok && r[v] == 0) s_n[v * 4 + wv][d[v]] = uint32_t(__popcll(peers));  // the shard's first lane in the wave
+  }
+  __syncthreads();
+  // exclusive prefix over the slots, per shard (thread = shard)
+  if (uint32_t(tid) < n_shards) {
+    uint32_t run = 0;
+    for (int k = 0; k < SLOTS; ++k) {
+      const uint32_t c = s_n[k][tid];
+      s_n[k][tid] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int v = 0; v < RP_B / 256; ++v) {
+    const uint64_t i = b * RP_B + uint64_t(v) * 256 + tid;
+    if (i >= n) continue;
+    const uint64_t p = pos[uint64_t(d[v]) * nblk + b] + s_n[v * 4 + wv][d[v]] + r[v];
+    perm[p] = uint32_t(i);
+    plen[p] = uint32_t(to[i + 1] - to[i]);
+  }
+}
+__global__ void k_part_split(const uint64_t* __restrict__ pos, const uint64_t* __restrict__ bpos, uint64_t nblk,
+                             uint32_t n_shards, uint64_t* __restrict__ split) {
+  const uint32_t s = threadIdx.x;
+  if (s < n_shards) {
+    split[2 * s] = pos[uint64_t(s + 1) * nblk] - pos[uint64_t(s) * nblk];
+    split[2 * s + 1] = bpos[uint64_t(s + 1) * nblk] - bpos[uint64_t(s) * nblk];
+  }
+}
+
 // out topic i = input topic perm[i]: lengths, then (after a scan) the bytes
 __global__ __launch_bounds__(256) void k_perm_lens(const uint64_t* __restrict__ to, const uint32_t* __restrict__ perm,
                                                    uint64_t n, uint64_t* __restrict__ lens) {
@@ -239,6 +331,40 @@ int route_topics_device(emqx_gm_ctx* ctx, emqx_gm_route* r, const uint8_t* d_tb,
   hipLaunchKernelGGL(k_route, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, ctx->stream,
                      static_cast<const RouteSlot*>(dev), uint32_t(r->slots.size() - 1),
                      static_cast<const uint8_t*>(dev) + o_arena, r->n_shards, d_tb, d_to, n, d_dest);
+  GM_HIP(ctx, hipGetLastError());
+  return EMQX_GM_OK;
+}
+
+int route_partition(emqx_gm_ctx* ctx, emqx_gm_route* r, const uint8_t* d_tb, const uint64_t* d_to, uint64_t n,
+                    uint32_t* d_perm, uint32_t* d_plen, uint64_t* d_split) {
+  const uint32_t W = r->n_shards;
+  if (W == 0 || W > 256) return set_err(ctx, EMQX_GM_EUNSUPPORTED, "route_partition: more than 256 shards");
+  if (int rc = route_topics_device(ctx, r, d_tb, d_to, 0, nullptr)) return rc;  // (uploads the route table)
+  const void* dev = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(r->mu);
+    dev = r->dev[ctx->device];
+  }
+  const size_t o_arena = (r->slots.size() * sizeof(RouteSlot) + 255) & ~size_t(255);
+  hipStream_t st = ctx->stream;
+  if (!n) {
+    GM_HIP(ctx, hipMemsetAsync(d_split, 0, 16 * W, st));
+    return EMQX_GM_OK;
+  }
+  const uint64_t nblk = (n + RP_B - 1) / RP_B;
+  PoolBuf dest(ctx->pool, n + 16), cnt(ctx->pool, W * nblk * 8 + 8), byt(ctx->pool, W * nblk * 8 + 8),
+      pos(ctx->pool, (W * nblk + 1) * 8), bpos(ctx->pool, (W * nblk + 1) * 8);
+  if (!dest.p || !cnt.p || !byt.p || !pos.p || !bpos.p) return set_err(ctx, EMQX_GM_ENOMEM, "route_partition: workspace");
+  hipLaunchKernelGGL(k_part_count, dim3(uint32_t(nblk)), dim3(256), 0, st, static_cast<const RouteSlot*>(dev),
+                     uint32_t(r->slots.size() - 1), static_cast<const uint8_t*>(dev) + o_arena, W, d_tb, d_to, n, nblk,
+                     dest.as<uint8_t>(), cnt.as<uint64_t>(), byt.as<uint64_t>());
+  GM_HIP(ctx, hipGetLastError());
+  if (int rc = scan_lengths(ctx, cnt.as<uint64_t>(), W * nblk, pos.as<uint64_t>())) return rc;
+  if (int rc = scan_lengths(ctx, byt.as<uint64_t>(), W * nblk, bpos.as<uint64_t>())) return rc;
+  hipLaunchKernelGGL(k_part_scatter, dim3(uint32_t(nblk)), dim3(256), 0, st, dest.as<uint8_t>(), d_to, n, nblk, W,
+                     pos.as<uint64_t>(), d_perm, d_plen);
+  GM_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(k_part_split, dim3(1), dim3(256), 0, st, pos.as<uint64_t>(), bpos.as<uint64_t>(), nblk, W, d_split);
   GM_HIP(ctx, hipGetLastError());
   return EMQX_GM_OK;
 }

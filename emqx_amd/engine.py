@@ -411,6 +411,13 @@ class Context:
         check(lib().emqx_gm_route_topics(self.h, route.h, C.c_void_p(d_tb), C.c_void_p(d_to), n,
                                          C.c_void_p(d_dest)), self.h, "route_topics")
 
+    def route_partition(self, route: "Route", d_tb: int, d_to: int, n: int, d_perm: int, d_plen: int, d_split: int):
+        """emqx_gm_route_partition: the batch's send order by shard (u32 perm and
+        lengths, n each) and the topics / bytes per shard (u64 pairs)."""
+        check(lib().emqx_gm_route_partition(self.h, route.h, C.c_void_p(d_tb), C.c_void_p(d_to), n,
+                                            C.c_void_p(d_perm), C.c_void_p(d_plen), C.c_void_p(d_split)),
+              self.h, "route_partition")
+
     def permute_topics(self, d_tb: int, d_to: int, n: int, d_perm: int, d_out: int, d_out_off: int):
         check(lib().emqx_gm_permute_topics(self.h, C.c_void_p(d_tb), C.c_void_p(d_to), n, C.c_void_p(d_perm),
                                            C.c_void_p(d_out), C.c_void_p(d_out_off)), self.h, "permute_topics")

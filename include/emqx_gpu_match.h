@@ -301,6 +301,14 @@ int emqx_gm_route_topics_host(const emqx_gm_route *route, const uint8_t *topic_b
 int emqx_gm_route_topics(emqx_gm_ctx *ctx, emqx_gm_route *route, const uint8_t *d_topic_bytes,
                          const uint64_t *d_topic_off, uint64_t n_topics, uint32_t *d_dest);
 int emqx_gm_route_release(emqx_gm_route *route);
+/* The send order of a routed device batch in one call (the step's route, sort
+ * and split sizes): d_perm[i] = the batch index of the i-th topic in order of
+ * (shard, batch index), d_plen[i] = its length in bytes, d_split[2 s] / [2 s + 1]
+ * = the topics / bytes bound for shard s (n_shards <= 256).  Device buffers:
+ * n_topics u32 each, 2 * n_shards u64.  Stream-ordered like the other calls. */
+int emqx_gm_route_partition(emqx_gm_ctx *ctx, emqx_gm_route *route, const uint8_t *d_topic_bytes,
+                            const uint64_t *d_topic_off, uint64_t n_topics, uint32_t *d_perm, uint32_t *d_plen,
+                            uint64_t *d_split);
 /* The exchange's device steps.  permute: out topic i = topic perm[i] (d_out
  * holds as many bytes as the input, d_out_off n+1 entries).  unpermute: row
  * perm[i] of the result = input row i, the input rows packed with u32 lengths

@@ -207,6 +207,41 @@ def test_device_route_equals_host_route(ctx, kind):
         route.release()
 
 
+@pytest.mark.parametrize("kind", ["random", "c1"])
+def test_route_partition_is_a_stable_sort_by_shard(ctx, kind):
+    """emqx_gm_route_partition (a counting sort by shard) == a stable argsort of
+    the host route's shards; the lengths follow the order; the split sizes are
+    the per-shard topic and byte counts.  Batches past one 1,024-topic block,
+    worlds 1 to 256, an empty batch."""
+    from emqx_amd.engine import pack, prefix_plan
+    fs, ts = _sets(kind)
+    fb, fo = pack(fs)
+    ts = ts * max(1, 5000 // max(len(ts), 1))  # several partition blocks
+    tb, to = pack(ts)
+    n = len(to) - 1
+    lens = np.diff(to.astype(np.int64))
+    for world in (1, 2, 3, 8, 256):
+        _, route = prefix_plan(fb, fo, world)
+        want_dest = route.route_host(tb, to).astype(np.int64)
+        order = np.argsort(want_dest, kind="stable")
+        d_tb, d_to = _to_device(ctx, tb, to)
+        d_perm, d_plen, d_split = ctx.dev_alloc(n * 4), ctx.dev_alloc(n * 4), ctx.dev_alloc(16 * world)
+        ctx.route_partition(route, d_tb, d_to, n, d_perm, d_plen, d_split)
+        perm, plen, split = np.zeros(n, np.uint32), np.zeros(n, np.uint32), np.zeros(2 * world, np.uint64)
+        ctx.memcpy_d2h(perm, d_perm, n * 4)
+        ctx.memcpy_d2h(plen, d_plen, n * 4)
+        ctx.memcpy_d2h(split, d_split, 16 * world)
+        assert np.array_equal(perm, order) and np.array_equal(plen, lens[order])
+        assert np.array_equal(split[0::2], np.bincount(want_dest, minlength=world))
+        assert np.array_equal(split[1::2], np.bincount(want_dest, weights=lens, minlength=world).astype(np.uint64))
+        ctx.route_partition(route, d_tb, d_to, 0, d_perm, d_plen, d_split)  # empty batch: zero sizes
+        ctx.memcpy_d2h(split, d_split, 16 * world)
+        assert not split.any()
+        for p in (d_tb, d_to, d_perm, d_plen, d_split):
+            ctx.dev_free(p)
+        route.release()
+
+
 @pytest.mark.timeout(600)
 def test_prefix_shards_each_walk_their_routed_topics(ctx, orc):
     """C5-shaped set (4M mixed filters) in 8 prefix shards built one after
