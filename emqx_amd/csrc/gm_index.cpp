@@ -441,7 +441,11 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       const bool filtered = x_keys[t] >= 4 * x_parents[t] && hot_n[t] <= (1u << 20) && !getenv("GM_MPH_NO_FILTERED");
       if (mt ? !((mask >> t) & 1u) : !(small || filtered)) continue;
       mph_cap[t] = uint32_t(hot_n[t] + hot_n[t] / 32 + 16);
-      mph_nb[t] = uint32_t((hot_n[t] + MPH_LAMBDA - 1) / MPH_LAMBDA);
+      // GM_MPH_LAMBDA (A/B knob): keys per bucket -- fewer bucket words (an L2-resident
+      // table) against a fuller 48-bit Bloom filter and harder displacement searches
+      uint32_t lam = MPH_LAMBDA;
+      if (const char* e = getenv("GM_MPH_LAMBDA")) lam = std::max<uint32_t>(1, std::min<uint32_t>(16, uint32_t(atoi(e))));
+      mph_nb[t] = uint32_t((hot_n[t] + lam - 1) / lam);
       mph_off[t] = mph_total;
       mph_total += mph_nb[t];
     }
