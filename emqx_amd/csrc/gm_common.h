@@ -289,7 +289,7 @@ GM_HD uint64_t hot_slot(uint64_t key, uint64_t cap) {
 // its keys land on distinct free slots (largest buckets first), which fills
 // the region to ~0.97 with ONE probe per lookup: the table is a quarter of its
 // open-addressing size (0.25 load) and stays in each XCD's L2.
-constexpr uint32_t MPH_LAMBDA = 5;     // keys per bucket (1.6 B of bucket word per key; 4 -> 5: C2 -1 %, 3: +2.7 %, profiles/r04_ab/mph_lambda_c2.txt)
+constexpr uint32_t MPH_LAMBDA = 6;     // keys per bucket (1.33 B of bucket word per key; 4 -> 5: C2 -1 %, 3: +2.7 %, 5 -> 6 with keys/16 spare slots: -0.4 %; profiles/r04_ab/mph_lambda_c2.txt)
 GM_HD uint32_t mph_hash(uint64_t key, uint32_t d) {
   uint32_t h = (uint32_t(key >> 32) * 0x7FEB352Du) ^ (uint32_t(key) * 0x846CA68Bu) ^ (d * 0x9E3779B9u);
   h ^= h >> 15;

@@ -440,7 +440,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       const bool small = hot_n[t] >= lo && hot_n[t] <= hi;
       const bool filtered = x_keys[t] >= 4 * x_parents[t] && hot_n[t] <= (1u << 20) && !getenv("GM_MPH_NO_FILTERED");
       if (mt ? !((mask >> t) & 1u) : !(small || filtered)) continue;
-      uint64_t slack = 32;  // GM_MPH_SLACK (A/B knob): spare slots = keys / slack
+      uint64_t slack = 16;  // GM_MPH_SLACK (A/B knob): spare slots = keys / slack (6 keys per bucket need 1/16 to place without overflow)
       if (const char* e = getenv("GM_MPH_SLACK")) slack = std::max<uint64_t>(4, strtoull(e, nullptr, 10));
       mph_cap[t] = uint32_t(hot_n[t] + hot_n[t] / slack + 16);
       // GM_MPH_LAMBDA (A/B knob): keys per bucket -- fewer bucket words (an L2-resident
