@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export PYTHONUNBUFFERED=1
-O=gpurun_out/r04_q
+O=gpurun_out/${QTAG:-r04_q}
 mkdir -p $O
 for plan in prefix hash; do
   timeout -k 10 400 python3 -u bench.py --config c5 --plan $plan --filters 10000000 --topics 100000000 --steps 3 --warmup 1 --no-cpu > $O/bench_c5_${plan}_100m.log 2>&1 || { tail -20 $O/bench_c5_${plan}_100m.log; exit 1; }
