@@ -281,8 +281,10 @@ class PrefixShardedMatcher:
 
         Host round trips per step: ONE device-to-host copy of the outbound
         split sizes (topics and bytes per peer, both directions: the byte total
-        is their sum), the match's own read-back (its match total), and ONE
-        copy of the return split sizes (ids per peer, both directions).  The
+        is their sum), the match's own read-back (its match total), the
+        synchronous device copy of the result ids into the collective's torch
+        buffer, and ONE copy of the return split sizes (ids per peer, both
+        directions).  The
         library and torch's ops run on the matcher's own stream (set in
         __init__), so route, sort, permute, the collectives and the walk are
         ordered by one stream."""
