@@ -31,8 +31,12 @@ class GpuMatchError(RuntimeError):
         super().__init__(f"{ERRNAMES.get(code, code)}: {msg}")
 
 
+MAX_DEVICES = 8
+
+
 class Opts(C.Structure):
-    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("reserved", C.c_uint64 * 7)]
+    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("n_devices", C.c_uint32),
+                ("devices", C.c_int32 * MAX_DEVICES), ("reserved0", C.c_uint32), ("reserved", C.c_uint64 * 2)]
 
 
 class Csr(C.Structure):
@@ -77,6 +81,9 @@ SIGNATURES = {
     "emqx_gm_match": (_i32, [_vp, _vp, _vp, _vp, _u64, _u32, C.POINTER(Csr)]),
     "emqx_gm_match_submit": (_i32, [_vp, _vp, _vp, _vp, _u64, _u32, C.POINTER(_vp)]),
     "emqx_gm_match_wait": (_i32, [_vp, _vp, C.POINTER(Csr)]),
+    "emqx_gm_host_alloc": (_i32, [_vp, _u64, C.POINTER(_vp)]),
+    "emqx_gm_host_free": (_i32, [_vp, _vp]),
+    "emqx_gm_devices": (_i32, [_vp, _vp, C.POINTER(_u32)]),
     "emqx_gm_fanout": (_i32, [_vp, _vp, C.POINTER(Csr), _u32, C.POINTER(Csr)]),
     "emqx_gm_csr_free": (_i32, [_vp, C.POINTER(Csr)]),
     "emqx_gm_last_stats": (_i32, [_vp, C.POINTER(MatchStats)]),

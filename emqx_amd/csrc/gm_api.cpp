@@ -87,23 +87,33 @@ void DevPool::reclaim(bool wait) {
 // past emqx_gm_close, so they are detached and leak as plain malloc'd memory
 // (what the CSRs were before the pool existed).
 HostPool::~HostPool() {
-  for (auto& kv : free_) free(kv.second);
+  for (int k = 0; k < 2; ++k)
+    for (auto& kv : free_[k]) drop(kv.second, k != 0);
 }
-void* HostPool::alloc(size_t bytes) {
+void HostPool::drop(void* p, bool pinned) {
+  if (pinned) (void)hipHostFree(p);
+  else free(p);
+}
+void* HostPool::alloc(size_t bytes, bool pinned) {
   constexpr size_t HUGE_PAGE = 2u << 20;
   const size_t r = bytes < HUGE_PAGE ? ((bytes + 4095) & ~size_t(4095)) : ((bytes + HUGE_PAGE - 1) & ~(HUGE_PAGE - 1));
-  auto it = free_.lower_bound(r);
-  if (it != free_.end() && it->first <= r + r / 4) {
+  auto& fl = free_[pinned ? 1 : 0];
+  auto it = fl.lower_bound(r);
+  if (it != fl.end() && it->first <= r + r / 4) {
     void* p = it->second;
     cached_ -= it->first;
-    live_[p] = it->first;
-    free_.erase(it);
+    live_[p] = Buf{it->first, pinned};
+    fl.erase(it);
     return p;
   }
   void* p = nullptr;
-  if (posix_memalign(&p, r >= HUGE_PAGE ? HUGE_PAGE : 64, r) != 0) return nullptr;
-  if (r >= HUGE_PAGE) (void)madvise(p, r, MADV_HUGEPAGE);
-  live_[p] = r;  // overwrite: an address freed behind the pool's back may come back
+  if (pinned) {
+    if (hipHostMalloc(&p, r, hipHostMallocPortable) != hipSuccess) return nullptr;
+  } else {
+    if (posix_memalign(&p, r >= HUGE_PAGE ? HUGE_PAGE : 64, r) != 0) return nullptr;
+    if (r >= HUGE_PAGE) (void)madvise(p, r, MADV_HUGEPAGE);
+  }
+  live_[p] = Buf{r, pinned};  // overwrite: an address freed behind the pool's back may come back
   return p;
 }
 void HostPool::release(void* p) {
@@ -113,20 +123,46 @@ void HostPool::release(void* p) {
     free(p);
     return;
   }
-  const size_t r = it->second;
+  const size_t r = it->second.bytes;
+  const bool pinned = it->second.pinned;
   live_.erase(it);
-  while (cached_ + r > kCap && !free_.empty()) {  // the largest cached ones go first
-    auto last = std::prev(free_.end());
+  for (;;) {  // the largest cached ones go first
+    auto* big = &free_[0];
+    if (free_[0].empty() || (!free_[1].empty() && std::prev(free_[1].end())->first > std::prev(free_[0].end())->first))
+      big = &free_[1];
+    if (cached_ + r <= kCap || big->empty()) break;
+    auto last = std::prev(big->end());
     cached_ -= last->first;
-    free(last->second);
-    free_.erase(last);
+    drop(last->second, big == &free_[1]);
+    big->erase(last);
   }
   if (r > kCap) {
-    free(p);
+    drop(p, pinned);
     return;
   }
-  free_.emplace(r, p);
+  free_[pinned ? 1 : 0].emplace(r, p);
   cached_ += r;
+}
+
+namespace {
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pinned;  // emqx_gm_host_alloc buffers: start -> bytes
+}  // namespace
+bool host_pinned_range(const void* p, size_t bytes) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pinned.upper_bound(a);
+  if (it == g_pinned.begin()) return false;
+  --it;
+  return a >= it->first && a - it->first <= it->second && bytes <= it->second - (a - it->first);
+}
+void host_pinned_add(void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pinned[reinterpret_cast<uintptr_t>(p)] = bytes;
+}
+bool host_pinned_remove(void* p) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  return g_pinned.erase(reinterpret_cast<uintptr_t>(p)) != 0;
 }
 
 static size_t round_size(size_t b) {
@@ -207,41 +243,111 @@ extern "C" {
 
 int emqx_gm_abi_version(void) { return EMQX_GM_ABI_VERSION; }
 
-int emqx_gm_open(const emqx_gm_opts* opts, emqx_gm_ctx** out) {
-  if (!out) return EMQX_GM_EINVAL;
-  *out = nullptr;
-  GM_GUARD_BEGIN
-  int dev = opts ? opts->device : 0;
-  int count = 0;
-  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return EMQX_GM_EDEVICE;
-  if (dev < 0 || dev >= count) return EMQX_GM_EINVAL;
+static int open_one(int dev, uint32_t flags, emqx_gm_ctx** out) {
   if (hipSetDevice(dev) != hipSuccess) return EMQX_GM_EDEVICE;
-  if (opts && (opts->flags & ~(EMQX_GM_OPEN_MIRROR_EAGER | EMQX_GM_OPEN_MIRROR_LAZY))) return EMQX_GM_EINVAL;
-  if (opts && (opts->flags & EMQX_GM_OPEN_MIRROR_EAGER) && (opts->flags & EMQX_GM_OPEN_MIRROR_LAZY))
-    return EMQX_GM_EINVAL;
   auto* ctx = new emqx_gm_ctx;
   ctx->device = dev;
-  ctx->open_flags = opts ? opts->flags : 0;
+  ctx->open_flags = flags;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return EMQX_GM_EDEVICE;
   }
   ctx->own_stream = true;
+  ctx->pool = new gm::DevPool(dev);
+  ctx->hpool = new gm::HostPool;
   for (auto& e : ctx->ev) {
     if (hipEventCreate(&e) != hipSuccess) {
-      delete ctx;
+      emqx_gm_close(ctx);
       return EMQX_GM_EDEVICE;
     }
   }
-  ctx->pool = new gm::DevPool(dev);
-  ctx->hpool = new gm::HostPool;
+  *out = ctx;
+  return EMQX_GM_OK;
+}
+
+int emqx_gm_open(const emqx_gm_opts* opts, emqx_gm_ctx** out) {
+  if (!out) return EMQX_GM_EINVAL;
+  *out = nullptr;
+  GM_GUARD_BEGIN
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return EMQX_GM_EDEVICE;
+  if (opts && (opts->flags & ~(EMQX_GM_OPEN_MIRROR_EAGER | EMQX_GM_OPEN_MIRROR_LAZY))) return EMQX_GM_EINVAL;
+  if (opts && (opts->flags & EMQX_GM_OPEN_MIRROR_EAGER) && (opts->flags & EMQX_GM_OPEN_MIRROR_LAZY))
+    return EMQX_GM_EINVAL;
+  std::vector<int> devs;
+  if (opts && opts->n_devices) {
+    if (opts->n_devices > EMQX_GM_MAX_DEVICES) return EMQX_GM_EINVAL;
+    devs.assign(opts->devices, opts->devices + opts->n_devices);
+  } else {
+    devs.push_back(opts ? opts->device : 0);
+  }
+  for (int d : devs)
+    if (d < 0 || d >= count) return EMQX_GM_EINVAL;
+  const uint32_t flags = opts ? opts->flags : 0;
+  emqx_gm_ctx* ctx = nullptr;
+  if (int rc = open_one(devs[0], flags, &ctx)) return rc;
+  for (size_t k = 1; k < devs.size(); ++k) {
+    emqx_gm_ctx* m = nullptr;
+    if (int rc = open_one(devs[k], flags, &m)) {
+      emqx_gm_close(ctx);
+      return rc;
+    }
+    ctx->members.push_back(m);
+    // replicas are copied GPU to GPU: peer access lets the copy engines go over
+    // xGMI directly (already enabled, or unsupported: the runtime stages it)
+    if (devs[k] != devs[0]) {
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, devs[k], devs[0]) == hipSuccess && can) {
+        hipSetDevice(devs[k]);
+        (void)hipDeviceEnablePeerAccess(devs[0], 0);
+        (void)hipGetLastError();  // (hipErrorPeerAccessAlreadyEnabled is fine)
+      }
+    }
+  }
+  hipSetDevice(devs[0]);
   *out = ctx;
   return EMQX_GM_OK;
   GM_GUARD_END(nullptr)
 }
 
+int emqx_gm_devices(const emqx_gm_ctx* ctx, int32_t* devices, uint32_t* n) {
+  if (!ctx || !n) return EMQX_GM_EINVAL;
+  *n = uint32_t(1 + ctx->members.size());
+  if (devices) {
+    devices[0] = ctx->device;
+    for (size_t k = 0; k < ctx->members.size(); ++k) devices[k + 1] = ctx->members[k]->device;
+  }
+  return EMQX_GM_OK;
+}
+
+int emqx_gm_host_alloc(emqx_gm_ctx* ctx, uint64_t bytes, void** p) {
+  if (!ctx || !p) return EMQX_GM_EINVAL;
+  *p = nullptr;
+  hipSetDevice(ctx->device);
+  void* q = nullptr;
+  const hipError_t e = hipHostMalloc(&q, bytes ? bytes : 1, hipHostMallocPortable);
+  if (e != hipSuccess) return gm::set_err(ctx, EMQX_GM_ENOMEM, std::string("host_alloc: ") + hipGetErrorString(e));
+  GM_GUARD_BEGIN
+  gm::host_pinned_add(q, bytes);
+  *p = q;
+  return EMQX_GM_OK;
+  GM_GUARD_END(ctx)
+}
+
+int emqx_gm_host_free(emqx_gm_ctx* ctx, void* p) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  if (!p) return EMQX_GM_OK;
+  if (!gm::host_pinned_remove(p)) return gm::set_err(ctx, EMQX_GM_EINVAL, "host_free: not an emqx_gm_host_alloc buffer");
+  // (a match call in flight on another thread may still read it: the caller's
+  // business, as for any input buffer)
+  GM_HIP(ctx, hipHostFree(p));
+  return EMQX_GM_OK;
+}
+
 int emqx_gm_close(emqx_gm_ctx* ctx) {
   if (!ctx) return EMQX_GM_EINVAL;
+  for (emqx_gm_ctx* m : ctx->members) emqx_gm_close(m);
+  ctx->members.clear();
   {
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     hipSetDevice(ctx->device);
@@ -296,10 +402,22 @@ int emqx_gm_set_stream(emqx_gm_ctx* ctx, void* s) {
 int emqx_gm_synchronize(emqx_gm_ctx* ctx) {
   if (!ctx) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  for (emqx_gm_ctx* m : ctx->members) {
+    hipSetDevice(m->device);
+    GM_HIP(ctx, hipStreamSynchronize(m->stream));
+  }
   hipSetDevice(ctx->device);
   GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->stream_asm) GM_HIP(ctx, hipStreamSynchronize(ctx->stream_asm));
   return EMQX_GM_OK;
+}
+
+// A snapshot made on a multi-device context gets its replicas (gm_multi.cpp);
+// `redo` repeats the call on a member for a result that cannot be copied.
+static int replicated(emqx_gm_ctx* ctx, int rc, emqx_gm_index* prev, emqx_gm_index** out,
+                      const std::function<int(emqx_gm_ctx*, emqx_gm_index*, emqx_gm_index**)>& redo = nullptr) {
+  if (rc || ctx->members.empty() || !out || !*out) return rc;
+  return gm::replicate_result(ctx, prev, out, redo);
 }
 
 int emqx_gm_index_build(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_t n,
@@ -309,7 +427,7 @@ int emqx_gm_index_build(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo,
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
-  return gm::build_index(ctx, fb, fo, n, sub_off, sub_ids, perm_out, out);
+  return replicated(ctx, gm::build_index(ctx, fb, fo, n, sub_off, sub_ids, perm_out, out), nullptr, out);
   GM_GUARD_END(ctx)
 }
 
@@ -321,7 +439,11 @@ int emqx_gm_index_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* f
     return gm::set_err(ctx, EMQX_GM_EINVAL, "index_update: index lives on another device");
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
-  return gm::update_index(ctx, prev, fb, fo, ops, n_ops, out);
+  return replicated(ctx, gm::update_index(ctx, prev, fb, fo, ops, n_ops, out), prev, out,
+                    [&](emqx_gm_ctx* m, emqx_gm_index* p, emqx_gm_index** o) {
+                      hipSetDevice(m->device);
+                      return gm::update_index(m, p, fb, fo, ops, n_ops, o);
+                    });
   GM_GUARD_END(ctx)
 }
 
@@ -333,7 +455,11 @@ int emqx_gm_index_update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8
     return gm::set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: index lives on another device");
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
-  return gm::update_subs(ctx, prev, fb, fo, subs, ops, n_ops, out);
+  return replicated(ctx, gm::update_subs(ctx, prev, fb, fo, subs, ops, n_ops, out), prev, out,
+                    [&](emqx_gm_ctx* m, emqx_gm_index* p, emqx_gm_index** o) {
+                      hipSetDevice(m->device);
+                      return gm::update_subs(m, p, fb, fo, subs, ops, n_ops, o);
+                    });
   GM_GUARD_END(ctx)
 }
 
@@ -358,7 +484,8 @@ int emqx_gm_index_import(emqx_gm_ctx* ctx, const uint8_t* image, uint64_t size, 
   if (!ctx) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   GM_GUARD_BEGIN
-  return gm::index_import(ctx, image, size, d_blob, out);
+  hipSetDevice(ctx->device);
+  return replicated(ctx, gm::index_import(ctx, image, size, d_blob, out), nullptr, out);
   GM_GUARD_END(ctx)
 }
 
@@ -600,7 +727,8 @@ int emqx_gm_index_build_shard(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_
   if (n && !global_ids) return gm::set_err(ctx, EMQX_GM_EINVAL, "index_build_shard: global_ids is NULL");
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
-  return gm::build_index(ctx, fb, fo, n, sub_off, sub_ids, perm_out, out, nullptr, global_ids);
+  return replicated(ctx, gm::build_index(ctx, fb, fo, n, sub_off, sub_ids, perm_out, out, nullptr, global_ids),
+                    nullptr, out);
   GM_GUARD_END(ctx)
 }
 

@@ -92,7 +92,7 @@ struct Pinned {
     p = nullptr;
     cap = 0;
     const size_t nb = std::max(b, size_t(1) << 20);
-    if (hipHostMalloc(&p, nb, hipHostMallocDefault) != hipSuccess) return false;
+    if (hipHostMalloc(&p, nb, hipHostMallocPortable) != hipSuccess) return false;
     cap = nb;
     return true;
   }
@@ -127,8 +127,11 @@ struct Slot {
   Pinned in_b, in_o, out_o, out_i;  // text, u32 offsets in; u32 row offsets, ids out
   Device d_b, d_o32, d_o64, d_r32;  // text, offsets u32 -> u64 in; row offsets u32 out
   hipEvent_t h2d = nullptr, comp = nullptr, d2h = nullptr;
-  std::vector<std::future<void>> out_f;  // this slot's last unpack
-  emqx_gm_csr csr{};                     // device rows of the chunk in flight
+  std::vector<std::future<void>> stage_f;  // this slot's staging (run_host_pipe)
+  std::vector<std::future<void>> out_f;    // this slot's last unpack
+  emqx_gm_csr csr{};                       // device rows of the chunk in flight
+  void* call = nullptr;                    // its match call until waited (run_host_pipe)
+  bool d2h_pending = false;                // its rows' copy-out is queued (run_host_pipe)
   uint64_t c0 = 0, nc = 0, nbytes = 0, nnz = 0;
 };
 
@@ -167,11 +170,12 @@ void free_host_pipe(emqx_gm_ctx* ctx) {
   ctx->host = nullptr;
 }
 
-static int host_pipe(emqx_gm_ctx* ctx, HostPipe** out) {
+static int host_pipe(emqx_gm_ctx* ctx, HostPipe** out, bool workers = true) {
   if (!ctx->host) {
     auto* hp = new HostPipe;
     hp->device = ctx->device;
     ctx->host = hp;
+    hipSetDevice(ctx->device);
     if (hipStreamCreateWithFlags(&hp->h2d, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&hp->d2h, hipStreamNonBlocking) != hipSuccess)
       return set_err(ctx, EMQX_GM_EDEVICE, "match: host pipe streams");
@@ -179,15 +183,21 @@ static int host_pipe(emqx_gm_ctx* ctx, HostPipe** out) {
       for (hipEvent_t* e : {&s.h2d, &s.comp, &s.d2h})
         if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
           return set_err(ctx, EMQX_GM_EDEVICE, "match: host pipe events");
+  }
+  if (workers && !ctx->host->w) {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    hp->w.reset(new Workers(unsigned(std::max<uint64_t>(1, env_u64("GM_HOST_THREADS", std::min(16u, hw))))));
+    ctx->host->w.reset(new Workers(unsigned(std::max<uint64_t>(1, env_u64("GM_HOST_THREADS", std::min(16u, hw))))));
   }
   *out = ctx->host;
   return 0;
 }
 
-int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
-                   uint32_t flags, emqx_gm_csr* out) {
+// One device, the chunks matched one after another (run_match per chunk, its
+// rows unpacked by the workers).  The path of a one-chunk call (the small
+// batches a NIF sends): its rows' copy-out rides the call's one host round
+// trip (MatchTail); GM_HOST_PIPE=serial forces it for any batch (A/B).
+static int run_host_serial(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to,
+                           uint64_t n, uint32_t flags, emqx_gm_csr* out) {
   HostPipe* hp = nullptr;
   int rc = host_pipe(ctx, &hp);
   if (rc) return rc;
@@ -436,6 +446,350 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
   out->on_device = 0;
   out->priv = ctx;  // the owning context (emqx_gm_csr_free checks it)
   return 0;
+}
+
+// The pipelined path: the chunks of one call spread over the context's
+// devices (chunk i on device i mod K, K = 1 + the members the index has
+// replicas on), each device with its own streams and slots, up to
+// PIPE_DEPTH chunks in flight per device.  Per chunk:
+//   workers      offsets validated and rebased to u32 (and the text copied
+//                into pinned staging, unless it already lies in an
+//                emqx_gm_host_alloc buffer: then it is sent from there)
+//   h2d stream   text + offsets to the device
+//   ctx stream   u32 -> u64 offsets, the match call queued (match_submit)
+//   host         the call waited for IN BATCH ORDER (match_wait), so the
+//                rows before it are known: its base
+//   d2h stream   row offsets + base (on the device), then rows and ids by
+//                DMA straight into the caller's result at their final place
+//                -- the result is page-locked (the context's host pool), so
+//                no host thread copies a row
+// A result that cannot be page-locked falls back to pinned bounce buffers
+// unpacked by the workers (the serial path's way).
+constexpr int PIPE_DEPTH = 2;
+
+static int run_host_pipe(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to,
+                         uint64_t n, uint32_t flags, const std::vector<emqx_gm_ctx*>& mem,
+                         const std::vector<const emqx_gm_index*>& rix, const std::vector<uint64_t>& cb,
+                         emqx_gm_csr* out) {
+  const int K = int(mem.size());
+  const int m = int(cb.size()) - 1;
+  std::vector<HostPipe*> hps(K);
+  for (int k = 0; k < K; ++k)
+    if (int rc = host_pipe(mem[k], &hps[k], k == 0)) return rc;
+  hipSetDevice(ctx->device);
+  Workers& W = *hps[0]->w;
+  const unsigned T = W.size();
+  const bool direct_in = host_pinned_range(tb + to[0], to[n] - to[0]);
+  // the caller-visible result, page-locked when the host allows it
+  uint64_t ids_cap = std::max<uint64_t>(1024, uint64_t(double(n) * std::max(4.0, 1.25 * ctx->ids_per_topic)));
+  // (GM_HOST_BOUNCE / GM_HOST_WIDE_ROWS: the bounce-buffer output, the latter
+  // with u64 row offsets over PCIe -- tests and A/Bs)
+  const bool wide_rows = env_u64("GM_HOST_WIDE_ROWS", 0) != 0;
+  bool direct_out = !env_u64("GM_HOST_BOUNCE", 0) && !wide_rows;
+  uint64_t* r_off = nullptr;
+  uint32_t* r_ids = nullptr;
+  if (direct_out) {
+    r_off = static_cast<uint64_t*>(ctx->hpool->alloc((n + 1) * 8, true));
+    r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(ids_cap * 4, true));
+    if (!r_off || !r_ids) {
+      ctx->hpool->release(r_off);
+      ctx->hpool->release(r_ids);
+      r_off = nullptr;
+      r_ids = nullptr;
+      direct_out = false;
+    }
+  }
+  if (!direct_out) {
+    r_off = static_cast<uint64_t*>(ctx->hpool->alloc((n + 1) * 8));
+    r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(ids_cap * 4));
+  }
+  if (!r_off || !r_ids) {
+    ctx->hpool->release(r_off);
+    ctx->hpool->release(r_ids);
+    return set_err(ctx, EMQX_GM_ENOMEM, "match: host result");
+  }
+  auto dev_of = [&](int i) { return i % K; };
+  auto slot_of = [&](int i) -> Slot& { return hps[i % K]->slot[(i / K) % SLOTS]; };
+  std::atomic<int> bad{0};
+  emqx_gm_match_stats tot{};
+  tot.n_topics = n;
+  uint64_t base = 0;
+
+  // a slot's previous chunk done: its copy-out landed, its unpack ran, its device rows back to the pool
+  auto retire = [&](int k, Slot& s) {
+    join(s.stage_f);
+    if (s.call) {  // (an abandoned call: only on the failure path)
+      emqx_gm_csr c{};
+      hipSetDevice(mem[k]->device);
+      (void)match_wait(mem[k], s.call, &c);
+      s.call = nullptr;
+      if (c.row_off || c.ids) s.csr = c;
+    }
+    if (s.d2h_pending) {
+      hipEventSynchronize(s.d2h);
+      s.d2h_pending = false;
+    }
+    join(s.out_f);
+    if (s.csr.row_off || s.csr.ids) {
+      mem[k]->pool->release(s.csr.row_off);
+      mem[k]->pool->release(s.csr.ids);
+      s.csr = emqx_gm_csr{};
+    }
+  };
+  auto fail = [&](int code, const char* msg) {
+    for (int k = 0; k < K; ++k) {
+      for (auto& s : hps[k]->slot) retire(k, s);
+      hipSetDevice(mem[k]->device);
+      hipStreamSynchronize(hps[k]->h2d);
+      hipStreamSynchronize(mem[k]->stream);
+      hipStreamSynchronize(hps[k]->d2h);
+    }
+    hipSetDevice(ctx->device);
+    ctx->hpool->release(r_off);
+    ctx->hpool->release(r_ids);
+    return msg ? set_err(ctx, code, msg) : code;  // nullptr: keep the message of the failing step
+  };
+
+  // chunk i's staging: the slot retired, buffers sized, the worker jobs queued
+  auto stage = [&](int i) -> int {
+    const int k = dev_of(i);
+    Slot& s = slot_of(i);
+    retire(k, s);
+    hipSetDevice(mem[k]->device);
+    hipEventSynchronize(s.h2d);  // (its last send has read the pinned input)
+    s.c0 = cb[i];
+    s.nc = cb[i + 1] - cb[i];
+    s.nbytes = to[cb[i + 1]] - to[cb[i]];
+    if ((!direct_in && !s.in_b.reserve(s.nbytes + 64)) || !s.in_o.reserve((s.nc + 1) * 4) ||
+        !s.d_b.reserve(s.nbytes + 64) || !s.d_o32.reserve((s.nc + 1) * 4) || !s.d_o64.reserve((s.nc + 1) * 8) ||
+        (!direct_out && (!s.d_r32.reserve((s.nc + 1) * 4) || !s.out_o.reserve((s.nc + 1) * 4)))) {
+      hipSetDevice(ctx->device);
+      return EMQX_GM_ENOMEM;
+    }
+    hipSetDevice(ctx->device);
+    const uint64_t c0 = s.c0, nc = s.nc, b0 = to[c0], b1 = to[c0 + nc];
+    uint32_t* o = s.in_o.as<uint32_t>();
+    uint8_t* b = direct_in ? nullptr : s.in_b.as<uint8_t>();
+    const uint64_t parts = nc < 65536 ? 1 : T;
+    for (uint64_t p = 0; p < parts; ++p) {
+      const uint64_t a = c0 + nc * p / parts, e = c0 + nc * (p + 1) / parts;
+      s.stage_f.push_back(W.submit([=, &bad] {
+        for (uint64_t j = a; j < e; ++j) {
+          if (to[j + 1] < to[j]) {
+            bad.store(1);
+            return;
+          }
+          o[j - c0] = uint32_t(to[j] - b0);
+        }
+        if (to[a] < b0 || to[e] > b1) {  // inside the chunk's text (plan() checked b0 <= b1)
+          bad.store(1);
+          return;
+        }
+        if (b && e > a) std::memcpy(b + (to[a] - b0), tb + to[a], to[e] - to[a]);
+        if (e == c0 + nc) {
+          o[nc] = uint32_t(to[e] - b0);
+          if (b) std::memset(b + (to[e] - b0), 0, 64);
+        }
+      }));
+    }
+    return 0;
+  };
+  // chunk i to its device (h2d stream)
+  auto send = [&](int i) -> int {
+    const int k = dev_of(i);
+    Slot& s = slot_of(i);
+    join(s.stage_f);
+    if (bad.load()) return EMQX_GM_EINVAL;
+    hipStream_t h = hps[k]->h2d;
+    hipSetDevice(mem[k]->device);
+    hipError_t e;
+    if (direct_in) {
+      e = s.nbytes ? hipMemcpyAsync(s.d_b.p, tb + to[s.c0], s.nbytes, hipMemcpyHostToDevice, h) : hipSuccess;
+      if (e == hipSuccess) e = hipMemsetAsync(s.d_b.as<uint8_t>() + s.nbytes, 0, 64, h);
+    } else {
+      e = hipMemcpyAsync(s.d_b.p, s.in_b.p, s.nbytes + 64, hipMemcpyHostToDevice, h);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(s.d_o32.p, s.in_o.p, (s.nc + 1) * 4, hipMemcpyHostToDevice, h);
+    if (e == hipSuccess) e = hipEventRecord(s.h2d, h);
+    hipSetDevice(ctx->device);
+    return e == hipSuccess ? 0 : EMQX_GM_EDEVICE;
+  };
+  // chunk i's match queued on its device
+  auto submit = [&](int i) -> int {
+    const int k = dev_of(i);
+    Slot& s = slot_of(i);
+    emqx_gm_ctx* mc = mem[k];
+    hipSetDevice(mc->device);
+    int rc = 0;
+    {
+      std::lock_guard<std::recursive_mutex> lk(mc->mu);
+      if (hipStreamWaitEvent(mc->stream, s.h2d, 0) != hipSuccess ||
+          launch_off32_to_64(mc->stream, s.d_o32.as<uint32_t>(), s.nc + 1, s.d_o64.as<uint64_t>()))
+        rc = set_err(ctx, EMQX_GM_EDEVICE, "match: offsets to device");
+      else
+        rc = match_submit(mc, rix[k], s.d_b.as<uint8_t>(), s.d_o64.as<uint64_t>(), s.nc, flags | EMQX_GM_DEVICE_IO,
+                          &s.call);
+    }
+    hipSetDevice(ctx->device);
+    return rc;
+  };
+  // chunk i waited for (batch order), its rows sent to their place in the result
+  auto finish = [&](int i) -> int {
+    const int k = dev_of(i);
+    Slot& s = slot_of(i);
+    emqx_gm_ctx* mc = mem[k];
+    hipSetDevice(mc->device);
+    void* call = s.call;
+    s.call = nullptr;
+    int rc = match_wait(mc, call, &s.csr);
+    if (rc) {
+      hipSetDevice(ctx->device);
+      return rc;
+    }
+    const emqx_gm_match_stats& cs = mc->stats;
+    tot.nnz += cs.nnz;
+    tot.n_overflow += cs.n_overflow;
+    tot.n_wildcard_topics += cs.n_wildcard_topics;
+    tot.probes += cs.probes;
+    tot.match_kernel_ms += cs.match_kernel_ms;
+    tot.total_device_ms += cs.total_device_ms;
+    s.nnz = s.csr.nnz;
+    if (base + s.nnz > ids_cap) {  // grow the result: nothing may be writing it meanwhile
+      for (int q = 0; q < K; ++q)
+        for (auto& z : hps[q]->slot) {
+          if (z.d2h_pending) {
+            hipEventSynchronize(z.d2h);
+            z.d2h_pending = false;
+          }
+          join(z.out_f);
+        }
+      uint64_t ncap = ids_cap;
+      while (ncap < base + s.nnz) ncap *= 2;
+      uint32_t* g = static_cast<uint32_t*>(ctx->hpool->alloc(ncap * 4, direct_out));
+      if (!g) {
+        hipSetDevice(ctx->device);
+        return set_err(ctx, EMQX_GM_ENOMEM, "match: host result grow");
+      }
+      if (base) std::memcpy(g, r_ids, base * 4);
+      ctx->hpool->release(r_ids);
+      r_ids = g;
+      ids_cap = ncap;
+    }
+    hipStream_t d = hps[k]->d2h;  // (the call is complete: no event to wait for)
+    hipError_t e = hipSuccess;
+    if (direct_out) {
+      if (launch_add_u64(d, s.csr.row_off, s.nc, base)) e = hipErrorLaunchFailure;
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(r_off + s.c0, s.csr.row_off, s.nc * 8, hipMemcpyDeviceToHost, d);
+      if (e == hipSuccess && s.nnz) e = hipMemcpyAsync(r_ids + base, s.csr.ids, s.nnz * 4, hipMemcpyDeviceToHost, d);
+      if (e == hipSuccess) e = hipEventRecord(s.d2h, d);
+    } else {
+      const bool wide = s.nnz > 0xFFFFFFFFull || wide_rows;
+      if (!s.out_i.reserve(s.nnz * 4 + 4) || !s.out_o.reserve((s.nc + 1) * (wide ? 8 : 4))) {
+        hipSetDevice(ctx->device);
+        return set_err(ctx, EMQX_GM_ENOMEM, "match: pinned rows");
+      }
+      if (!wide && launch_off64_to_32(d, s.csr.row_off, s.nc + 1, s.d_r32.as<uint32_t>())) e = hipErrorLaunchFailure;
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(s.out_o.p, wide ? static_cast<void*>(s.csr.row_off) : s.d_r32.p,
+                           (s.nc + 1) * (wide ? 8 : 4), hipMemcpyDeviceToHost, d);
+      if (e == hipSuccess && s.nnz) e = hipMemcpyAsync(s.out_i.p, s.csr.ids, s.nnz * 4, hipMemcpyDeviceToHost, d);
+      if (e == hipSuccess) e = hipEventRecord(s.d2h, d);
+      if (e == hipSuccess) {
+        const uint64_t parts = s.nc < 65536 ? 1 : T;
+        const uint32_t* ro = s.out_o.as<uint32_t>();
+        const uint64_t* ro64 = s.out_o.as<uint64_t>();
+        const uint32_t* ri = s.out_i.as<uint32_t>();
+        const hipEvent_t ev = s.d2h;
+        const uint64_t sc0 = s.c0, snc = s.nc, sbase = base;
+        uint32_t* dst_ids = r_ids;
+        for (uint64_t p = 0; p < parts; ++p) {
+          const uint64_t a = snc * p / parts, z = snc * (p + 1) / parts;
+          s.out_f.push_back(W.submit([=] {
+            hipEventSynchronize(ev);
+            auto row = [&](uint64_t j) -> uint64_t { return wide ? ro64[j] : uint64_t(ro[j]); };
+            for (uint64_t j = a; j < z; ++j) r_off[sc0 + j] = sbase + row(j);
+            if (z > a) std::memcpy(dst_ids + sbase + row(a), ri + row(a), (row(z) - row(a)) * 4);
+          }));
+        }
+      }
+    }
+    hipSetDevice(ctx->device);
+    if (e != hipSuccess) return set_err(ctx, EMQX_GM_EDEVICE, "match: rows to host");
+    s.d2h_pending = true;
+    base += s.nnz;
+    return 0;
+  };
+
+  auto pipe_err = [](int code) {
+    return code == EMQX_GM_EINVAL ? "match: topic offsets not monotone"
+                                  : code == EMQX_GM_ENOMEM ? "match: pinned staging" : "match: host pipe copy";
+  };
+  int ns = 0, nh = 0, nu = 0;  // next chunk to stage, to send, to submit
+  for (int i = 0; i < m; ++i) {
+    const int lim = std::min(m, i + K * PIPE_DEPTH);
+    while (nu < lim) {
+      while (nh <= nu) {
+        while (ns < std::min(m, nh + K + 1))
+          if (int rc = stage(ns++)) return fail(rc, pipe_err(rc));
+        if (int rc = send(nh++)) return fail(rc, pipe_err(rc));
+      }
+      if (int rc = submit(nu++)) return fail(rc, nullptr);
+    }
+    if (int rc = finish(i)) return fail(rc, nullptr);
+  }
+  for (int k = 0; k < K; ++k)
+    for (auto& s : hps[k]->slot) retire(k, s);
+  hipSetDevice(ctx->device);
+  r_off[n] = base;
+  tot.nnz = base;
+  ctx->stats = tot;
+  out->n_rows = n;
+  out->nnz = base;
+  out->row_off = r_off;
+  out->ids = r_ids;
+  out->on_device = 0;
+  out->priv = ctx;  // the owning context (emqx_gm_csr_free checks it)
+  return 0;
+}
+
+int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                   uint32_t flags, emqx_gm_csr* out) {
+  // the devices: this context, then the members the index has replicas on
+  std::vector<emqx_gm_ctx*> mem{ctx};
+  std::vector<const emqx_gm_index*> rix{idx};
+  for (size_t k = 0; k < ctx->members.size() && k < idx->reps.size(); ++k) {
+    mem.push_back(ctx->members[k]);
+    rix.push_back(idx->reps[k]);
+  }
+  const uint64_t K = mem.size();
+  // chunks: ~6 per device and call (so PCIe in, the kernels and PCIe out
+  // overlap) of 256K..4M topics, at most 512 MiB of text; GM_HOST_CHUNK pins
+  // the size (tests)
+  const uint64_t CH = std::max<uint64_t>(
+      1024, env_u64("GM_HOST_CHUNK", std::min<uint64_t>(4u << 20, std::max<uint64_t>(256u << 10, n / (6 * K)))));
+  const uint64_t CB = 512ull << 20;
+  std::vector<uint64_t> cb{0};
+  while (cb.back() < n) {
+    const uint64_t c0 = cb.back();
+    uint64_t lo = c0 + 1, hi = std::min(n, c0 + CH);
+    if (to[hi] < to[c0] || to[lo] < to[c0]) return set_err(ctx, EMQX_GM_EINVAL, "match: topic offsets not monotone");
+    if (to[hi] - to[c0] > CB) {
+      while (lo < hi) {  // largest c1 with the chunk's text <= CB
+        const uint64_t mm = (lo + hi + 1) / 2;
+        if (to[mm] >= to[c0] && to[mm] - to[c0] <= CB) lo = mm;
+        else hi = mm - 1;
+      }
+      hi = lo;
+    }
+    if (to[hi] < to[c0] || to[hi] - to[c0] >= (1ull << 32))
+      return set_err(ctx, EMQX_GM_EINVAL, "match: topic offsets not monotone");
+    cb.push_back(hi);
+  }
+  const char* pe = getenv("GM_HOST_PIPE");  // A/B: "serial" = the one-device serial path for every batch
+  const bool serial = pe && !std::strcmp(pe, "serial") && K == 1;
+  if (cb.size() <= 2 || serial) return run_host_serial(ctx, idx, tb, to, n, flags, out);
+  return run_host_pipe(ctx, idx, tb, to, n, flags, mem, rix, cb, out);
 }
 
 }  // namespace gm

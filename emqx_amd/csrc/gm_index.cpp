@@ -988,6 +988,9 @@ __attribute__((weak)) int refresh_d0(emqx_gm_ctx*, const IndexView&, void*) { re
 
 void free_index(emqx_gm_index* idx) {
   if (!idx) return;
+  for (emqx_gm_index* r : idx->reps)
+    if (r && r->refs.fetch_sub(1) == 1) free_index(r);
+  idx->reps.clear();
   if (idx->ov) free_overlay(idx);
   delete idx->mirror;
   if (idx->dev_base || idx->dev_subs) {

@@ -50,19 +50,34 @@ class DevPool {
 // steady stream of calls does no first-touch page faults on fresh pages (2 GB
 // per 100M-topic call).  Large buffers are 2 MiB aligned and advised as huge
 // pages.  At most kCap bytes stay cached.
+// pinned: page-locked (hipHostMalloc, portable to every device) buffers that
+// the device writes by DMA -- the multi-chunk host-buffer match copies its rows
+// straight into them (gm_host.cpp) instead of through a bounce buffer.
 class HostPool {
  public:
   ~HostPool();
-  void* alloc(size_t bytes);  // nullptr on failure
+  void* alloc(size_t bytes, bool pinned = false);  // nullptr on failure
   void release(void* p);      // a buffer of this pool (any other pointer: free())
   size_t cached_bytes() const { return cached_; }
 
  private:
   static constexpr size_t kCap = 8ull << 30;
-  std::multimap<size_t, void*> free_;  // rounded size -> ptr
-  std::map<void*, size_t> live_;
+  struct Buf {
+    size_t bytes;
+    bool pinned;
+  };
+  std::multimap<size_t, void*> free_[2];  // [pinned] rounded size -> ptr
+  std::map<void*, Buf> live_;
   size_t cached_ = 0;
+  void drop(void* p, bool pinned);
 };
+
+// Page-locked host buffers handed out by emqx_gm_host_alloc: the host-buffer
+// match sends topic text that lies in one of them by DMA, without staging it
+// (gm_host.cpp).  Process-wide, so a buffer is found from any context.
+bool host_pinned_range(const void* p, size_t bytes);
+void host_pinned_add(void* p, size_t bytes);
+bool host_pinned_remove(void* p);
 
 // RAII handle on a pool buffer.
 struct PoolBuf {
@@ -137,6 +152,12 @@ struct emqx_gm_ctx {
   void* ctr_ring = nullptr;
   uint8_t ctr_state[CTR_RING] = {};
   int ctr_next = 0;
+  // A multi-device context (emqx_gm_opts.n_devices > 1): this context is the
+  // first listed device; members[k - 1] serves devices[k] (its own stream,
+  // pools and host pipeline; used only under this context's lock).  Every
+  // index made through this context carries a replica per member
+  // (emqx_gm_index::reps).
+  std::vector<emqx_gm_ctx*> members;
 };
 
 namespace gm {
@@ -203,6 +224,7 @@ struct emqx_gm_index {
   int device = 0;
   void* dev_base = nullptr;     // one allocation holding every table
   void* dev_subs = nullptr;     // a subscriber CSR of its own (after emqx_gm_index_update_subs), or nullptr
+  size_t subs_bytes = 0;        // ... its bytes
   emqx_gm_index* blob_owner = nullptr;  // set: dev_base is that (retained) snapshot's blob, shared
   size_t dev_bytes = 0;
   gm::IndexView view{};
@@ -220,6 +242,11 @@ struct emqx_gm_index {
   gm::Mirror* mirror = nullptr;    // host copy of the blob (updatable plain index), see gm::Mirror
   std::mutex mirror_mu;            // an in-place update holds it while it patches and hands the mirror on
   emqx_gm_index_info_t info{};
+  // made through a multi-device context: reps[k - 1] = this snapshot on that
+  // context's members[k - 1] (same rows; its own device tables, or the tables
+  // of an older replica it shares as this snapshot shares its owner's).  Owned:
+  // released with this snapshot.
+  std::vector<emqx_gm_index*> reps;
 };
 
 namespace gm {
@@ -349,10 +376,26 @@ int set_err(emqx_gm_ctx* ctx, int code, const std::string& msg);
 // gm_match.hip: offset conversions of the host-buffer path (n1 = entries)
 int launch_off32_to_64(hipStream_t st, const uint32_t* in, uint64_t n1, uint64_t* out);
 int launch_off64_to_32(hipStream_t st, const uint64_t* in, uint64_t n1, uint32_t* out);
+int launch_add_u64(hipStream_t st, uint64_t* p, uint64_t n1, uint64_t add);
 // gm_host.cpp: emqx_gm_match on host buffers, chunked and pipelined (H2D / match / D2H overlap)
 int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                    uint32_t flags, emqx_gm_csr* out);
 void free_host_pipe(emqx_gm_ctx* ctx);
+// gm_multi.cpp: multi-device contexts (emqx_gm_opts.n_devices).
+// A copy of flat snapshot `src` (any device) on member context m's device:
+// the host tables shared or copied, the device tables copied device to device
+// (peer copy across devices) -- or, with `share` (a replica on m whose device
+// tables hold the bytes src's own tables hold: src shares its owner's blob and
+// share is that owner's replica), those tables shared.  No host mirror (the
+// primary snapshot's line owns it).
+int replicate_index(emqx_gm_ctx* m, const emqx_gm_index* src, emqx_gm_index* share, emqx_gm_index** out);
+// After an index call on a multi-device context made `out` from `prev` (NULL
+// for a build / import): give `out` its replicas.  A flat result is copied
+// (sharing prev's replica's tables when out shares prev's); an overlay result
+// repeats the call on each member (`redo(member, prev's replica, &rep)`).  On
+// failure `out` is released and *out_p cleared.
+int replicate_result(emqx_gm_ctx* ctx, emqx_gm_index* prev, emqx_gm_index** out_p,
+                     const std::function<int(emqx_gm_ctx*, emqx_gm_index*, emqx_gm_index**)>& redo);
 }  // namespace gm
 
 #define GM_HIP(ctx, expr)                                                                     \

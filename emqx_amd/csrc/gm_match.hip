@@ -2531,6 +2531,16 @@ int launch_off64_to_32(hipStream_t st, const uint64_t* in, uint64_t n1, uint32_t
   hipLaunchKernelGGL(k_off64_to_32, dim3(g ? g : 1), dim3(256), 0, st, in, n1, out);
   return hipGetLastError() == hipSuccess ? 0 : EMQX_GM_EDEVICE;
 }
+// p[0..n1) += add, in place (a chunk's row offsets rebased to the whole call's rows)
+__global__ __launch_bounds__(256) void k_add_u64(uint64_t* __restrict__ p, uint64_t n1, uint64_t add) {
+  for (uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x; i < n1; i += uint64_t(gridDim.x) * 256u) p[i] += add;
+}
+int launch_add_u64(hipStream_t st, uint64_t* p, uint64_t n1, uint64_t add) {
+  if (!n1) return 0;
+  const uint64_t g = std::min<uint64_t>(2048, (n1 + 255) / 256);
+  hipLaunchKernelGGL(k_add_u64, dim3(g), dim3(256), 0, st, p, n1, add);
+  return hipGetLastError() == hipSuccess ? 0 : EMQX_GM_EDEVICE;
+}
 
 // ---- in-place update (gm_overlay.cpp, patch_update) -----------------------
 // The host-patched byte ranges, cut into pieces of <= PATCH_PIECE bytes, one
@@ -2782,6 +2792,7 @@ int rebuild_subs_device(emqx_gm_ctx* ctx, const emqx_gm_index* prev, emqx_gm_ind
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t o_ids = al((nf + 1) * 8);
   GM_HIP(ctx, hipMalloc(&idx->dev_subs, o_ids + total * 4 + 16));
+  idx->subs_bytes = o_ids + total * 4 + 16;
   uint8_t* D = static_cast<uint8_t*>(idx->dev_subs);
   hipStream_t st = ctx->stream;
   GM_HIP(ctx, hipMemcpyAsync(D, new_soff.data(), (nf + 1) * 8, hipMemcpyHostToDevice, st));

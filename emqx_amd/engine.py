@@ -202,23 +202,72 @@ class Index:
             pass
 
 
-class Context:
-    """One process per GPU: a context binds one HIP device and one stream."""
+def _init_torch_runtime():
+    """torch's HIP runtime must come up before the library's when both live in
+    one process (a library-first process leaves torch with "No HIP
+    GPUs are available").  So a context initialises torch's device runtime
+    first whenever torch is importable; a process without torch is unaffected."""
+    try:
+        import torch
+    except Exception:  # (no torch: nothing to order)
+        return
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
 
-    def __init__(self, device: int = 0, mirror: Optional[str] = None):
+
+class Context:
+    """A context binds one HIP device (one process per GPU), or -- with
+    ``devices`` -- a list of them: every index is then replicated to each
+    listed device and a host-buffer match spreads its batch over all of them
+    (emqx_gm_opts.n_devices)."""
+
+    def __init__(self, device: int = 0, mirror: Optional[str] = None, devices: Optional[Sequence[int]] = None):
         """``mirror``: None (library default: the host copy of a plain index's
         tables is kept from the build up to 8 GiB, loaded on the first update
-        above), "eager" or "lazy" (EMQX_GM_OPEN_MIRROR_*)."""
+        above), "eager" or "lazy" (EMQX_GM_OPEN_MIRROR_*).  ``devices``: the
+        device list of a multi-device context (repeats allowed: replicas on one
+        device)."""
+        _init_torch_runtime()
         o = Opts()
         o.device = device
         o.flags = {None: 0, "eager": _lib.OPEN_MIRROR_EAGER, "lazy": _lib.OPEN_MIRROR_LAZY}[mirror]
+        if devices is not None:
+            devices = list(devices)
+            if not 1 <= len(devices) <= _lib.MAX_DEVICES:
+                raise ValueError(f"1..{_lib.MAX_DEVICES} devices")
+            o.n_devices = len(devices)
+            for k, d in enumerate(devices):
+                o.devices[k] = d
+            device = devices[0]
         h = C.c_void_p()
         rc = lib().emqx_gm_open(C.byref(o), C.byref(h))
         if rc != _lib.OK:
-            raise GpuMatchError(rc, f"emqx_gm_open(device={device}) failed (no MI355X visible?)")
+            raise GpuMatchError(rc, f"emqx_gm_open(devices={devices if devices else [device]}) failed "
+                                    f"(no MI355X visible?)")
         self.h = h
         self.device = device
         self._stats_buf = MatchStats()
+
+    @property
+    def devices(self) -> List[int]:
+        n = C.c_uint32()
+        check(lib().emqx_gm_devices(self.h, None, C.byref(n)), self.h, "devices")
+        arr = (C.c_int32 * n.value)()
+        check(lib().emqx_gm_devices(self.h, arr, C.byref(n)), self.h, "devices")
+        return list(arr)
+
+    def host_alloc(self, nbytes: int) -> np.ndarray:
+        """A page-locked uint8 buffer (emqx_gm_host_alloc): topics packed into it
+        cross PCIe by DMA without a staging copy.  Free with host_free()."""
+        p = C.c_void_p()
+        check(lib().emqx_gm_host_alloc(self.h, nbytes, C.byref(p)), self.h, "host_alloc")
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(max(nbytes, 1),))[:nbytes]
+
+    def host_free(self, buf: np.ndarray):
+        check(lib().emqx_gm_host_free(self.h, C.c_void_p(buf.ctypes.data)), self.h, "host_free")
 
     def close(self):
         if self.h:

@@ -82,10 +82,31 @@ typedef struct emqx_gm_ctx emqx_gm_ctx;
 typedef struct emqx_gm_index emqx_gm_index;
 typedef struct emqx_gm_call emqx_gm_call;
 
+/* Device list (the opts "select the device list (1-8)").  A BEAM
+ * node loads its NIF once, so one context must be able to serve the whole
+ * node's GPUs, as the reference's match_routes/1 runs in every publisher
+ * process on all schedulers at once (apps/emqx/src/emqx_trie.erl:66-70,
+ * emqx_router.erl:75-84, 128-145).  With n_devices = k > 0 the context owns
+ * one replica of every index per listed device (a device may be listed more
+ * than once: several replicas, e.g. a one-GPU rehearsal):
+ *   - an index is compiled ONCE on the host and its device tables are copied
+ *     to the other devices (device to device / peer copy over xGMI); every
+ *     emqx_gm_index_update / _update_subs / _import result is replicated too;
+ *   - emqx_gm_match on host buffers cuts the batch into chunks that run on
+ *     all the devices at once (one host pipeline per device); the rows come
+ *     back in the caller's ONE CSR, in batch order;
+ *   - device-buffer calls (EMQX_GM_DEVICE_IO, emqx_gm_match_submit), the
+ *     fan-out, the sharding helpers, emqx_gm_set_stream and
+ *     emqx_gm_index_device_blob / _export use the first listed device.
+ * n_devices = 0 is the single-device context on `device`. */
+#define EMQX_GM_MAX_DEVICES 8
 typedef struct {
-  int32_t device;        /* HIP device ordinal; one process per GPU            */
+  int32_t device;        /* HIP device ordinal (n_devices == 0)                 */
   uint32_t flags;        /* EMQX_GM_OPEN_* (0: defaults)                        */
-  uint64_t reserved[7];
+  uint32_t n_devices;    /* 0: `device` alone; 1..EMQX_GM_MAX_DEVICES: devices[] */
+  int32_t devices[EMQX_GM_MAX_DEVICES];
+  uint32_t reserved0;
+  uint64_t reserved[2];
 } emqx_gm_opts;
 
 /* emqx_gm_opts.flags: the host copy of a plain index's device tables that an
@@ -245,6 +266,17 @@ int emqx_gm_match(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const uint8_t *top
 int emqx_gm_match_submit(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const uint8_t *topic_bytes,
                          const uint64_t *topic_off, uint64_t n_topics, uint32_t flags, emqx_gm_call **call);
 int emqx_gm_match_wait(emqx_gm_ctx *ctx, emqx_gm_call *call, emqx_gm_csr *out);
+/* Pinned host buffers for the host-buffer emqx_gm_match: topic text (and
+ * offsets) that a caller packs straight into memory from emqx_gm_host_alloc
+ * crosses PCIe by DMA from where it lies, with no staging copy by the
+ * library's workers (the NIF packs a publish batch's binaries here).  The
+ * memory is page-locked and visible to every device of the context; free it
+ * with emqx_gm_host_free on the same context. */
+int emqx_gm_host_alloc(emqx_gm_ctx *ctx, uint64_t bytes, void **p);
+int emqx_gm_host_free(emqx_gm_ctx *ctx, void *p);
+/* The devices of a context, in emqx_gm_opts order (*n = 1 for a single-device
+ * context); devices may be NULL to ask for the count. */
+int emqx_gm_devices(const emqx_gm_ctx *ctx, int32_t *devices, uint32_t *n);
 int emqx_gm_fanout(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const emqx_gm_csr *matches,
                    uint32_t flags, emqx_gm_csr *out_subs);
 int emqx_gm_csr_free(emqx_gm_ctx *ctx, emqx_gm_csr *csr);

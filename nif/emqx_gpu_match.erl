@@ -16,9 +16,14 @@
 
 -on_load(init/0).
 
+%% LoadInfo: the node's GPUs (application env `gpu_match_devices`, e.g.
+%% [0,1,2,3,4,5,6,7]; a single ordinal is one GPU).  With a list, the one NIF
+%% context replicates every index to all of them and spreads each batch over
+%% them (emqx_gm_opts.n_devices).
 init() ->
     Priv = case code:priv_dir(emqx) of {error, _} -> "priv"; D -> D end,
-    erlang:load_nif(filename:join(Priv, "emqx_gpu_match_nif"), 0).
+    Devices = application:get_env(emqx, gpu_match_devices, 0),
+    erlang:load_nif(filename:join(Priv, "emqx_gpu_match_nif"), Devices).
 
 %% The route filters (emqx_route topics; wildcard ones are the emqx_trie
 %% entries) -> an immutable index snapshot in HBM.

@@ -37,13 +37,29 @@ static void index_dtor(ErlNifEnv *env, void *obj) {
   if (r->idx) emqx_gm_index_release(r->idx);
 }
 
+/* LoadInfo (erlang:load_nif/2): a device ordinal, or the node's device list
+ * [D0, D1, ...] (1..EMQX_GM_MAX_DEVICES entries; repeats give several replicas
+ * on one GPU).  With a list, the ONE context of this node replicates every
+ * index to all listed GPUs and each match_*_batch / fanout_batch spreads its
+ * batch over them (emqx_gm_opts.n_devices), as the reference's match_routes/1
+ * runs on all schedulers at once (emqx_trie.erl:66-70, emqx_router.erl:128-145). */
 static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
   int device = 0;
+  unsigned nl = 0;
   emqx_gm_opts o;
   (void)priv;
-  enif_get_int(env, info, &device);
   memset(&o, 0, sizeof(o));
-  o.device = device;
+  if (enif_get_list_length(env, info, &nl) && nl > 0) {
+    ERL_NIF_TERM h, t = info;
+    if (nl > EMQX_GM_MAX_DEVICES) return 1;
+    while (enif_get_list_cell(env, t, &h, &t)) {
+      if (!enif_get_int(env, h, &device)) return 1;
+      o.devices[o.n_devices++] = device;
+    }
+  } else {
+    enif_get_int(env, info, &device);
+    o.device = device;
+  }
   INDEX_RT = enif_open_resource_type(env, NULL, "emqx_gm_index", index_dtor, ERL_NIF_RT_CREATE, NULL);
   A_OK = enif_make_atom(env, "ok");
   A_ERROR = enif_make_atom(env, "error");
@@ -95,6 +111,56 @@ static int pack_list(ErlNifEnv *env, ERL_NIF_TERM list, uint8_t **bytes, uint64_
   memset(*bytes + total, 0, 64);
   *n = len;
   return 1;
+}
+
+/* A publish batch packed straight into page-locked memory (emqx_gm_host_alloc):
+ * the library then sends the text to the GPUs by DMA from here, with no
+ * staging copy of its own.  One buffer per dirty scheduler thread, grown as
+ * batches grow; the offsets stay in ordinary memory (the library validates and
+ * rebases them anyway). */
+static __thread uint8_t *PIN_BUF;
+static __thread uint64_t PIN_CAP;
+
+static int pack_topics(ErlNifEnv *env, ERL_NIF_TERM list, uint8_t **bytes, uint64_t **off, uint64_t *n) {
+  unsigned len;
+  ERL_NIF_TERM h, t = list;
+  ErlNifBinary b;
+  uint64_t total = 0, i = 0;
+  if (!enif_get_list_length(env, list, &len)) return 0;
+  while (enif_get_list_cell(env, t, &h, &t)) {
+    if (!enif_inspect_binary(env, h, &b)) return 0;
+    total += b.size;
+  }
+  if (PIN_CAP < total + 64) {
+    void *p = NULL;
+    uint64_t cap = PIN_CAP ? PIN_CAP : (1u << 20);
+    while (cap < total + 64) cap *= 2;
+    if (PIN_BUF) emqx_gm_host_free(CTX, PIN_BUF);
+    PIN_BUF = NULL;
+    PIN_CAP = 0;
+    if (emqx_gm_host_alloc(CTX, cap, &p) == EMQX_GM_OK) {
+      PIN_BUF = p;
+      PIN_CAP = cap;
+    }
+  }
+  if (!PIN_BUF) return pack_list(env, list, bytes, off, n);  /* (no page-locked memory: the plain way) */
+  *bytes = PIN_BUF;
+  *off = enif_alloc((len + 1) * sizeof(uint64_t));
+  (*off)[0] = 0;
+  t = list;
+  while (enif_get_list_cell(env, t, &h, &t)) {
+    enif_inspect_binary(env, h, &b);
+    memcpy(*bytes + (*off)[i], b.data, b.size);
+    (*off)[i + 1] = (*off)[i] + b.size;
+    ++i;
+  }
+  memset(*bytes + total, 0, 64);
+  *n = len;
+  return 1;
+}
+static void free_topics(uint8_t *bytes, uint64_t *off) {
+  if (bytes != PIN_BUF) enif_free(bytes);
+  enif_free(off);
 }
 
 static ERL_NIF_TERM make_index_term(ErlNifEnv *env, emqx_gm_index *idx) {
@@ -269,10 +335,9 @@ static ERL_NIF_TERM do_match(ErlNifEnv *env, const ERL_NIF_TERM argv[], uint32_t
   ERL_NIF_TERM bin, result, *rows;
   int rc;
   if (!enif_get_resource(env, argv[0], INDEX_RT, (void **)&r)) return enif_make_badarg(env);
-  if (!pack_list(env, argv[1], &tb, &to, &n)) return enif_make_badarg(env);
+  if (!pack_topics(env, argv[1], &tb, &to, &n)) return enif_make_badarg(env);
   rc = emqx_gm_match(CTX, r->idx, tb, to, n, flags, &out);
-  enif_free(tb);
-  enif_free(to);
+  free_topics(tb, to);
   if (rc != EMQX_GM_OK) return error_tuple(env, rc);
   /* each filter is a binary over the snapshot's own host bytes, kept alive by the resource */
   rows = enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1));
@@ -320,10 +385,9 @@ static ERL_NIF_TERM fanout_batch(ErlNifEnv *env, int argc, const ERL_NIF_TERM ar
   int rc;
   (void)argc;
   if (!enif_get_resource(env, argv[0], INDEX_RT, (void **)&r)) return enif_make_badarg(env);
-  if (!pack_list(env, argv[1], &tb, &to, &n)) return enif_make_badarg(env);
+  if (!pack_topics(env, argv[1], &tb, &to, &n)) return enif_make_badarg(env);
   rc = emqx_gm_match(CTX, r->idx, tb, to, n, EMQX_GM_WITH_EXACT, &m);
-  enif_free(tb);
-  enif_free(to);
+  free_topics(tb, to);
   if (rc != EMQX_GM_OK) return error_tuple(env, rc);
   rc = emqx_gm_fanout(CTX, r->idx, &m, 0, &d);
   if (rc != EMQX_GM_OK) {

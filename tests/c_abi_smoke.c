@@ -136,6 +136,72 @@ int main(void) {
   emqx_gm_index_release(copy);
   emqx_gm_index_release(idx);
   emqx_gm_close(ctx);
+
+  /* a two-device context (device 0 listed twice: two replicas on one GPU, the
+   * one-GPU rehearsal of a node's device list): one build replicated, a
+   * 600k-topic host batch spread over both in 256K-topic chunks, from a
+   * page-locked buffer (emqx_gm_host_alloc) and from plain memory, an update
+   * replicated; every row as expected */
+  ctx = NULL;
+  memset(&o, 0, sizeof o);
+  o.n_devices = 2;
+  o.devices[0] = 0;
+  o.devices[1] = 0;
+  CHECK(emqx_gm_open(&o, &ctx) == EMQX_GM_OK, "open two devices");
+  int32_t devs[EMQX_GM_MAX_DEVICES];
+  uint32_t ndev = 0;
+  CHECK(emqx_gm_devices(ctx, devs, &ndev) == EMQX_GM_OK && ndev == 2 && devs[0] == 0 && devs[1] == 0, "devices");
+  CHECK(emqx_gm_index_build(ctx, fb, fo, nf, NULL, NULL, NULL, &idx) == EMQX_GM_OK, "two-device build");
+  const uint64_t big = 600000;
+  uint64_t bytes_big = 0;
+  for (uint64_t i = 0; i < big; ++i) bytes_big += strlen(topics[i % nt]);
+  uint8_t *pb = NULL;
+  CHECK(emqx_gm_host_alloc(ctx, bytes_big + 64, (void **)&pb) == EMQX_GM_OK && pb, "host_alloc");
+  uint8_t *plain = malloc(bytes_big + 64);
+  uint64_t *bo = malloc((big + 1) * sizeof(uint64_t));
+  CHECK(plain && bo, "malloc");
+  bo[0] = 0;
+  for (uint64_t i = 0; i < big; ++i) {
+    const uint64_t l = strlen(topics[i % nt]);
+    memcpy(pb + bo[i], topics[i % nt], l);
+    bo[i + 1] = bo[i] + l;
+  }
+  memset(pb + bytes_big, 0, 64);
+  memcpy(plain, pb, bytes_big + 64);
+  for (int pass = 0; pass < 3; ++pass) {
+    if (pass == 2) {  /* an update (filter 'x/#' added), replicated to both devices */
+      static const char *nf_s[] = {"x/#"};
+      uint8_t ub[80];
+      uint64_t uo[2];
+      uint8_t op = 1;
+      emqx_gm_index *nidx = NULL;
+      pack(nf_s, 1, ub, uo);
+      CHECK(emqx_gm_index_update(ctx, idx, ub, uo, &op, 1, &nidx) == EMQX_GM_OK, "two-device update");
+      emqx_gm_index_release(idx);
+      idx = nidx;
+    }
+    CHECK(emqx_gm_match(ctx, idx, pass == 1 ? plain : pb, bo, big, EMQX_GM_WITH_EXACT, &out) == EMQX_GM_OK,
+          "two-device match");
+    CHECK(out.n_rows == big && !out.on_device, "two-device rows");
+    for (uint64_t i = 0; i < big; i += 997) {
+      row_str(idx, &out, i, buf);
+      const char *w = want_routes[i % nt];
+      if (pass == 2 && i % nt == 3) w = "#|x/#";
+      if (strcmp(buf, w)) {
+        fprintf(stderr, "FAIL two-device row %llu (pass %d): got '%s' want '%s'\n", (unsigned long long)i, pass, buf, w);
+        return 1;
+      }
+    }
+    row_str(idx, &out, big - 1, buf);
+    CHECK(!strcmp(buf, want_routes[(big - 1) % nt]), "two-device last row");
+    emqx_gm_csr_free(ctx, &out);
+  }
+  CHECK(emqx_gm_host_free(ctx, pb) == EMQX_GM_OK, "host_free");
+  CHECK(emqx_gm_host_free(ctx, plain) == EMQX_GM_EINVAL, "host_free of a malloc'd buffer");
+  free(plain);
+  free(bo);
+  emqx_gm_index_release(idx);
+  emqx_gm_close(ctx);
   printf("C_ABI_SMOKE_OK\n");
   return 0;
 }
