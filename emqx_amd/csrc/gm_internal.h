@@ -329,6 +329,19 @@ bool well_formed_filter(const uint8_t* p, uint64_t len);
 int index_export(emqx_gm_ctx* ctx, const emqx_gm_index* idx, uint32_t flags, uint8_t* buf, uint64_t* size);
 int index_import(emqx_gm_ctx* ctx, const uint8_t* img, uint64_t size, const void* d_blob, emqx_gm_index** out);
 int load_mirror_blob(emqx_gm_ctx* ctx, emqx_gm_index* idx);
+// an image's every count and offset checked against its own bytes (no device);
+// EMQX_GM_EINVAL with the reason in *why
+int validate_image(const uint8_t* img, uint64_t size, bool have_blob, std::string* why);
+// the host half of an import (validate_image, then the host tables into idx;
+// its view's pointer fields hold blob offsets + 1, 0 = null)
+int import_host_part(const uint8_t* img, uint64_t size, bool have_blob, emqx_gm_index* idx, std::string* why);
+// test support (tests/asan): a named u64 header field of an image (nullptr:
+// unknown name), a u32 count of its view (0 n_nodes, 1 efilt_mask[t], 2
+// mph_nb[t]), and the checksum recomputed after a change
+uint64_t* image_field(uint8_t* img, const std::string& name);
+uint32_t image_view_u32(uint8_t* img, int which, int t);
+void image_view_set_u32(uint8_t* img, int which, int t, uint32_t x);
+void image_reseal(uint8_t* img, uint64_t size);
 // gm_match.hip: write the root's '+' record (IndexView::d0_root) from view v's
 // depth-1 hot table on the device; d0 is the region's device address (v's own
 // pointer is const).  0: written (the caller sets IX_D0), 1: not wanted

@@ -5,6 +5,11 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export PYTHONUNBUFFERED=1
 mkdir -p gpurun_out/r05_b
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_image.py \
+  tests/test_gpu_multi.py::test_updates_replicated > gpurun_out/r05_b/pytest.log 2>&1
+rc=$?
+tail -n 15 gpurun_out/r05_b/pytest.log
+[ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python3 -u bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/r05_b/bench_c2.log 2>&1
 rc=$?
 tail -c 1500 gpurun_out/r05_b/bench_c2.log

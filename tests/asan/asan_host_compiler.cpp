@@ -370,6 +370,108 @@ int patch_sequences() {
   }
   return bad;
 }
+
+// ---- index images (gm_image.cpp): validate_image / import_host_part fed a
+// valid image cut at every section boundary, with byte flips anywhere in its
+// header and host sections, and with counts and offsets rewritten (the
+// checksum resealed, as a crafted image would carry): every cut and flip is
+// refused with EMQX_GM_EINVAL, every rewritten oversized count too, and
+// nothing reads out of bounds (ASan) -- what index_import checks before it
+// touches a device.
+int image_fuzz() {
+  int bad = 0;
+  std::mt19937_64 rng(5);
+  std::set<std::string> fs;
+  for (int i = 0; i < 500; ++i) fs.insert(rand_filter(rng, 6));
+  emqx_gm_index* idx = host_build(fs);
+  if (!idx) return 1;
+  uint64_t size = 0;
+  if (gm::index_export(nullptr, idx, 0, nullptr, &size)) return 1;
+  std::vector<uint8_t> img(size);
+  if (gm::index_export(nullptr, idx, 0, img.data(), &size)) return 1;
+  auto attempt = [&](const std::vector<uint8_t>& b, uint64_t sz, bool have_blob) {
+    emqx_gm_index t;
+    std::string why;
+    const int rc = gm::import_host_part(b.data(), sz, have_blob, &t, &why);
+    if (rc == 0 && t.ft.size() != t.info.n_filters) ++bad;
+    delete t.mirror;
+    t.mirror = nullptr;
+    return rc;
+  };
+  if (attempt(img, size, false) != 0) {
+    std::fprintf(stderr, "image: the intact image is refused\n");
+    ++bad;
+  }
+  // cuts: every section boundary (and one byte either side), then random sizes
+  std::vector<uint64_t> cuts = {0, 1, 8, 100, sizeof(uint64_t) * 3};
+  for (int k = 0; k < 6; ++k) {
+    const uint64_t o = *gm::image_field(img.data(), "sec_off" + std::to_string(k));
+    cuts.insert(cuts.end(), {o - 1, o, o + 1});
+  }
+  for (int i = 0; i < 200; ++i) cuts.push_back(rng() % size);
+  for (uint64_t c : cuts) {
+    if (c >= size) continue;
+    std::vector<uint8_t> b(img.begin(), img.begin() + c);
+    b.resize(std::max<uint64_t>(c, 1));
+    if (attempt(b, c, false) != EMQX_GM_EINVAL) {
+      std::fprintf(stderr, "image: a cut at %llu is not refused\n", (unsigned long long)c);
+      ++bad;
+    }
+  }
+  // byte flips: the header and the host sections (the checksum covers both)
+  const uint64_t host_end = *gm::image_field(img.data(), "sec_off5");
+  for (int i = 0; i < 3000; ++i) {
+    std::vector<uint8_t> b(img);
+    const uint64_t at = i < 1500 ? rng() % 2048 : rng() % host_end;
+    b[at] ^= uint8_t(1 + rng() % 255);
+    if (attempt(b, size, false) != EMQX_GM_EINVAL) {
+      std::fprintf(stderr, "image: a flip at %llu is not refused\n", (unsigned long long)at);
+      ++bad;
+    }
+  }
+  // rewritten counts and offsets, resealed: oversized ones are refused; any
+  // other value may be accepted or refused but is never read out of bounds
+  const char* names[] = {"dev_bytes", "flen_off", "n_filters", "ft_bytes", "gmap_n", "soff_n", "pinned_n",
+                         "blob_in_image", "total_bytes", "info.n_filters", "info.n_subs", "view.dict_mask",
+                         "view.hot_cap1", "view.hot_off2", "view.etab_mask0", "mirror.blob_size", "mirror.nodes_cap",
+                         "mirror.arena_cap", "mirror.flen_cap", "mirror.o_hot", "mirror.hot_used1",
+                         "mirror.edge_used0", "sec_off0", "sec_off1", "sec_off2", "sec_off3", "sec_off4", "sec_off5",
+                         "ptr_off0", "ptr_off1", "ptr_off2", "ptr_off3", "ptr_off4", "ptr_off8", "ptr_off9",
+                         "ptr_off10"};
+  for (const char* nm : names) {
+    const uint64_t orig = *gm::image_field(img.data(), nm);
+    const uint64_t vals[] = {orig + size, orig * 2 + 1, ~0ull, ~0ull / 2, 1ull << 40, orig + 1, orig ? orig - 1 : 7, 0};
+    for (int vi = 0; vi < 8; ++vi) {
+      std::vector<uint8_t> b(img);
+      *gm::image_field(b.data(), nm) = vals[vi];
+      gm::image_reseal(b.data(), size);
+      const int rc = attempt(b, size, false);
+      // (the oversized values: past the image / the blob / 2^40; a host-only
+      // index has no subscriber tables, so its info.n_subs is a bare count)
+      const bool oversized = vi == 0 || (vi >= 2 && vi <= 4);
+      // (~0 in a ptr_off field is the encoding of an absent table)
+      const bool null_ptr = std::string(nm).compare(0, 7, "ptr_off") == 0 && vals[vi] == ~0ull;
+      if (oversized && !null_ptr && vals[vi] != orig && rc != EMQX_GM_EINVAL && std::string(nm) != "info.n_subs") {
+        std::fprintf(stderr, "image: %s = %llu is not refused\n", nm, (unsigned long long)vals[vi]);
+        ++bad;
+      }
+    }
+  }
+  // the view's u32 counts (nodes, edge filter and MPH bucket extents) oversized
+  for (int which = 0; which < 3; ++which)
+    for (int t = 0; t < 16; ++t) {
+      std::vector<uint8_t> b(img);
+      gm::image_view_set_u32(b.data(), which, t, 0x7FFFFFFFu);
+      gm::image_reseal(b.data(), size);
+      if (attempt(b, size, false) != EMQX_GM_EINVAL && !(which == 2 && !gm::image_view_u32(img.data(), which, t))) {
+        std::fprintf(stderr, "image: view count %d/%d oversized is not refused\n", which, t);
+        ++bad;
+      }
+      if (which == 0) break;
+    }
+  gm::free_index(idx);
+  return bad;
+}
 }  // namespace
 
 int main() {
@@ -444,6 +546,7 @@ int main() {
   }
   bad += filter_table_check();
   bad += patch_sequences();
+  bad += image_fuzz();
   std::printf(bad ? "ASAN_HOST_CHECK_FAILED %d\n" : "ASAN_HOST_CHECK_OK\n", bad);
   return bad ? 1 : 0;
 }

@@ -215,7 +215,12 @@ def test_host_compiler_under_asan(mph_min):
     (gm_overlay.cpp) built with AddressSanitizer + UBSan and fed random,
     empty, NUL-laden, 65,535-byte and 5,000-level filters (SURVEY.md §5;
     tests/asan/asan_host_compiler.cpp): no sanitizer report, every input gets
-    a valid id."""
+    a valid id.  Index images (gm_image.cpp validate_image / import_host_part,
+    what index_import runs before it touches a device): an exported image cut
+    at every section boundary and at random sizes, 3,000 byte flips in its
+    header and host sections, and 36 header counts / offsets rewritten and
+    resealed -- every cut, flip and oversized value refused with EINVAL, no
+    out-of-bounds read."""
     import subprocess
     b = subprocess.run(["make", "-C", os.path.join(ROOT, "emqx_amd", "csrc"), "asan"], capture_output=True, text=True)
     assert b.returncode == 0, b.stderr[-3000:]
