@@ -71,6 +71,8 @@ def parse():
     p.add_argument("--index-cache", default=None,
                    help="replicated configs: an index image file (emqx_gm_index_export); imported when it exists, "
                         "written after the build otherwise (profiling passes of C3/C5 skip the host build)")
+    p.add_argument("--subs-update", action="store_true",
+                   help="C5: also measure subscriber updates on a 100M-filter index with subscriber lists")
     p.add_argument("--no-host-replicas", action="store_true",
                    help="skip the two-replica (multi-device context) host-buffer rehearsal")
     p.add_argument("--no-host-io", action="store_true",
@@ -433,6 +435,40 @@ def heartbeat(every_s: float = 60.0):
     threading.Thread(target=beat, daemon=True).start()
 
 
+def subs_update(ctx, fpack, n_ops=100, batches=7):
+    """Subscriber maintenance at this config's filter count (emqx_broker:
+    subscribe/unsubscribe, apps/emqx/src/emqx_broker.erl:147-165), outside the
+    timed region: an index over the same filters built with one subscriber
+    each, then batches of n_ops subscriber-only ops (a new subscriber joins a
+    filter, its old one leaves: no route changes) through
+    emqx_gm_index_update_subs -- the O(delta) path (gm_subs.cpp, SubTable).
+    Wall time of each call (host work + the new subscriber CSR's device copy)."""
+    import numpy as np
+    fb, fo = fpack
+    n = len(fo) - 1
+    t0 = time.perf_counter()
+    sidx = ctx.build_index(fpack, subs=(np.arange(n + 1, dtype=np.uint64), np.arange(n, dtype=np.uint32)))
+    build_s = time.perf_counter() - t0
+    rng = np.random.default_rng(3)
+    ms = []
+    cur = sidx
+    for b in range(batches):
+        ops = []
+        for k, i in enumerate(rng.choice(n, n_ops // 2, replace=False).tolist()):
+            f = bytes(fb[int(fo[i]):int(fo[i + 1])])
+            ops += [(f, 1_000_000_000 + b * n_ops + k, "subscribe"), (f, i, "unsubscribe")]
+        t0 = time.perf_counter()
+        nxt = ctx.update_subs(cur, ops)
+        ms.append((time.perf_counter() - t0) * 1e3)
+        cur.release()
+        cur = nxt
+    ok = cur.n_filters == n
+    cur.release()
+    ms_sorted = sorted(ms[1:])  # (the first call warms the pools)
+    return {"filters": n, "ops_per_batch": n_ops, "batches": batches, "ms_median": ms_sorted[len(ms_sorted) // 2],
+            "ms_max": ms_sorted[-1], "ms_first": ms[0], "build_with_subscribers_s": build_s, "filters_unchanged": ok}
+
+
 def host_io(ctx, idx, db, do, tbytes, n_topics, nnz, local, replicas=True, reps=2):
     """The host-buffer emqx_gm_match (the NIF's call, gm_host.cpp), best of
     ``reps`` after a warm-up: topics from page-locked memory (emqx_gm_host_alloc:
@@ -646,6 +682,8 @@ def main():
         out["detail"]["index_update"] = {"ops": 200, "update_ms": upd_ms, "match_kernel_ms_after": min(ks),
                                          "vs_flat": min(ks) / min(kern_ms)}
         new.release()
+    if rank == 0 and world == 1 and not a.no_update and (cfg != "c5" or a.subs_update):
+        out["detail"]["subs_update"] = subs_update(ctx, fpack)
     big = cfg == "c5" and n_filters >= 50_000_000  # the oracle over this many keys does not fit the box
     if big and rank == 0 and not a.no_parity:
         # the oracle over 100M keys does not fit the box's memory: the committed C5

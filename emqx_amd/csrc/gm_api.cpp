@@ -523,7 +523,7 @@ int emqx_gm_index_filter(const emqx_gm_index* idx, uint32_t id, const uint8_t** 
 int emqx_gm_index_subscriber_count(const emqx_gm_index* idx, uint32_t id, uint64_t* n) {
   if (!idx || !n || idx->ov || !idx->gmap.empty()) return EMQX_GM_EINVAL;
   if (id >= idx->info.n_filters) return EMQX_GM_EINVAL;
-  *n = idx->soff.empty() ? 0 : idx->soff[id + 1] - idx->soff[id];
+  *n = idx->subs.empty() ? 0 : idx->subs.count(id);
   return EMQX_GM_OK;
 }
 

@@ -202,4 +202,111 @@ class FilterTable {
   uint64_t ins_rank(uint64_t k) const { return ipos_[k] - tomb_lt(ipos_[k]) + k; }
 };
 
+// The host side of an index's subscriber lists, per filter id: the offset of
+// its segment in the subscriber CSR and its route mark (the filter is routed
+// to another destination too: emqx_gm_index_update_subs ROUTE_ADD).  Like
+// FilterTable, a shared immutable base plus a small delta, so a
+// subscriber-only update (emqx_broker:subscribe/unsubscribe that add or drop
+// no route, apps/emqx/src/emqx_broker.erl:147-165) derives the next
+// snapshot's table in O(delta): the touched ids with their new counts (every
+// offset past a touched id moves by the sum of the count changes before it)
+// and the touched ids' marks.  Lookups are binary searches over the delta.
+// Compacted (one O(n) pass) once the delta passes max(4096, n / 16).
+class SubTable {
+ public:
+  SubTable() = default;
+  // a materialized table: off[n + 1]; marks empty = a built index, where a
+  // filter without subscribers is route-only
+  SubTable(std::vector<uint64_t> off, std::vector<uint8_t> marks) {
+    auto b = std::make_shared<Base>();
+    b->off = std::move(off);
+    b->pin = std::move(marks);
+    base_ = std::move(b);
+  }
+  bool empty() const { return !base_ || base_->off.empty(); }  // no subscriber lists
+  uint64_t n() const { return empty() ? 0 : base_->off.size() - 1; }
+  uint64_t delta() const { return did_.size() + pover_.size(); }
+  uint64_t off(uint64_t f) const {  // f in [0, n]
+    const uint64_t k = uint64_t(std::lower_bound(did_.begin(), did_.end(), uint32_t(std::min<uint64_t>(f, ~0u))) -
+                                did_.begin());
+    return uint64_t(int64_t(base_->off[f]) + (k ? dcum_[k - 1] : 0));
+  }
+  uint64_t count(uint64_t f) const {
+    auto it = std::lower_bound(did_.begin(), did_.end(), uint32_t(f));
+    if (it != did_.end() && *it == f) return dnew_[it - did_.begin()];
+    return base_->off[f + 1] - base_->off[f];
+  }
+  uint64_t total() const { return empty() ? 0 : off(n()); }
+  bool pinned(uint64_t f) const {
+    auto it = std::lower_bound(pover_.begin(), pover_.end(), std::make_pair(uint32_t(f), uint8_t(0)));
+    if (it != pover_.end() && it->first == f) return it->second != 0;
+    if (!base_->pin.empty()) return base_->pin[f] != 0;
+    return base_->off[f + 1] == base_->off[f];
+  }
+  // the touched ids (ascending) and their running count changes: the device
+  // derives the new offsets from these (new off[f] = old off[f] + the change
+  // summed over touched ids below f)
+  // The next snapshot's table, ids unchanged: `cnt` = (id, new count) for the
+  // touched filters, `pin` = (id, mark) for the touched marks, both ascending.
+  SubTable apply(const std::vector<std::pair<uint32_t, uint64_t>>& cnt,
+                 const std::vector<std::pair<uint32_t, uint8_t>>& pin) const {
+    SubTable o;
+    o.base_ = base_;
+    // counts: the old delta merged with the new (a new count replaces an old one)
+    size_t a = 0, b = 0;
+    while (a < did_.size() || b < cnt.size()) {
+      uint32_t id;
+      uint64_t c;
+      if (b == cnt.size() || (a < did_.size() && did_[a] < cnt[b].first)) {
+        id = did_[a], c = dnew_[a], ++a;
+      } else {
+        if (a < did_.size() && did_[a] == cnt[b].first) ++a;
+        id = cnt[b].first, c = cnt[b].second, ++b;
+      }
+      const int64_t d = int64_t(c) - int64_t(base_->off[id + 1] - base_->off[id]);
+      o.did_.push_back(id);
+      o.dnew_.push_back(c);
+      o.dcum_.push_back((o.dcum_.empty() ? 0 : o.dcum_.back()) + d);
+    }
+    a = b = 0;
+    while (a < pover_.size() || b < pin.size()) {
+      if (b == pin.size() || (a < pover_.size() && pover_[a].first < pin[b].first)) {
+        o.pover_.push_back(pover_[a++]);
+      } else {
+        if (a < pover_.size() && pover_[a].first == pin[b].first) ++a;
+        o.pover_.push_back(pin[b++]);
+      }
+    }
+    if (o.delta() > std::max<uint64_t>(4096, n() / 16)) o.compact();
+    return o;
+  }
+  const std::vector<uint32_t>& delta_ids() const { return did_; }
+  const std::vector<int64_t>& delta_cum() const { return dcum_; }
+  std::vector<uint64_t> offsets() const {  // materialized (index images)
+    std::vector<uint64_t> r(n() + 1);
+    for (uint64_t f = 0, k = 0; f <= n(); ++f) {
+      while (k < did_.size() && did_[k] < f) ++k;
+      r[f] = uint64_t(int64_t(base_->off[f]) + (k ? dcum_[k - 1] : 0));
+    }
+    return r;
+  }
+  std::vector<uint8_t> marks() const {
+    std::vector<uint8_t> r(n());
+    for (uint64_t f = 0; f < n(); ++f) r[f] = pinned(f) ? 1 : 0;
+    return r;
+  }
+  void compact() { *this = SubTable(offsets(), marks()); }
+
+ private:
+  struct Base {
+    std::vector<uint64_t> off;  // subscriber CSR offsets, n + 1
+    std::vector<uint8_t> pin;   // route marks, n (empty: a count of 0 is the mark)
+  };
+  std::shared_ptr<const Base> base_;
+  std::vector<uint32_t> did_;    // touched ids, ascending
+  std::vector<uint64_t> dnew_;   // their counts
+  std::vector<int64_t> dcum_;    // dcum_[k] = the count changes of did_[0..k] summed
+  std::vector<std::pair<uint32_t, uint8_t>> pover_;  // touched marks, ascending
+};
+
 }  // namespace gm

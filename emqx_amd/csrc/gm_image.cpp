@@ -163,8 +163,10 @@ int index_export(emqx_gm_ctx* ctx, const emqx_gm_index* idx, uint32_t flags, uin
   idx->ft.for_each([&](uint64_t, const uint8_t*, uint64_t l) { fbytes += l; });
   h.ft_bytes = fbytes;
   h.gmap_n = idx->gmap.size();
-  h.soff_n = idx->soff.size();
-  h.pinned_n = idx->pinned.size();
+  const std::vector<uint64_t> soff = idx->subs.empty() ? std::vector<uint64_t>() : idx->subs.offsets();
+  const std::vector<uint8_t> marks = idx->subs.empty() ? std::vector<uint8_t>() : idx->subs.marks();
+  h.soff_n = soff.size();
+  h.pinned_n = marks.size();
   h.blob_in_image = (flags & EMQX_GM_IMAGE_NO_BLOB) ? 0 : 1;
   h.flen_stale = idx->flen_stale.load() ? 1 : 0;
   uint64_t o = al(sizeof(ImageHeader));
@@ -192,8 +194,8 @@ int index_export(emqx_gm_ctx* ctx, const emqx_gm_index* idx, uint32_t flags, uin
     fo[r + 1] = at;
   });
   if (h.gmap_n) std::memcpy(buf + h.sec_off[2], idx->gmap.data(), h.gmap_n * 4);
-  if (h.soff_n) std::memcpy(buf + h.sec_off[3], idx->soff.data(), h.soff_n * 8);
-  if (h.pinned_n) std::memcpy(buf + h.sec_off[4], idx->pinned.data(), h.pinned_n);
+  if (h.soff_n) std::memcpy(buf + h.sec_off[3], soff.data(), h.soff_n * 8);
+  if (h.pinned_n) std::memcpy(buf + h.sec_off[4], marks.data(), h.pinned_n);
   if (h.blob_in_image && host_only) {
     std::memcpy(buf + h.sec_off[5], base, h.dev_bytes);
   } else if (h.blob_in_image) {
@@ -339,8 +341,9 @@ int import_host_part(const uint8_t* img, uint64_t size, bool have_blob, emqx_gm_
   const uint32_t* gm = reinterpret_cast<const uint32_t*>(img + h.sec_off[2]);
   idx->gmap.assign(gm, gm + h.gmap_n);
   const uint64_t* so = reinterpret_cast<const uint64_t*>(img + h.sec_off[3]);
-  idx->soff.assign(so, so + h.soff_n);
-  idx->pinned.assign(img + h.sec_off[4], img + h.sec_off[4] + h.pinned_n);
+  if (h.soff_n)
+    idx->subs = SubTable(std::vector<uint64_t>(so, so + h.soff_n),
+                         std::vector<uint8_t>(img + h.sec_off[4], img + h.sec_off[4] + h.pinned_n));
   if (h.mirror.present) {  // the updatable line continues here; its host copy loads on the first update
     const MirrorMeta& mm = h.mirror;
     auto* m = new Mirror;

@@ -967,7 +967,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     if (rc == 0) v.flags |= IX_D0;
   }
 
-  if (sub_off) idx->soff = std::move(soff);
+  if (sub_off) idx->subs = SubTable(std::move(soff), {});
   emqx_gm_index_info_t& in = idx->info;
   in.n_filters = nf;
   in.n_wildcard = n_wild;

@@ -234,9 +234,8 @@ struct emqx_gm_index {
   // host copies
   gm::FilterTable ft;           // the sorted unique filters (id = rank), gm_filters.h
   std::vector<uint32_t> gmap;   // shard index: global id of each local filter (ascending); empty otherwise
-  std::vector<uint64_t> soff;   // subscriber CSR offsets per filter id (host copy; empty without subscribers)
-  std::vector<uint8_t> pinned;  // per filter: its route is held by another destination (emqx_gm_index_update_subs
-                                // ROUTE_ADD); empty: a built index, where a filter without subscribers is route-only
+  gm::SubTable subs;            // per filter id: subscriber CSR offset and route mark (emqx_gm_index_update_subs
+                                // ROUTE_ADD); empty without subscriber lists.  gm_filters.h
   gm::OverlayState* ov = nullptr;  // overlay snapshot (emqx_gm_index_update); tables above unused then
   uint64_t level_nodes = 0;        // an upper bound on the trie nodes of any one depth (the slow path's frontier); 0: unknown
   gm::Mirror* mirror = nullptr;    // host copy of the blob (updatable plain index), see gm::Mirror
@@ -362,6 +361,11 @@ bool is_pinned(const emqx_gm_index* idx, uint64_t f);
 // device gather + one copy back
 int gather_segments(emqx_gm_ctx* ctx, const uint32_t* src, const std::vector<uint64_t>& src_off,
                     const std::vector<uint64_t>& dst_off, uint32_t* out);
+// gm_match.hip: the new subscriber CSR of a subscriber-only update_subs batch
+// (ids unchanged; O(delta) host work, see there)
+int shift_subs_device(emqx_gm_ctx* ctx, const emqx_gm_index* prev, emqx_gm_index* idx,
+                      const std::vector<uint32_t>& aff_ids, const std::vector<uint64_t>& aff_off,
+                      const std::vector<uint32_t>& aff_buf);
 // gm_match.hip: the new subscriber CSR of update_subs (see there)
 int rebuild_subs_device(emqx_gm_ctx* ctx, const emqx_gm_index* prev, emqx_gm_index* idx,
                         const std::vector<uint64_t>& new_soff, const std::vector<uint32_t>& inv,

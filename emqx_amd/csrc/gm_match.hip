@@ -2740,7 +2740,24 @@ __global__ __launch_bounds__(256) void k_subs_copy(const uint64_t* __restrict__ 
       if (aff_ids[m] < f) a = m + 1;
       else b = m;
     }
-    out[p] = (a < n_aff && aff_ids[a] == f) ? aff_buf[aff_off[a] + q] : oids[osoff[inv[f]] + q];
+    out[p] = (a < n_aff && aff_ids[a] == f) ? aff_buf[aff_off[a] + q] : oids[osoff[inv ? inv[f] : f] + q];
+  }
+}
+
+// A subscriber-only batch (ids unchanged): new sub_off[i] = old sub_off[i] +
+// the count changes of the touched filters below i (tid ascending, tcum their
+// running sum) -- the host uploads only the touched ids
+__global__ __launch_bounds__(256) void k_soff_shift(const uint64_t* __restrict__ osoff, uint64_t n1,
+                                                    const uint32_t* __restrict__ tid, const int64_t* __restrict__ tcum,
+                                                    uint64_t nt, uint64_t* __restrict__ nsoff) {
+  for (uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x; i < n1; i += uint64_t(gridDim.x) * 256u) {
+    uint64_t a = 0, b = nt;  // touched ids below i
+    while (a < b) {
+      const uint64_t m = (a + b) >> 1;
+      if (tid[m] < i) a = m + 1;
+      else b = m;
+    }
+    nsoff[i] = uint64_t(int64_t(osoff[i]) + (a ? tcum[a - 1] : 0));
   }
 }
 
@@ -2777,6 +2794,63 @@ int gather_segments(emqx_gm_ctx* ctx, const uint32_t* src, const std::vector<uin
   GM_HIP(ctx, hipGetLastError());
   GM_HIP(ctx, hipMemcpyAsync(out, buf.p, total * 4, hipMemcpyDeviceToHost, st));
   GM_HIP(ctx, hipStreamSynchronize(st));
+  return EMQX_GM_OK;
+}
+
+// The new subscriber CSR of a subscriber-only emqx_gm_index_update_subs batch
+// (gm_subs.cpp; filter ids unchanged): O(delta) host work -- the touched
+// filters' ids, count changes and lists go up -- and the device derives the
+// offsets (k_soff_shift) and copies every other filter's segment from prev's
+// CSR (k_subs_copy with the identity id map).
+int shift_subs_device(emqx_gm_ctx* ctx, const emqx_gm_index* prev, emqx_gm_index* idx,
+                      const std::vector<uint32_t>& aff_ids, const std::vector<uint64_t>& aff_off,
+                      const std::vector<uint32_t>& aff_buf) {
+  const uint64_t nf = prev->info.n_filters, na = aff_ids.size();
+  std::vector<int64_t> tcum(na + 1, 0);
+  int64_t cum = 0;
+  for (uint64_t k = 0; k < na; ++k) {
+    if (aff_ids[k] >= nf || (k && aff_ids[k] <= aff_ids[k - 1]))
+      return set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: touched ids");
+    cum += int64_t(aff_off[k + 1] - aff_off[k]) - int64_t(prev->subs.count(aff_ids[k]));
+    tcum[k] = cum;
+  }
+  const uint64_t total = uint64_t(int64_t(prev->subs.total()) + cum);
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t o_ids = al((nf + 1) * 8);
+  GM_HIP(ctx, hipMalloc(&idx->dev_subs, o_ids + total * 4 + 16));
+  idx->subs_bytes = o_ids + total * 4 + 16;
+  uint8_t* D = static_cast<uint8_t*>(idx->dev_subs);
+  hipStream_t st = ctx->stream;
+  // staging: tid | tcum | aff_off | aff_buf
+  const size_t o_cum = al(na * 4 + 4), o_aoff = o_cum + al((na + 1) * 8), o_abuf = o_aoff + al(aff_off.size() * 8),
+               n_st = o_abuf + aff_buf.size() * 4 + 4;
+  std::vector<uint8_t> h(n_st, 0);
+  if (na) std::memcpy(h.data(), aff_ids.data(), na * 4);
+  std::memcpy(h.data() + o_cum, tcum.data(), (na + 1) * 8);
+  std::memcpy(h.data() + o_aoff, aff_off.data(), aff_off.size() * 8);
+  if (!aff_buf.empty()) std::memcpy(h.data() + o_abuf, aff_buf.data(), aff_buf.size() * 4);
+  PoolBuf sbuf(ctx->pool, n_st);
+  if (!sbuf.p) return set_err(ctx, EMQX_GM_ENOMEM, "index_update_subs: staging");
+  GM_HIP(ctx, hipMemcpyAsync(sbuf.p, h.data(), n_st, hipMemcpyHostToDevice, st));
+  const uint8_t* S = sbuf.as<uint8_t>();
+  const uint64_t g = std::min<uint64_t>(4096, (nf + 1 + 255) / 256);
+  hipLaunchKernelGGL(k_soff_shift, dim3(g), dim3(256), 0, st, prev->view.sub_off, nf + 1,
+                     reinterpret_cast<const uint32_t*>(S), reinterpret_cast<const int64_t*>(S + o_cum), na,
+                     reinterpret_cast<uint64_t*>(D));
+  GM_HIP(ctx, hipGetLastError());
+  if (total) {
+    const uint64_t per = fan_per_block(total);
+    hipLaunchKernelGGL(k_subs_copy, dim3((total + per - 1) / per), dim3(256), 0, st,
+                       reinterpret_cast<const uint64_t*>(D), nf, static_cast<const uint32_t*>(nullptr),
+                       prev->view.sub_off, prev->view.sub_ids, reinterpret_cast<const uint32_t*>(S), na,
+                       reinterpret_cast<const uint64_t*>(S + o_aoff), reinterpret_cast<const uint32_t*>(S + o_abuf),
+                       total, per, reinterpret_cast<uint32_t*>(D + o_ids));
+    GM_HIP(ctx, hipGetLastError());
+  }
+  GM_HIP(ctx, hipStreamSynchronize(st));  // the staging goes back to the pool / the host
+  idx->view.sub_off = reinterpret_cast<const uint64_t*>(D);
+  idx->view.sub_ids = reinterpret_cast<const uint32_t*>(D + o_ids);
+  idx->info.device_bytes += o_ids + total * 4 + 16;
   return EMQX_GM_OK;
 }
 

@@ -72,8 +72,7 @@ int replicate_index(emqx_gm_ctx* m, const emqx_gm_index* src, emqx_gm_index* sha
   r->view = src->view;
   r->ft = src->ft;  // (a shared base + a small delta: cheap)
   r->gmap = src->gmap;
-  r->soff = src->soff;
-  r->pinned = src->pinned;
+  r->subs = src->subs;  // (a shared base + a small delta: cheap)
   r->ov = nullptr;
   r->level_nodes = src->level_nodes;
   r->flen_stale = src->flen_stale.load();

@@ -647,7 +647,7 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
   if (n_ops && (!fb || !fo || !ops)) return set_err(ctx, EMQX_GM_EINVAL, "index_update: NULL op buffers");
   if (!prev->gmap.empty()) return set_err(ctx, EMQX_GM_EUNSUPPORTED, "index_update: shard index");
   emqx_gm_index* base = prev->ov ? prev->ov->base : prev;
-  if (!base->soff.empty())  // (its CSR may live outside the tables: emqx_gm_index_update_subs)
+  if (!base->subs.empty())  // (its CSR may live outside the tables: emqx_gm_index_update_subs)
     return set_err(ctx, EMQX_GM_EUNSUPPORTED, "index_update: index with subscriber lists (use index_update_subs)");
   std::set<uint32_t> tomb;
   std::set<std::string> dset;

@@ -75,7 +75,7 @@ int rebuild(emqx_gm_ctx* ctx, const emqx_gm_index* prev, const std::map<std::str
             emqx_gm_index** out) {
   std::vector<uint8_t> pin_in;  // per input filter, in the order they are added below
   const uint64_t nb = prev->info.n_filters;
-  std::vector<uint32_t> all(prev->soff.back());
+  std::vector<uint32_t> all(prev->subs.total());
   if (!all.empty())
     GM_HIP(ctx, hipMemcpy(all.data(), prev->view.sub_ids, all.size() * 4, hipMemcpyDeviceToHost));
   std::vector<const FilterEdit*> edit_of(nb, nullptr);
@@ -97,7 +97,7 @@ int rebuild(emqx_gm_ctx* ctx, const emqx_gm_index* prev, const std::map<std::str
       const std::vector<uint32_t> l = e->final_list();
       add(p, len, l.data(), l.size(), e->pinned());
     } else {
-      add(p, len, all.data() + prev->soff[f], prev->soff[f + 1] - prev->soff[f], is_pinned(prev, f));
+      add(p, len, all.data() + prev->subs.off(f), prev->subs.count(f), is_pinned(prev, f));
     }
   });
   for (const auto& kv : ed)
@@ -110,16 +110,17 @@ int rebuild(emqx_gm_ctx* ctx, const emqx_gm_index* prev, const std::map<std::str
   std::vector<uint32_t> perm(pin_in.size() + 1);
   const int rc = build_index(ctx, fb.data(), fo.data(), fo.size() - 1, so.data(), si.data(), perm.data(), out);
   if (rc) return rc;
-  (*out)->pinned.assign((*out)->info.n_filters, 0);
-  for (size_t i = 0; i < pin_in.size(); ++i) (*out)->pinned[perm[i]] = pin_in[i];
+  std::vector<uint8_t> marks((*out)->info.n_filters, 0);
+  for (size_t i = 0; i < pin_in.size(); ++i) marks[perm[i]] = pin_in[i];
+  (*out)->subs = SubTable((*out)->subs.offsets(), std::move(marks));
   return 0;
 }
 
 }  // namespace
 
 bool is_pinned(const emqx_gm_index* idx, uint64_t f) {
-  if (!idx->pinned.empty()) return idx->pinned[f] != 0;
-  return idx->soff.empty() || idx->soff[f + 1] == idx->soff[f];  // built: a filter without subscribers is route-only
+  // (built: a filter without subscribers is route-only; gm_filters.h SubTable)
+  return idx->subs.empty() || idx->subs.pinned(f);
 }
 
 int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo, const uint32_t* subs,
@@ -128,7 +129,7 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
   if (n_ops && (!fb || !fo || !subs || !ops)) return set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: NULL op buffers");
   if (prev->ov) return set_err(ctx, EMQX_GM_EUNSUPPORTED, "index_update_subs: overlay snapshot");
   if (!prev->gmap.empty()) return set_err(ctx, EMQX_GM_EUNSUPPORTED, "index_update_subs: shard index");
-  if (prev->soff.empty())
+  if (prev->subs.empty())
     return set_err(ctx, EMQX_GM_EUNSUPPORTED,
                    "index_update_subs: index without subscriber lists (route updates: emqx_gm_index_update)");
   for (uint64_t i = 0; i < n_ops; ++i)
@@ -154,8 +155,8 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
       if (kv.second.old_id != NONE) {
         const uint32_t id = kv.second.old_id;
         touched.push_back(&kv.second);
-        src_off.push_back(prev->soff[id]);
-        dst_off.push_back(dst_off.back() + (prev->soff[id + 1] - prev->soff[id]));
+        src_off.push_back(prev->subs.off(id));
+        dst_off.push_back(dst_off.back() + prev->subs.count(id));
       }
     std::vector<uint32_t> all(dst_off.back());
     if (!all.empty()) {
@@ -198,11 +199,13 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
   emqx_gm_index* idx = nullptr;
   std::vector<uint32_t> rmap;
   int rc = 1;
+  bool same_routes = false;
   {
     std::unique_lock<std::mutex> lk(prev->mirror_mu);
-    if (prev->mirror && tomb.empty() && dset.empty()) {
-      // no route changed: the new snapshot shares prev's tables (retained), the
-      // mirror moves on with it; only the subscriber CSR is new
+    if (tomb.empty() && dset.empty()) {
+      // No route changed (a subscriber-only batch): the new snapshot shares
+      // prev's tables (retained; the mirror, if any, moves on with it) and its
+      // filter ids; only the subscriber CSR is new.  O(delta) on the host.
       idx = new emqx_gm_index;
       idx->device = prev->device;
       idx->dev_base = prev->dev_base;
@@ -214,13 +217,13 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
       idx->info = prev->info;
       idx->info.device_bytes = prev->dev_bytes;  // the tables; the new CSR is added below
       idx->ft = prev->ft;
+      idx->gmap = prev->gmap;
       idx->dev_flen = prev->dev_flen;
       idx->flen_stale = prev->flen_stale.load();
       idx->level_nodes = prev->level_nodes;
       idx->mirror = prev->mirror;
       prev->mirror = nullptr;
-      rmap.resize(nb);
-      for (uint64_t f = 0; f < nb; ++f) rmap[f] = uint32_t(f);
+      same_routes = true;
       rc = 0;
     } else if (prev->mirror && wf && tomb.size() + dset.size() <= std::max<uint64_t>(4096, nb / 8)) {
       rc = patch_update(ctx, prev, tomb, dset, &idx, &rmap, /*trie_only=*/true);
@@ -228,7 +231,32 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
   }
   if (rc < 0) return rc;
   if (rc == 1) return rebuild(ctx, prev, ed, out);
-  // ---- the new CSR: new id -> old id, the touched filters' final lists by new id
+  if (same_routes) {
+    // the touched filters' counts and marks (ids ascending = byte order: ed's order)
+    std::vector<std::pair<uint32_t, uint64_t>> cnt;
+    std::vector<std::pair<uint32_t, uint8_t>> pin;
+    std::vector<uint32_t> aff_ids, aff_buf;
+    std::vector<uint64_t> aff_off{0};
+    for (const auto& kv : ed) {
+      if (kv.second.old_id == NONE) continue;  // (an absent filter that stays absent)
+      const std::vector<uint32_t> l = kv.second.final_list();
+      cnt.emplace_back(kv.second.old_id, l.size());
+      pin.emplace_back(kv.second.old_id, kv.second.pinned() ? 1 : 0);
+      aff_ids.push_back(kv.second.old_id);
+      aff_buf.insert(aff_buf.end(), l.begin(), l.end());
+      aff_off.push_back(aff_buf.size());
+    }
+    idx->subs = prev->subs.apply(cnt, pin);
+    rc = shift_subs_device(ctx, prev, idx, aff_ids, aff_off, aff_buf);
+    if (rc) {
+      free_index(idx);
+      return rc;
+    }
+    idx->info.n_subs = idx->subs.total();
+    *out = idx;
+    return EMQX_GM_OK;
+  }
+  // ---- route changes (ids renumbered): the new CSR from new id -> old id, the touched filters' final lists
   const uint64_t nf = idx->info.n_filters;
   std::vector<uint32_t> inv(nf, NONE);
   for (uint64_t f = 0; f < nb; ++f)
@@ -248,7 +276,7 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
   std::vector<uint64_t> aff_off{0};
   std::vector<uint64_t> cnt(nf, 0);
   for (uint64_t f = 0; f < nf; ++f)
-    if (inv[f] != NONE) cnt[f] = prev->soff[inv[f] + 1] - prev->soff[inv[f]];
+    if (inv[f] != NONE) cnt[f] = prev->subs.count(inv[f]);
   for (auto& a : aff) {
     aff_ids.push_back(a.first);
     aff_buf.insert(aff_buf.end(), a.second.begin(), a.second.end());
@@ -264,19 +292,19 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
   }
   idx->info.n_subs = new_soff.back();
   // the route-only marks of the new ids: untouched filters keep prev's, touched ones their final state
-  idx->pinned.assign(nf, 0);
+  std::vector<uint8_t> marks(nf, 0);
   for (uint64_t f = 0; f < nf; ++f)
-    if (inv[f] != NONE) idx->pinned[f] = is_pinned(prev, inv[f]) ? 1 : 0;
+    if (inv[f] != NONE) marks[f] = is_pinned(prev, inv[f]) ? 1 : 0;
   {
     uint64_t k = 0;
     for (const auto& kv : ed) {
       uint32_t nid = NONE;
       if (kv.second.old_id != NONE) nid = rmap[kv.second.old_id];
       else if (dset.count(kv.first)) nid = rmap[nb + k++];
-      if (nid != NONE) idx->pinned[nid] = kv.second.pinned() ? 1 : 0;
+      if (nid != NONE) marks[nid] = kv.second.pinned() ? 1 : 0;
     }
   }
-  idx->soff = std::move(new_soff);
+  idx->subs = SubTable(std::move(new_soff), std::move(marks));
   *out = idx;
   return EMQX_GM_OK;
 }

@@ -83,28 +83,46 @@ def _own_stream(ctx):
     library's kernels, torch's tensor ops and the collectives then share one
     ordered stream.  torch's DEFAULT stream cannot serve: its handle is NULL,
     which the library reads as "keep your own (non-blocking) stream", and
-    nothing would order the two."""
+    nothing would order the two.
+
+    torch's device runtime must have come up before the library's (DESIGN.md
+    §7): emqx_amd.Context initialises it first whenever torch is importable; a
+    process that made its HIP context some other way first gets this error
+    instead of torch's bare "No HIP GPUs are available"."""
     import torch
-    s = torch.cuda.Stream(device=torch.device("cuda", ctx.device))
+    try:
+        s = torch.cuda.Stream(device=torch.device("cuda", ctx.device))
+    except RuntimeError as e:
+        raise RuntimeError(
+            "emqx_amd: torch cannot see the device because the HIP runtime was initialised before torch's; "
+            "create torch's device state first (emqx_amd.Context does when torch is importable, or call "
+            "torch.cuda.init() before any library call)") from e
     ctx.set_stream(s.cuda_stream)
     return s
 
 
 class _on:
-    """``with torch.cuda.stream(s)`` for a stream that may be None (host path)."""
+    """``with torch.cuda.stream(s)`` for a stream that may be None (host path),
+    ordered against the caller's stream both ways: the matcher's stream first
+    waits for the work the caller queued (e.g. the torch ops that wrote its
+    input topics), and on exit the caller's stream waits for the matcher's (so
+    its consumers of the returned rows run after the kernels that wrote them)."""
 
     def __init__(self, stream):
-        self.stream, self.cm = stream, None
+        self.stream, self.cm, self.caller = stream, None, None
 
     def __enter__(self):
         if self.stream is not None:
             import torch
+            self.caller = torch.cuda.current_stream(self.stream.device)
+            self.stream.wait_stream(self.caller)
             self.cm = torch.cuda.stream(self.stream)
             self.cm.__enter__()
 
     def __exit__(self, *a):
         if self.cm is not None:
             self.cm.__exit__(*a)
+            self.caller.wait_stream(self.stream)
 
 
 class ShardedMatcher:

@@ -5,8 +5,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export PYTHONUNBUFFERED=1
 mkdir -p gpurun_out/r05_b
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_image.py \
-  tests/test_gpu_multi.py::test_updates_replicated > gpurun_out/r05_b/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_image.py \
+  tests/test_gpu_multi.py tests/test_gpu_updates.py \
+  tests/test_gpu_sharded.py::test_prefix_device_path_library_first_default_stream_inputs \
+  tests/test_gpu_sharded.py::test_prefix_device_path_world1 > gpurun_out/r05_b/pytest.log 2>&1
 rc=$?
 tail -n 15 gpurun_out/r05_b/pytest.log
 [ $rc -ne 0 ] && exit $rc

@@ -13,7 +13,13 @@ Every rank's rows of its own batch must equal the unsharded index's rows, and
 rank 0's first window the oracle's.  torch's device runtime is initialised
 before the library, as in bench.py.
 
-usage: _prefix_device_worker.py WORLD N_FILTERS TOPICS_PER_RANK
+usage: _prefix_device_worker.py WORLD N_FILTERS TOPICS_PER_RANK [libfirst]
+
+libfirst (world 1): the library's Context is made BEFORE anything touches
+torch's device (emqx_amd.Context brings torch's runtime up first itself), and
+the topics are written by torch ops on torch's default stream with
+non-blocking copies -- the matcher's stream must wait for them, and the
+caller's stream for the matcher's rows.
 """
 
 import os
@@ -66,7 +72,11 @@ class LockstepExchange:
 
 def main():
     W, n_f, n = (int(x) for x in sys.argv[1:4])
-    torch.zeros(1, device="cuda:0")  # torch's runtime first
+    libfirst = len(sys.argv) > 4 and sys.argv[4] == "libfirst"
+    if libfirst:
+        from emqx_amd import Context
+        Context(0).close()  # the library first: its Context initialises torch's runtime itself
+    torch.zeros(1, device="cuda:0")
     from emqx_amd import Context
     from emqx_amd.engine import gen_filter_codes, render_codes
     from emqx_amd.sharded import PrefixShardedMatcher, plan_prefix_shard
@@ -76,6 +86,16 @@ def main():
     plans = [plan_prefix_shard(fb, fo, W, q) for q in range(W)]
     idxs = [ctxs[q].build_index_shard((plans[q][0], plans[q][1]), plans[q][2]) for q in range(W)]
     batches = [ctxs[q].gen_topics_device(codes, 1, q * n, n) for q in range(W)]
+    keep = []
+    if libfirst:  # the same topics written by torch ops on the default stream, not yet complete when matched
+        from oracle import oracle as orc
+        tb, to = orc.render_codes(orc.gen_topic_codes(1, 0, n, codes))
+        t_tb = torch.from_numpy(np.concatenate([tb, np.zeros(64, np.uint8)])).pin_memory().to("cuda:0",
+                                                                                              non_blocking=True)
+        t_to = torch.from_numpy(to.view(np.int64)).pin_memory().to("cuda:0", non_blocking=True)
+        t_tb2 = t_tb.clone()  # (more default-stream work in front of the match)
+        keep = [t_tb, t_to, t_tb2]
+        batches = [(t_tb2.data_ptr(), t_to.data_ptr(), int(to[-1]))]
     ex = LockstepExchange(W)
     results, walked, errors, matchers = [None] * W, [0] * W, [], [None] * W
 
@@ -127,14 +147,16 @@ def main():
     for q in range(W):
         results[q].free()
         ctxs[q].set_stream(0)
-        ctxs[q].dev_free(batches[q][0])
-        ctxs[q].dev_free(batches[q][1])
+        if not libfirst:
+            ctxs[q].dev_free(batches[q][0])
+            ctxs[q].dev_free(batches[q][1])
         idxs[q].release()
         plans[q][4].release()
         ctxs[q].close()
     full.release()
     full_ctx.close()
-    print(f"PREFIX_DEVICE_PATH_OK world={W} walked={walked}", flush=True)
+    del keep
+    print(f"PREFIX_DEVICE_PATH_OK world={W} walked={walked}{' libfirst' if libfirst else ''}", flush=True)
 
 
 if __name__ == "__main__":

@@ -416,6 +416,17 @@ def test_prefix_device_path_world1():
     assert "PREFIX_DEVICE_PATH_OK world=1" in _run_worker("_prefix_device_worker.py", 1, 200_000, 300_000)
 
 
+def test_prefix_device_path_library_first_default_stream_inputs():
+    """The library's Context made before anything touches torch's device
+    (PrefixShardedMatcher then failed with "No HIP GPUs are
+    available"; emqx_amd.Context now brings torch's runtime up first), and the
+    topics written by torch ops on torch's default stream with non-blocking
+    copies (the matcher's stream waits for the caller's, the
+    caller's for the matcher's rows): rows == the unsharded index == the oracle."""
+    out = _run_worker("_prefix_device_worker.py", 1, 200_000, 300_000, "libfirst")
+    assert "PREFIX_DEVICE_PATH_OK world=1" in out and "libfirst" in out
+
+
 @pytest.mark.timeout(600)
 def test_prefix_device_path_world8_lockstep():
     """The 4M-filter set in 8 prefix shards, 8 ranks as threads on one device,
