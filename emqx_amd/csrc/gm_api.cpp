@@ -778,6 +778,8 @@ int emqx_gm_route_topics(emqx_gm_ctx* ctx, emqx_gm_route* route, const uint8_t* 
   if (!ctx) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   if (!route || (n && (!d_tb || !d_to || !d_dest))) return gm::set_err(ctx, EMQX_GM_EINVAL, "route_topics: NULL argument");
+  if (n >= 0xFFFFFFFFull)  // (u32 batch indices: perm, dest)
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "route_topics: batch too large (>= 2^32 topics)");
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
   return gm::route_topics_device(ctx, route, d_tb, d_to, n, d_dest);
@@ -790,6 +792,8 @@ int emqx_gm_route_partition(emqx_gm_ctx* ctx, emqx_gm_route* route, const uint8_
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   if (!route || !d_split || (n && (!d_tb || !d_to || !d_perm || !d_plen)))
     return gm::set_err(ctx, EMQX_GM_EINVAL, "route_partition: NULL argument");
+  if (n >= 0xFFFFFFFFull)  // (u32 batch indices: perm, dest)
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "route_partition: batch too large (>= 2^32 topics)");
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
   return gm::route_partition(ctx, route, d_tb, d_to, n, d_perm, d_plen, d_split);
@@ -808,6 +812,8 @@ int emqx_gm_permute_topics(emqx_gm_ctx* ctx, const uint8_t* d_tb, const uint64_t
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   if (!d_out_off || (n && (!d_tb || !d_to || !d_perm || !d_out)))
     return gm::set_err(ctx, EMQX_GM_EINVAL, "permute_topics: NULL argument");
+  if (n >= 0xFFFFFFFFull)  // (u32 batch indices: perm, dest)
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "permute_topics: batch too large (>= 2^32 topics)");
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
   return gm::permute_topics(ctx, d_tb, d_to, n, d_perm, d_out, d_out_off);
@@ -820,6 +826,8 @@ int emqx_gm_unpermute_rows(emqx_gm_ctx* ctx, uint64_t n, const uint32_t* d_perm,
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   if (!out || (n && (!d_perm || !d_lens || !d_ids)))
     return gm::set_err(ctx, EMQX_GM_EINVAL, "unpermute_rows: NULL argument");
+  if (n >= 0xFFFFFFFFull)  // (u32 batch indices: perm, dest)
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "unpermute_rows: batch too large (>= 2^32 topics)");
   if (flags & ~EMQX_GM_DEVICE_IO) return gm::set_err(ctx, EMQX_GM_EINVAL, "unpermute_rows: flags");
   std::memset(out, 0, sizeof(*out));
   GM_GUARD_BEGIN

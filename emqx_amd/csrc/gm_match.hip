@@ -3473,10 +3473,6 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   // block offsets -- one launch fewer; GM_SCAN_SPLIT=0 turns it off)
   const char* se = getenv("GM_SCAN_SPLIT");
   split = cmp && (!se || atoi(se) != 0);
-  int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p,
-                     SideSum{probe_tile.as<unsigned long long>(), n_tiles, probe_ctr}, split ? &scan_blk : nullptr, sa,
-                     split && sums_mode() ? &split_sums : nullptr);
-  if (rc) return rc;
   // Speculative assembly: the rows are written before the host has read the
   // match total, into an ids buffer sized from this context's recent matches
   // per topic (x1.25), so a call makes ONE host round trip.  The total, the
@@ -3487,8 +3483,17 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   cap_spec = 1024 + uint64_t(double(n) * std::min(ctx->ids_per_topic, double(FAST_MC)));
   // (no room for the speculative buffer: skip speculation, the rows are
   // assembled at their exact size once the total is known)
-  ids = PoolBuf(ctx->pool, cap_spec * 4 + 16);
+  if (!getenv("GM_NO_SPEC_IDS")) ids = PoolBuf(ctx->pool, cap_spec * 4 + 16);  // (test knob: as if it failed)
   spec = ids.p != nullptr;
+  // The scan may hand back block SUMS (split_sums) only when the speculative
+  // assembly runs: that kernel sums them and writes the grand total to
+  // toff[n_tiles], which the read-back below copies.  Without it the total
+  // would still be k_scan_local's block-local prefix, so the scan
+  // then writes its block offsets and total itself.
+  int rc = scan_excl(ctx, LoadU64{tsum.as<uint64_t>()}, n_tiles, toff_p,
+                     SideSum{probe_tile.as<unsigned long long>(), n_tiles, probe_ctr}, split ? &scan_blk : nullptr, sa,
+                     split && spec && sums_mode() ? &split_sums : nullptr);
+  if (rc) return rc;
   // (compact staging with no host copy-out queued behind: the assembly kernel
   // writes the read-back words itself and its stop event is the call's end --
   // a copy and an event record fewer, ~10 us of idle stream per call at C1)

@@ -341,6 +341,8 @@ int emqx_gm_route_release(emqx_gm_route *route);
 int emqx_gm_route_partition(emqx_gm_ctx *ctx, emqx_gm_route *route, const uint8_t *d_topic_bytes,
                             const uint64_t *d_topic_off, uint64_t n_topics, uint32_t *d_perm, uint32_t *d_plen,
                             uint64_t *d_split);
+/* (route_topics / route_partition / permute_topics / unpermute_rows index the
+ * batch with u32: n_topics / n_rows < 2^32 - 1, else EMQX_GM_EINVAL) */
 /* The exchange's device steps.  permute: out topic i = topic perm[i] (d_out
  * holds as many bytes as the input, d_out_off n+1 entries).  unpermute: row
  * perm[i] of the result = input row i, the input rows packed with u32 lengths

@@ -1028,3 +1028,32 @@ def test_c_abi_smoke_program():
                         "-Wl,-rpath," + os.path.join(root, "emqx_amd"), "-o", exe], check=True)
     p = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and "C_ABI_SMOKE_OK" in p.stdout, p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("n", [1_000_000, 3_000_000])
+def test_no_speculative_ids_split_scan(ctx, orc, monkeypatch, n):
+    """with compact staging the tile scan of a 2..64-block call hands
+    back block SUMS, which only the speculative assembly turns into the grand
+    total.  When the speculative ids buffer cannot be allocated
+    (GM_NO_SPEC_IDS=1 forces that), the scan must write its offsets and total
+    itself: the rows equal the default path's and the oracle's."""
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    codes = gen_filter_codes(9, 50_000, wildcard_only=True)
+    fpack = render_codes(codes)
+    idx = ctx.build_index(fpack)
+    db, do, _ = ctx.gen_topics_device(codes, 9, 0, n)
+    ref = ctx.match_device(idx, db, do, n, exact=True)
+    ro0, ids0 = ref.to_host()
+    ref.free()
+    monkeypatch.setenv("GM_NO_SPEC_IDS", "1")
+    res = ctx.match_device(idx, db, do, n, exact=True)
+    ro, ids = res.to_host()
+    res.free()
+    assert np.array_equal(ro, ro0) and np.array_equal(ids, ids0)
+    filters = sorted(set(orc.unpack(*fpack)))
+    tb, to = orc.render_codes(orc.gen_topic_codes(9, 0, 20_000, codes))
+    oro, oids = _oracle_rows(orc, filters, orc.unpack(tb, to), 1)
+    assert np.array_equal(ro[:20_001], oro) and np.array_equal(ids[:int(oro[-1])], oids)
+    ctx.dev_free(db)
+    ctx.dev_free(do)
+    idx.release()
