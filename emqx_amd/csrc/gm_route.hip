@@ -95,6 +95,65 @@ GM_HD uint32_t rt_route(const RouteSlot* slots, uint32_t mask, const uint8_t* ar
   return s == RT_EMPTY || (s & RT_SPLIT) ? fallback : s;
 }
 
+// The device form of rt_route, 8 bytes at a time: a topic's bytes come as
+// little-endian u64 chunks (two aligned loads and a funnel shift each; the
+// batch is padded by 64 readable bytes), the first '/' is found by a SWAR
+// compare, the key hash takes whole chunks (bytes past the key zeroed, as
+// rt_hash's zero padding), and a hit is verified chunk by chunk against the
+// arena (padded by 8).  Same shard as rt_route for every topic
+// (test_device_route_equals_host_route); byte-at-a-time global loads had
+// made the route 3.1 ms of a 100M-topic step (profiles/r04_l).
+__device__ __forceinline__ uint64_t ld8(const uint8_t* base, uint64_t pos) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(base + pos) & ~uintptr_t(7));
+  const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(base + pos) & 7u) * 8u;
+  const uint64_t lo = w[0];
+  return sh ? (lo >> sh) | (w[1] << (64u - sh)) : lo;
+}
+__device__ __forceinline__ uint64_t keep_bytes(uint64_t c, uint32_t nb) {  // the low nb bytes of c (nb <= 8)
+  return nb >= 8 ? c : (c & ((1ull << (8u * nb)) - 1ull));
+}
+__device__ __forceinline__ uint32_t first_slash(const uint8_t* t, uint32_t from, uint32_t len) {
+  for (uint32_t i = from; i < len; i += 8) {
+    const uint64_t x = ld8(t, i) ^ 0x2F2F2F2F2F2F2F2Full;  // '/' -> 0x00
+    const uint64_t z = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+    if (z) {
+      const uint32_t at = i + uint32_t(__builtin_ctzll(z) >> 3);
+      return at < len ? at : len;
+    }
+  }
+  return len;
+}
+__device__ uint32_t rt_route_dev(const RouteSlot* slots, uint32_t mask, const uint8_t* arena, uint32_t n_shards,
+                                 const uint8_t* t, uint32_t len) {
+  auto hash = [&](uint32_t klen) {
+    uint32_t h = DICT_HASH_SEED;
+    for (uint32_t i = 0; i < klen; i += 8) h = dict_hash_step(h, keep_bytes(ld8(t, i), klen - i));
+    return dict_hash_final(h, klen);
+  };
+  auto find = [&](uint32_t klen) -> uint32_t {
+    const uint32_t h = hash(klen);
+    for (uint32_t s = h & mask;; s = (s + 1) & mask) {
+      const RouteSlot r = slots[s];
+      if (r.len == RT_EMPTY) return RT_EMPTY;
+      if (r.hash == h && r.len == klen) {
+        bool eq = true;
+        for (uint32_t i = 0; i < klen && eq; i += 8)
+          eq = keep_bytes(ld8(arena, r.off + i) ^ ld8(t, i), klen - i) == 0;
+        if (eq) return r.shard;
+      }
+    }
+  };
+  const uint32_t e0 = first_slash(t, 0, len);
+  const uint32_t fallback = fmix32(hash(e0) ^ 0x2545F491u) % n_shards;
+  uint32_t s = find(e0);
+  if (s == RT_EMPTY) return fallback;
+  if (!(s & RT_SPLIT)) return s;
+  if (e0 == len) return fallback;  // a one-word topic under a split word: only replicated filters match it
+  const uint32_t e1 = first_slash(t, e0 + 1, len);
+  s = find(e1);
+  return s == RT_EMPTY || (s & RT_SPLIT) ? fallback : s;
+}
+
 __global__ __launch_bounds__(256) void k_route(const RouteSlot* __restrict__ slots, uint32_t mask,
                                                const uint8_t* __restrict__ arena, uint32_t n_shards,
                                                const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
@@ -102,7 +161,7 @@ __global__ __launch_bounds__(256) void k_route(const RouteSlot* __restrict__ slo
   const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
   if (i >= n) return;
   const uint64_t a = to[i], b = to[i + 1];
-  dest[i] = rt_route(slots, mask, arena, n_shards, tb + a, uint32_t(b - a));
+  dest[i] = rt_route_dev(slots, mask, arena, n_shards, tb + a, uint32_t(b - a));
 }
 
 // ---- the send order in one pass pair (emqx_gm_route_partition): a counting
@@ -131,7 +190,7 @@ __global__ __launch_bounds__(256) void k_part_count(const RouteSlot* __restrict_
     const uint64_t i = b * RP_B + uint64_t(v) * 256 + tid;
     if (i < n) {
       const uint64_t a = to[i], e = to[i + 1];
-      uint32_t d = rt_route(slots, mask, arena, n_shards, tb + a, uint32_t(e - a));
+      uint32_t d = rt_route_dev(slots, mask, arena, n_shards, tb + a, uint32_t(e - a));
       d = d < n_shards ? d : d % n_shards;  // (rt_route returns a shard < n_shards; the LDS tables hold 256)
       dest[i] = uint8_t(d);
       atomicAdd(&s_c[d], 1u);
@@ -298,7 +357,7 @@ int route_plan(const uint8_t* fb, const uint64_t* fo, uint64_t n, uint32_t n_sha
     r->arena.insert(r->arena.end(), p, p + len);
     if (r->arena.size() >= 0xFFFFFFF0ull) throw std::length_error("prefix_plan: route keys exceed 4 GiB");
   }
-  r->arena.resize(r->arena.size() + 8, 0);
+  r->arena.resize(r->arena.size() + 16, 0);  // (rt_route_dev reads whole aligned u64 words)
   *out = r;
   return EMQX_GM_OK;
 }

@@ -61,7 +61,7 @@ def test_bench_two_ranks_c5_exchange():
 def test_bench_two_ranks_c5_replicated():
     """C5's default plan (north_star: replicate while the index fits): the
     unsharded index on every rank, the batch partitioned, weak scaling."""
-    out = _run_ranks(["--config", "c5", "--filters", "50000", "--topics", "200000"], world=2)
+    out = _run_ranks(["--config", "c5", "--filters", "2000000", "--topics", "200000"], world=2)
     assert out["n_gpus"] == 2 and out["scaling"] == "weak"
     assert out["config"]["topics_per_gpu"] == 200_000 and "replicated" in out["config"]["workload"]
     assert out["parity_sample"]["ok"]
@@ -69,6 +69,9 @@ def test_bench_two_ranks_c5_replicated():
     d = out["detail"]
     assert d["index_source"] == "built" and d["ranks_compiled"] == 1, d
     assert d["replicas_agree"] is True and d["host_peak_rss_gb_max"] > 0
+    # the importing rank neither renders the filter strings nor compiles: less host memory
+    rss = d["host_peak_rss_gb_per_rank"]
+    assert len(rss) == 2 and rss[1] < rss[0], rss
 
 
 @pytest.mark.gpu
