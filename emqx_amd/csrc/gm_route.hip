@@ -188,13 +188,31 @@ __global__ __launch_bounds__(256) void k_part_count(const RouteSlot* __restrict_
   const uint64_t b = blockIdx.x;
   for (int v = 0; v < RP_B / 256; ++v) {
     const uint64_t i = b * RP_B + uint64_t(v) * 256 + tid;
-    if (i < n) {
+    const bool ok = i < n;
+    uint32_t d = 0xFFFFFFFFu, len = 0;
+    if (ok) {
       const uint64_t a = to[i], e = to[i + 1];
-      uint32_t d = rt_route_dev(slots, mask, arena, n_shards, tb + a, uint32_t(e - a));
+      len = uint32_t(e - a);
+      d = rt_route_dev(slots, mask, arena, n_shards, tb + a, len);
       d = d < n_shards ? d : d % n_shards;  // (rt_route returns a shard < n_shards; the LDS tables hold 256)
       dest[i] = uint8_t(d);
-      atomicAdd(&s_c[d], 1u);
-      atomicAdd(&s_b[d], (unsigned long long)(e - a));
+    }
+    // the wave's counts per shard: one LDS atomic per distinct shard in the wave,
+    // not one per topic (a wave's topics mostly share few shards -- at one shard
+    // all of them: 1,024 same-address atomics per block were most of the kernel)
+    unsigned long long left = __ballot(ok);
+    while (left) {
+      const int leader = __builtin_ctzll(left);
+      const uint32_t dl = uint32_t(__shfl(int(d), leader, 64));
+      const unsigned long long m = __ballot(ok && d == dl);
+      uint64_t x = (ok && d == dl) ? len : 0u;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) x += uint64_t(__shfl_xor((long long)x, o, 64));
+      if ((tid & 63) == leader) {
+        atomicAdd(&s_c[dl], uint32_t(__popcll(m)));
+        atomicAdd(&s_b[dl], (unsigned long long)x);
+      }
+      left &= ~m;
     }
   }
   __syncthreads();

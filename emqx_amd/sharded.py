@@ -339,33 +339,28 @@ class PrefixShardedMatcher:
         cs, bs = both[0:2 * W:2], both[1:2 * W:2]
         rc, rb = both[2 * W::2], both[2 * W + 1::2]
         tot, m = sum(bs), sum(rc)
+        if W == 1:
+            # one shard: the stable send order is the batch order (perm = identity), so the
+            # permuted batch IS the batch and the rows come back in order -- both copies alias
+            res = ctx.match_device(self.index, d_tb, d_to, n, exact)
+            self.last_topics_walked = n
+            self.last_exchange_bytes = 0
+            return res
         pbytes = torch.empty(tot + 64, dtype=torch.uint8, device=dev)
         poff = torch.empty(n + 1, dtype=torch.int64, device=dev)
         ctx.permute_topics(d_tb, d_to, n, perm.data_ptr(), pbytes.data_ptr(), poff.data_ptr())
-        if W == 1:
-            rbytes = pbytes  # (its 64 bytes of slack past the text are readable: the tokenizer's)
-        else:
-            rbytes = torch.empty(sum(rb) + 64, dtype=torch.uint8, device=dev)
-            self.dist.all_to_all_single(rbytes[:sum(rb)], pbytes[:tot], output_split_sizes=rb,
-                                        input_split_sizes=bs, group=self.group)
-            rbytes[sum(rb):].zero_()
+        rbytes = torch.empty(sum(rb) + 64, dtype=torch.uint8, device=dev)
+        self.dist.all_to_all_single(rbytes[:sum(rb)], pbytes[:tot], output_split_sizes=rb, input_split_sizes=bs,
+                                    group=self.group)
+        rbytes[sum(rb):].zero_()
         rlens = self._xchg(plen, m, rc, cs)
-        if W == 1:
-            roff = poff  # the permuted batch's own offsets
-        else:
-            roff = torch.zeros(m + 1, dtype=torch.int64, device=dev)
-            roff[1:] = rlens.to(torch.int64).cumsum(0)
+        roff = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+        roff[1:] = rlens.to(torch.int64).cumsum(0)
         res = ctx.match_device(self.index, rbytes.data_ptr(), roff.data_ptr(), m, exact)  # read-back: nnz
         self.last_topics_walked = m
         nnz = res.nnz
         rowlen = torch.empty(max(m, 1), dtype=torch.int32, device=dev)[:m]
         ctx.csr_row_lengths(res, rowlen.data_ptr())
-        if W == 1:
-            # rows straight back into batch order from the match's own ids (no copy into a torch buffer)
-            out = ctx.unpermute_rows(n, perm.data_ptr(), rowlen.data_ptr(), _ptr(res.csr.ids))
-            res.free()
-            self.last_exchange_bytes = 0
-            return out
         ids = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
         ctx.memcpy_d2d(ids.data_ptr(), _ptr(res.csr.ids), nnz * 4)
         res.free()

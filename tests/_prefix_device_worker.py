@@ -1,8 +1,9 @@
 """The device-tensor path of PrefixShardedMatcher.match_device on one GPU
 (tests/test_gpu_sharded.py::test_prefix_device_path_*).
 
-World 1: the `_a2a` copy path -- route on the device, torch.sort / bincount,
-emqx_gm_permute_topics, the walk of the received topics, emqx_gm_unpermute_rows.
+World 1: route_partition on the device, then -- one shard, so the send order
+is the batch order -- the batch walked in place (the permute and un-permute
+would be identity copies: aliased).
 
 World W > 1: W ranks run as W threads of this process, each with its own
 library context and matcher (own stream) over its own prefix shard, and the
