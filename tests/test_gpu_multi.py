@@ -205,3 +205,51 @@ def test_update_subs_replicated(ctx2, monkeypatch):
         b.unsubscribe(fl[k], 1000 + k)
     b.subscribe(b"s/+/x", 7)
     check()
+
+
+def test_concurrent_callers_three_replicas(orc, monkeypatch):
+    """NIF-style use: one context over three replicas (device 0 listed three
+    times) shared by four threads (dirty schedulers), each matching its own
+    host batches -- some small (the one-chunk serial path), some spread over
+    the replicas in 1,024-topic chunks -- while a fifth thread swaps in
+    updated snapshots (RCU): every result equals the oracle's rows for the
+    snapshot that call used."""
+    import random
+    import threading
+    from emqx_amd import Context
+    monkeypatch.setenv("GM_HOST_CHUNK", "1024")
+    rng = random.Random(3)
+    words = ["a", "b", "c", "+"]
+    base = sorted({"/".join(rng.choice(words) for _ in range(rng.randint(1, 4))).encode() for _ in range(200)})
+    extra = [b"z/%d/#" % i for i in range(20)]
+    topics = [["/".join(rng.choice("abcz") for _ in range(rng.randint(1, 5))).encode() for _ in range(k)]
+              for k in (50, 700, 5000, 9000)]
+    want = {}
+    for fs_key, fs in (("base", base), ("more", sorted(base + extra))):
+        for k, ts in enumerate(topics):
+            want[(fs_key, k)] = _oracle_rows(orc, fs, ts)
+    with Context(devices=[0, 0, 0]) as c:
+        snaps = {"base": c.build_index(base)}
+        snaps["more"] = c.update_index(snaps["base"], [(f, True) for f in extra])
+        errors = []
+
+        def caller(tid):
+            try:
+                for it in range(6):
+                    key = "base" if (tid + it) % 2 else "more"
+                    k = (tid + it) % len(topics)
+                    ro, ids = c.match(snaps[key], topics[k], exact=True)
+                    wro, wids = want[(key, k)]
+                    if not (np.array_equal(ro, wro) and np.array_equal(ids, wids)):
+                        errors.append((tid, it, key, k))
+            except Exception as e:  # noqa: BLE001
+                errors.append((tid, repr(e)))
+
+        th = [threading.Thread(target=caller, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errors, errors
+        for s in snaps.values():
+            s.release()
