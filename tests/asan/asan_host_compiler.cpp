@@ -371,6 +371,59 @@ int patch_sequences() {
   return bad;
 }
 
+
+// gm_filters.h SubTable: random batches of (id, new count) and (id, mark)
+// against plain vectors, with deltas over deltas and compactions (n = 5,000:
+// compaction past 4,096 touched ids); every offset, count and mark checked,
+// and the running changes the device shift kernel consumes.
+int sub_table_check() {
+  int bad = 0;
+  std::mt19937_64 rng(13);
+  const uint64_t n = 5000;
+  std::vector<uint64_t> cnt(n), off(n + 1, 0);
+  std::vector<uint8_t> mark(n);
+  for (uint64_t f = 0; f < n; ++f) cnt[f] = rng() % 4;
+  for (uint64_t f = 0; f < n; ++f) off[f + 1] = off[f] + cnt[f];
+  for (uint64_t f = 0; f < n; ++f) mark[f] = cnt[f] == 0;  // a built index: no subscribers = route-only
+  gm::SubTable t(off, {});
+  for (int round = 0; round < 300; ++round) {
+    std::set<uint32_t> ids;
+    const int k = 1 + int(rng() % 40);
+    for (int i = 0; i < k; ++i) ids.insert(uint32_t(rng() % n));
+    std::vector<std::pair<uint32_t, uint64_t>> c;
+    std::vector<std::pair<uint32_t, uint8_t>> m;
+    for (uint32_t id : ids) {
+      cnt[id] = rng() % 6;
+      mark[id] = uint8_t(rng() % 2);
+      c.emplace_back(id, cnt[id]);
+      m.emplace_back(id, mark[id]);
+    }
+    const gm::SubTable prev = t;
+    t = t.apply(c, m);
+    for (uint64_t f = 0; f < n; ++f) off[f + 1] = off[f] + cnt[f];
+    for (uint64_t f = 0; f <= n; ++f)
+      if (t.off(f) != off[f] && bad++ < 5) std::fprintf(stderr, "sub table: off %llu\n", (unsigned long long)f);
+    for (uint64_t f = 0; f < n; ++f) {
+      if (t.count(f) != cnt[f] && bad++ < 5) std::fprintf(stderr, "sub table: count %llu\n", (unsigned long long)f);
+      if (t.pinned(f) != (mark[f] != 0) && bad++ < 5) std::fprintf(stderr, "sub table: mark %llu\n", (unsigned long long)f);
+    }
+    if (t.total() != off[n] && bad++ < 5) std::fprintf(stderr, "sub table: total\n");
+    // what shift_subs_device derives from prev: new off = prev off + the batch's changes below
+    int64_t run = 0;
+    auto it = ids.begin();
+    for (uint64_t f = 0; f <= n; ++f) {
+      while (it != ids.end() && *it < f) {
+        run += int64_t(cnt[*it]) - int64_t(prev.count(*it));
+        ++it;
+      }
+      if (uint64_t(int64_t(prev.off(f)) + run) != off[f] && bad++ < 5)
+        std::fprintf(stderr, "sub table: shifted off %llu\n", (unsigned long long)f);
+    }
+  }
+  if (t.offsets() != off && bad++ < 5) std::fprintf(stderr, "sub table: materialized offsets\n");
+  return bad;
+}
+
 // ---- index images (gm_image.cpp): validate_image / import_host_part fed a
 // valid image cut at every section boundary, with byte flips anywhere in its
 // header and host sections, and with counts and offsets rewritten (the
@@ -547,6 +600,7 @@ int main() {
   bad += filter_table_check();
   bad += patch_sequences();
   bad += image_fuzz();
+  bad += sub_table_check();
   std::printf(bad ? "ASAN_HOST_CHECK_FAILED %d\n" : "ASAN_HOST_CHECK_OK\n", bad);
   return bad ? 1 : 0;
 }
