@@ -40,6 +40,7 @@ template <class F> void for_blob_ptrs(IndexView& v, F f) {
   f(reinterpret_cast<const void**>(&v.efilt));
   f(reinterpret_cast<const void**>(&v.mph_word));
   f(reinterpret_cast<const void**>(&v.d0_root));
+  f(reinterpret_cast<const void**>(&v.hot_dict));
 }
 
 // dst (on m's device) = src (on src_dev), `bytes` bytes, on m's stream
