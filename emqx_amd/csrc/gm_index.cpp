@@ -774,11 +774,14 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // first words, the 64 fourth and the 16 fifth -- 3 of a topic's 5 lookups).
   // Depths by ascending distinct-word count, their words of <= 8 bytes (a hit
   // is exact from length + head) into 2-way sets; a full set skips the word.
-  // GM_HDICT=0 (A/B knob, at build): none.
+  // Off by default (GM_HDICT=1 at build: on): a same-box A/B had C2's kernel at
+  // 8.54 ms with it against 8.39 without, C3's at 12.63 against 12.69
+  // (profiles/r05_e/hdict_ab_c2_c3.txt): the LDS check in front of every
+  // dictionary read costs C2's tokenizer more than the L2 requests it saves.
   std::vector<DictSlot> hdict;
   {
     const char* he = getenv("GM_HDICT");
-    if (!he || atoi(he) != 0) {
+    if (he && atoi(he) != 0) {
       constexpr int HD = 16;            // depths considered
       constexpr size_t CAP = 2048;      // past this many distinct words a depth is not hot
       std::vector<std::unordered_set<uint32_t>> per(HD);
