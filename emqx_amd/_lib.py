@@ -125,7 +125,12 @@ def lib():
             raise GpuMatchError(EUNSUPPORTED, f"{LIB_PATH} is not built (run __graft_entry__.build() "
                                               f"or `make -C emqx_amd/csrc`)")
         L = C.CDLL(LIB_PATH)
+        # an older build loaded for a same-box A/B (EMQX_GM_LIB) may lack the newest
+        # entry points: those stay unbound there; the shipped library must have them all
+        ab = bool(os.environ.get("EMQX_GM_LIB"))
         for name, (res, args) in SIGNATURES.items():
+            if ab and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
