@@ -160,16 +160,7 @@ struct IndexView {
   // 16-B load per wave): {hot id (NONE: no '+' at the root), sig, hf,
   // end_filter}, written from the depth-1 hot table by k_d0_refresh
   const uint32_t* d0_root;
-  // The hot-word cache (gm_index.cpp 4b): 2-way sets of HDICT_SETS, the
-  // dictionary slots of the words of the depths with the fewest distinct words
-  // (the words nearly every topic carries: a topic's word at depth d is one of
-  // that depth's distinct words).  k_match_fused copies it into the LDS its
-  // walk lists take later, and its tokenizer resolves those words there
-  // instead of with an L2 request each; nullptr: none.
-  const DictSlot* hot_dict;
 };
-constexpr uint32_t HDICT_SETS = 112;  // 224 slots = 3,584 B: the LDS k_match_fused's walk lists have beyond the staged text
-
 
 GM_HD uint64_t fmix64(uint64_t k) {
   k ^= k >> 33;
@@ -253,7 +244,6 @@ GM_HD uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
-GM_HD uint32_t hdict_set(uint32_t h) { return uint32_t((uint64_t(fmix32(h ^ 0x9E3779B9u)) * HDICT_SETS) >> 32); }
 GM_HD uint32_t sig_bit(uint32_t word_id);
 // a slot's exact-child signature (a chain node holds its one child's word id)
 GM_HD uint32_t hot_sig(uint32_t hf, uint32_t sig) { return (hf & HOT_CHAIN) ? sig_bit(sig) : sig; }

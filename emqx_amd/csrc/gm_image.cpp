@@ -34,8 +34,8 @@ namespace gm {
 namespace {
 
 constexpr char kMagic[8] = {'E', 'M', 'Q', 'X', 'G', 'M', 'I', '1'};
-constexpr uint32_t kVersion = 4;
-constexpr int kPtrs = 12;  // the view's device pointers, in ptr_fields() order
+constexpr uint32_t kVersion = 3;
+constexpr int kPtrs = 11;  // the view's device pointers, in ptr_fields() order
 
 uint64_t layout_signature() {
   uint64_t h = 0x9E3779B97F4A7C15ull;
@@ -53,7 +53,7 @@ template <class V> auto ptr_fields(V& v) {
       reinterpret_cast<const void**>(&v.arena),   reinterpret_cast<const void**>(&v.sub_off),
       reinterpret_cast<const void**>(&v.sub_ids), reinterpret_cast<const void**>(&v.gmap),
       reinterpret_cast<const void**>(&v.efilt),   reinterpret_cast<const void**>(&v.mph_word),
-      reinterpret_cast<const void**>(&v.d0_root), reinterpret_cast<const void**>(&v.hot_dict)};
+      reinterpret_cast<const void**>(&v.d0_root)};
 }
 
 struct MirrorMeta {  // gm::Mirror without its blob (an imported index loads it lazily)
@@ -287,7 +287,6 @@ int validate_image(const uint8_t* img, uint64_t size, bool have_blob, std::strin
   const uint64_t dict = (v.dict_mask + 1) * sizeof(DictSlot);
   if (!within(0, uint64_t(v.n_nodes) * sizeof(Node)) || !within(1, dict) || !within(2, edges) || !within(3, hot) ||
       !within(8, efilt) || !within(9, mph) || (h.ptr_off[10] != ~0ull && !within(10, 16)) ||
-      (h.ptr_off[11] != ~0ull && !within(11, 2 * HDICT_SETS * sizeof(DictSlot))) ||
       (h.ptr_off[5] != ~0ull && !within(5, (nf + 1) * 8)) || (h.ptr_off[6] != ~0ull && !within(6, h.info.n_subs * 4)) ||
       (h.ptr_off[7] != ~0ull && !within(7, nf * 4)) || h.ptr_off[0] == ~0ull || h.ptr_off[1] == ~0ull ||
       h.ptr_off[3] == ~0ull || h.ptr_off[4] == ~0ull)

@@ -19,7 +19,6 @@
 #include <string_view>
 #include <thread>
 #include <unordered_map>
-#include <unordered_set>
 
 #include "gm_internal.h"
 
@@ -768,63 +767,6 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     if (it != wid.end()) hash_word = it->second;
   }
 
-  // ---- 4b. the hot-word cache (IndexView::hot_dict): a topic's word at depth d
-  // is one of that depth's distinct words, so the words of the depths with the
-  // fewest distinct words are the ones nearly every topic carries (C2: the 64
-  // first words, the 64 fourth and the 16 fifth -- 3 of a topic's 5 lookups).
-  // Depths by ascending distinct-word count, their words of <= 8 bytes (a hit
-  // is exact from length + head) into 2-way sets; a full set skips the word.
-  // Off by default (GM_HDICT=1 at build: on): a same-box A/B had C2's kernel at
-  // 8.54 ms with it against 8.39 without, C3's at 12.63 against 12.69
-  // (profiles/r05_e/hdict_ab_c2_c3.txt): the LDS check in front of every
-  // dictionary read costs C2's tokenizer more than the L2 requests it saves.
-  std::vector<DictSlot> hdict;
-  {
-    const char* he = getenv("GM_HDICT");
-    if (he && atoi(he) != 0) {
-      constexpr int HD = 16;            // depths considered
-      constexpr size_t CAP = 2048;      // past this many distinct words a depth is not hot
-      std::vector<std::unordered_set<uint32_t>> per(HD);
-      std::vector<uint8_t> big(HD, 0);
-      for (uint64_t i = 1; i < NN; ++i) {
-        const HNode& h = nodes[i];
-        if (h.kind != 0 || h.depth >= uint32_t(HD) || big[h.depth]) continue;
-        per[h.depth].insert(h.word);
-        if (per[h.depth].size() > CAP) big[h.depth] = 1;
-      }
-      std::vector<int> order;
-      for (int d = 0; d < HD; ++d)
-        if (!big[d] && !per[d].empty()) order.push_back(d);
-      std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return per[a].size() < per[b].size(); });
-      std::unordered_map<uint32_t, uint64_t> k_of;  // word id -> its index k (the candidate words only)
-      for (int d : order)
-        for (uint32_t w : per[d]) k_of.emplace(w, 0);
-      for (uint64_t k = 0; k < nw; ++k) {
-        auto it = k_of.find(word_ids[k]);
-        if (it != k_of.end()) it->second = k;
-      }
-      hdict.assign(2 * HDICT_SETS, DictSlot{0, DICT_EMPTY_LEN, 0});
-      uint64_t placed = 0;
-      std::unordered_set<uint32_t> done;
-      for (int d : order) {
-        std::vector<uint32_t> ws(per[d].begin(), per[d].end());
-        std::sort(ws.begin(), ws.end());  // deterministic
-        for (uint32_t w : ws) {
-          const uint64_t k = k_of[w];
-          if (word_len[k] > 8 || !done.insert(w).second) continue;
-          const uint32_t set = hdict_set(word_hash[k]);
-          for (int way = 0; way < 2; ++way)
-            if (hdict[2 * set + way].len == DICT_EMPTY_LEN) {
-              hdict[2 * set + way] = DictSlot{word_head[k], word_len[k], word_ids[k]};
-              ++placed;
-              break;
-            }
-        }
-      }
-      if (!placed) hdict.clear();
-    }
-  }
-
   phase("dictionary");
   // ---- 5. subscriber CSR per unique filter id (duplicates concatenated)
   std::vector<uint64_t> soff(nf + 1, 0);
@@ -874,8 +816,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   size_t o_efilt = o_gmap + al(idx->gmap.size() * 4 + 4);
   size_t o_mph = o_efilt + al(efilt.size() * 4 + 4);
   size_t o_d0 = o_mph + al(mph_word.size() * 8);
-  size_t o_hdict = o_d0 + al(16);
-  size_t o_soff = o_hdict + al(hdict.size() * sizeof(DictSlot));
+  size_t o_soff = o_d0 + al(16);
   // (a plain index's offsets stay zero past nf: appended filters have no subscribers)
   size_t o_sids = o_soff + al((keep_mirror && !sub_off ? flen_cap + 1 : soff.size()) * 8);
   size_t total = o_sids + al(sids.size() * 4 + 4);
@@ -915,7 +856,6 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   {
     const uint32_t d0[4] = {NONE, 0, HF_NONE, NONE};
     put(o_d0, d0, sizeof d0);
-    put(o_hdict, hdict.data(), hdict.size() * sizeof(DictSlot));
   }
   put(o_edges, dedges.data(), dedges.size() * sizeof(EdgeSlot));
   put(o_hot, hot.data(), hot.size() * sizeof(HotSlot));
@@ -974,7 +914,6 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.nodes = reinterpret_cast<const Node*>(B + o_nodes);
   v.dict = reinterpret_cast<const DictSlot*>(B + o_dict);
   v.d0_root = reinterpret_cast<const uint32_t*>(B + o_d0);
-  v.hot_dict = hdict.empty() ? nullptr : reinterpret_cast<const DictSlot*>(B + o_hdict);
   v.edges = reinterpret_cast<const EdgeSlot*>(B + o_edges);
   v.hot = reinterpret_cast<const HotSlot*>(B + o_hot);
   v.arena = B + o_arena;

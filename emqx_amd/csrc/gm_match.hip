@@ -157,18 +157,6 @@ __device__ __forceinline__ uint32_t dict_resolve(const IndexView& ix, const Word
 __device__ __forceinline__ DictSlot dict_first(const IndexView& ix, const WordTok& w) {
   return dict_at(ix, dict_slot(w.h, ix.dict_mask));
 }
-// The word's first dictionary slot, from the block's LDS copy of the hot-word
-// cache when it holds the word (IndexView::hot_dict: an exact hit, so
-// dict_resolve takes it at once; no L2 request), else from the dictionary.
-__device__ __forceinline__ DictSlot hot_first(const IndexView& ix, const WordTok& w, const DictSlot* hot) {
-  if (hot && w.len <= 8) {
-    const uint32_t s = 2u * hdict_set(w.h);
-    const DictSlot a = hot[s], b = hot[s + 1];
-    if (a.len == w.len && a.head == w.head) return a;
-    if (b.len == w.len && b.head == w.head) return b;
-  }
-  return dict_first(ix, w);
-}
 
 
 __device__ __forceinline__ uint32_t edge_lookup(const IndexView& ix, uint32_t depth, uint32_t parent,
@@ -773,8 +761,7 @@ struct WidsToRegs {
 
 template <int G, class SINK>
 __device__ __forceinline__ uint32_t tokenize_grouped(const uint64_t* lds, uint32_t pos, uint32_t end,
-                                                     const IndexView& ix, const uint8_t* tb_lo, SINK&& sink,
-                                                     const DictSlot* hot = nullptr) {
+                                                     const IndexView& ix, const uint8_t* tb_lo, SINK&& sink) {
   uint32_t lev = 0, fl = 0;
   bool more = true, wild = false;
   while (more && lev < uint32_t(TOK_LMAX)) {
@@ -795,7 +782,7 @@ __device__ __forceinline__ uint32_t tokenize_grouped(const uint64_t* lds, uint32
           hd[g] = w.head;
           hh[g] = w.h;
           sl[g] = uint32_t(w.start) | (w.len << 16);
-          d[g] = hot_first(ix, w, hot);
+          d[g] = dict_first(ix, w);
           more = pos < end;
           pos += more ? 1u : 0u;
         }
@@ -1612,10 +1599,6 @@ struct WordsFromRegs {
 };
 
 constexpr size_t FUSED_LDS = sizeof(CoopLds) * 4 > (TOK_STAGE + 8) ? sizeof(CoopLds) * 4 : (TOK_STAGE + 8);
-// the hot-word cache's LDS (tokenizer phase only): the tail of the region past
-// the staged text (at most TOK_STAGE + 8 bytes), which the walk's lists take later
-constexpr size_t HDICT_LDS_OFF = (FUSED_LDS - 2 * HDICT_SETS * sizeof(DictSlot)) & ~size_t(15);
-static_assert(HDICT_LDS_OFF >= TOK_STAGE + 8, "the hot-word cache must not overlap the staged text");
 
 template <int G, bool EXACT, bool NT, bool TOKPRIO, bool CMP, bool D0 = true>
 __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restrict__ tb,
@@ -1648,14 +1631,6 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
     const uint64_t nw = ((hi - lo + 7) >> 3) + 1;  // topic buffers are padded by 64 bytes
     for (uint64_t i = threadIdx.x; i < nw; i += 256) s_txt[i] = ld_s<NT>(reinterpret_cast<const uint64_t*>(tb + lo + 8 * i));
   }
-  // the hot-word cache into the LDS the walk's lists take later (behind the
-  // staged text): one 16-B load per thread, an L2 hit every block shares
-  const DictSlot* hot = nullptr;
-  if (staged && ix.hot_dict) {  // (block-uniform)
-    DictSlot* hl = reinterpret_cast<DictSlot*>(s_raw + HDICT_LDS_OFF);
-    if (threadIdx.x < 2 * HDICT_SETS) hl[threadIdx.x] = ix.hot_dict[threadIdx.x];
-    hot = hl;
-  }
   __syncthreads();
   PhaseRec PH{};
 #ifdef GM_PHASE_STATS
@@ -1670,7 +1645,7 @@ __global__ __launch_bounds__(256, 8) void k_match_fused(const uint8_t* __restric
   if (valid) {
     const uint64_t pos = toff[t], end = toff[t + 1];
     if (staged) {
-      h = tokenize_grouped<G>(s_txt, uint32_t(pos - lo), uint32_t(end - lo), ix, tb + lo, WidsToRegs{w}, hot);
+      h = tokenize_grouped<G>(s_txt, uint32_t(pos - lo), uint32_t(end - lo), ix, tb + lo, WidsToRegs{w});
     } else {
       ByteReader rd{tb, ~0ull, 0};
       h = tokenize_topic(rd, pos, end, ix, tb, WidsToRegs{w});
@@ -3457,8 +3432,6 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   IndexView vcall = idx->view;
   if (const char* de = getenv("GM_D0"))
     if (!atoi(de)) vcall.flags &= ~IX_D0;
-  if (const char* he = getenv("GM_HDICT_CALL"))  // A/B knob (read per call): 0 = no hot-word cache
-    if (!atoi(he)) vcall.hot_dict = nullptr;
   if (const char* se = getenv("GM_STAGE_SC1"))  // A/B knobs (read per call)
     if (atoi(se)) vcall.flags |= IX_STAGE_SC1;
   if (const char* be = getenv("GM_L1_BYPASS")) vcall.l1_bypass = uint32_t(strtoul(be, nullptr, 0));

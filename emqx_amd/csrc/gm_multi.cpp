@@ -40,7 +40,6 @@ template <class F> void for_blob_ptrs(IndexView& v, F f) {
   f(reinterpret_cast<const void**>(&v.efilt));
   f(reinterpret_cast<const void**>(&v.mph_word));
   f(reinterpret_cast<const void**>(&v.d0_root));
-  f(reinterpret_cast<const void**>(&v.hot_dict));
 }
 
 // dst (on m's device) = src (on src_dev), `bytes` bytes, on m's stream
@@ -131,6 +130,9 @@ int replicate_result(emqx_gm_ctx* ctx, emqx_gm_index* prev, emqx_gm_index** out_
     return rc;
   };
   if (out->reps.size()) return fail(set_err(ctx, EMQX_GM_EINVAL, "replicate: a snapshot of another context"));
+  // an overlay made from a snapshot without replicas (one made through another
+  // context) stays on the first device: it is matched there, as its base is
+  if (out->ov && (!prev || prev->reps.size() != K)) return EMQX_GM_OK;
   // the snapshot whose device tables `out` shares (update_subs without a route
   // change) and, when prev is that one or shares it too, prev's replica of it
   const emqx_gm_index* own = out->blob_owner;
@@ -140,8 +142,7 @@ int replicate_result(emqx_gm_ctx* ctx, emqx_gm_index* prev, emqx_gm_index** out_
     emqx_gm_index* rep = nullptr;
     int rc;
     if (out->ov) {
-      if (!prev || prev->reps.size() != K) rc = set_err(ctx, EMQX_GM_EINVAL, "replicate: no replica to update");
-      else rc = redo(m, prev->reps[k], &rep);
+      rc = redo(m, prev->reps[k], &rep);
     } else {
       rc = replicate_index(m, out, share ? prev->reps[k] : nullptr, &rep);
     }

@@ -606,7 +606,6 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
   v.nodes = rebase(v.nodes);
   v.dict = rebase(v.dict);
   v.d0_root = rebase(v.d0_root);
-  v.hot_dict = rebase(v.hot_dict);
   v.edges = rebase(v.edges);
   v.hot = rebase(v.hot);
   v.arena = rebase(v.arena);

@@ -97,7 +97,9 @@ typedef struct emqx_gm_call emqx_gm_call;
  *     back in the caller's ONE CSR, in batch order;
  *   - device-buffer calls (EMQX_GM_DEVICE_IO, emqx_gm_match_submit), the
  *     fan-out, the sharding helpers, emqx_gm_set_stream and
- *     emqx_gm_index_device_blob / _export use the first listed device.
+ *     emqx_gm_index_device_blob / _export use the first listed device; so
+ *     does any call on an index made through another context (it has no
+ *     replicas here).
  * n_devices = 0 is the single-device context on `device`. */
 #define EMQX_GM_MAX_DEVICES 8
 typedef struct {

@@ -490,7 +490,7 @@ int image_fuzz() {
                          "mirror.arena_cap", "mirror.flen_cap", "mirror.o_hot", "mirror.hot_used1",
                          "mirror.edge_used0", "sec_off0", "sec_off1", "sec_off2", "sec_off3", "sec_off4", "sec_off5",
                          "ptr_off0", "ptr_off1", "ptr_off2", "ptr_off3", "ptr_off4", "ptr_off8", "ptr_off9",
-                         "ptr_off10", "ptr_off11"};
+                         "ptr_off10"};
   for (const char* nm : names) {
     const uint64_t orig = *gm::image_field(img.data(), nm);
     const uint64_t vals[] = {orig + size, orig * 2 + 1, ~0ull, ~0ull / 2, 1ull << 40, orig + 1, orig ? orig - 1 : 7, 0};
