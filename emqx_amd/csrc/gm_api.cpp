@@ -600,6 +600,8 @@ int emqx_gm_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr
   std::memset(out, 0, sizeof(*out));
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
+  if (!ctx->members.empty() && !(flags & EMQX_GM_DEVICE_IO) && !m->on_device)
+    return gm::run_fanout_multi(ctx, idx, m, flags, out);
   return gm::run_fanout(ctx, idx, m, flags, out);
   GM_GUARD_END(ctx)
 }

@@ -413,6 +413,10 @@ int replicate_index(emqx_gm_ctx* m, const emqx_gm_index* src, emqx_gm_index* sha
 // failure `out` is released and *out_p cleared.
 int replicate_result(emqx_gm_ctx* ctx, emqx_gm_index* prev, emqx_gm_index** out_p,
                      const std::function<int(emqx_gm_ctx*, emqx_gm_index*, emqx_gm_index**)>& redo);
+// emqx_gm_fanout of host rows over a multi-device context's replicas (one
+// slice per device, one page-locked result); small batches: run_fanout
+int run_fanout_multi(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
+                     emqx_gm_csr* out);
 }  // namespace gm
 
 #define GM_HIP(ctx, expr)                                                                     \

@@ -18,8 +18,10 @@
 //     filter with '#' inside) repeats the same update on each replica;
 //   * a host-buffer emqx_gm_match runs its chunks on every device at once
 //     (gm_host.cpp) and returns ONE CSR in batch order.
+#include <algorithm>
 #include <cstring>
 #include <memory>
+#include <thread>
 
 #include "gm_internal.h"
 
@@ -153,6 +155,160 @@ int replicate_result(emqx_gm_ctx* ctx, emqx_gm_index* prev, emqx_gm_index** out_
     out->reps.push_back(rep);
   }
   hipSetDevice(ctx->device);
+  return EMQX_GM_OK;
+}
+
+}  // namespace gm
+
+namespace gm {
+
+// emqx_gm_fanout on host rows through a multi-device context: the rows are cut
+// into one contiguous slice per device, balanced by matches; each device (a
+// thread of its own, its own stream and pools) fans its slice out against its
+// replica's subscriber CSR; then, in slice order, each slice's delivery
+// offsets are rebased on its device and its rows DMA'd into their final place
+// of ONE page-locked result.  The reference's dispatch runs in every publisher
+// process at once (emqx_broker.erl:296-322, 506-530); a node's publish batch
+// thus fans out over all its GPUs' PCIe links.  Small batches (fewer than
+// GM_FANOUT_MULTI_MIN rows, default 65,536) take the first device alone.
+int run_fanout_multi(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
+                     emqx_gm_csr* out) {
+  std::vector<emqx_gm_ctx*> mem{ctx};
+  std::vector<const emqx_gm_index*> rix{idx};
+  for (size_t k = 0; k < ctx->members.size() && k < idx->reps.size(); ++k) {
+    mem.push_back(ctx->members[k]);
+    rix.push_back(idx->reps[k]);
+  }
+  const uint64_t n = m->n_rows, nnz = m->nnz;
+  const char* me = getenv("GM_FANOUT_MULTI_MIN");
+  const uint64_t min_rows = me ? strtoull(me, nullptr, 10) : 65536;
+  if (mem.size() < 2 || n < min_rows) return run_fanout(ctx, idx, m, flags, out);
+  for (uint64_t i = 0; i < nnz; ++i)
+    if (m->ids[i] >= idx->view.n_filters) return set_err(ctx, EMQX_GM_EINVAL, "fanout: filter id out of range");
+  if (m->row_off[0] != 0 || m->row_off[n] != nnz) return set_err(ctx, EMQX_GM_EINVAL, "fanout: row offsets");
+  for (uint64_t i = 0; i < n; ++i)
+    if (m->row_off[i + 1] < m->row_off[i]) return set_err(ctx, EMQX_GM_EINVAL, "fanout: row offsets not monotone");
+  const int K = int(mem.size());
+  struct Part {
+    uint64_t r0 = 0, r1 = 0, o0 = 0, o1 = 0;
+    PoolBuf d_off, d_ids;
+    emqx_gm_csr res{};
+    int rc = 0;
+    std::string err;
+    emqx_gm_match_stats st{};
+  };
+  std::vector<Part> P(K);
+  for (int k = 0; k < K; ++k) {  // row bounds: the first row at or past the k-th share of the matches
+    P[k].r0 = k == 0 ? 0 : uint64_t(std::lower_bound(m->row_off, m->row_off + n, nnz * uint64_t(k) / K) - m->row_off);
+    if (k) P[k - 1].r1 = P[k].r0;
+  }
+  P[K - 1].r1 = n;
+  for (auto& p : P) p.o0 = m->row_off[p.r0], p.o1 = m->row_off[p.r1];
+  const uint32_t fl = (flags & EMQX_GM_WITH_EXACT) | EMQX_GM_DEVICE_IO;
+  auto work = [&](int k) {
+    Part& p = P[k];
+    emqx_gm_ctx* mc = mem[k];
+    hipSetDevice(mc->device);
+    std::unique_lock<std::recursive_mutex> lk(mc->mu, std::defer_lock);
+    if (mc != ctx) lk.lock();  // (the caller holds the first device's lock)
+    const uint64_t rows = p.r1 - p.r0, cnt = p.o1 - p.o0;
+    p.d_off = PoolBuf(mc->pool, (rows + 1) * 8);
+    p.d_ids = PoolBuf(mc->pool, cnt * 4 + 16);
+    if (!p.d_off.p || !p.d_ids.p) {
+      p.rc = EMQX_GM_ENOMEM;
+      p.err = "fanout: slice workspace";
+      return;
+    }
+    hipError_t e = hipMemcpyAsync(p.d_off.p, m->row_off + p.r0, (rows + 1) * 8, hipMemcpyHostToDevice, mc->stream);
+    if (e == hipSuccess && cnt)
+      e = hipMemcpyAsync(p.d_ids.p, m->ids + p.o0, cnt * 4, hipMemcpyHostToDevice, mc->stream);
+    if (e != hipSuccess || launch_add_u64(mc->stream, p.d_off.as<uint64_t>(), rows + 1, uint64_t(0) - p.o0)) {
+      p.rc = EMQX_GM_EDEVICE;
+      p.err = "fanout: slice upload";
+      return;
+    }
+    emqx_gm_csr sub{};
+    sub.n_rows = rows;
+    sub.nnz = cnt;
+    sub.row_off = p.d_off.as<uint64_t>();
+    sub.ids = p.d_ids.as<uint32_t>();
+    sub.on_device = 1;
+    p.rc = run_fanout(mc, rix[k], &sub, fl, &p.res);
+    if (p.rc) p.err = std::string(emqx_gm_last_error(mc));
+    p.st = mc->stats;
+  };
+  {
+    std::vector<std::thread> th;
+    for (int k = 1; k < K; ++k) th.emplace_back(work, k);
+    work(0);
+    for (auto& t : th) t.join();
+  }
+  auto drop = [&]() {
+    for (int k = 0; k < K; ++k) {
+      hipSetDevice(mem[k]->device);
+      hipStreamSynchronize(mem[k]->stream);
+      if (P[k].res.row_off || P[k].res.ids) {
+        mem[k]->pool->release(P[k].res.row_off);
+        mem[k]->pool->release(P[k].res.ids);
+      }
+      P[k].d_off.reset();
+      P[k].d_ids.reset();
+    }
+    hipSetDevice(ctx->device);
+  };
+  for (int k = 0; k < K; ++k)
+    if (P[k].rc) {
+      const int rc = P[k].rc;
+      const std::string msg = P[k].err;
+      drop();
+      return set_err(ctx, rc, msg);
+    }
+  uint64_t total = 0;
+  for (auto& p : P) total += p.res.nnz;
+  uint64_t* r_off = static_cast<uint64_t*>(ctx->hpool->alloc((n + 1) * 8, true));
+  uint32_t* r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(total * 4 + 16, true));
+  if (!r_off || !r_ids) {
+    ctx->hpool->release(r_off);
+    ctx->hpool->release(r_ids);
+    drop();
+    return set_err(ctx, EMQX_GM_ENOMEM, "fanout: host result");
+  }
+  uint64_t base = 0;
+  int rc = 0;
+  for (int k = 0; k < K && !rc; ++k) {  // each slice's rows into place, rebased on its device
+    Part& p = P[k];
+    emqx_gm_ctx* mc = mem[k];
+    hipSetDevice(mc->device);
+    const uint64_t rows = p.r1 - p.r0;
+    hipError_t e = launch_add_u64(mc->stream, p.res.row_off, rows, base) ? hipErrorLaunchFailure : hipSuccess;
+    if (e == hipSuccess && rows)
+      e = hipMemcpyAsync(r_off + p.r0, p.res.row_off, rows * 8, hipMemcpyDeviceToHost, mc->stream);
+    if (e == hipSuccess && p.res.nnz)
+      e = hipMemcpyAsync(r_ids + base, p.res.ids, p.res.nnz * 4, hipMemcpyDeviceToHost, mc->stream);
+    if (e != hipSuccess) rc = set_err(ctx, EMQX_GM_EDEVICE, "fanout: rows to host");
+    base += p.res.nnz;
+  }
+  drop();  // (waits for every copy)
+  if (rc) {
+    ctx->hpool->release(r_off);
+    ctx->hpool->release(r_ids);
+    return rc;
+  }
+  r_off[n] = total;
+  emqx_gm_match_stats tot{};
+  tot.n_topics = n;
+  tot.nnz = total;
+  for (auto& p : P) {
+    tot.match_kernel_ms = std::max(tot.match_kernel_ms, p.st.match_kernel_ms);
+    tot.total_device_ms = std::max(tot.total_device_ms, p.st.total_device_ms);
+  }
+  ctx->stats = tot;
+  out->n_rows = n;
+  out->nnz = total;
+  out->row_off = r_off;
+  out->ids = r_ids;
+  out->on_device = 0;
+  out->priv = ctx;
   return EMQX_GM_OK;
 }
 

@@ -253,3 +253,41 @@ def test_concurrent_callers_three_replicas(orc, monkeypatch):
         assert not errors, errors
         for s in snaps.values():
             s.release()
+
+
+@pytest.mark.parametrize("replicas", [2, 3])
+def test_fanout_spread_over_replicas(ctx1, orc, monkeypatch, replicas):
+    """emqx_gm_fanout of host rows through a multi-device context: one slice of
+    the rows per replica (balanced by matches), each fanned out on its device,
+    the slices' deliveries put back in order into one result -- equal to the
+    single-device fan-out and the oracle's dispatch fold, including empty rows,
+    rows of one hot filter and slices that start and end anywhere."""
+    from emqx_amd import Context
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    monkeypatch.setenv("GM_FANOUT_MULTI_MIN", "1")
+    codes = gen_filter_codes(5, 20_000)
+    fb, fo = render_codes(codes)
+    filters = sorted(set(orc.unpack(fb, fo)))
+    rng = np.random.default_rng(2)
+    subs = [rng.integers(0, 10**6, size=int(rng.integers(0, 6))).tolist() for _ in filters]
+    subs[7] = list(range(5000))  # one hot filter
+    tb, to = orc.render_codes(orc.gen_topic_codes(5, 0, 40_000, codes))
+    i1 = ctx1.build_index(filters, subs=subs)
+    ro, ids = ctx1.match(i1, (tb, to), exact=True)
+    ids = ids.copy()
+    ids[::97] = 7  # hot rows
+    want = ctx1.fanout(i1, ro, ids)
+    so = np.zeros(len(filters) + 1, np.uint64)
+    so[1:] = np.cumsum([len(s) for s in subs])
+    si = np.array([x for s in subs for x in s], np.uint32)
+    oro, oids = orc.fanout(ro, ids, so, si)
+    assert np.array_equal(want[0], oro) and np.array_equal(want[1], oids)
+    with Context(devices=[0] * replicas) as c:
+        ix = c.build_index(filters, subs=subs)
+        got = c.fanout(ix, ro, ids)
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+        e = np.zeros(1, np.uint64), np.zeros(0, np.uint32)  # no rows at all
+        got0 = c.fanout(ix, *e)
+        assert got0[0].tolist() == [0] and len(got0[1]) == 0
+        ix.release()
+    i1.release()
