@@ -117,6 +117,22 @@ SIGNATURES = {
 _LIB = None
 
 
+def _one_hip_runtime():
+    """torch-ROCm ships its own HIP / HSA runtime (torch/lib/libamdhip64.so,
+    SONAME libamdhip64.so.7, the same as /opt/rocm's).  Loaded before it, the
+    library would pull /opt/rocm's copy in and torch would still load its own
+    by path: two HSA runtimes in one process, and whichever initialises second
+    finds no device (round 5: a host-only call such as gen_filter_codes before
+    the first Context, then torch.cuda, then emqx_gm_open -> EDEVICE;
+    scripts/smoke_order_diag.py).  Importing torch first makes the library
+    bind to torch's runtime by SONAME: one runtime.  A process without torch
+    loads /opt/rocm's."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def lib():
     """Load the HIP library; raise loudly if it is not built."""
     global _LIB
@@ -124,6 +140,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise GpuMatchError(EUNSUPPORTED, f"{LIB_PATH} is not built (run __graft_entry__.build() "
                                               f"or `make -C emqx_amd/csrc`)")
+        _one_hip_runtime()
         L = C.CDLL(LIB_PATH)
         # an older build loaded for a same-box A/B (EMQX_GM_LIB) may lack the newest
         # entry points: those stay unbound there; the shipped library must have them all

@@ -365,7 +365,9 @@ GM_HD uint32_t edge_filter_word(uint32_t h, uint32_t mask) { return (h >> 10) & 
 // empty value (NONE or HF_NONE) and `flag` the flag bits it carries (END_WILD,
 // HF_FLAGS, or 0 for the level-trie fields).
 constexpr uint32_t HF_FLAGS = HOT_PLUS | HOT_CHAIN;
-GM_HD uint32_t renum_field(uint32_t f, uint32_t none, uint32_t flag, const uint32_t* rmap) {
+// (rmap: the id table, or anything indexed like it -- the host's IdShift view)
+template <class R>
+GM_HD uint32_t renum_field(uint32_t f, uint32_t none, uint32_t flag, const R& rmap) {
   if (f == none) return f;
   const uint32_t fl = f & flag, id = f & ~flag;
   if (id == (none & ~flag)) return f;

@@ -182,6 +182,8 @@ struct IdShift {
     return uint32_t(id - (std::lower_bound(dels.begin(), dels.end(), id) - dels.begin()) +
                     (std::upper_bound(addpos.begin(), addpos.end(), id) - addpos.begin()));
   }
+  // indexed like the table (renum_field): map() without materializing it
+  uint32_t operator[](uint64_t id) const { return map(id); }
   std::vector<uint32_t> table() const {
     std::vector<uint32_t> r(nb + addpos.size());
     uint64_t d = 0, a = 0;
@@ -381,7 +383,10 @@ constexpr uint64_t PATCH_AND = 1ull << 63;
 // src (bytes), then the host-patched byte ranges (offset, length) of `host`
 // written over it, the OR / AND ops (offset of a word, bits) applied, then every
 // filter-id field of the hot slots and of nodes [0, n_nodes) renumbered by
-// the shift (its table built on the device)
+// the shift (its table built on the device).  Done in one pass over the blob:
+// the hot slots and nodes are renumbered while copied and the patched ranges
+// go up already renumbered (GM_UPDATE_UNFUSED: copy, patch, then renumber in
+// place -- the A/B twin).
 int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t bytes,
                        const std::vector<std::pair<uint64_t, uint32_t>>& ranges, const uint8_t* host,
                        const IndexView& v, uint64_t o_hot, uint64_t o_nodes, uint64_t n_nodes,

@@ -2613,10 +2613,76 @@ __global__ __launch_bounds__(256) void k_renumber(HotSlot* __restrict__ hot, uin
   }
 }
 
+// k_renumber fused with the blob copy: dst's hot slots and nodes = src's,
+// renumbered (every slot written, empty ones as they are), so an update reads
+// and writes the id-bearing tables once instead of copying them and then
+// renumbering them in place (C5: ~26 of the 38 GB blob)
+__global__ __launch_bounds__(256) void k_renumber_copy(const HotSlot* __restrict__ shot, HotSlot* __restrict__ hot,
+                                                       uint64_t n_hot, const Node* __restrict__ snodes,
+                                                       Node* __restrict__ nodes, uint64_t n_nodes,
+                                                       const uint32_t* __restrict__ rmap) {
+  const uint64_t stride = uint64_t(gridDim.x) * 256u;
+  for (uint64_t s = uint64_t(blockIdx.x) * 256u + threadIdx.x; s < n_hot; s += stride) {
+    HotSlot h = shot[s];
+    if (h.key != EDGE_EMPTY) {
+      h.hf = renum_field(h.hf, HF_NONE, HF_FLAGS, rmap);
+      h.end_filter = renum_field(h.end_filter, NONE, END_WILD, rmap);
+      h.p_hf = renum_field(h.p_hf, HF_NONE, HF_FLAGS, rmap);
+      h.p_end = renum_field(h.p_end, NONE, END_WILD, rmap);
+    }
+    hot[s] = h;
+  }
+  for (uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x; i < n_nodes; i += stride) {
+    Node nd = snodes[i];
+    nd.hash_filter = renum_field(nd.hash_filter, NONE, 0, rmap);
+    nd.end_filter = renum_field(nd.end_filter, NONE, 0, rmap);
+    nodes[i] = nd;
+  }
+}
+
+namespace {
+// The filter-id fields of the records k_renumber rewrites: (offset, empty value, flag bits)
+struct IdField {
+  uint32_t off, none, flag;
+};
+constexpr IdField kHotIds[] = {{offsetof(HotSlot, hf), HF_NONE, HF_FLAGS},
+                               {offsetof(HotSlot, end_filter), NONE, END_WILD},
+                               {offsetof(HotSlot, p_hf), HF_NONE, HF_FLAGS},
+                               {offsetof(HotSlot, p_end), NONE, END_WILD}};
+constexpr IdField kNodeIds[] = {{offsetof(Node, hash_filter), NONE, 0u}, {offsetof(Node, end_filter), NONE, 0u}};
+// The id fields of the table [o, o + n * rec) lying inside the patched range
+// [a, b) (buf = its bytes), renumbered in place by the shift (IdShift::map:
+// O(log delta) per field).  false: a field holds an id outside the shift.
+template <size_t K>
+bool renum_payload(uint8_t* buf, uint64_t a, uint64_t b, uint64_t o, uint64_t n, uint64_t rec,
+                   const IdField (&fs)[K], const IdShift& sh, uint64_t n_map) {
+  const uint64_t lo = std::max(a, o), hi = std::min(b, o + n * rec);
+  for (uint64_t r = lo < hi ? (lo - o) / rec : 0, re = lo < hi ? (hi - o + rec - 1) / rec : 0; r < re; ++r)
+    for (const IdField& f : fs) {
+      const uint64_t at = o + r * rec + f.off;
+      if (at < a || at + 4 > b) continue;  // (the patcher writes id fields whole)
+      uint32_t x;
+      std::memcpy(&x, buf + (at - a), 4);
+      const uint32_t id = x & ~f.flag;
+      if (x != f.none && id != (f.none & ~f.flag) && id >= n_map) return false;
+      x = renum_field(x, f.none, f.flag, sh);
+      std::memcpy(buf + (at - a), &x, 4);
+    }
+  return true;
+}
+}  // namespace
+
 int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t bytes,
                        const std::vector<std::pair<uint64_t, uint32_t>>& ranges, const uint8_t* host,
                        const IndexView& v, uint64_t o_hot, uint64_t o_nodes, uint64_t n_nodes,
                        const IdShift& shift, const std::vector<std::pair<uint64_t, uint32_t>>& orops) {
+  uint64_t n_hot = 0;
+  for (int t = 0; t < HOT_TABLES; ++t) n_hot = std::max<uint64_t>(n_hot, v.hot_off[t] + v.hot_cap[t]);
+  const uint64_t hot_end = o_hot + n_hot * sizeof(HotSlot), nodes_end = o_nodes + n_nodes * sizeof(Node);
+  if (hot_end > bytes || nodes_end > bytes) return set_err(ctx, EMQX_GM_EINVAL, "index_update: tables outside the blob");
+  const bool unfused = getenv("GM_UPDATE_UNFUSED") != nullptr;
+  // fused (one pass): the two id-bearing tables must not overlap
+  const bool fused = !unfused && (hot_end <= o_nodes || nodes_end <= o_hot);
   // coalesce overlapping / adjacent ranges only (the bytes between two written
   // fields may differ: the host mirror's untouched filter ids are stale), then
   // cut into pieces
@@ -2659,7 +2725,12 @@ int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t byte
   {
     uint64_t q = o_pay;
     for (const auto& g : seg) {
-      std::memcpy(st.data() + q, host + g.first, g.second - g.first);
+      uint8_t* const pb = st.data() + q;
+      std::memcpy(pb, host + g.first, g.second - g.first);
+      // fused: the range's filter ids (this update's temporary numbering) go up final
+      if (fused && !(renum_payload(pb, g.first, g.second, o_hot, n_hot, sizeof(HotSlot), kHotIds, shift, n_map) &&
+                     renum_payload(pb, g.first, g.second, o_nodes, n_nodes, sizeof(Node), kNodeIds, shift, n_map)))
+        return set_err(ctx, EMQX_GM_EINVAL, "index_update: a patched filter id outside the update's ids");
       q += g.second - g.first;
     }
   }
@@ -2672,10 +2743,39 @@ int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t byte
   PoolBuf dbuf(ctx->pool, total);
   if (!dbuf.p) return set_err(ctx, EMQX_GM_ENOMEM, "index_update: staging buffer");
   hipStream_t s = ctx->stream;
-  GM_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
-  GM_HIP(ctx, hipMemcpyAsync(dbuf.p, st.data(), up, hipMemcpyHostToDevice, s));
   uint8_t* D = static_cast<uint8_t*>(dst);
   const uint8_t* S = dbuf.as<uint8_t>();
+  uint32_t* const RM = reinterpret_cast<uint32_t*>(dbuf.as<uint8_t>() + o_rmap);
+  auto shift_table = [&]() -> int {
+    if (n_map) {
+      hipLaunchKernelGGL(k_shift_table, dim3(uint32_t((n_map + 255) / 256)), dim3(256), 0, s, RM, shift.nb,
+                         reinterpret_cast<const uint32_t*>(S + o_dels), uint32_t(nd),
+                         reinterpret_cast<const uint32_t*>(S + o_adds), uint32_t(na));
+      GM_HIP(ctx, hipGetLastError());
+    }
+    return 0;
+  };
+  const uint64_t g = std::min<uint64_t>(8192, (std::max(n_hot, n_nodes) + 255) / 256);
+  if (fused) {
+    GM_HIP(ctx, hipMemcpyAsync(dbuf.p, st.data(), up, hipMemcpyHostToDevice, s));
+    if (const int rc = shift_table()) return rc;
+    // the bytes around the two tables as they are, the tables renumbered on the way
+    const uint64_t a0 = std::min(o_hot, o_nodes), a1 = std::min(hot_end, nodes_end);
+    const uint64_t b0 = std::max(o_hot, o_nodes), b1 = std::max(hot_end, nodes_end);
+    const uint64_t gaps[3][2] = {{0, a0}, {a1, b0}, {b1, bytes}};
+    for (const auto& gp : gaps)
+      if (gp[1] > gp[0])
+        GM_HIP(ctx, hipMemcpyAsync(D + gp[0], static_cast<const uint8_t*>(src) + gp[0], gp[1] - gp[0],
+                                   hipMemcpyDeviceToDevice, s));
+    const uint8_t* SRC = static_cast<const uint8_t*>(src);
+    hipLaunchKernelGGL(k_renumber_copy, dim3(uint32_t(g ? g : 1)), dim3(256), 0, s,
+                       reinterpret_cast<const HotSlot*>(SRC + o_hot), reinterpret_cast<HotSlot*>(D + o_hot), n_hot,
+                       reinterpret_cast<const Node*>(SRC + o_nodes), reinterpret_cast<Node*>(D + o_nodes), n_nodes, RM);
+    GM_HIP(ctx, hipGetLastError());
+  } else {
+    GM_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+    GM_HIP(ctx, hipMemcpyAsync(dbuf.p, st.data(), up, hipMemcpyHostToDevice, s));
+  }
   if (n_pieces) {
     hipLaunchKernelGGL(k_patch_scatter, dim3(uint32_t(n_pieces)), dim3(256), 0, s, D,
                        reinterpret_cast<const uint64_t*>(S), S + o_pay);
@@ -2687,19 +2787,12 @@ int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t byte
                        uint64_t(orops.size()));
     GM_HIP(ctx, hipGetLastError());
   }
-  uint32_t* const RM = reinterpret_cast<uint32_t*>(dbuf.as<uint8_t>() + o_rmap);
-  if (n_map) {
-    hipLaunchKernelGGL(k_shift_table, dim3(uint32_t((n_map + 255) / 256)), dim3(256), 0, s, RM, shift.nb,
-                       reinterpret_cast<const uint32_t*>(S + o_dels), uint32_t(nd),
-                       reinterpret_cast<const uint32_t*>(S + o_adds), uint32_t(na));
+  if (!fused) {
+    if (const int rc = shift_table()) return rc;
+    hipLaunchKernelGGL(k_renumber, dim3(uint32_t(g ? g : 1)), dim3(256), 0, s, reinterpret_cast<HotSlot*>(D + o_hot),
+                       n_hot, reinterpret_cast<Node*>(D + o_nodes), n_nodes, RM);
     GM_HIP(ctx, hipGetLastError());
   }
-  uint64_t n_hot = 0;
-  for (int t = 0; t < HOT_TABLES; ++t) n_hot = std::max<uint64_t>(n_hot, v.hot_off[t] + v.hot_cap[t]);
-  const uint64_t g = std::min<uint64_t>(4096, (std::max(n_hot, n_nodes) + 255) / 256);
-  hipLaunchKernelGGL(k_renumber, dim3(uint32_t(g ? g : 1)), dim3(256), 0, s, reinterpret_cast<HotSlot*>(D + o_hot),
-                     n_hot, reinterpret_cast<Node*>(D + o_nodes), n_nodes, RM);
-  GM_HIP(ctx, hipGetLastError());
   GM_HIP(ctx, hipStreamSynchronize(s));  // the staging buffers go back to the pool / the host
   return EMQX_GM_OK;
 }

@@ -427,6 +427,33 @@ def test_prefix_device_path_library_first_default_stream_inputs():
     assert "PREFIX_DEVICE_PATH_OK world=1" in out and "libfirst" in out
 
 
+@pytest.mark.parametrize("order", ["lib_first", "torch_first", "ctx_first"])
+def test_one_hip_runtime_whatever_the_order(order):
+    """A host-only library call before the first Context (the order of
+    __graft_entry__.smoke: gen_filter_codes, then Context) used to load
+    /opt/rocm's HIP runtime beside torch's own copy; torch came up first on its
+    copy and emqx_gm_open then found no device (round 5 smoke: EDEVICE).  The
+    library now binds to torch's runtime in every order: the context opens and
+    one libamdhip64 is mapped (scripts/smoke_order_diag.py)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-u", os.path.join(root, "scripts", "smoke_order_diag.py"), order], cwd=root,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0 and f"{order} open ok" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
+    assert f"{order} hip runtimes: 1" in p.stdout, p.stdout[-2000:]
+
+
+def test_graft_smoke_in_a_fresh_process():
+    """The driver's smoke(), as the driver runs it: a fresh interpreter."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-u", "-c", "import __graft_entry__ as g; g.smoke()"], cwd=root,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0 and "smoke ok" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
+
+
 @pytest.mark.timeout(600)
 def test_prefix_device_path_world8_lockstep():
     """The 4M-filter set in 8 prefix shards, 8 ranks as threads on one device,

@@ -19,8 +19,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["patch", "patch_mph", "overlay"])
+@pytest.fixture(params=["patch", "patch_mph", "patch_unfused", "overlay"])
 def form(request, monkeypatch):
+    # patch_unfused: the device side as copy, patch, renumber in place (the A/B
+    # twin of the default one-pass copy-and-renumber, gm_match.hip apply_patch_device)
+    if request.param == "patch_unfused":
+        monkeypatch.setenv("GM_UPDATE_UNFUSED", "1")
+    else:
+        monkeypatch.delenv("GM_UPDATE_UNFUSED", raising=False)
     if request.param == "overlay":
         monkeypatch.setenv("GM_UPDATE_OVERLAY", "1")
     else:
@@ -28,7 +34,7 @@ def form(request, monkeypatch):
     if request.param == "patch_mph":  # every per-depth table hash-and-displace placed: inserts take the overflow region
         monkeypatch.setenv("GM_MPH_MIN_KEYS", "1")
         monkeypatch.setenv("GM_CHAIN", "1")  # and chain nodes, which the patch turns back into plain nodes
-    return "patch" if request.param == "patch_mph" else request.param
+    return "patch" if request.param in ("patch_mph", "patch_unfused") else request.param
 
 
 def _is_flat(ctx, idx):
@@ -100,6 +106,53 @@ def test_update_sequences_vs_oracle(ctx, orc, form):
         idx.release()
         idx = new
     idx.release()
+
+
+def _blob(ctx, idx):
+    ptr, nb = idx.device_blob()
+    out = np.empty(nb, np.uint8)
+    ctx.memcpy_d2h(out, ptr, nb)
+    return out
+
+
+def test_fused_update_equals_copy_patch_renumber(ctx, monkeypatch):
+    """The one-pass device update (hot slots and nodes renumbered while copied,
+    the patched ranges renumbered on the host by IdShift::map) writes the same
+    device tables, byte for byte, as the copy + patch + in-place renumber
+    (GM_UPDATE_UNFUSED): two imports of one image, the same ops on each,
+    inserts and deletes spread over the id range (every id after the first
+    change shifts)."""
+    from tests.test_gpu_image import _workload
+    monkeypatch.delenv("GM_UPDATE_OVERLAY", raising=False)
+    fp, tp = _workload(30_000, 20_000)
+    base = ctx.build_index(fp)
+    img = base.export()
+    rng = random.Random(5)
+    from tests.test_gpu_parity import _rand_filter
+    fb, fo = fp
+    names = [bytes(fb[int(fo[i]):int(fo[i + 1])]) for i in range(0, len(fo) - 1, 97)]
+    rounds = [[(f, False) for f in rng.sample(names, 40)] + [(_rand_filter(rng).encode(), True) for _ in range(60)],
+              [(_rand_filter(rng).encode(), True) for _ in range(30)] + [(f, False) for f in rng.sample(names, 10)]]
+    out = {}
+    for mode in ("fused", "unfused"):
+        if mode == "unfused":
+            monkeypatch.setenv("GM_UPDATE_UNFUSED", "1")
+        else:
+            monkeypatch.delenv("GM_UPDATE_UNFUSED", raising=False)
+        idx = ctx.import_index(img)
+        for ops in rounds:
+            new = ctx.update_index(idx, ops)
+            assert _is_flat(ctx, new)
+            idx.release()
+            idx = new
+        out[mode] = (_blob(ctx, idx), ctx.match(idx, tp, exact=True))
+        idx.release()
+    base.release()
+    a, b = out["fused"], out["unfused"]
+    assert a[0].nbytes == b[0].nbytes
+    diff = np.flatnonzero(a[0] != b[0])
+    assert diff.size == 0, f"{diff.size} bytes differ, first at {diff[:8]}"
+    assert np.array_equal(a[1][0], b[1][0]) and np.array_equal(a[1][1], b[1][1])
 
 
 def test_update_breaks_chain_nodes(ctx, orc, form, monkeypatch):
