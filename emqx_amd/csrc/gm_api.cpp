@@ -352,6 +352,7 @@ int emqx_gm_close(emqx_gm_ctx* ctx) {
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    gm::trim_spare_blob(ctx->device);
     gm::free_host_pipe(ctx);
     delete ctx->pool;
     delete ctx->hpool;
@@ -842,6 +843,11 @@ int emqx_gm_pool_trim(emqx_gm_ctx* ctx) {
   if (!ctx) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   ctx->pool->trim();
+  gm::trim_spare_blob(ctx->device);
+  for (emqx_gm_ctx* m : ctx->members) {
+    m->pool->trim();
+    gm::trim_spare_blob(m->device);
+  }
   return EMQX_GM_OK;
 }
 

@@ -986,6 +986,60 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
 // this file links this stand-in, which reports "not written")
 __attribute__((weak)) int refresh_d0(emqx_gm_ctx*, const IndexView&, void*) { return 1; }
 
+namespace {
+struct SpareBlob {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+constexpr int kSpareDevices = 64;
+std::mutex g_spare_mu;
+SpareBlob g_spare[kSpareDevices];
+// blobs below this size allocate quickly anyway (GM_SPARE_BLOB_MIN, bytes; 0: off)
+size_t spare_min() {
+  const char* e = getenv("GM_SPARE_BLOB_MIN");
+  return e ? size_t(strtoull(e, nullptr, 10)) : size_t(256) << 20;
+}
+}  // namespace
+
+void* take_spare_blob(int device, size_t bytes) {
+  const size_t lo = spare_min();
+  if (device < 0 || device >= kSpareDevices || !lo || bytes < lo) return nullptr;
+  std::lock_guard<std::mutex> lk(g_spare_mu);
+  SpareBlob& s = g_spare[device];
+  if (!s.p || s.bytes < bytes || s.bytes - bytes > bytes / 4) return nullptr;
+  void* p = s.p;
+  s = SpareBlob{};
+  return p;
+}
+
+void give_spare_blob(int device, void* p, size_t bytes) {
+  if (!p) return;
+  const size_t lo = spare_min();
+  void* drop = p;
+  if (device >= 0 && device < kSpareDevices && lo && bytes >= lo) {
+    // hipFree waits for the device's work; so does keeping the blob for reuse
+    (void)hipDeviceSynchronize();
+    std::lock_guard<std::mutex> lk(g_spare_mu);
+    std::swap(drop, g_spare[device].p);  // the newest blob stays (a line of updates frees its own size)
+    g_spare[device].bytes = bytes;
+  }
+  if (drop) (void)hipFree(drop);
+}
+
+void trim_spare_blob(int device) {
+  if (device < 0 || device >= kSpareDevices) return;
+  void* p;
+  {
+    std::lock_guard<std::mutex> lk(g_spare_mu);
+    p = g_spare[device].p;
+    g_spare[device] = SpareBlob{};
+  }
+  if (p) {
+    (void)hipSetDevice(device);
+    (void)hipFree(p);
+  }
+}
+
 void free_index(emqx_gm_index* idx) {
   if (!idx) return;
   for (emqx_gm_index* r : idx->reps)
@@ -995,7 +1049,7 @@ void free_index(emqx_gm_index* idx) {
   delete idx->mirror;
   if (idx->dev_base || idx->dev_subs) {
     (void)hipSetDevice(idx->device);
-    if (idx->dev_base && !idx->blob_owner) (void)hipFree(idx->dev_base);
+    if (idx->dev_base && !idx->blob_owner) give_spare_blob(idx->device, idx->dev_base, idx->dev_bytes);
     if (idx->dev_subs) (void)hipFree(idx->dev_subs);
   }
   if (idx->blob_owner && idx->blob_owner->refs.fetch_sub(1) == 1) free_index(idx->blob_owner);

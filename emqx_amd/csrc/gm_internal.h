@@ -257,6 +257,15 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
                 emqx_gm_index_info_t* host_only = nullptr, const uint32_t* gids = nullptr);
 void sort_filters(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t* fo);
 void free_index(emqx_gm_index* idx);
+// gm_index.cpp: a freed snapshot's device blob kept, one per device, for the
+// next in-place update of that size (a large fresh hipMalloc after a few
+// update / free cycles stalls: C5's 38 GB blob took ~1 s from the 7th update on,
+// 0.3 ms before).  take: a spare of at least `bytes` (at most 1.25x), or null;
+// give: keeps p (the device synchronized first, as hipFree does) or frees it;
+// trim: frees the device's spare (emqx_gm_pool_trim, emqx_gm_close).
+void* take_spare_blob(int device, size_t bytes);
+void give_spare_blob(int device, void* p, size_t bytes);
+void trim_spare_blob(int device);
 // gm_match.hip
 // A caller's work queued on the context stream right behind the speculative
 // assembly of a DEVICE_IO match, before run_match's one host round trip (the

@@ -572,7 +572,8 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
   const size_t blob_bytes = trie_only ? M.blob.size() : prev->dev_bytes;  // the mirror ends at the CSR
   if (!host) {
     hipError_t e = hipSetDevice(prev->device);
-    if (e == hipSuccess) e = hipMalloc(&idx->dev_base, blob_bytes);
+    if (e == hipSuccess && !(idx->dev_base = take_spare_blob(prev->device, blob_bytes)))
+      e = hipMalloc(&idx->dev_base, blob_bytes);
     if (e != hipSuccess) {
       P.rollback();
       delete idx;

@@ -3,7 +3,7 @@
 three in a row (each on the previous result), with the device match time of
 10M topics on the flat and the last patched snapshot.  One JSON line per config;
 GM_UPDATE_TIMING=1 adds the phase times on stderr.  --ab: eight updates in a
-row alternating the one-pass device update and GM_UPDATE_UNFUSED (copy, patch,
+row (ten with --ab) alternating the one-pass device update and GM_UPDATE_UNFUSED (copy, patch,
 renumber in place), each mode's times reported apart.
 usage: update_c23.py [--ab] [c2] [c3] [c5]"""
 import json
@@ -41,7 +41,7 @@ def run(cfg):
     rng = np.random.default_rng(7)
     times, cur = [], idx
     modes = []
-    for rep in range(8 if AB else 3):
+    for rep in range(10 if AB else 3):
         if AB:
             modes.append("unfused" if rep % 2 else "fused")
             if rep % 2:
