@@ -2,8 +2,8 @@
 + 100 inserts) patched into the 1M-wildcard (C2) or 10M-mixed (C3) index,
 three in a row (each on the previous result), with the device match time of
 10M topics on the flat and the last patched snapshot.  One JSON line per config;
-GM_UPDATE_TIMING=1 adds the phase times on stderr.  --ab: eight updates in a
-row (ten with --ab) alternating the one-pass device update and GM_UPDATE_UNFUSED (copy, patch,
+GM_UPDATE_TIMING=1 adds the phase times on stderr.  --ab: ten updates in a row
+alternating the one-pass device update and GM_UPDATE_UNFUSED (copy, patch,
 renumber in place), each mode's times reported apart.
 usage: update_c23.py [--ab] [c2] [c3] [c5]"""
 import json
