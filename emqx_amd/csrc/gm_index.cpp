@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <numeric>
 #include <string_view>
 #include <thread>
@@ -232,9 +233,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     total_words += 1 + std::count(FBV.begin() + a, FBV.begin() + b, uint8_t('/'));
   }
   wid.reserve(std::min<uint64_t>(total_words, 1u << 26));
-  EdgeMap edges(std::min<uint64_t>(total_words + 1, 1ull << 30));
   std::vector<HNode> nodes(1);
-  nodes.reserve(std::min<uint64_t>(total_words + 1, 1ull << 30));
   uint64_t n_wild = 0;
   uint32_t max_depth = 0;
   const uint8_t* FB = FBV.data();
@@ -255,73 +254,242 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     return off;
   };
 
-  // Filters are in byte order, so a filter usually shares its leading words
-  // with the previous one: those words' nodes are taken from the previous
-  // filter's path (no interning, no edge lookup).  Word j of the previous
-  // filter (ending at byte e) is shared when the two agree on every byte up
-  // to e and the word ends at e in both.
-  std::vector<uint32_t> pnode;  // node after word j of the previous filter
-  std::vector<uint64_t> pend;   // end byte of word j
-  std::vector<uint8_t> pwild;   // a wildcard word among words 0..j
-  const uint8_t* ps = nullptr;
-  uint64_t plen = 0;
-  for (uint32_t f = 0; f < nf; ++f) {
-    const uint8_t* s = FB + FOV[f];
-    uint64_t len = FOV[f + 1] - FOV[f];
-    uint64_t cp = 0;
-    if (ps) {
-      const uint64_t m = std::min(len, plen);
-      while (cp < m && s[cp] == ps[cp]) ++cp;
+  // The trie is built in parallel over runs of filters: filters are in byte
+  // order, and runs cut where no first word continues across the cut
+  // (safe_cut) share no node but the root.  Each run
+  // builds a local trie (local node and word numbers, its own edge map); the
+  // runs are then merged IN FILTER ORDER -- nodes concatenated, words interned
+  // in each run's first-occurrence order -- which is exactly the serial
+  // build's creation order and word order (the BFS renumbering, the arena
+  // and every table below come out the same).
+  struct TrieRun {
+    uint32_t f0 = 0, f1 = 0;                 // filters [f0, f1)
+    std::vector<HNode> nodes;                // [0]: the root's stand-in (its changes merged below)
+    std::vector<std::string_view> words;     // distinct words, first occurrence first
+    uint64_t n_wild = 0;
+    uint32_t max_depth = 0;
+  };
+  auto first_word = [&](uint32_t f) {
+    const uint8_t* p = FB + FOV[f];
+    const uint64_t len = FOV[f + 1] - FOV[f];
+    const void* q = std::memchr(p, '/', len);
+    return std::string_view(reinterpret_cast<const char*>(p), q ? uint64_t(static_cast<const uint8_t*>(q) - p) : len);
+  };
+  auto filt = [&](uint32_t f) {
+    return std::string_view(reinterpret_cast<const char*>(FB + FOV[f]), FOV[f + 1] - FOV[f]);
+  };
+  auto lower = [&](std::string_view key) {  // the first filter >= key (byte order)
+    uint32_t lo = 0, hi = nf;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      const std::string_view m = filt(mid);
+      if (less_bytes(reinterpret_cast<const uint8_t*>(m.data()), m.size(),
+                     reinterpret_cast<const uint8_t*>(key.data()), key.size()))
+        lo = mid + 1;
+      else
+        hi = mid;
     }
-    size_t j = 0;
-    while (j < pend.size()) {
-      const uint64_t e = pend[j];
-      const bool shared = e < cp || (e == cp && (cp == len || (cp == plen && cp < len && s[cp] == '/')));
-      if (!shared) break;
-      ++j;
+    return lo;
+  };
+  // Whether filters [0, e) and [e, nf) share no first word.  The filters with
+  // first word W are "W" itself and a contiguous block "W/...", but between
+  // the two may lie filters "W" + c... with c < '/' (e.g. "a", "a-b", "a/c"):
+  // so besides the two neighbours' first words, a single-word filter W before
+  // the cut whose block starts after it must not exist -- and such a W is a
+  // byte prefix of the filter just before the cut (every filter between "W"
+  // and "W/" starts with W).
+  auto safe_cut = [&](uint32_t e) {
+    const std::string_view a = first_word(e - 1);
+    if (a == first_word(e)) return false;
+    std::string key;
+    for (size_t L = 0; L <= a.size(); ++L) {
+      key.assign(a.data(), L);
+      const uint32_t x = lower(key);
+      if (!(x < e && filt(x) == key)) continue;  // "W" is no filter before the cut
+      key.push_back('/');
+      const uint32_t b = lower(key);
+      if (b >= e && b < nf && filt(b).substr(0, key.size()) == key) return false;
     }
-    pnode.resize(j);
-    pend.resize(j);
-    pwild.resize(j);
-    uint32_t node = j ? pnode[j - 1] : 0, depth = uint32_t(j);
-    bool wild = j ? pwild[j - 1] != 0 : false;
-    const uint64_t ws0 = j ? pend[j - 1] + 1 : 0;
-    uint64_t ws = ws0;
-    ps = s;
-    plen = len;
-    for (uint64_t i = ws0; i <= len; ++i) {
-      if (i < len && s[i] != '/') continue;
-      const uint8_t* w = s + ws;
-      uint64_t wl = i - ws;
-      bool plus = wl == 1 && w[0] == '+', hash = wl == 1 && w[0] == '#';
-      wild |= plus || hash;
-      uint32_t id = intern(w, wl);
-      uint64_t key = edge_key(node, id);
-      uint32_t child = edges.get(key);
-      if (child == NONE) {
-        child = uint32_t(nodes.size());
-        if (child >= REF_X) throw std::length_error("too many trie nodes (>= 2^31)");
-        nodes.push_back(HNode{});
-        nodes.back().depth = depth + 1;
-        nodes.back().parent = node;
-        nodes.back().word = id;
-        nodes.back().kind = plus ? 1 : hash ? 2 : 0;
-        edges.put(key, child);
-        if (plus) { nodes[node].plus_child = child; nodes[node].flags |= NF_HAS_PLUS; }
-        else if (hash) nodes[node].hash_child = child;
-        else { nodes[node].flags |= NF_HAS_EXACT; nodes[node].sig |= sig_bit(id); }
-      }
-      node = child;
-      ++depth;
-      ws = i + 1;
-      pnode.push_back(node);
-      pend.push_back(i);
-      pwild.push_back(wild);
+    return true;
+  };
+  const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<TrieRun> runs;
+  {
+    // GM_TRIE_RUNS: the number of runs asked for (1: the serial build; tests)
+    const char* rk = getenv("GM_TRIE_RUNS");
+    const uint32_t want = rk ? std::max(1u, uint32_t(strtoul(rk, nullptr, 10)))
+                             : (nf < 200000 || T == 1) ? 1u : 4u * T;
+    uint32_t f0 = 0;
+    for (uint32_t k = 1; k <= want && f0 < nf; ++k) {
+      uint32_t e = k == want ? nf : uint32_t(uint64_t(nf) * k / want);
+      if (e <= f0) continue;
+      while (e < nf && !safe_cut(e)) ++e;
+      TrieRun r;
+      r.f0 = f0;
+      r.f1 = e;
+      runs.push_back(std::move(r));
+      f0 = e;
     }
-    nodes[node].end_filter = f;
-    if (wild) { nodes[node].flags |= NF_END_WILD; ++n_wild; }
-    max_depth = std::max(max_depth, depth);
   }
+  // one run: the serial walk below, on local numbers
+  auto build_run = [&](TrieRun& R) {
+    uint64_t tw = 0;
+    for (uint32_t f = R.f0; f < R.f1; ++f) tw += 1 + std::count(FB + FOV[f], FB + FOV[f + 1], uint8_t('/'));
+    std::unordered_map<std::string_view, uint32_t, ViewHash> lw;  // word -> local word number
+    lw.reserve(std::min<uint64_t>(tw, 1u << 26));
+    EdgeMap edges(std::min<uint64_t>(tw + 1, 1ull << 30));
+    std::vector<HNode>& nd = R.nodes;
+    nd.assign(1, HNode{});
+    nd.reserve(std::min<uint64_t>(tw + 1, 1ull << 30));
+    auto lintern = [&](const uint8_t* p, uint64_t len) -> uint32_t {
+      std::string_view v(reinterpret_cast<const char*>(p), len);
+      auto it = lw.find(v);
+      if (it != lw.end()) return it->second;
+      const uint32_t id = uint32_t(R.words.size());
+      R.words.push_back(v);
+      lw.emplace(v, id);
+      return id;
+    };
+    // Filters are in byte order, so a filter usually shares its leading words
+    // with the previous one: those words' nodes are taken from the previous
+    // filter's path (no interning, no edge lookup).  Word j of the previous
+    // filter (ending at byte e) is shared when the two agree on every byte up
+    // to e and the word ends at e in both.
+    std::vector<uint32_t> pnode;  // node after word j of the previous filter
+    std::vector<uint64_t> pend;   // end byte of word j
+    std::vector<uint8_t> pwild;   // a wildcard word among words 0..j
+    const uint8_t* ps = nullptr;
+    uint64_t plen = 0;
+    for (uint32_t f = R.f0; f < R.f1; ++f) {
+      const uint8_t* s = FB + FOV[f];
+      uint64_t len = FOV[f + 1] - FOV[f];
+      uint64_t cp = 0;
+      if (ps) {
+        const uint64_t m = std::min(len, plen);
+        while (cp < m && s[cp] == ps[cp]) ++cp;
+      }
+      size_t j = 0;
+      while (j < pend.size()) {
+        const uint64_t e = pend[j];
+        const bool shared = e < cp || (e == cp && (cp == len || (cp == plen && cp < len && s[cp] == '/')));
+        if (!shared) break;
+        ++j;
+      }
+      pnode.resize(j);
+      pend.resize(j);
+      pwild.resize(j);
+      uint32_t node = j ? pnode[j - 1] : 0, depth = uint32_t(j);
+      bool wild = j ? pwild[j - 1] != 0 : false;
+      const uint64_t ws0 = j ? pend[j - 1] + 1 : 0;
+      uint64_t ws = ws0;
+      ps = s;
+      plen = len;
+      for (uint64_t i = ws0; i <= len; ++i) {
+        if (i < len && s[i] != '/') continue;
+        const uint8_t* w = s + ws;
+        uint64_t wl = i - ws;
+        bool plus = wl == 1 && w[0] == '+', hash = wl == 1 && w[0] == '#';
+        wild |= plus || hash;
+        uint32_t id = lintern(w, wl);
+        uint64_t key = edge_key(node, id);
+        uint32_t child = edges.get(key);
+        if (child == NONE) {
+          if (nd.size() >= REF_X) throw std::length_error("too many trie nodes (>= 2^31)");
+          child = uint32_t(nd.size());
+          nd.push_back(HNode{});
+          nd.back().depth = depth + 1;
+          nd.back().parent = node;
+          nd.back().word = id;
+          nd.back().kind = plus ? 1 : hash ? 2 : 0;
+          edges.put(key, child);
+          if (plus) { nd[node].plus_child = child; nd[node].flags |= NF_HAS_PLUS; }
+          else if (hash) nd[node].hash_child = child;
+          else nd[node].flags |= NF_HAS_EXACT;  // (sig: from the final word ids, after the merge)
+        }
+        node = child;
+        ++depth;
+        ws = i + 1;
+        pnode.push_back(node);
+        pend.push_back(i);
+        pwild.push_back(wild);
+      }
+      nd[node].end_filter = f;
+      if (wild) { nd[node].flags |= NF_END_WILD; ++R.n_wild; }
+      R.max_depth = std::max(R.max_depth, depth);
+    }
+  };
+  {
+    std::atomic<size_t> next{0};
+    std::vector<std::exception_ptr> errs(runs.size());
+    auto worker = [&] {
+      for (size_t r; (r = next.fetch_add(1)) < runs.size();) {
+        try {
+          build_run(runs[r]);
+        } catch (...) {
+          errs[r] = std::current_exception();
+        }
+      }
+    };
+    const unsigned nt = unsigned(std::min<size_t>(T, runs.size()));
+    std::vector<std::thread> th;
+    for (unsigned k = 1; k < nt; ++k) th.emplace_back(worker);
+    worker();
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+  }
+  // merge in filter order: words first (the serial first-occurrence order), then nodes
+  std::vector<uint32_t> base(runs.size());
+  uint64_t n_all = 1;
+  for (size_t r = 0; r < runs.size(); ++r) {
+    base[r] = uint32_t(std::min<uint64_t>(n_all, NONE));
+    n_all += runs[r].nodes.size() - 1;
+  }
+  if (n_all > REF_X) throw std::length_error("too many trie nodes (>= 2^31)");
+  std::vector<std::vector<uint32_t>> gword(runs.size());
+  for (size_t r = 0; r < runs.size(); ++r) {
+    gword[r].reserve(runs[r].words.size());
+    for (std::string_view v : runs[r].words) gword[r].push_back(intern(reinterpret_cast<const uint8_t*>(v.data()), v.size()));
+    std::vector<std::string_view>().swap(runs[r].words);
+  }
+  nodes.resize(n_all);
+  {
+    auto merge_run = [&](size_t r) {
+      TrieRun& R = runs[r];
+      const uint32_t b = base[r];
+      auto g = [&](uint32_t l) { return l == NONE ? NONE : l == 0 ? 0u : b + l - 1; };
+      for (size_t l = 1; l < R.nodes.size(); ++l) {
+        HNode h = R.nodes[l];
+        h.parent = g(h.parent);
+        h.word = gword[r][h.word];
+        h.plus_child = g(h.plus_child);
+        h.hash_child = g(h.hash_child);
+        nodes[b + l - 1] = h;
+      }
+      std::vector<HNode>(1, R.nodes[0]).swap(R.nodes);  // (only the root's stand-in is still needed)
+    };
+    std::atomic<size_t> next{0};
+    auto worker = [&] {
+      for (size_t r; (r = next.fetch_add(1)) < runs.size();) merge_run(r);
+    };
+    const unsigned nt = unsigned(std::min<size_t>(T, runs.size()));
+    std::vector<std::thread> th;
+    for (unsigned k = 1; k < nt; ++k) th.emplace_back(worker);
+    worker();
+    for (auto& t : th) t.join();
+  }
+  for (size_t r = 0; r < runs.size(); ++r) {  // the root: the union of the runs' changes
+    const HNode& h = runs[r].nodes[0];
+    nodes[0].flags |= h.flags;
+    if (h.plus_child != NONE) nodes[0].plus_child = base[r] + h.plus_child - 1;
+    if (h.hash_child != NONE) nodes[0].hash_child = base[r] + h.hash_child - 1;
+    n_wild += runs[r].n_wild;
+    max_depth = std::max(max_depth, runs[r].max_depth);
+  }
+  std::vector<TrieRun>().swap(runs);
+  // exact-child signatures over the final word ids (a child's parent is older: one pass)
+  for (uint64_t i = 1; i < nodes.size(); ++i)
+    if (nodes[i].kind == 0) nodes[nodes[i].parent].sig |= sig_bit(nodes[i].word);
 
   phase("trie");
   // ---- 3. breadth-first renumbering (stable by creation order within a level)
@@ -349,17 +517,14 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // edge tables partitioned by the parent's depth
   // (each depth's table built on its own thread from its bucket of edges)
   std::vector<std::vector<std::pair<uint64_t, uint32_t>>> by_tab(EDGE_DEPTHS);
-  {
+  {  // (every non-root node is the child of exactly one edge: (parent, word))
     std::vector<uint64_t> per_tab(EDGE_DEPTHS, 0);
-    for (auto& s : edges.slots)
-      if (s.key != EDGE_EMPTY) per_tab[edge_depth(nodes[uint32_t(s.key >> 32)].depth)]++;
+    for (uint64_t i = 1; i < NN; ++i) per_tab[edge_depth(nodes[i].depth - 1)]++;
     for (int d = 0; d < EDGE_DEPTHS; ++d) by_tab[d].reserve(per_tab[d]);
-    for (auto& s : edges.slots)
-      if (s.key != EDGE_EMPTY) {
-        const uint32_t par = uint32_t(s.key >> 32);
-        by_tab[edge_depth(nodes[par].depth)].emplace_back(edge_key(newid[par], uint32_t(s.key)), ref(s.child));
-      }
-    std::vector<EdgeSlot>().swap(edges.slots);  // the build-time map is done
+    for (uint64_t i = 1; i < NN; ++i) {
+      const uint32_t par = nodes[i].parent;
+      by_tab[edge_depth(nodes[i].depth - 1)].emplace_back(edge_key(newid[par], nodes[i].word), ref(uint32_t(i)));
+    }
   }
   std::vector<EdgeMap> tabs;
   tabs.reserve(EDGE_DEPTHS);
