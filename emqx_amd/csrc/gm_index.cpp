@@ -11,6 +11,7 @@
 // Layout (gm_common.h): nodes are numbered breadth-first so the hot upper
 // levels of the trie are contiguous in HBM and stay resident in L2/MALL.
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -140,6 +141,56 @@ void sort_filters_impl(std::vector<uint32_t>& ord, const uint8_t* fb, const uint
     }
   }
   for (size_t k = 0; k < n; ++k) ord[k] = ks[k].i;
+}
+
+// An allocator that default-initialises (a vector of PODs left unwritten until
+// parallel_for fills it).
+template <class T> struct DefaultInit : std::allocator<T> {
+  template <class U> struct rebind {
+    using other = DefaultInit<U>;
+  };
+  DefaultInit() = default;
+  template <class U> DefaultInit(const DefaultInit<U>&) {}
+  template <class U> void construct(U* p) { ::new (static_cast<void*>(p)) U; }
+  template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+
+// f(begin, end) over [0, n) in one contiguous range per thread (small n: one call).
+template <class F> void parallel_for(uint64_t n, F f) {
+  const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (n < (1u << 16) || T == 1) {
+    f(uint64_t(0), n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned k = 1; k < T; ++k) th.emplace_back([&, k] { f(n * k / T, n * (k + 1) / T); });
+  f(uint64_t(0), n / T);
+  for (auto& t : th) t.join();
+}
+
+// Parallel sort of u64 values (chunked std::sort + pairwise merges).
+void sort_u64(std::vector<uint64_t>& v) {
+  const size_t n = v.size();
+  const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (n < 200000 || T == 1) {
+    std::sort(v.begin(), v.end());
+    return;
+  }
+  std::vector<size_t> b(T + 1);
+  for (unsigned k = 0; k <= T; ++k) b[k] = n * k / T;
+  {
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < T; ++k) th.emplace_back([&, k] { std::sort(v.begin() + b[k], v.begin() + b[k + 1]); });
+    for (auto& t : th) t.join();
+  }
+  for (size_t width = 1; width < T; width *= 2) {
+    std::vector<std::thread> th;
+    for (size_t k = 0; k + width < T; k += 2 * width) {
+      const size_t lo = b[k], mid = b[k + width], hi = b[std::min<size_t>(k + 2 * width, T)];
+      th.emplace_back([&, lo, mid, hi] { std::inplace_merge(v.begin() + lo, v.begin() + mid, v.begin() + hi); });
+    }
+    for (auto& t : th) t.join();
+  }
 }
 
 }  // namespace
@@ -501,52 +552,91 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   std::vector<uint32_t> newid(NN);
   for (uint64_t i = 0; i < NN; ++i) newid[i] = uint32_t(per_depth[nodes[i].depth]++);
 
+  phase("v1: renumber");
   auto ref = [&](uint32_t old) -> uint32_t {  // child reference with the child's HAS_EXACT bit
     if (old == NONE) return NONE;
     return newid[old] | ((nodes[old].flags & NF_HAS_EXACT) ? REF_X : 0u);
   };
   std::vector<Node> dnodes(NN);
-  for (uint64_t i = 0; i < NN; ++i) {
-    const HNode& h = nodes[i];
-    Node& d = dnodes[newid[i]];
-    d.plus_child = ref(h.plus_child);
-    d.hash_filter = h.hash_child == NONE ? NONE : nodes[h.hash_child].end_filter;
-    d.end_filter = h.end_filter;
-    d.flags = h.flags;
-  }
+  parallel_for(NN, [&](uint64_t a, uint64_t b) {  // (newid is a permutation: distinct writes)
+    for (uint64_t i = a; i < b; ++i) {
+      const HNode& h = nodes[i];
+      Node& d = dnodes[newid[i]];
+      d.plus_child = ref(h.plus_child);
+      d.hash_filter = h.hash_child == NONE ? NONE : nodes[h.hash_child].end_filter;
+      d.end_filter = h.end_filter;
+      d.flags = h.flags;
+    }
+  });
   // edge tables partitioned by the parent's depth
   // (each depth's table built on its own thread from its bucket of edges)
   std::vector<std::vector<std::pair<uint64_t, uint32_t>>> by_tab(EDGE_DEPTHS);
-  {  // (every non-root node is the child of exactly one edge: (parent, word))
-    std::vector<uint64_t> per_tab(EDGE_DEPTHS, 0);
-    for (uint64_t i = 1; i < NN; ++i) per_tab[edge_depth(nodes[i].depth - 1)]++;
-    for (int d = 0; d < EDGE_DEPTHS; ++d) by_tab[d].reserve(per_tab[d]);
-    for (uint64_t i = 1; i < NN; ++i) {
-      const uint32_t par = nodes[i].parent;
-      by_tab[edge_depth(nodes[i].depth - 1)].emplace_back(edge_key(newid[par], nodes[i].word), ref(uint32_t(i)));
+  {  // (every non-root node is the child of exactly one edge: (parent, word)); the
+     // buckets filled in node order by all threads: per-range counts, then offsets
+    const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned R = NN < (1u << 16) ? 1u : T;
+    std::vector<std::array<uint64_t, EDGE_DEPTHS>> cnt(R);
+    auto range = [&](unsigned r, auto f) {
+      for (uint64_t i = std::max<uint64_t>(1, NN * r / R), e = NN * (r + 1) / R; i < e; ++i) f(i);
+    };
+    auto run_ranges = [&](auto body) {
+      std::vector<std::thread> th;
+      for (unsigned r = 1; r < R; ++r) th.emplace_back([&, r] { body(r); });
+      body(0u);
+      for (auto& t : th) t.join();
+    };
+    run_ranges([&](unsigned r) {
+      cnt[r].fill(0);
+      range(r, [&](uint64_t i) { cnt[r][edge_depth(nodes[i].depth - 1)]++; });
+    });
+    for (int d = 0; d < EDGE_DEPTHS; ++d) {
+      uint64_t o = 0;
+      for (unsigned r = 0; r < R; ++r) {
+        const uint64_t c = cnt[r][d];
+        cnt[r][d] = o;
+        o += c;
+      }
+      by_tab[d].resize(o);
     }
+    run_ranges([&](unsigned r) {
+      range(r, [&](uint64_t i) {
+        const int d = edge_depth(nodes[i].depth - 1);
+        by_tab[d][cnt[r][d]++] = {edge_key(newid[nodes[i].parent], nodes[i].word), ref(uint32_t(i))};
+      });
+    });
   }
+  phase("v1: buckets");
   std::vector<EdgeMap> tabs;
   tabs.reserve(EDGE_DEPTHS);
-  for (int d = 0; d < EDGE_DEPTHS; ++d) tabs.emplace_back(by_tab[d].size() + 1);
+  for (int d = 0; d < EDGE_DEPTHS; ++d) tabs.emplace_back(by_tab[d].empty() ? 1 : 0);  // (sized on its thread)
   {
     std::vector<std::thread> th;
     for (int d = 0; d < EDGE_DEPTHS; ++d)
       if (!by_tab[d].empty())
         th.emplace_back([&, d] {
+          tabs[d] = EdgeMap(by_tab[d].size() + 1);
           for (const auto& kv : by_tab[d]) tabs[d].put(kv.first, kv.second);
           std::vector<std::pair<uint64_t, uint32_t>>().swap(by_tab[d]);
         });
     for (auto& t : th) t.join();
   }
-  std::vector<EdgeSlot> dedges;
-  uint64_t etab_off[EDGE_DEPTHS], etab_mask[EDGE_DEPTHS], n_edges = 0;
+  phase("v1: edge maps");
+  uint64_t etab_off[EDGE_DEPTHS], etab_mask[EDGE_DEPTHS], n_edges = 0, n_eslots = 0;
   for (int d = 0; d < EDGE_DEPTHS; ++d) {
-    etab_off[d] = dedges.size();
+    etab_off[d] = n_eslots;
     etab_mask[d] = tabs[d].mask;
     n_edges += tabs[d].used;
-    dedges.insert(dedges.end(), tabs[d].slots.begin(), tabs[d].slots.end());
-    std::vector<EdgeSlot>().swap(tabs[d].slots);
+    n_eslots += tabs[d].slots.size();
+  }
+  std::vector<EdgeSlot, DefaultInit<EdgeSlot>> dedges(n_eslots);  // (each table copied in by a thread of its own)
+  {
+    std::vector<std::thread> th;
+    for (int d = 0; d < EDGE_DEPTHS; ++d)
+      th.emplace_back([&, d] {
+        std::copy(tabs[d].slots.begin(), tabs[d].slots.end(), dedges.begin() + etab_off[d]);
+        std::vector<EdgeSlot>().swap(tabs[d].slots);
+      });
+    for (auto& t : th) t.join();
   }
 
   phase("v1 tables");
@@ -647,7 +737,13 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     hot_off[t] = hot_total;
     hot_total += hot_cap[t];
   }
-  std::vector<HotSlot> hot(hot_total, HotSlot{EDGE_EMPTY, 0, HF_NONE, NONE, 0, HF_NONE, NONE});
+  phase("hot: counts");
+  // (uninitialised, then filled by all threads: the first touch of GBs of pages is the cost)
+  std::vector<HotSlot, DefaultInit<HotSlot>> hot(hot_total);
+  parallel_for(hot_total, [&](uint64_t a, uint64_t b) {
+    std::fill(hot.begin() + a, hot.begin() + b, HotSlot{EDGE_EMPTY, 0, HF_NONE, NONE, 0, HF_NONE, NONE});
+  });
+  phase("hot: alloc");
   std::vector<uint32_t> hid(NN, NONE);
   hid[0] = 0;  // the root (depth 0) is not stored; its record goes to IndexView
   auto end_of = [&](const HNode& h) -> uint32_t {
@@ -667,6 +763,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // is in (the next depth's keys hold them).  The shared last table keeps
   // plain linear probing (its earlier depths' ids are already referenced).
   std::vector<uint32_t> occ;  // old node index per slot of the table being placed
+  const bool rh_insert = getenv("GM_HOT_RH_INSERT") != nullptr;  // A/B: RH insertion key by key
+  const bool verify = getenv("GM_INDEX_VERIFY") != nullptr;
   auto fill_slot = [&](HotSlot& o, const HNode& h) {
     o.sig = h.sig;
     o.hf = hf_of(h);
@@ -749,11 +847,64 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     }
     const bool rh = t < HOT_TABLES - 1;
     if (rh) occ.assign(cap, NONE);
+    if (rh && !rh_insert) {
+      // Robin Hood placement in one sweep (no random probes): the depth's keys
+      // sorted by home slot (ties in node order), each at max(its home, the
+      // next free slot); keys that run past the end continue at slot 0 ahead of
+      // the keys homed there.  A Robin Hood layout like inserting them one by
+      // one (GM_HOT_RH_INSERT=1, the A/B twin), up to the order of keys with
+      // the same home (insertion's depends on which resident got displaced).
+      std::vector<uint64_t> hk;  // (home << 32) | position in keys
+      std::vector<uint64_t> keys;
+      std::vector<uint32_t> owner;
+      for (uint32_t k = by_depth_off[d]; k < by_depth_off[d + 1]; ++k) {
+        const uint32_t i = by_depth[k];
+        const HNode& h = nodes[i];
+        if (h.kind == 2 || hid[h.parent] == NONE) continue;
+        if (inl[i]) {
+          HotSlot& p = hot[hot_off[hot_table(d - 1)] + hid[h.parent]];
+          p.p_sig = h.sig;
+          p.p_hf = hf_of(h);
+          p.p_end = end_of(h);
+          hid[i] = hid[h.parent] | HOT_INLINE;
+          continue;
+        }
+        const uint64_t key = hot_key(hid[h.parent], h.word, d - 1);
+        hk.push_back((hot_slot(key, cap) << 32) | keys.size());
+        keys.push_back(key);
+        owner.push_back(i);
+      }
+      sort_u64(hk);
+      uint64_t pos = 0;
+      std::vector<uint32_t> wrap;  // positions in keys that ran past the end
+      for (const uint64_t e : hk) {
+        const uint64_t home = e >> 32;
+        const uint32_t j = uint32_t(e);
+        if (pos < home) pos = home;
+        if (pos >= cap) {
+          wrap.push_back(j);
+          continue;
+        }
+        occ[pos] = j;
+        tab[pos].key = keys[j];
+        ++pos;
+      }
+      // the wrapped keys take slots 0.. and push the residents there along
+      // (a FIFO: the wrapped keys, then each resident met, one per slot)
+      for (size_t head = 0, sl = 0; head < wrap.size(); ++sl) {
+        if (sl >= cap) throw std::length_error("hot table full");
+        if (occ[sl] != NONE) wrap.push_back(occ[sl]);
+        occ[sl] = wrap[head++];
+        tab[sl].key = keys[occ[sl]];
+      }
+      for (uint64_t sl = 0; sl < cap; ++sl)  // owners: from positions to nodes
+        if (occ[sl] != NONE) occ[sl] = owner[occ[sl]];
+    }
     auto home_dist = [&](uint64_t key, uint64_t pos) {
       const uint64_t h = hot_slot(key, cap);
       return pos >= h ? pos - h : pos + cap - h;
     };
-    for (uint32_t k = by_depth_off[d]; k < by_depth_off[d + 1]; ++k) {
+    for (uint32_t k = rh && !rh_insert ? by_depth_off[d + 1] : by_depth_off[d]; k < by_depth_off[d + 1]; ++k) {
       const uint32_t i = by_depth[k];
       const HNode& h = nodes[i];
       if (h.kind == 2 || hid[h.parent] == NONE) continue;  // '#' nodes and their (unmatchable) subtrees
@@ -795,18 +946,34 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
         ++dist;
       }
     }
-    if (rh)
-      for (uint64_t s = 0; s < cap; ++s)
-        if (occ[s] != NONE) {
-          const HNode& h = nodes[occ[s]];
-          HotSlot& o = tab[s];
-          o.sig = h.sig;
-          o.hf = hf_of(h);
-          o.end_filter = end_of(h);
-          hid[occ[s]] = uint32_t(s);
-        }
+    if (rh && verify) {  // GM_INDEX_VERIFY: the table is Robin Hood ordered (what hot_resolve's early exit needs)
+      auto dist_at = [&](uint64_t sl) {
+        const uint64_t h = hot_slot(tab[sl].key, cap);
+        return sl >= h ? sl - h : sl + cap - h;
+      };
+      for (uint64_t sl = 0; sl < cap; ++sl) {
+        if (tab[sl].key == EDGE_EMPTY) continue;
+        const uint64_t pv = sl ? sl - 1 : cap - 1;
+        const uint64_t dd = dist_at(sl);
+        if (tab[pv].key == EDGE_EMPTY ? dd != 0 : dd > dist_at(pv) + 1)
+          throw std::logic_error("hot table not in Robin Hood order");
+      }
+    }
+    if (rh)  // (slot ranges on all threads: each slot's owner is its own node)
+      parallel_for(cap, [&](uint64_t a, uint64_t b) {
+        for (uint64_t s = a; s < b; ++s)
+          if (occ[s] != NONE) {
+            const HNode& h = nodes[occ[s]];
+            HotSlot& o = tab[s];
+            o.sig = h.sig;
+            o.hf = hf_of(h);
+            o.end_filter = end_of(h);
+            hid[occ[s]] = uint32_t(s);
+          }
+      });
   }
 
+  phase("hot: place");
   // ---- 3b'. chain nodes (gm_common.h): path compression of single-filter
   // tails.  tcl[i] = the length of the chain that starts at exact node i (1: i
   // is a leaf holding a filter; 2: i holds nothing but one exact child that is

@@ -526,18 +526,26 @@ int image_fuzz() {
   return bad;
 }
 // ---- the parallel trie build (gm_index.cpp: runs of filters with one first
-// word, built apart and merged in filter order): the image of a host-only
-// index -- every table -- is the same byte for byte whether the trie was
-// built as one run (GM_TRIE_RUNS=1, the serial walk) or as 2, 3, 7 or 64 runs,
-// on random sets over separators, wildcards, NULs and empty words.
+// word, built apart and merged in filter order) and the hot tables' one-sweep
+// Robin Hood placement: the image of a host-only index -- every table -- is
+// the same byte for byte whether the trie was built as one run
+// (GM_TRIE_RUNS=1, the serial walk) or as 2, 3, 7 or 64 runs, and whether the
+// hot tables were swept or filled by RH insertion key by key
+// (GM_HOT_RH_INSERT: the same sizes; its ties among keys of one home differ),
+// on random sets over separators, wildcards, NULs and empty words (small
+// tables: keys wrap past the end); with GM_INDEX_VERIFY (set by the test)
+// every Robin Hood table is checked in order as it is built.
 int trie_runs_check() {
   int bad = 0;
   std::mt19937_64 rng(11);
   const char alpha[] = {'a', 'b', '/', '+', '#', '\0', 'z', 'c'};
   auto image = [&](const std::set<std::string>& fs, const char* runs, std::vector<uint8_t>& img) {
-    setenv("GM_TRIE_RUNS", runs, 1);
+    const bool insert = std::strcmp(runs, "insert") == 0;  // the hot tables by RH insertion, key by key
+    setenv("GM_TRIE_RUNS", insert ? "1" : runs, 1);
+    if (insert) setenv("GM_HOT_RH_INSERT", "1", 1);
     emqx_gm_index* idx = host_build(fs);
     unsetenv("GM_TRIE_RUNS");
+    unsetenv("GM_HOT_RH_INSERT");
     if (!idx) return false;
     uint64_t size = 0;
     bool ok = gm::index_export(nullptr, idx, 0, nullptr, &size) == 0;
@@ -564,15 +572,17 @@ int trie_runs_check() {
       ++bad;
       continue;
     }
-    for (const char* runs : {"2", "3", "7", "64"}) {
-      // (the header holds the build's own host pointers in its view: compared
-      // from the end of the header -- host sections and every table)
-      uint32_t hb = 0;
-      std::memcpy(&hb, one.data() + 12, 4);
+    // (the header holds the build's own host pointers in its view: compared
+    // from the end of the header -- host sections and every table)
+    uint32_t hb = 0;
+    std::memcpy(&hb, one.data() + 12, 4);
+    // (RH insertion orders keys of one home by history: the same sizes and a
+    // valid Robin Hood layout -- GM_INDEX_VERIFY, set by the test -- not the same bytes)
+    for (const char* runs : {"2", "3", "7", "64", "insert"}) {
+      const bool bytes = std::strcmp(runs, "insert") != 0;
       if (!image(fs, runs, many) || many.size() != one.size() || hb > one.size() ||
-          !std::equal(one.begin() + hb, one.end(), many.begin() + hb)) {
-        size_t d0 = 0;
-        d0 = hb;
+          (bytes && !std::equal(one.begin() + hb, one.end(), many.begin() + hb))) {
+        size_t d0 = hb;
         while (d0 < one.size() && d0 < many.size() && one[d0] == many[d0]) ++d0;
         std::fprintf(stderr, "trie runs %s: image differs (round %d, %zu filters; sizes %zu/%zu, first diff %zu)\n",
                      runs, round, fs.size(), one.size(), many.size(), d0);

@@ -225,7 +225,8 @@ def test_host_compiler_under_asan(mph_min):
     b = subprocess.run(["make", "-C", os.path.join(ROOT, "emqx_amd", "csrc"), "asan"], capture_output=True, text=True)
     assert b.returncode == 0, b.stderr[-3000:]
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1",
-               GM_CHAIN="1")  # chain nodes on every index (by default only past 256 MiB of hot tables)
+               GM_CHAIN="1",  # chain nodes on every index (by default only past 256 MiB of hot tables)
+               GM_INDEX_VERIFY="1")  # every Robin Hood hot table checked in order as it is built
     if mph_min:  # every per-depth table placed by hash-and-displace, in-place inserts into its overflow region
         env["GM_MPH_MIN_KEYS"] = mph_min
     p = subprocess.run([os.path.join(ROOT, "tests", "asan", "asan_host_compiler")], capture_output=True, text=True,
