@@ -560,9 +560,13 @@ def main():
     # generate their topics
     compiles = world == 1 or rank == 0 or a.build_each
     fpack = render_codes(codes) if compiles else None
+    t_gen = time.perf_counter() - t_build0  # the synthetic filter set (codes, rendered strings): bench-side
     idx, source = replicated_index(a, ctx, world, rank, local, pg, fpack)
     t_build = time.perf_counter() - t_build0
-    build_info = {"index_source": source, "index_build_s": t_build}
+    # index_build_s: filter generation + the index (compile, or import); index_compile_s: the
+    # library's part alone (emqx_gm_index_build, or the image broadcast and import)
+    build_info = {"index_source": source, "index_build_s": t_build, "filters_gen_s": t_gen,
+                  "index_compile_s": t_build - t_gen}
     if pg is not None:  # how many ranks compiled, the slowest rank's build, the largest host RSS
         n_built = _reduce_tensor(local, float(source == "built"))
         pg.all_reduce(n_built)

@@ -95,54 +95,6 @@ bool less_bytes(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
   return la < lb;
 }
 
-// Parallel sort of filter indices by bytes: (big-endian first 8 bytes, index)
-// pairs, so most comparisons are one integer compare on contiguous memory and
-// only equal prefixes compare the filters' bytes; chunked std::sort + pairwise
-// merges.
-void sort_filters_impl(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t* fo) {
-  const size_t n = ord.size();
-  struct K {
-    uint64_t key;
-    uint32_t i;
-  };
-  std::vector<K> ks(n);
-  for (size_t k = 0; k < n; ++k) {
-    const uint32_t x = ord[k];
-    const uint64_t len = fo[x + 1] - fo[x];
-    uint64_t key = 0;
-    for (uint64_t b = 0; b < 8; ++b) key = (key << 8) | (b < len ? fb[fo[x] + b] : 0u);
-    ks[k] = K{key, x};
-  }
-  auto cmp = [&](const K& a, const K& b) {
-    if (a.key != b.key) return a.key < b.key;
-    return less_bytes(fb + fo[a.i], fo[a.i + 1] - fo[a.i], fb + fo[b.i], fo[b.i + 1] - fo[b.i]);
-  };
-  unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  if (n < 200000 || T == 1) {
-    std::sort(ks.begin(), ks.end(), cmp);
-  } else {
-    std::vector<size_t> b(T + 1);
-    for (unsigned k = 0; k <= T; ++k) b[k] = n * k / T;
-    {
-      std::vector<std::thread> th;
-      for (unsigned k = 0; k < T; ++k)
-        th.emplace_back([&, k] { std::sort(ks.begin() + b[k], ks.begin() + b[k + 1], cmp); });
-      for (auto& t : th) t.join();
-    }
-    for (size_t width = 1; width < T; width *= 2) {
-      std::vector<std::thread> th;
-      for (size_t k = 0; k + width < T; k += 2 * width) {
-        size_t lo = b[k], mid = b[k + width], hi = b[std::min<size_t>(k + 2 * width, T)];
-        th.emplace_back([&, lo, mid, hi] {
-          std::inplace_merge(ks.begin() + lo, ks.begin() + mid, ks.begin() + hi, cmp);
-        });
-      }
-      for (auto& t : th) t.join();
-    }
-  }
-  for (size_t k = 0; k < n; ++k) ord[k] = ks[k].i;
-}
-
 // An allocator that default-initialises (a vector of PODs left unwritten until
 // parallel_for fills it).
 template <class T> struct DefaultInit : std::allocator<T> {
@@ -168,29 +120,162 @@ template <class F> void parallel_for(uint64_t n, F f) {
   for (auto& t : th) t.join();
 }
 
-// Parallel sort of u64 values (chunked std::sort + pairwise merges).
-void sort_u64(std::vector<uint64_t>& v) {
+// A parallel merge sort: T chunks sorted with std::sort on T threads, then
+// rounds of pairwise merges, each merge cut into pieces along its merge path
+// (co-ranks by binary search) so every round keeps all T threads busy.
+template <class V, class Cmp> void par_sort(V& v, Cmp cmp) {
+  using K = typename V::value_type;
   const size_t n = v.size();
   const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   if (n < 200000 || T == 1) {
-    std::sort(v.begin(), v.end());
+    std::sort(v.begin(), v.end(), cmp);
     return;
   }
   std::vector<size_t> b(T + 1);
   for (unsigned k = 0; k <= T; ++k) b[k] = n * k / T;
   {
     std::vector<std::thread> th;
-    for (unsigned k = 0; k < T; ++k) th.emplace_back([&, k] { std::sort(v.begin() + b[k], v.begin() + b[k + 1]); });
+    for (unsigned k = 0; k < T; ++k) th.emplace_back([&, k] { std::sort(v.begin() + b[k], v.begin() + b[k + 1], cmp); });
     for (auto& t : th) t.join();
   }
-  for (size_t width = 1; width < T; width *= 2) {
-    std::vector<std::thread> th;
-    for (size_t k = 0; k + width < T; k += 2 * width) {
-      const size_t lo = b[k], mid = b[k + width], hi = b[std::min<size_t>(k + 2 * width, T)];
-      th.emplace_back([&, lo, mid, hi] { std::inplace_merge(v.begin() + lo, v.begin() + mid, v.begin() + hi); });
+  std::vector<K, DefaultInit<K>> tmp(n);
+  K* src = v.data();
+  K* dst = tmp.data();
+  // how many of a's first elements the first d outputs of merge(a, b) take (a first on ties)
+  auto corank = [&](const K* a, size_t na, const K* bb, size_t nb, size_t d) {
+    size_t lo = d > nb ? d - nb : 0, hi = std::min(d, na);
+    while (lo < hi) {
+      const size_t i = (lo + hi) / 2, j = d - i;
+      if (j > 0 && i < na && !cmp(bb[j - 1], a[i])) lo = i + 1;
+      else hi = i;
     }
+    return lo;
+  };
+  for (size_t width = 1; width < T; width *= 2) {
+    std::vector<std::function<void()>> jobs;
+    for (size_t k = 0; k < T; k += 2 * width) {
+      const size_t lo = b[k], mid = b[std::min<size_t>(k + width, T)], hi = b[std::min<size_t>(k + 2 * width, T)];
+      const unsigned P = unsigned(std::min<size_t>(T, 2 * width));  // threads per merge
+      for (unsigned p = 0; p < P; ++p)
+        jobs.emplace_back([&, lo, mid, hi, P, p] {
+          const K* a = src + lo;
+          const K* bb = src + mid;
+          const size_t na = mid - lo, nb = hi - mid, tot = na + nb;
+          const size_t d0 = tot * p / P, d1 = tot * (p + 1) / P;
+          const size_t i0 = corank(a, na, bb, nb, d0), i1 = corank(a, na, bb, nb, d1);
+          std::merge(a + i0, a + i1, bb + (d0 - i0), bb + (d1 - i1), dst + lo + d0, cmp);
+        });
+    }
+    std::vector<std::thread> th;
+    for (size_t j = 1; j < jobs.size(); ++j) th.emplace_back(jobs[j]);
+    jobs[0]();
     for (auto& t : th) t.join();
+    std::swap(src, dst);
   }
+  if (src != v.data()) std::copy(src, src + n, v.data());
+}
+
+// Parallel sort of filter indices by bytes: (big-endian first 8 bytes, index)
+// pairs, so most comparisons are one integer compare on contiguous memory and
+// only equal prefixes compare the filters' bytes.
+void sort_filters_impl(std::vector<uint32_t>& ord, const uint8_t* fb, const uint64_t* fo) {
+  const size_t n = ord.size();
+  struct K {
+    uint64_t key;
+    uint32_t i;
+  };
+  std::vector<K, DefaultInit<K>> ks(n);
+  parallel_for(n, [&](uint64_t a, uint64_t z) {
+    for (size_t k = a; k < z; ++k) {
+      const uint32_t x = ord[k];
+      const uint64_t len = fo[x + 1] - fo[x];
+      uint64_t key = 0;
+      for (uint64_t q = 0; q < 8; ++q) key = (key << 8) | (q < len ? fb[fo[x] + q] : 0u);
+      ks[k] = K{key, x};
+    }
+  });
+  par_sort(ks, [&](const K& a, const K& b) {
+    if (a.key != b.key) return a.key < b.key;
+    return less_bytes(fb + fo[a.i], fo[a.i + 1] - fo[a.i], fb + fo[b.i], fo[b.i + 1] - fo[b.i]);
+  });
+  parallel_for(n, [&](uint64_t a, uint64_t z) {
+    for (size_t k = a; k < z; ++k) ord[k] = ks[k].i;
+  });
+}
+
+// Parallel sort of u64 values.
+void sort_u64(std::vector<uint64_t>& v) { par_sort(v, std::less<uint64_t>()); }
+
+// Host tables to a device blob without assembling it on the host: the blob
+// zeroed on the device, each region (offset, source, bytes) copied into
+// page-locked staging by all threads and sent by DMA, two buffers in turn.
+hipError_t upload_regions(emqx_gm_ctx* ctx, uint8_t* dev, size_t total,
+                          const std::pair<size_t, std::pair<const void*, size_t>>* regions, size_t n_regions,
+                          size_t o_small, const void* small, size_t small_bytes) {
+  const size_t CH = std::min<size_t>(size_t(128) << 20, (total + 4095) & ~size_t(4095));
+  hipStream_t st = ctx->stream;
+  hipError_t e = hipMemsetAsync(dev, 0, total, st);
+  void* buf[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+    e = hipHostMalloc(&buf[k], CH, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&done[k], hipEventDisableTiming);
+  }
+  int k = 0;
+  bool used[2] = {false, false};
+  auto send = [&](size_t off, const uint8_t* src, size_t bytes) {
+    for (size_t c = 0; c < bytes && e == hipSuccess; c += CH) {
+      const size_t n = std::min(CH, bytes - c);
+      if (used[k]) e = hipEventSynchronize(done[k]);  // (the buffer's previous chunk has crossed)
+      if (e != hipSuccess) break;
+      uint8_t* b = static_cast<uint8_t*>(buf[k]);
+      parallel_for(n, [&](uint64_t a, uint64_t z) { std::memcpy(b + a, src + c + a, z - a); });
+      e = hipMemcpyAsync(dev + off + c, b, n, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess) e = hipEventRecord(done[k], st);
+      used[k] = true;
+      k ^= 1;
+    }
+  };
+  for (size_t r = 0; r < n_regions; ++r)
+    if (regions[r].second.second)
+      send(regions[r].first, static_cast<const uint8_t*>(regions[r].second.first), regions[r].second.second);
+  send(o_small, static_cast<const uint8_t*>(small), small_bytes);
+  const hipError_t es = hipStreamSynchronize(st);
+  if (e == hipSuccess) e = es;
+  for (int q = 0; q < 2; ++q) {
+    if (done[q]) (void)hipEventDestroy(done[q]);
+    if (buf[q]) (void)hipHostFree(buf[q]);
+  }
+  return e;
+}
+
+// An empty EdgeMap filled with distinct keys in one sweep instead of key-by-key
+// probes (random lines): the keys sorted by home slot, each at max(its home,
+// the next free slot); the few that run past the end take the first free
+// slots from 0 (where their probe continues).  A valid linear-probing table.
+void sweep_fill(EdgeMap& m, const std::vector<std::pair<uint64_t, uint32_t>>& kv) {
+  const uint64_t cap = m.slots.size();
+  std::vector<uint64_t> hk(kv.size());
+  for (size_t j = 0; j < kv.size(); ++j) hk[j] = (edge_slot(kv[j].first, m.mask) << 32) | j;
+  sort_u64(hk);
+  std::vector<uint32_t> wrap;
+  uint64_t pos = 0;
+  for (const uint64_t x : hk) {
+    const uint64_t home = x >> 32;
+    const uint32_t j = uint32_t(x);
+    if (pos < home) pos = home;
+    if (pos >= cap) {
+      wrap.push_back(j);
+      continue;
+    }
+    m.slots[pos++] = EdgeSlot{kv[j].first, kv[j].second, 0};
+  }
+  uint64_t sl = 0;
+  for (const uint32_t j : wrap) {
+    while (m.slots[sl].key != EDGE_EMPTY) ++sl;
+    m.slots[sl] = EdgeSlot{kv[j].first, kv[j].second, 0};
+  }
+  m.used = kv.size();
 }
 
 }  // namespace
@@ -229,20 +314,58 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   auto sorted = std::make_shared<SortedFilters>();  // becomes idx->ft's base
   std::vector<uint8_t>& FBV = sorted->bytes;
   std::vector<uint64_t>& FOV = sorted->off;
-  for (uint64_t k = 0; k < n; ++k) {
-    uint32_t i = ord[k];
-    bool dup = false;
-    if (k) {
-      uint32_t p = ord[k - 1];
-      uint64_t lp = fo[p + 1] - fo[p], li = fo[i + 1] - fo[i];
-      dup = lp == li && std::memcmp(fb + fo[p], fb + fo[i], li) == 0;
+  {
+    // duplicates collapse; the unique filters packed in order.  On all threads:
+    // per range of the sorted order, its uniques and their bytes are counted,
+    // then each range writes its part at its prefix offsets
+    const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned R = n < (1u << 16) ? 1u : T;
+    auto same_as_prev = [&](uint64_t k) {
+      if (!k) return false;
+      const uint32_t p = ord[k - 1], i = ord[k];
+      const uint64_t lp = fo[p + 1] - fo[p], li = fo[i + 1] - fo[i];
+      return lp == li && std::memcmp(fb + fo[p], fb + fo[i], li) == 0;
+    };
+    std::vector<uint64_t> r_uni(R + 1, 0), r_bytes(R + 1, 0);
+    std::vector<uint8_t> dup(n);
+    auto run_ranges = [&](auto body) {
+      std::vector<std::thread> th;
+      for (unsigned r = 1; r < R; ++r) th.emplace_back([&, r] { body(r, n * r / R, n * (r + 1) / R); });
+      body(0u, uint64_t(0), n / R);
+      for (auto& t : th) t.join();
+    };
+    run_ranges([&](unsigned r, uint64_t a, uint64_t b) {
+      uint64_t u = 0, by = 0;
+      for (uint64_t k = a; k < b; ++k) {
+        dup[k] = same_as_prev(k);
+        if (!dup[k]) {
+          ++u;
+          by += fo[ord[k] + 1] - fo[ord[k]];
+        }
+      }
+      r_uni[r + 1] = u;
+      r_bytes[r + 1] = by;
+    });
+    for (unsigned r = 0; r < R; ++r) {
+      r_uni[r + 1] += r_uni[r];
+      r_bytes[r + 1] += r_bytes[r];
     }
-    if (!dup) {
-      FBV.insert(FBV.end(), fb + fo[i], fb + fo[i + 1]);
-      FOV.push_back(FBV.size());
-      ++nf;
-    }
-    id_of[i] = nf - 1;
+    nf = uint32_t(std::min<uint64_t>(r_uni[R], 0xFFFFFFFFull));
+    FBV.resize(r_bytes[R]);
+    FOV.assign(r_uni[R] + 1, 0);
+    run_ranges([&](unsigned r, uint64_t a, uint64_t b) {
+      uint64_t u = r_uni[r], by = r_bytes[r];
+      for (uint64_t k = a; k < b; ++k) {
+        const uint32_t i = ord[k];
+        if (!dup[k]) {
+          const uint64_t l = fo[i + 1] - fo[i];
+          if (l) std::memcpy(FBV.data() + by, fb + fo[i], l);
+          by += l;
+          FOV[++u] = by;
+        }
+        id_of[i] = uint32_t(u - 1);
+      }
+    });
   }
   idx->ft.set_base(sorted);  // (the same vectors: FBV / FOV stay valid)
   if (perm_out)
@@ -606,6 +729,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     });
   }
   phase("v1: buckets");
+  const bool verify_tables = getenv("GM_INDEX_VERIFY") != nullptr;
   std::vector<EdgeMap> tabs;
   tabs.reserve(EDGE_DEPTHS);
   for (int d = 0; d < EDGE_DEPTHS; ++d) tabs.emplace_back(by_tab[d].empty() ? 1 : 0);  // (sized on its thread)
@@ -615,7 +739,10 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       if (!by_tab[d].empty())
         th.emplace_back([&, d] {
           tabs[d] = EdgeMap(by_tab[d].size() + 1);
-          for (const auto& kv : by_tab[d]) tabs[d].put(kv.first, kv.second);
+          sweep_fill(tabs[d], by_tab[d]);  // (each edge once: distinct keys)
+          if (verify_tables)  // GM_INDEX_VERIFY: every edge found by the probe the kernels make
+            for (const auto& kv : by_tab[d])
+              if (tabs[d].get(kv.first) != kv.second) throw std::logic_error("edge table: an edge not found");
           std::vector<std::pair<uint64_t, uint32_t>>().swap(by_tab[d]);
         });
     for (auto& t : th) t.join();
@@ -854,26 +981,53 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       // the keys homed there.  A Robin Hood layout like inserting them one by
       // one (GM_HOT_RH_INSERT=1, the A/B twin), up to the order of keys with
       // the same home (insertion's depends on which resident got displaced).
-      std::vector<uint64_t> hk;  // (home << 32) | position in keys
-      std::vector<uint64_t> keys;
-      std::vector<uint32_t> owner;
-      for (uint32_t k = by_depth_off[d]; k < by_depth_off[d + 1]; ++k) {
-        const uint32_t i = by_depth[k];
+      // the depth's keys in node order, on all threads (per range: count, then
+      // fill at the range's offset); an inline '+' node goes into its parent's
+      // slot instead (one per parent: distinct writes)
+      const uint64_t k0 = by_depth_off[d], nk = by_depth_off[d + 1] - k0;
+      const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+      const unsigned R = nk < (1u << 16) ? 1u : T;
+      std::vector<uint64_t> r_off(R + 1, 0);
+      auto owns_slot = [&](uint32_t i) {
         const HNode& h = nodes[i];
-        if (h.kind == 2 || hid[h.parent] == NONE) continue;
-        if (inl[i]) {
-          HotSlot& p = hot[hot_off[hot_table(d - 1)] + hid[h.parent]];
-          p.p_sig = h.sig;
-          p.p_hf = hf_of(h);
-          p.p_end = end_of(h);
-          hid[i] = hid[h.parent] | HOT_INLINE;
-          continue;
+        return h.kind != 2 && hid[h.parent] != NONE && !inl[i];
+      };
+      auto ranges = [&](auto body) {
+        std::vector<std::thread> th;
+        for (unsigned r = 1; r < R; ++r) th.emplace_back([&, r] { body(r, k0 + nk * r / R, k0 + nk * (r + 1) / R); });
+        body(0u, k0, k0 + nk / R);
+        for (auto& t : th) t.join();
+      };
+      ranges([&](unsigned r, uint64_t a, uint64_t b) {
+        uint64_t c = 0;
+        for (uint64_t k = a; k < b; ++k) c += owns_slot(by_depth[k]);
+        r_off[r + 1] = c;
+      });
+      for (unsigned r = 0; r < R; ++r) r_off[r + 1] += r_off[r];
+      std::vector<uint64_t> hk(r_off[R]);  // (home << 32) | position in keys
+      std::vector<uint64_t> keys(r_off[R]);
+      std::vector<uint32_t> owner(r_off[R]);
+      ranges([&](unsigned r, uint64_t a, uint64_t b) {
+        uint64_t q = r_off[r];
+        for (uint64_t k = a; k < b; ++k) {
+          const uint32_t i = by_depth[k];
+          const HNode& h = nodes[i];
+          if (h.kind == 2 || hid[h.parent] == NONE) continue;
+          if (inl[i]) {
+            HotSlot& p = hot[hot_off[hot_table(d - 1)] + hid[h.parent]];
+            p.p_sig = h.sig;
+            p.p_hf = hf_of(h);
+            p.p_end = end_of(h);
+            hid[i] = hid[h.parent] | HOT_INLINE;
+            continue;
+          }
+          const uint64_t key = hot_key(hid[h.parent], h.word, d - 1);
+          hk[q] = (hot_slot(key, cap) << 32) | q;
+          keys[q] = key;
+          owner[q] = i;
+          ++q;
         }
-        const uint64_t key = hot_key(hid[h.parent], h.word, d - 1);
-        hk.push_back((hot_slot(key, cap) << 32) | keys.size());
-        keys.push_back(key);
-        owner.push_back(i);
-      }
+      });
       sort_u64(hk);
       uint64_t pos = 0;
       std::vector<uint32_t> wrap;  // positions in keys that ran past the end
@@ -1178,39 +1332,48 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     }
   }
   idx->dev_bytes = total;
-  // the blob assembled on the host (the mirror, when kept) and sent in one copy
-  std::vector<uint8_t> hb(total, 0);
-  auto put = [&](size_t off, const void* src, size_t bytes) {
-    if (bytes) std::memcpy(hb.data() + off, src, bytes);
-  };
-  put(o_nodes, dnodes.data(), NN * sizeof(Node));
-  put(o_dict, dict.data(), dcap * sizeof(DictSlot));
-  {
-    const uint32_t d0[4] = {NONE, 0, HF_NONE, NONE};
-    put(o_d0, d0, sizeof d0);
+  bool eager = host_mirror || o_soff <= kEagerMirrorBytes;  // (keep_mirror: the mirror's policy)
+  if (keep_mirror && !host_mirror) {
+    if (const char* pol = getenv("GM_MIRROR")) eager = !strcmp(pol, "eager");  // A/B and test knob
+    if (ctx->open_flags & EMQX_GM_OPEN_MIRROR_EAGER) eager = true;
+    if (ctx->open_flags & EMQX_GM_OPEN_MIRROR_LAZY) eager = false;
   }
-  put(o_edges, dedges.data(), dedges.size() * sizeof(EdgeSlot));
-  put(o_hot, hot.data(), hot.size() * sizeof(HotSlot));
-  put(o_arena, arena.data(), arena.size());
-  put(o_soff, soff.data(), soff.size() * 8);
-  put(o_sids, sids.data(), sids.size() * 4);
-  put(o_flen, flen.data(), flen.size() * 2);
-  put(o_gmap, idx->gmap.data(), idx->gmap.size() * 4);
-  put(o_efilt, efilt.data(), efilt.size() * 4);
-  put(o_mph, mph_word.data(), mph_word.size() * 8);
-  if (!host_mirror) e = hipMemcpy(idx->dev_base, hb.data(), total, hipMemcpyHostToDevice);
+  // the tables, region by region (offset in the blob, source, bytes)
+  const std::pair<size_t, std::pair<const void*, size_t>> regions[] = {
+      {o_nodes, {dnodes.data(), NN * sizeof(Node)}},
+      {o_dict, {dict.data(), dcap * sizeof(DictSlot)}},
+      {o_edges, {dedges.data(), dedges.size() * sizeof(EdgeSlot)}},
+      {o_hot, {hot.data(), hot.size() * sizeof(HotSlot)}},
+      {o_arena, {arena.data(), arena.size()}},
+      {o_soff, {soff.data(), soff.size() * 8}},
+      {o_sids, {sids.data(), sids.size() * 4}},
+      {o_flen, {flen.data(), flen.size() * 2}},
+      {o_gmap, {idx->gmap.data(), idx->gmap.size() * 4}},
+      {o_efilt, {efilt.data(), efilt.size() * 4}},
+      {o_mph, {mph_word.data(), mph_word.size() * 8}}};
+  const uint32_t d0_none[4] = {NONE, 0, HF_NONE, NONE};
+  std::vector<uint8_t> hb;
+  if (host_mirror || (keep_mirror && eager) || total < (size_t(1) << 20)) {
+    // the blob assembled on the host (it stays as the mirror) and sent in one copy
+    hb.assign(total, 0);
+    for (const auto& r : regions)
+      if (r.second.second) std::memcpy(hb.data() + r.first, r.second.first, r.second.second);
+    std::memcpy(hb.data() + o_d0, d0_none, sizeof d0_none);
+    if (!host_mirror) e = hipMemcpy(idx->dev_base, hb.data(), total, hipMemcpyHostToDevice);
+  } else {
+    // no host copy of the blob is kept: the device blob zeroed, then each table
+    // streamed through two page-locked buffers (all threads fill one while the
+    // other crosses PCIe) -- no 38-GB host assembly, no pageable copy (C5: 11.3 s
+    // for the assembly and the copy before)
+    e = upload_regions(ctx, static_cast<uint8_t*>(idx->dev_base), total, regions, sizeof regions / sizeof regions[0],
+                       o_d0, d0_none, sizeof d0_none);
+  }
   if (e != hipSuccess) {
     (void)hipFree(idx->dev_base);
     delete idx;
     return set_err(ctx, EMQX_GM_EDEVICE, std::string("index_build: upload: ") + hipGetErrorString(e));
   }
   if (keep_mirror) {
-    bool eager = host_mirror || o_soff <= kEagerMirrorBytes;
-    if (!host_mirror) {
-      if (const char* pol = getenv("GM_MIRROR")) eager = !strcmp(pol, "eager");  // A/B and test knob
-      if (ctx->open_flags & EMQX_GM_OPEN_MIRROR_EAGER) eager = true;
-      if (ctx->open_flags & EMQX_GM_OPEN_MIRROR_LAZY) eager = false;
-    }
     auto* m = new Mirror;
     m->blob_size = o_soff;  // the mirror stops at the subscriber CSR
     if (eager) {

@@ -209,6 +209,32 @@ def test_nif_exports_match_erlang_module():
     assert nif == stubs, (nif ^ stubs)
 
 
+@pytest.mark.timeout(300)
+def test_index_compiler_parallel_sort_and_dedup_ranks():
+    """Above 200k filters the host compiler sorts on all threads (chunk sorts,
+    then merges cut along their merge paths) and collapses duplicates per
+    thread range (gm_index.cpp par_sort / the dedup pass): every input filter's
+    id must still be its rank among the distinct filters in byte order
+    (Python's sort of the bytes), duplicates spread over the input included."""
+    import ctypes as C
+    from emqx_amd import _lib
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    n, k = 400_000, 60_000
+    fb, fo = render_codes(gen_filter_codes(3, n))
+    fb2 = np.concatenate([fb[:int(fo[n])], fb[:int(fo[k])], np.zeros(64, np.uint8)])
+    fo2 = np.concatenate([fo[:n + 1], fo[1:k + 1] + fo[n]]).astype(np.uint64)
+    m = n + k
+    perm = np.zeros(m, np.uint32)
+    info = _lib.IndexInfo()
+    rc = _lib.lib().emqx_gm_index_compile_host(C.c_void_p(fb2.ctypes.data), C.c_void_p(fo2.ctypes.data), m, None,
+                                               None, C.c_void_p(perm.ctypes.data), C.byref(info))
+    assert rc == 0
+    strs = [bytes(fb2[int(fo2[i]):int(fo2[i + 1])]) for i in range(m)]
+    rank = {f: r for r, f in enumerate(sorted(set(strs)))}
+    assert info.n_filters == len(rank)
+    assert np.array_equal(perm, np.array([rank[f] for f in strs], np.uint32))
+
+
 @pytest.mark.parametrize("mph_min", [None, "1"], ids=["default", "mph_all_tables"])
 def test_host_compiler_under_asan(mph_min):
     """The host index compiler (gm_index.cpp) and the overlay id mapping
