@@ -8,7 +8,7 @@
 
 #include <cstring>
 #include <string>
-#include <unordered_set>
+#include <thread>
 #include <vector>
 
 #include "../../include/emqx_gm_ext.h"
@@ -119,8 +119,22 @@ int emqx_gm_gen_filter_codes(uint64_t seed, uint64_t n, int wildcard_only, int16
   if (!codes && n) return EMQX_GM_EINVAL;
   try {
     Rng r{mix(seed ^ 0xF17E5ull)};
-    std::unordered_set<uint64_t> seen;
-    seen.reserve(n * 2);
+    // the filters drawn so far (a flat open-addressing set of their keys + 1:
+    // C5 draws 100M, which a node-based set made the slowest part of the bench's setup)
+    uint64_t cap = 64;
+    while (cap < 2 * n + 16) cap <<= 1;
+    std::vector<uint64_t> seen(cap, 0);
+    const uint64_t mask = cap - 1;
+    auto insert = [&](uint64_t key) {
+      const uint64_t k1 = key + 1;
+      for (uint64_t h = mix(key) & mask;; h = (h + 1) & mask) {
+        if (seen[h] == k1) return false;
+        if (!seen[h]) {
+          seen[h] = k1;
+          return true;
+        }
+      }
+    };
     uint64_t got = 0;
     while (got < n) {
       int16_t c[kLevels];
@@ -143,7 +157,7 @@ int emqx_gm_gen_filter_codes(uint64_t seed, uint64_t n, int wildcard_only, int16
       }
       uint64_t key = 0;
       for (int l = 0; l < kLevels; ++l) key = key * 1031 + uint64_t(c[l] + 3);
-      if (!seen.insert(key).second) continue;
+      if (!insert(key)) continue;
       std::memcpy(codes + got * kLevels, c, sizeof(c));
       ++got;
     }
@@ -153,23 +167,57 @@ int emqx_gm_gen_filter_codes(uint64_t seed, uint64_t n, int wildcard_only, int16
   return EMQX_GM_OK;
 }
 
+// "l<level>w<code>" words joined by '/' ('+' / '#' for the wildcards), on all
+// threads: each range of filters measured, then written at its prefix offset
 uint64_t emqx_gm_render_codes(const int16_t* codes, uint64_t n, uint8_t* bytes, uint64_t* off) {
-  uint64_t pos = 0;
-  for (uint64_t i = 0; i < n; ++i) {
-    if (off) off[i] = pos;
+  auto len_of = [&](uint64_t i) {
+    const int16_t* c = codes + i * kLevels;
+    uint64_t L = 0;
+    for (int l = 0; l < kLevels && c[l] != C_END; ++l)
+      L += (l ? 1u : 0u) + ((c[l] == C_PLUS || c[l] == C_HASH) ? 1u : 3u + ndigits(uint32_t(c[l])));
+    return L;
+  };
+  auto write = [&](uint64_t i, uint8_t* p) {
     const int16_t* c = codes + i * kLevels;
     for (int l = 0; l < kLevels && c[l] != C_END; ++l) {
-      std::string w;
-      if (l) w.push_back('/');
-      if (c[l] == C_PLUS) w += "+";
-      else if (c[l] == C_HASH) w += "#";
-      else w += "l" + std::to_string(l) + "w" + std::to_string(c[l]);
-      if (bytes) std::memcpy(bytes + pos, w.data(), w.size());
-      pos += w.size();
+      if (l) *p++ = '/';
+      if (c[l] == C_PLUS || c[l] == C_HASH) {
+        *p++ = c[l] == C_PLUS ? '+' : '#';
+        continue;
+      }
+      *p++ = 'l';
+      *p++ = uint8_t('0' + l);
+      *p++ = 'w';
+      const uint32_t v = uint32_t(c[l]), d = ndigits(v);
+      for (uint32_t k = 0, x = v; k < d; ++k, x /= 10) p[d - 1 - k] = uint8_t('0' + x % 10);
+      p += d;
     }
-  }
-  if (off) off[n] = pos;
-  return pos;
+  };
+  const unsigned T = n < (1u << 16) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<uint64_t> part(T + 1, 0);
+  auto ranges = [&](auto body) {
+    std::vector<std::thread> th;
+    for (unsigned r = 1; r < T; ++r) th.emplace_back([&, r] { body(r, n * r / T, n * (r + 1) / T); });
+    body(0u, uint64_t(0), n / T);
+    for (auto& t : th) t.join();
+  };
+  ranges([&](unsigned r, uint64_t a, uint64_t b) {
+    uint64_t L = 0;
+    for (uint64_t i = a; i < b; ++i) L += len_of(i);
+    part[r + 1] = L;
+  });
+  for (unsigned r = 0; r < T; ++r) part[r + 1] += part[r];
+  if (off || bytes)
+    ranges([&](unsigned r, uint64_t a, uint64_t b) {
+      uint64_t pos = part[r];
+      for (uint64_t i = a; i < b; ++i) {
+        if (off) off[i] = pos;
+        if (bytes) write(i, bytes + pos);
+        pos += len_of(i);
+      }
+    });
+  if (off) off[n] = part[T];
+  return part[T];
 }
 
 int emqx_gm_gen_topics(emqx_gm_ctx* ctx, const int16_t* fcodes, uint64_t nf, uint64_t seed, uint64_t start,
