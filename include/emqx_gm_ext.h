@@ -28,6 +28,9 @@ int emqx_gm_gen_topics(emqx_gm_ctx *ctx, const int16_t *filter_codes, uint64_t n
 int emqx_gm_dev_alloc(emqx_gm_ctx *ctx, uint64_t bytes, void **out);
 int emqx_gm_dev_free(emqx_gm_ctx *ctx, void *p);
 int emqx_gm_memcpy(emqx_gm_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind);
+/* Returns the context's cached device buffers to the runtime, and the device
+ * blob kept from the last released index snapshot of 256 MiB or more (reused
+ * by the next in-place update of its size; emqx_gm_close frees it too). */
 int emqx_gm_pool_trim(emqx_gm_ctx *ctx);
 
 /* Host-only self check of the index compiler (no device needed): compiles the

@@ -180,7 +180,9 @@ int emqx_gm_index_build(emqx_gm_ctx *ctx, const uint8_t *filter_bytes, const uin
  * it: RCU).  The newest snapshot of a line is patched in place on a device
  * copy of its tables: the result is a flat snapshot, a match on it costs what
  * a match on a rebuilt index costs, and the update costs O(delta) host work +
- * one device copy of the index.  A plain index keeps a host copy of its device
+ * one device pass over the index (read once, written once into the new
+ * snapshot's tables; those of the last released snapshot of the same size are
+ * reused when there are any -- emqx_gm_pool_trim frees them).  A plain index keeps a host copy of its device
  * tables for this (host RAM ~ emqx_gm_index_info().device_bytes), handed on
  * to each newer snapshot.  Otherwise -- a filter with '#' before its last
  * word, or an update of a snapshot that is no longer the newest -- the new
