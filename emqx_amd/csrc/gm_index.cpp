@@ -217,9 +217,23 @@ hipError_t upload_regions(emqx_gm_ctx* ctx, uint8_t* dev, size_t total,
   hipError_t e = hipMemsetAsync(dev, 0, total, st);
   void* buf[2] = {nullptr, nullptr};
   hipEvent_t done[2] = {nullptr, nullptr};
-  for (int k = 0; k < 2 && e == hipSuccess; ++k) {
-    e = hipHostMalloc(&buf[k], CH, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&done[k], hipEventDisableTiming);
+  bool staged = e == hipSuccess;
+  for (int k = 0; k < 2 && staged; ++k)
+    staged = hipHostMalloc(&buf[k], CH, hipHostMallocDefault) == hipSuccess &&
+             hipEventCreateWithFlags(&done[k], hipEventDisableTiming) == hipSuccess;
+  if (e == hipSuccess && !staged) {  // no page-locked memory to spare: each region from where it lies
+    (void)hipGetLastError();
+    for (size_t r = 0; r < n_regions && e == hipSuccess; ++r)
+      if (regions[r].second.second)
+        e = hipMemcpyAsync(dev + regions[r].first, regions[r].second.first, regions[r].second.second,
+                           hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(dev + o_small, small, small_bytes, hipMemcpyHostToDevice, st);
+    const hipError_t es = hipStreamSynchronize(st);
+    for (int q = 0; q < 2; ++q) {
+      if (done[q]) (void)hipEventDestroy(done[q]);
+      if (buf[q]) (void)hipHostFree(buf[q]);
+    }
+    return e == hipSuccess ? es : e;
   }
   int k = 0;
   bool used[2] = {false, false};
