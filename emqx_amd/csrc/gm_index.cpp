@@ -81,13 +81,16 @@ struct EdgeMap {
   }
 };
 
+// (a plain aggregate, so that a vector of 10^8 of them can be left unwritten
+// until the merge fills it: kNewNode is a node's starting value)
 struct HNode {
-  uint32_t plus_child = NONE, hash_child = NONE, end_filter = NONE, flags = 0;
-  uint32_t depth = 0;
-  uint32_t parent = NONE, word = NONE;  // incoming edge
-  uint32_t sig = 0;                     // exact-child word signature (HotSlot::sig)
-  uint8_t kind = 0;                     // incoming edge: 0 exact, 1 '+', 2 '#'
+  uint32_t plus_child, hash_child, end_filter, flags;
+  uint32_t depth;
+  uint32_t parent, word;  // incoming edge
+  uint32_t sig;           // exact-child word signature (HotSlot::sig)
+  uint8_t kind;           // incoming edge: 0 exact, 1 '+', 2 '#'
 };
+constexpr HNode kNewNode{NONE, NONE, NONE, 0u, 0u, NONE, NONE, 0u, 0u};
 
 bool less_bytes(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
   int c = std::memcmp(a, b, std::min(la, lb));
@@ -421,7 +424,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     total_words += 1 + std::count(FBV.begin() + a, FBV.begin() + b, uint8_t('/'));
   }
   wid.reserve(std::min<uint64_t>(total_words, 1u << 26));
-  std::vector<HNode> nodes(1);
+  std::vector<HNode, DefaultInit<HNode>> nodes(1, kNewNode);
   uint64_t n_wild = 0;
   uint32_t max_depth = 0;
   const uint8_t* FB = FBV.data();
@@ -527,7 +530,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     lw.reserve(std::min<uint64_t>(tw, 1u << 26));
     EdgeMap edges(std::min<uint64_t>(tw + 1, 1ull << 30));
     std::vector<HNode>& nd = R.nodes;
-    nd.assign(1, HNode{});
+    nd.assign(1, kNewNode);
     nd.reserve(std::min<uint64_t>(tw + 1, 1ull << 30));
     auto lintern = [&](const uint8_t* p, uint64_t len) -> uint32_t {
       std::string_view v(reinterpret_cast<const char*>(p), len);
@@ -584,7 +587,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
         if (child == NONE) {
           if (nd.size() >= REF_X) throw std::length_error("too many trie nodes (>= 2^31)");
           child = uint32_t(nd.size());
-          nd.push_back(HNode{});
+          nd.push_back(kNewNode);
           nd.back().depth = depth + 1;
           nd.back().parent = node;
           nd.back().word = id;
@@ -648,11 +651,18 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       auto g = [&](uint32_t l) { return l == NONE ? NONE : l == 0 ? 0u : b + l - 1; };
       for (size_t l = 1; l < R.nodes.size(); ++l) {
         HNode h = R.nodes[l];
-        h.parent = g(h.parent);
+        const uint32_t lp = h.parent;
+        h.parent = g(lp);
         h.word = gword[r][h.word];
         h.plus_child = g(h.plus_child);
         h.hash_child = g(h.hash_child);
         nodes[b + l - 1] = h;
+        // exact-child signatures over the final word ids (a parent is older: already
+        // written; the root's, shared by every run, are gathered apart)
+        if (h.kind == 0) {
+          if (lp) nodes[h.parent].sig |= sig_bit(h.word);
+          else R.nodes[0].sig |= sig_bit(h.word);
+        }
       }
       std::vector<HNode>(1, R.nodes[0]).swap(R.nodes);  // (only the root's stand-in is still needed)
     };
@@ -669,15 +679,13 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (size_t r = 0; r < runs.size(); ++r) {  // the root: the union of the runs' changes
     const HNode& h = runs[r].nodes[0];
     nodes[0].flags |= h.flags;
+    nodes[0].sig |= h.sig;
     if (h.plus_child != NONE) nodes[0].plus_child = base[r] + h.plus_child - 1;
     if (h.hash_child != NONE) nodes[0].hash_child = base[r] + h.hash_child - 1;
     n_wild += runs[r].n_wild;
     max_depth = std::max(max_depth, runs[r].max_depth);
   }
   std::vector<TrieRun>().swap(runs);
-  // exact-child signatures over the final word ids (a child's parent is older: one pass)
-  for (uint64_t i = 1; i < nodes.size(); ++i)
-    if (nodes[i].kind == 0) nodes[nodes[i].parent].sig |= sig_bit(nodes[i].word);
 
   phase("trie");
   // ---- 3. breadth-first renumbering (stable by creation order within a level)
