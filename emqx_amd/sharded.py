@@ -225,9 +225,15 @@ class PrefixShardedMatcher:
     match (tests: the oracle over the rank's shard)."""
 
     def __init__(self, ctx: Optional[Context], index: Optional[Index], route, world: int, rank: int, dist=None,
-                 group=None, device_tensors: bool = True, match_fn=None):
+                 group=None, device_tensors: bool = True, match_fn=None, chunks: int = 2):
+        """``chunks`` (device path, world > 1; the same on every rank): the step
+        runs as that many contiguous chunks of the batch, each chunk's outbound
+        exchange issued asynchronously before the previous chunk's walk, so the
+        all-to-all of chunk k+1 crosses xGMI while chunk k walks, and chunk k's
+        return exchange while chunk k+1 walks (1: the unchunked step)."""
         self.ctx, self.index, self.route, self.world, self.rank = ctx, index, route, world, rank
         self.dist, self.group, self.device_tensors, self.match_fn = dist, group, device_tensors, match_fn
+        self.chunks = max(1, int(chunks))
         self.last_exchange_bytes = 0
         self.last_topics_walked = 0
         # also at world 1: torch's sort / bincount read what the library's kernels write
@@ -324,6 +330,8 @@ class PrefixShardedMatcher:
     def _match_device(self, d_tb: int, d_to: int, n: int, exact: bool) -> DeviceCsr:
         import torch
         ctx, W = self.ctx, self.world
+        if W > 1 and self.chunks > 1:
+            return self._match_device_chunked(d_tb, d_to, n, exact)
         dev = torch.device("cuda", ctx.device)
         # the send order (emqx_gm_route_partition: a counting sort of the batch by
         # shard, stable in batch order) with the topics' lengths in that order and
@@ -378,3 +386,96 @@ class PrefixShardedMatcher:
                                     input_split_sizes=idsplit, group=self.group)
         self.last_exchange_bytes = tot + 4 * n + 4 * m + 4 * nnz
         return ctx.unpermute_rows(n, perm.data_ptr(), back_lens.data_ptr(), back_ids.untyped_storage().data_ptr())
+
+    def _match_device_chunked(self, d_tb: int, d_to: int, n: int, exact: bool) -> DeviceCsr:
+        """The step in self.chunks contiguous chunks of the batch (world > 1).
+        Every rank issues the same collectives in the same order: the split
+        sizes of all chunks in one exchange; then, per chunk, its topic bytes
+        and lengths (asynchronous); then per chunk, walk -> return split sizes
+        -> row lengths and ids (asynchronous).  So chunk k+1's outbound
+        all-to-all runs on the collective's stream while chunk k walks on the
+        matcher's, and chunk k's return exchange while chunk k+1 walks.  The
+        rows of all chunks are un-permuted in one pass at the end (received row
+        j of chunk c is topic start_c + perm_c[j])."""
+        import torch
+        ctx, W, K = self.ctx, self.world, self.chunks
+        dev = torch.device("cuda", ctx.device)
+        bounds = [n * c // K for c in range(K + 1)]
+        ch = []
+        sizes_all = torch.empty((K, 2 * W), dtype=torch.int64, device=dev)
+        for c in range(K):
+            s0, m = bounds[c], bounds[c + 1] - bounds[c]
+            perm = torch.empty(max(m, 1), dtype=torch.int32, device=dev)[:m]
+            plen = torch.empty(max(m, 1), dtype=torch.int32, device=dev)[:m]
+            # a chunk's topics: the offsets array from topic s0 on (offsets are absolute in d_tb)
+            if m:
+                ctx.route_partition(self.route, d_tb, d_to + 8 * s0, m, perm.data_ptr(), plen.data_ptr(),
+                                    sizes_all[c].data_ptr())
+            else:
+                sizes_all[c].zero_()
+            ch.append({"s": s0, "m": m, "perm": perm, "plen": plen})
+        send = sizes_all.view(K, W, 2).permute(1, 0, 2).contiguous().view(-1)  # [peer][chunk][count, bytes]
+        recv = self._xchg(send)
+        sz = torch.cat([send, recv]).cpu().view(2, W, K, 2).tolist()  # D2H 1: every chunk's split sizes
+        for c, C in enumerate(ch):
+            C["cs"] = [sz[0][p][c][0] for p in range(W)]
+            C["bs"] = [sz[0][p][c][1] for p in range(W)]
+            C["rc"] = [sz[1][p][c][0] for p in range(W)]
+            C["rb"] = [sz[1][p][c][1] for p in range(W)]
+        # outbound: every chunk's permute and its two exchanges, issued now (asynchronous)
+        for C in ch:
+            tot, rbt, mr = sum(C["bs"]), sum(C["rb"]), sum(C["rc"])
+            pbytes = torch.empty(tot + 64, dtype=torch.uint8, device=dev)
+            poff = torch.empty(C["m"] + 1, dtype=torch.int64, device=dev)
+            if C["m"]:
+                ctx.permute_topics(d_tb, d_to + 8 * C["s"], C["m"], C["perm"].data_ptr(), pbytes.data_ptr(),
+                                   poff.data_ptr())
+            rbytes = torch.empty(rbt + 64, dtype=torch.uint8, device=dev)
+            rbytes[rbt:].zero_()
+            rlens = torch.empty(mr, dtype=torch.int32, device=dev)
+            C["w_in"] = [self.dist.all_to_all_single(rbytes[:rbt], pbytes[:tot], output_split_sizes=C["rb"],
+                                                     input_split_sizes=C["bs"], group=self.group, async_op=True),
+                         self.dist.all_to_all_single(rlens, C["plen"], output_split_sizes=C["rc"],
+                                                     input_split_sizes=C["cs"], group=self.group, async_op=True)]
+            C.update(pbytes=pbytes, poff=poff, rbytes=rbytes, rlens=rlens, mr=mr)
+        walked = 0
+        xbytes = 0
+        for C in ch:
+            for w in C.pop("w_in"):
+                w.wait()  # (the matcher's stream waits for the chunk's inbound exchange)
+            mr = C["mr"]
+            roff = torch.zeros(mr + 1, dtype=torch.int64, device=dev)
+            roff[1:] = C["rlens"].to(torch.int64).cumsum(0)
+            res = ctx.match_device(self.index, C["rbytes"].data_ptr(), roff.data_ptr(), mr, exact)  # read-back: nnz
+            walked += mr
+            nnz = res.nnz
+            rowlen = torch.empty(max(mr, 1), dtype=torch.int32, device=dev)[:mr]
+            ctx.csr_row_lengths(res, rowlen.data_ptr())
+            ids = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
+            ctx.memcpy_d2d(ids.data_ptr(), _ptr(res.csr.ids), nnz * 4)
+            res.free()
+            rbnd = torch.tensor(np.r_[0, np.cumsum(C["rc"])].astype(np.int64), device=dev)
+            rcum = torch.zeros(mr + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(rowlen, 0, out=rcum[1:])
+            idsplit_t = rcum[rbnd[1:]] - rcum[rbnd[:-1]]
+            rbsz = self._xchg(idsplit_t)
+            b2 = torch.cat([idsplit_t, rbsz]).cpu().tolist()  # D2H: the chunk's return split sizes
+            idsplit, backsplit = b2[:W], b2[W:]
+            back_lens = torch.empty(C["m"], dtype=torch.int32, device=dev)
+            back_ids = torch.empty(max(sum(backsplit), 1), dtype=torch.int32, device=dev)
+            C["w_out"] = [self.dist.all_to_all_single(back_lens, rowlen, output_split_sizes=C["cs"],
+                                                      input_split_sizes=C["rc"], group=self.group, async_op=True),
+                          self.dist.all_to_all_single(back_ids[:sum(backsplit)], ids, output_split_sizes=backsplit,
+                                                      input_split_sizes=idsplit, group=self.group, async_op=True)]
+            C.update(rowlen=rowlen, ids=ids, back_lens=back_lens, back_ids=back_ids[:sum(backsplit)])
+            xbytes += sum(C["bs"]) + 4 * C["m"] + 4 * mr + 4 * nnz
+        for C in ch:
+            for w in C.pop("w_out"):
+                w.wait()
+        self.last_topics_walked = walked
+        self.last_exchange_bytes = xbytes
+        perm_all = torch.cat([C["perm"] + C["s"] for C in ch]).to(torch.int32)
+        lens_all = torch.cat([C["back_lens"] for C in ch])
+        ids_all = torch.cat([C["back_ids"] for C in ch] + [torch.zeros(1, dtype=torch.int32, device=dev)])
+        # (the buffers go back to torch's cache on this stream: later users queue behind the un-permute)
+        return ctx.unpermute_rows(n, perm_all.data_ptr(), lens_all.data_ptr(), ids_all.data_ptr())

@@ -14,7 +14,10 @@ Every rank's rows of its own batch must equal the unsharded index's rows, and
 rank 0's first window the oracle's.  torch's device runtime is initialised
 before the library, as in bench.py.
 
-usage: _prefix_device_worker.py WORLD N_FILTERS TOPICS_PER_RANK [libfirst]
+usage: _prefix_device_worker.py WORLD N_FILTERS TOPICS_PER_RANK [libfirst | chunks=K]
+
+chunks=K (world > 1): the matcher's step in K chunks (default 2: each chunk's
+exchange issued before the previous chunk's walk; 1: unchunked).
 
 libfirst (world 1): the library's Context is made BEFORE anything touches
 torch's device (emqx_amd.Context brings torch's runtime up first itself), and
@@ -47,7 +50,8 @@ class LockstepExchange:
         ex = self
 
         class View:
-            def all_to_all_single(self, out, inp, output_split_sizes=None, input_split_sizes=None, group=None):
+            def all_to_all_single(self, out, inp, output_split_sizes=None, input_split_sizes=None, group=None,
+                                  async_op=False):
                 W = ex.world
                 torch.cuda.current_stream().synchronize()  # this rank's send buffer is written
                 ex.slots[r] = (inp, input_split_sizes)
@@ -68,12 +72,18 @@ class LockstepExchange:
                     out.copy_(got)
                 torch.cuda.current_stream().synchronize()  # copied before a peer reuses its buffer
                 ex.barrier.wait()
+                if async_op:  # (done already: a completed work handle)
+                    class Done:
+                        def wait(self):
+                            return True
+                    return Done()
         return View()
 
 
 def main():
     W, n_f, n = (int(x) for x in sys.argv[1:4])
     libfirst = len(sys.argv) > 4 and sys.argv[4] == "libfirst"
+    chunks = int(sys.argv[4].split("=")[1]) if len(sys.argv) > 4 and sys.argv[4].startswith("chunks=") else 2
     if libfirst:
         from emqx_amd import Context
         Context(0).close()  # the library first: its Context initialises torch's runtime itself
@@ -103,7 +113,7 @@ def main():
     def rank_main(q):
         try:
             m = matchers[q] = PrefixShardedMatcher(ctxs[q], idxs[q], plans[q][4], W, q,
-                                                   dist=ex.rank(q) if W > 1 else None)
+                                                   dist=ex.rank(q) if W > 1 else None, chunks=chunks)
             db, do, _ = batches[q]
             for _ in range(2):  # twice: the second step reuses the matcher's stream and buffers
                 if results[q] is not None:
@@ -125,7 +135,9 @@ def main():
     assert sum(walked) == W * n, walked
     if W > 1:
         assert max(walked) < 2 * n, walked  # each rank walks about its share, not the whole job
-        assert ex.calls[0] == 2 * 6, ex.calls  # six collectives per step
+        K = matchers[0].chunks
+        # per step: six collectives unchunked; chunked, one for every chunk's sizes + five per chunk
+        assert ex.calls[0] == 2 * (6 if K == 1 else 1 + 5 * K), ex.calls
     full_ctx = Context(0)
     full = full_ctx.build_index((fb, fo))
     for q in range(W):
@@ -157,7 +169,8 @@ def main():
     full.release()
     full_ctx.close()
     del keep
-    print(f"PREFIX_DEVICE_PATH_OK world={W} walked={walked}{' libfirst' if libfirst else ''}", flush=True)
+    print(f"PREFIX_DEVICE_PATH_OK world={W} walked={walked} chunks={chunks}{' libfirst' if libfirst else ''}",
+          flush=True)
 
 
 if __name__ == "__main__":

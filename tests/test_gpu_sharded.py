@@ -455,11 +455,14 @@ def test_graft_smoke_in_a_fresh_process():
 
 
 @pytest.mark.timeout(600)
-def test_prefix_device_path_world8_lockstep():
+@pytest.mark.parametrize("chunks", [2, 1], ids=["chunked", "unchunked"])
+def test_prefix_device_path_world8_lockstep(chunks):
     """The 4M-filter set in 8 prefix shards, 8 ranks as threads on one device,
-    each with its own context, stream and 500k-topic batch; the six
-    all_to_all_single calls of a step run in lock step across the ranks.  Every
+    each with its own context, stream and 500k-topic batch; the
+    all_to_all_single calls of a step run in lock step across the ranks (six
+    unchunked; chunked -- the default, each chunk's exchange issued before the
+    previous chunk's walk -- one for the sizes plus five per chunk).  Every
     rank's rows == the unsharded index on its batch; rank 0's window == the
     oracle; no rank walks twice its share."""
-    out = _run_worker("_prefix_device_worker.py", 8, 4_000_000, 500_000)
-    assert "PREFIX_DEVICE_PATH_OK world=8" in out
+    out = _run_worker("_prefix_device_worker.py", 8, 4_000_000, 500_000, f"chunks={chunks}")
+    assert "PREFIX_DEVICE_PATH_OK world=8" in out and f"chunks={chunks}" in out
