@@ -28,6 +28,8 @@
 #include <memory>
 #include <string>
 
+#include <thread>
+
 #include "gm_internal.h"
 
 namespace gm {
@@ -436,18 +438,71 @@ int index_import(emqx_gm_ctx* ctx, const uint8_t* img, uint64_t size, const void
 // kEagerMirrorBytes, EMQX_GM_OPEN_MIRROR_LAZY, imported snapshots).  The device
 // tables ARE the current state (filter-id fields included), so one download
 // up to the subscriber CSR gives exactly what an eager mirror would hold.
+// dev[0, bytes) to host memory nothing has touched yet, through two page-locked
+// buffers: one chunk crosses PCIe while all threads copy the previous one out
+// (so the destination's pages are first touched in parallel too).  The C5
+// mirror (38 GB): one pass instead of a serial zero-fill, a page-pinning of the
+// whole destination and the copy (7.7 s for the first update, round 5).
+hipError_t download_blob(uint8_t* host, const uint8_t* dev, size_t bytes) {
+  if (!bytes) return hipSuccess;
+  const size_t CH = std::min<size_t>(size_t(128) << 20, (bytes + 4095) & ~size_t(4095));
+  hipStream_t st = nullptr;
+  void* buf[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  bool staged = e == hipSuccess;
+  for (int k = 0; k < 2 && staged; ++k)
+    staged = hipHostMalloc(&buf[k], CH, hipHostMallocDefault) == hipSuccess &&
+             hipEventCreateWithFlags(&done[k], hipEventDisableTiming) == hipSuccess;
+  auto copy_out = [&](uint8_t* dst, const uint8_t* src, size_t n) {
+    const unsigned T = n < (size_t(1) << 22) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (unsigned r = 1; r < T; ++r)
+      th.emplace_back([=] { std::memcpy(dst + n * r / T, src + n * r / T, n * (r + 1) / T - n * r / T); });
+    std::memcpy(dst, src, n / T);
+    for (auto& t : th) t.join();
+  };
+  if (e == hipSuccess && staged) {
+    const size_t nch = (bytes + CH - 1) / CH;
+    auto issue = [&](size_t c) {  // chunk c into buffer c & 1
+      const size_t n = std::min(CH, bytes - c * CH);
+      hipError_t r = hipMemcpyAsync(buf[c & 1], dev + c * CH, n, hipMemcpyDeviceToHost, st);
+      if (r == hipSuccess) r = hipEventRecord(done[c & 1], st);
+      return r;
+    };
+    e = issue(0);
+    for (size_t c = 0; c < nch && e == hipSuccess; ++c) {
+      if (c + 1 < nch) e = issue(c + 1);  // (the next chunk crosses while this one is copied out)
+      if (e == hipSuccess) e = hipEventSynchronize(done[c & 1]);
+      if (e != hipSuccess) break;
+      copy_out(host + c * CH, static_cast<const uint8_t*>(buf[c & 1]), std::min(CH, bytes - c * CH));
+      // (buffer c & 1 is free again: chunk c + 2 is issued next round, after this copy)
+    }
+  } else if (e == hipSuccess) {  // no page-locked memory to spare: one pageable copy
+    (void)hipGetLastError();
+    e = hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost);
+  }
+  if (st) {
+    const hipError_t es = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = es;
+    (void)hipStreamDestroy(st);
+  }
+  for (int k = 0; k < 2; ++k) {
+    if (done[k]) (void)hipEventDestroy(done[k]);
+    if (buf[k]) (void)hipHostFree(buf[k]);
+  }
+  return e;
+}
+
 int load_mirror_blob(emqx_gm_ctx* ctx, emqx_gm_index* idx) {
   Mirror& M = *idx->mirror;
   if (!M.blob.empty() || !idx->dev_base) return EMQX_GM_OK;
-  M.blob.resize(M.blob_size);
   hipSetDevice(idx->device);
   if (ctx) GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  // pinned for the copy (several times the pageable rate), when the host allows it
-  const bool reg = hipHostRegister(M.blob.data(), M.blob_size, hipHostRegisterDefault) == hipSuccess;
-  const hipError_t e = hipMemcpy(M.blob.data(), idx->dev_base, M.blob_size, hipMemcpyDeviceToHost);
-  if (reg) (void)hipHostUnregister(M.blob.data());
+  M.blob.resize(M.blob_size);  // (left unwritten: the download below fills every byte)
+  const hipError_t e = download_blob(M.blob.data(), static_cast<const uint8_t*>(idx->dev_base), M.blob_size);
   if (e != hipSuccess) {
-    std::vector<uint8_t>().swap(M.blob);
+    HostBytes().swap(M.blob);
     return set_err(ctx, EMQX_GM_EDEVICE, std::string("index_update: mirror download: ") + hipGetErrorString(e));
   }
   return EMQX_GM_OK;

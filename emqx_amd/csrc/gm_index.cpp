@@ -98,18 +98,6 @@ bool less_bytes(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
   return la < lb;
 }
 
-// An allocator that default-initialises (a vector of PODs left unwritten until
-// parallel_for fills it).
-template <class T> struct DefaultInit : std::allocator<T> {
-  template <class U> struct rebind {
-    using other = DefaultInit<U>;
-  };
-  DefaultInit() = default;
-  template <class U> DefaultInit(const DefaultInit<U>&) {}
-  template <class U> void construct(U* p) { ::new (static_cast<void*>(p)) U; }
-  template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
-};
-
 // f(begin, end) over [0, n) in one contiguous range per thread (small n: one call).
 template <class F> void parallel_for(uint64_t n, F f) {
   const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -1374,7 +1362,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       {o_efilt, {efilt.data(), efilt.size() * 4}},
       {o_mph, {mph_word.data(), mph_word.size() * 8}}};
   const uint32_t d0_none[4] = {NONE, 0, HF_NONE, NONE};
-  std::vector<uint8_t> hb;
+  HostBytes hb;
   if (host_mirror || (keep_mirror && eager) || total < (size_t(1) << 20)) {
     // the blob assembled on the host (it stays as the mirror) and sent in one copy
     hb.assign(total, 0);
@@ -1424,7 +1412,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   }
   // the view's base: the device blob, or (host-only index) the mirror
   uint8_t* B = host_mirror ? idx->mirror->blob.data() : static_cast<uint8_t*>(idx->dev_base);
-  std::vector<uint8_t>().swap(hb);  // (a lazy mirror: no host copy of the tables stays)
+  HostBytes().swap(hb);  // (a lazy mirror: no host copy of the tables stays)
 
   phase("upload");
   IndexView& v = idx->view;

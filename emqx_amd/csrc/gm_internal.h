@@ -18,6 +18,20 @@
 
 namespace gm {
 
+// An allocator that default-initialises: a vector of PODs is left unwritten
+// by resize() until its owner fills it (GBs of index tables filled by all
+// threads, or by a copy, instead of first zeroed by one).
+template <class T> struct DefaultInit : std::allocator<T> {
+  template <class U> struct rebind {
+    using other = DefaultInit<U>;
+  };
+  DefaultInit() = default;
+  template <class U> DefaultInit(const DefaultInit<U>&) {}
+  template <class U> void construct(U* p) { ::new (static_cast<void*>(p)) U; }
+  template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+using HostBytes = std::vector<uint8_t, DefaultInit<uint8_t>>;
+
 // Caching device allocator: buffers are returned to a size-keyed free list and
 // reused, so steady-state batches do no hipMalloc/hipFree.
 class DevPool {
@@ -208,7 +222,7 @@ struct IdShift {
 // an update moves it from the old snapshot (which stays valid for its readers)
 // to the new one.
 struct Mirror {
-  std::vector<uint8_t> blob;             // empty until the first update when built lazily (load_mirror_blob)
+  HostBytes blob;                        // empty until the first update when built lazily (load_mirror_blob)
   size_t blob_size = 0;                  // bytes of the blob: the device tables up to the subscriber CSR
   size_t o_nodes = 0, o_dict = 0, o_edges = 0, o_hot = 0, o_arena = 0, o_flen = 0, o_efilt = 0, o_mph = 0;
   uint64_t nodes_n = 0, nodes_cap = 0;   // v1 level-trie nodes used / capacity
