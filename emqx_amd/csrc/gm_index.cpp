@@ -433,31 +433,30 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     return off;
   };
 
-  // The trie is built in parallel over runs of filters: filters are in byte
-  // order, and runs cut where no first word continues across the cut
-  // (safe_cut) share no node but the root.  Each run
-  // builds a local trie (local node and word numbers, its own edge map); the
-  // runs are then merged IN FILTER ORDER -- nodes concatenated, words interned
-  // in each run's first-occurrence order -- which is exactly the serial
-  // build's creation order and word order (the BFS renumbering, the arena
-  // and every table below come out the same).
+  // The trie is built in parallel over runs of filters, cut at filters
+  // where the walk may start from a path of nodes the earlier runs made (the
+  // k words the cut's two neighbours share: the run's seed) and every deeper
+  // node of the run is new (safe_cut).  Each run builds a local trie (local
+  // node and word numbers, its own edge map) with the root and its seed as
+  // stand-ins; the runs are then merged IN FILTER ORDER -- new nodes
+  // concatenated, words interned in each run's first-occurrence order, each
+  // stand-in's changes folded into the node it stands for -- which is exactly
+  // the serial build's creation order and word order (the BFS renumbering,
+  // the arena and every table below come out the same).
   struct TrieRun {
-    uint32_t f0 = 0, f1 = 0;                 // filters [f0, f1)
-    std::vector<HNode> nodes;                // [0]: the root's stand-in (its changes merged below)
-    std::vector<std::string_view> words;     // distinct words, first occurrence first
+    uint32_t f0 = 0, f1 = 0;              // filters [f0, f1)
+    uint32_t k = 0;                       // seed depth: nodes[1..k] stand for the path of f0's first k words
+    std::vector<uint64_t> seed_end;       // end byte of each seed word (in f0 and f0 - 1 alike)
+    std::vector<HNode> nodes;             // [0]: the root's stand-in, [1..k]: the seed's
+    std::vector<std::string_view> words;  // distinct words, first occurrence first
+    std::vector<uint32_t> last_path;      // local nodes of the last filter's words
     uint64_t n_wild = 0;
     uint32_t max_depth = 0;
-  };
-  auto first_word = [&](uint32_t f) {
-    const uint8_t* p = FB + FOV[f];
-    const uint64_t len = FOV[f + 1] - FOV[f];
-    const void* q = std::memchr(p, '/', len);
-    return std::string_view(reinterpret_cast<const char*>(p), q ? uint64_t(static_cast<const uint8_t*>(q) - p) : len);
   };
   auto filt = [&](uint32_t f) {
     return std::string_view(reinterpret_cast<const char*>(FB + FOV[f]), FOV[f + 1] - FOV[f]);
   };
-  auto lower = [&](std::string_view key) {  // the first filter >= key (byte order)
+  auto lower_filter = [&](std::string_view key) {  // the first filter >= key (byte order)
     uint32_t lo = 0, hi = nf;
     while (lo < hi) {
       const uint32_t mid = lo + (hi - lo) / 2;
@@ -470,26 +469,48 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     }
     return lo;
   };
-  // Whether filters [0, e) and [e, nf) share no first word.  The filters with
-  // first word W are "W" itself and a contiguous block "W/...", but between
-  // the two may lie filters "W" + c... with c < '/' (e.g. "a", "a-b", "a/c"):
-  // so besides the two neighbours' first words, a single-word filter W before
-  // the cut whose block starts after it must not exist -- and such a W is a
-  // byte prefix of the filter just before the cut (every filter between "W"
-  // and "W/" starts with W).
-  auto safe_cut = [&](uint32_t e) {
-    const std::string_view a = first_word(e - 1);
-    if (a == first_word(e)) return false;
-    std::string key;
-    for (size_t L = 0; L <= a.size(); ++L) {
-      key.assign(a.data(), L);
-      const uint32_t x = lower(key);
-      if (!(x < e && filt(x) == key)) continue;  // "W" is no filter before the cut
-      key.push_back('/');
-      const uint32_t b = lower(key);
-      if (b >= e && b < nf && filt(b).substr(0, key.size()) == key) return false;
+  auto exists = [&](std::string_view key) {
+    const uint32_t x = lower_filter(key);
+    return x < nf && filt(x) == key;
+  };
+  // the end bytes of the words filter b shares with filter a (the walk's own rule below)
+  auto shared_ends = [&](uint32_t a, uint32_t b) {
+    const std::string_view pa = filt(a), pb = filt(b);
+    const uint64_t m = std::min(pa.size(), pb.size());
+    uint64_t cp = 0;
+    while (cp < m && pa[cp] == pb[cp]) ++cp;
+    std::vector<uint64_t> ends;
+    for (uint64_t i = 0; i <= pb.size(); ++i) {
+      if (i < pb.size() && pb[i] != '/') continue;
+      const bool sh = i < cp || (i == cp && (cp == pb.size() || (cp == pa.size() && cp < pb.size() && pb[cp] == '/')));
+      if (!sh) break;
+      ends.push_back(i);
     }
-    return true;
+    return ends;
+  };
+  // A cut before filter e is safe when every node the filters from e on make
+  // -- beyond the k words e shares with e - 1, the seed -- is new.  The
+  // filters whose words start with a path P are "P" itself and the contiguous
+  // block "P/...", and between the two only filters "P" + c... (c < '/') can
+  // lie.  So P's node is made on both sides of the cut only when the filter
+  // "P" lies before it and P's block at or after it; then every filter in
+  // between starts with P's bytes, e - 1 included.  Safe: no byte prefix P of
+  // e - 1 is a filter whose block reaches past the cut, unless P is one of the
+  // seed's paths (a word prefix of e of at most k words).  Returns k, or -1.
+  auto safe_cut = [&](uint32_t e, std::vector<uint64_t>& seed) -> int {
+    seed = shared_ends(e - 1, e);
+    const std::string_view pa = filt(e - 1);
+    std::string key;
+    for (uint64_t L = 0; L <= pa.size(); ++L) {
+      const std::string_view P = pa.substr(0, L);
+      if (!exists(P)) continue;
+      if (std::find(seed.begin(), seed.end(), L) != seed.end()) continue;  // a seed node: shared, not made twice
+      key.assign(P.data(), P.size());
+      key.push_back('/');
+      const uint32_t b = lower_filter(key);
+      if (b >= e && b < nf && filt(b).substr(0, key.size()) == key) return -1;
+    }
+    return int(seed.size());
   };
   const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   std::vector<TrieRun> runs;
@@ -499,15 +520,22 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     const uint32_t want = rk ? std::max(1u, uint32_t(strtoul(rk, nullptr, 10)))
                              : (nf < 200000 || T == 1) ? 1u : 4u * T;
     uint32_t f0 = 0;
-    for (uint32_t k = 1; k <= want && f0 < nf; ++k) {
-      uint32_t e = k == want ? nf : uint32_t(uint64_t(nf) * k / want);
+    std::vector<uint64_t> seed, next_seed;
+    int k0 = 0;
+    for (uint32_t q = 1; q <= want && f0 < nf; ++q) {
+      uint32_t e = q == want ? nf : uint32_t(uint64_t(nf) * q / want);
       if (e <= f0) continue;
-      while (e < nf && !safe_cut(e)) ++e;
+      int k = -1;
+      while (e < nf && (k = safe_cut(e, next_seed)) < 0) ++e;
       TrieRun r;
       r.f0 = f0;
       r.f1 = e;
+      r.k = uint32_t(k0);
+      r.seed_end = seed;
       runs.push_back(std::move(r));
       f0 = e;
+      k0 = k < 0 ? 0 : k;
+      seed.swap(next_seed);
     }
   }
   // one run: the serial walk below, on local numbers
@@ -518,8 +546,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     lw.reserve(std::min<uint64_t>(tw, 1u << 26));
     EdgeMap edges(std::min<uint64_t>(tw + 1, 1ull << 30));
     std::vector<HNode>& nd = R.nodes;
-    nd.assign(1, kNewNode);
-    nd.reserve(std::min<uint64_t>(tw + 1, 1ull << 30));
+    nd.assign(1 + R.k, kNewNode);
+    nd.reserve(std::min<uint64_t>(tw + 1 + R.k, 1ull << 30));
     auto lintern = [&](const uint8_t* p, uint64_t len) -> uint32_t {
       std::string_view v(reinterpret_cast<const char*>(p), len);
       auto it = lw.find(v);
@@ -533,12 +561,30 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     // with the previous one: those words' nodes are taken from the previous
     // filter's path (no interning, no edge lookup).  Word j of the previous
     // filter (ending at byte e) is shared when the two agree on every byte up
-    // to e and the word ends at e in both.
+    // to e and the word ends at e in both.  A run starts from its seed: the
+    // previous filter (the last of the run before) and the stand-ins of the
+    // words the two share.
     std::vector<uint32_t> pnode;  // node after word j of the previous filter
     std::vector<uint64_t> pend;   // end byte of word j
     std::vector<uint8_t> pwild;   // a wildcard word among words 0..j
     const uint8_t* ps = nullptr;
     uint64_t plen = 0;
+    if (R.k) {
+      ps = FB + FOV[R.f0 - 1];
+      plen = FOV[R.f0] - FOV[R.f0 - 1];
+      bool wild = false;
+      for (uint32_t d = 0; d < R.k; ++d) {
+        const uint64_t ws = d ? R.seed_end[d - 1] + 1 : 0, wl = R.seed_end[d] - ws;
+        const bool plus = wl == 1 && ps[ws] == '+', hash = wl == 1 && ps[ws] == '#';
+        wild |= plus || hash;
+        nd[d + 1].depth = d + 1;
+        nd[d + 1].parent = d;
+        nd[d + 1].kind = plus ? 1 : hash ? 2 : 0;
+        pnode.push_back(d + 1);
+        pend.push_back(R.seed_end[d]);
+        pwild.push_back(wild);
+      }
+    }
     for (uint32_t f = R.f0; f < R.f1; ++f) {
       const uint8_t* s = FB + FOV[f];
       uint64_t len = FOV[f + 1] - FOV[f];
@@ -596,6 +642,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       if (wild) { nd[node].flags |= NF_END_WILD; ++R.n_wild; }
       R.max_depth = std::max(R.max_depth, depth);
     }
+    R.last_path = pnode;
   };
   {
     std::atomic<size_t> next{0};
@@ -617,61 +664,80 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     for (auto& e : errs)
       if (e) std::rethrow_exception(e);
   }
-  // merge in filter order: words first (the serial first-occurrence order), then nodes
-  std::vector<uint32_t> base(runs.size());
+  // merge in filter order: words first (the serial first-occurrence order), then
+  // the runs' new nodes; a run's seed stand-ins are the nodes of the previous
+  // run's last filter's first k words
+  const size_t NR = runs.size();
+  std::vector<uint32_t> base(NR);
+  std::vector<std::vector<uint32_t>> seedg(NR), lastg(NR);
   uint64_t n_all = 1;
-  for (size_t r = 0; r < runs.size(); ++r) {
+  for (size_t r = 0; r < NR; ++r) {
+    TrieRun& R = runs[r];
     base[r] = uint32_t(std::min<uint64_t>(n_all, NONE));
-    n_all += runs[r].nodes.size() - 1;
+    n_all += R.nodes.size() - 1 - R.k;
+    if (n_all > REF_X) throw std::length_error("too many trie nodes (>= 2^31)");
+    if (R.k && (!r || lastg[r - 1].size() < R.k)) throw std::logic_error("trie run: seed outside the previous run");
+    seedg[r].assign(R.k ? lastg[r - 1].begin() : lastg[0].begin(), R.k ? lastg[r - 1].begin() + R.k : lastg[0].begin());
+    lastg[r].reserve(R.last_path.size());
+    for (const uint32_t l : R.last_path)
+      lastg[r].push_back(l == 0 ? 0u : l <= R.k ? seedg[r][l - 1] : base[r] + (l - 1 - R.k));
   }
-  if (n_all > REF_X) throw std::length_error("too many trie nodes (>= 2^31)");
-  std::vector<std::vector<uint32_t>> gword(runs.size());
-  for (size_t r = 0; r < runs.size(); ++r) {
+  std::vector<std::vector<uint32_t>> gword(NR);
+  for (size_t r = 0; r < NR; ++r) {
     gword[r].reserve(runs[r].words.size());
     for (std::string_view v : runs[r].words) gword[r].push_back(intern(reinterpret_cast<const uint8_t*>(v.data()), v.size()));
     std::vector<std::string_view>().swap(runs[r].words);
   }
   nodes.resize(n_all);
+  auto gmap = [&](size_t r, uint32_t l) {
+    const TrieRun& R = runs[r];
+    return l == NONE ? NONE : l == 0 ? 0u : l <= R.k ? seedg[r][l - 1] : base[r] + (l - 1 - R.k);
+  };
   {
     auto merge_run = [&](size_t r) {
       TrieRun& R = runs[r];
-      const uint32_t b = base[r];
-      auto g = [&](uint32_t l) { return l == NONE ? NONE : l == 0 ? 0u : b + l - 1; };
-      for (size_t l = 1; l < R.nodes.size(); ++l) {
+      const uint32_t b = base[r], K = R.k;
+      for (size_t l = K + 1; l < R.nodes.size(); ++l) {
         HNode h = R.nodes[l];
         const uint32_t lp = h.parent;
-        h.parent = g(lp);
+        h.parent = gmap(r, lp);
         h.word = gword[r][h.word];
-        h.plus_child = g(h.plus_child);
-        h.hash_child = g(h.hash_child);
-        nodes[b + l - 1] = h;
-        // exact-child signatures over the final word ids (a parent is older: already
-        // written; the root's, shared by every run, are gathered apart)
+        h.plus_child = gmap(r, h.plus_child);
+        h.hash_child = gmap(r, h.hash_child);
+        nodes[b + (l - 1 - K)] = h;
+        // exact-child signatures over the final word ids (a new parent is older:
+        // already written; a stand-in's, which other runs share, gathered apart)
         if (h.kind == 0) {
-          if (lp) nodes[h.parent].sig |= sig_bit(h.word);
-          else R.nodes[0].sig |= sig_bit(h.word);
+          if (lp > K) nodes[h.parent].sig |= sig_bit(h.word);
+          else R.nodes[lp].sig |= sig_bit(h.word);
         }
       }
-      std::vector<HNode>(1, R.nodes[0]).swap(R.nodes);  // (only the root's stand-in is still needed)
+      R.nodes.resize(K + 1);  // (only the stand-ins are still needed)
+      R.nodes.shrink_to_fit();
     };
     std::atomic<size_t> next{0};
     auto worker = [&] {
-      for (size_t r; (r = next.fetch_add(1)) < runs.size();) merge_run(r);
+      for (size_t r; (r = next.fetch_add(1)) < NR;) merge_run(r);
     };
-    const unsigned nt = unsigned(std::min<size_t>(T, runs.size()));
+    const unsigned nt = unsigned(std::min<size_t>(T, NR));
     std::vector<std::thread> th;
     for (unsigned k = 1; k < nt; ++k) th.emplace_back(worker);
     worker();
     for (auto& t : th) t.join();
   }
-  for (size_t r = 0; r < runs.size(); ++r) {  // the root: the union of the runs' changes
-    const HNode& h = runs[r].nodes[0];
-    nodes[0].flags |= h.flags;
-    nodes[0].sig |= h.sig;
-    if (h.plus_child != NONE) nodes[0].plus_child = base[r] + h.plus_child - 1;
-    if (h.hash_child != NONE) nodes[0].hash_child = base[r] + h.hash_child - 1;
-    n_wild += runs[r].n_wild;
-    max_depth = std::max(max_depth, runs[r].max_depth);
+  for (size_t r = 0; r < NR; ++r) {  // the root and the seeds: the union of the runs' changes
+    const TrieRun& R = runs[r];
+    for (uint32_t l = 0; l <= R.k; ++l) {
+      const HNode& h = R.nodes[l];
+      HNode& g = nodes[gmap(r, l)];
+      g.flags |= h.flags;
+      g.sig |= h.sig;
+      if (h.plus_child != NONE) g.plus_child = gmap(r, h.plus_child);
+      if (h.hash_child != NONE) g.hash_child = gmap(r, h.hash_child);
+      if (h.end_filter != NONE) g.end_filter = h.end_filter;
+    }
+    n_wild += R.n_wild;
+    max_depth = std::max(max_depth, R.max_depth);
   }
   std::vector<TrieRun>().swap(runs);
 
@@ -745,6 +811,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   for (int d = 0; d < EDGE_DEPTHS; ++d) tabs.emplace_back(by_tab[d].empty() ? 1 : 0);  // (sized on its thread)
   {
     std::vector<std::thread> th;
+    std::atomic<bool> lost{false};
     for (int d = 0; d < EDGE_DEPTHS; ++d)
       if (!by_tab[d].empty())
         th.emplace_back([&, d] {
@@ -752,10 +819,11 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
           sweep_fill(tabs[d], by_tab[d]);  // (each edge once: distinct keys)
           if (verify_tables)  // GM_INDEX_VERIFY: every edge found by the probe the kernels make
             for (const auto& kv : by_tab[d])
-              if (tabs[d].get(kv.first) != kv.second) throw std::logic_error("edge table: an edge not found");
+              if (tabs[d].get(kv.first) != kv.second) lost = true;
           std::vector<std::pair<uint64_t, uint32_t>>().swap(by_tab[d]);
         });
     for (auto& t : th) t.join();
+    if (lost) throw std::logic_error("edge table: an edge not found");
   }
   phase("v1: edge maps");
   uint64_t etab_off[EDGE_DEPTHS], etab_mask[EDGE_DEPTHS], n_edges = 0, n_eslots = 0;
