@@ -235,6 +235,45 @@ def test_index_compiler_parallel_sort_and_dedup_ranks():
     assert np.array_equal(perm, np.array([rank[f] for f in strs], np.uint32))
 
 
+@pytest.mark.timeout(300)
+def test_index_compiler_trie_runs_under_one_root_word(monkeypatch):
+    """A set under one root word ("devices/...", one deployment's topic tree)
+    above the parallel threshold: the trie is cut into runs below the root
+    (gm_index.cpp safe_cut: a run starts from the path it shares with the one
+    before) and merged in filter order -- the same ids and the same node,
+    edge, word and byte counts as the one-run build (GM_TRIE_RUNS=1); the
+    tables themselves are compared byte for byte in the ASan harness."""
+    import ctypes as C
+    from emqx_amd import _lib
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    n = 250_000
+    fb, fo = render_codes(gen_filter_codes(5, n))
+    strs = [b"devices/" + bytes(fb[int(fo[i]):int(fo[i + 1])]) for i in range(n)]
+    strs += [b"devices", b"devices-x/a", b"devices/l0w1"]  # the root word as a filter, an interloper, a prefix
+    fb2 = np.frombuffer(b"".join(strs) + bytes(64), np.uint8)
+    fo2 = np.zeros(len(strs) + 1, np.uint64)
+    fo2[1:] = np.cumsum([len(x) for x in strs])
+
+    def compile_(runs):
+        if runs:
+            monkeypatch.setenv("GM_TRIE_RUNS", runs)
+        else:
+            monkeypatch.delenv("GM_TRIE_RUNS", raising=False)
+        perm = np.zeros(len(strs), np.uint32)
+        info = _lib.IndexInfo()
+        rc = _lib.lib().emqx_gm_index_compile_host(C.c_void_p(fb2.ctypes.data), C.c_void_p(fo2.ctypes.data),
+                                                   len(strs), None, None, C.c_void_p(perm.ctypes.data),
+                                                   C.byref(info))
+        assert rc == 0
+        return perm, (info.n_filters, info.n_wildcard, info.n_nodes, info.n_edges, info.n_words, info.device_bytes,
+                      info.max_depth)
+
+    p1, i1 = compile_("1")
+    for runs in (None, "97"):
+        p2, i2 = compile_(runs)
+        assert np.array_equal(p1, p2) and i1 == i2, (runs, i1, i2)
+
+
 @pytest.mark.parametrize("mph_min", [None, "1"], ids=["default", "mph_all_tables"])
 def test_host_compiler_under_asan(mph_min):
     """The host index compiler (gm_index.cpp) and the overlay id mapping
