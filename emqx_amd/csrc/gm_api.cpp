@@ -253,6 +253,7 @@ static int open_one(int dev, uint32_t flags, emqx_gm_ctx** out) {
     return EMQX_GM_EDEVICE;
   }
   ctx->own_stream = true;
+  gm::note_ctx_open(dev);
   ctx->pool = new gm::DevPool(dev);
   ctx->hpool = new gm::HostPool;
   for (auto& e : ctx->ev) {
@@ -352,6 +353,7 @@ int emqx_gm_close(emqx_gm_ctx* ctx) {
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    gm::note_ctx_close(ctx->device);
     gm::trim_spare_blob(ctx->device);
     gm::free_host_pipe(ctx);
     delete ctx->pool;

@@ -1567,6 +1567,7 @@ struct SpareBlob {
 constexpr int kSpareDevices = 64;
 std::mutex g_spare_mu;
 SpareBlob g_spare[kSpareDevices];
+int g_ctx_open[kSpareDevices] = {};  // (under g_spare_mu)
 // blobs below this size allocate quickly anyway (GM_SPARE_BLOB_MIN, bytes; 0: off)
 size_t spare_min() {
   const char* e = getenv("GM_SPARE_BLOB_MIN");
@@ -1589,7 +1590,12 @@ void give_spare_blob(int device, void* p, size_t bytes) {
   if (!p) return;
   const size_t lo = spare_min();
   void* drop = p;
-  if (device >= 0 && device < kSpareDevices && lo && bytes >= lo) {
+  bool keep = device >= 0 && device < kSpareDevices && lo && bytes >= lo;
+  if (keep) {
+    std::lock_guard<std::mutex> lk(g_spare_mu);
+    keep = g_ctx_open[device] > 0;  // (no context left on the device: nothing would reuse or trim it)
+  }
+  if (keep) {
     // hipFree waits for the device's work; so does keeping the blob for reuse
     (void)hipDeviceSynchronize();
     std::lock_guard<std::mutex> lk(g_spare_mu);
@@ -1597,6 +1603,18 @@ void give_spare_blob(int device, void* p, size_t bytes) {
     g_spare[device].bytes = bytes;
   }
   if (drop) (void)hipFree(drop);
+}
+
+void note_ctx_open(int device) {
+  if (device < 0 || device >= kSpareDevices) return;
+  std::lock_guard<std::mutex> lk(g_spare_mu);
+  ++g_ctx_open[device];
+}
+
+void note_ctx_close(int device) {
+  if (device < 0 || device >= kSpareDevices) return;
+  std::lock_guard<std::mutex> lk(g_spare_mu);
+  if (g_ctx_open[device] > 0) --g_ctx_open[device];
 }
 
 void trim_spare_blob(int device) {

@@ -280,6 +280,10 @@ void free_index(emqx_gm_index* idx);
 void* take_spare_blob(int device, size_t bytes);
 void give_spare_blob(int device, void* p, size_t bytes);
 void trim_spare_blob(int device);
+// open contexts per device (emqx_gm_open / _close): a blob freed while none is
+// open on its device is not kept (nothing would trim it)
+void note_ctx_open(int device);
+void note_ctx_close(int device);
 // gm_match.hip
 // A caller's work queued on the context stream right behind the speculative
 // assembly of a DEVICE_IO match, before run_match's one host round trip (the

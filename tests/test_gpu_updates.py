@@ -155,6 +155,38 @@ def test_fused_update_equals_copy_patch_renumber(ctx, monkeypatch):
     assert np.array_equal(a[1][0], b[1][0]) and np.array_equal(a[1][1], b[1][1])
 
 
+def test_spare_blob_reuse_and_release_after_close(orc, monkeypatch):
+    """A released snapshot's device blob is kept for the next in-place update
+    of its size (gm_index.cpp take/give_spare_blob; GM_SPARE_BLOB_MIN=1: every
+    blob, not only those of 256 MiB or more): a chain of updates reuses them
+    with rows equal to the oracle after each; snapshots released after their
+    context closed free their blobs (no context is left to trim them), and a
+    new context then updates normally."""
+    from emqx_amd import Context
+    from tests.test_gpu_parity import _rand_filter, _rand_topic
+    monkeypatch.setenv("GM_SPARE_BLOB_MIN", "1")
+    monkeypatch.delenv("GM_UPDATE_OVERLAY", raising=False)
+    rng = random.Random(9)
+    current = {_rand_filter(rng).encode() for _ in range(3000)}
+    topics = [_rand_topic(rng).encode() for _ in range(2000)]
+    c = Context(0)
+    idx = c.build_index(sorted(current))
+    for _ in range(6):
+        new = c.update_index(idx, _rand_ops(rng, current, 40))
+        idx.release()  # (its blob becomes the spare the next update takes)
+        idx = new
+        _check(c, orc, idx, current, topics)
+    c.close()
+    idx.release()  # after the close: freed, not kept
+    c2 = Context(0)
+    idx = c2.build_index(sorted(current))
+    new = c2.update_index(idx, _rand_ops(rng, current, 40))
+    _check(c2, orc, new, current, topics)
+    idx.release()
+    new.release()
+    c2.close()
+
+
 def test_update_breaks_chain_nodes(ctx, orc, form, monkeypatch):
     """In-place updates through chain nodes (gm_common.h): a new branch below a
     chain node, its tail's filter deleted or re-inserted, a '+' child (whose
