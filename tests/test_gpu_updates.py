@@ -159,9 +159,9 @@ def test_spare_blob_reuse_and_release_after_close(orc, monkeypatch):
     """A released snapshot's device blob is kept for the next in-place update
     of its size (gm_index.cpp take/give_spare_blob; GM_SPARE_BLOB_MIN=1: every
     blob, not only those of 256 MiB or more): a chain of updates reuses them
-    with rows equal to the oracle after each; snapshots released after their
-    context closed free their blobs (no context is left to trim them), and a
-    new context then updates normally."""
+    with rows equal to the oracle after each; a snapshot released after its
+    own context closed is freed (or kept while another context is open on the
+    device: the module's), and a new context then updates normally."""
     from emqx_amd import Context
     from tests.test_gpu_parity import _rand_filter, _rand_topic
     monkeypatch.setenv("GM_SPARE_BLOB_MIN", "1")
@@ -177,7 +177,7 @@ def test_spare_blob_reuse_and_release_after_close(orc, monkeypatch):
         idx = new
         _check(c, orc, idx, current, topics)
     c.close()
-    idx.release()  # after the close: freed, not kept
+    idx.release()  # after its context's close
     c2 = Context(0)
     idx = c2.build_index(sorted(current))
     new = c2.update_index(idx, _rand_ops(rng, current, 40))
