@@ -95,8 +95,10 @@ typedef struct emqx_gm_call emqx_gm_call;
  *   - emqx_gm_match on host buffers cuts the batch into chunks that run on
  *     all the devices at once (one host pipeline per device); the rows come
  *     back in the caller's ONE CSR, in batch order;
- *   - device-buffer calls (EMQX_GM_DEVICE_IO, emqx_gm_match_submit), the
- *     fan-out, the sharding helpers, emqx_gm_set_stream and
+ *   - emqx_gm_fanout on host rows (65,536 rows or more) cuts them into one
+ *     slice per device, balanced by matches, into the caller's ONE result;
+ *   - device-buffer calls (EMQX_GM_DEVICE_IO, emqx_gm_match_submit, a
+ *     device-row fan-out), the sharding helpers, emqx_gm_set_stream and
  *     emqx_gm_index_device_blob / _export use the first listed device; so
  *     does any call on an index made through another context (it has no
  *     replicas here).
