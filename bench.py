@@ -73,8 +73,12 @@ def parse():
                         "written after the build otherwise (profiling passes of C3/C5 skip the host build)")
     p.add_argument("--subs-update", action="store_true",
                    help="C5: also measure subscriber updates on a 100M-filter index with subscriber lists")
-    p.add_argument("--no-host-replicas", action="store_true",
-                   help="skip the two-replica (multi-device context) host-buffer rehearsal")
+    p.add_argument("--replicas", type=int, default=2,
+                   help="N=1: the multi-device context's rehearsal lists this GPU this many times (0: skip); "
+                        "N>1: rank 0 opens one context over all N GPUs instead (the drop-in NIF's form)")
+    p.add_argument("--no-multi", action="store_true",
+                   help="skip the multi-device context (one library context over the GPUs: replication, "
+                        "host-buffer match spread over the devices, replicated updates)")
     p.add_argument("--no-host-io", action="store_true",
                    help="skip the host-buffer call (PCIe-inclusive rate, reported in detail, never `value`)")
     a = p.parse_args()
@@ -112,7 +116,19 @@ def dist_setup(n_gpus):
         else:
             dist.init_process_group(BACKEND)
         pg = dist
+        global HOST_GROUP
+        # a CPU-side group: ranks waiting while rank 0 works on their GPUs (the
+        # multi-device context) wait on the host, not in a collective kernel
+        HOST_GROUP = dist.new_group(backend="gloo") if BACKEND == "nccl" else None
     return world, rank, local, pg
+
+
+HOST_GROUP = None
+
+
+def host_barrier(pg):
+    if pg is not None:
+        pg.barrier(group=HOST_GROUP) if HOST_GROUP is not None else pg.barrier()
 
 
 def torch_first(local):
@@ -477,15 +493,38 @@ def subs_update(ctx, fpack, n_ops=100, batches=7):
             "ms_max": ms_sorted[-1], "ms_first": ms[0], "build_with_subscribers_s": build_s, "filters_unchanged": ok}
 
 
-def host_io(ctx, idx, db, do, tbytes, n_topics, nnz, local, replicas=True, reps=2):
+def link_peaks(ctx, nbytes=1 << 30):
+    """This box's measured PCIe copy rates, one pinned buffer to / from this
+    GPU (hipMemcpy, best of 3): the link roofline of the host-buffer path."""
+    import numpy as np
+    hb = ctx.host_alloc(nbytes)
+    hb[:] = 1
+    d = ctx.dev_alloc(nbytes)
+    out = {}
+    for name, fn in (("h2d", lambda: ctx.memcpy_h2d(d, hb, nbytes)), ("d2h", lambda: ctx.memcpy_d2h(hb, d, nbytes))):
+        fn()
+        best = None
+        for _ in range(3):
+            t0 = time.perf_counter()
+            fn()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        out[name + "_peak_gbs"] = nbytes / best / 1e9
+    ctx.dev_free(d)
+    ctx.host_free(hb)
+    del np
+    return out
+
+
+def host_io(ctx, idx, db, do, tbytes, n_topics, nnz, reps=2):
     """The host-buffer emqx_gm_match (the NIF's call, gm_host.cpp), best of
     ``reps`` after a warm-up: topics from page-locked memory (emqx_gm_host_alloc:
     what the NIF packs into, sent by DMA with no staging copy) and from plain
-    pageable memory; and the one-GPU rehearsal of a multi-device context
-    (emqx_gm_opts.n_devices: this device listed twice -- two replicas, the batch
-    spread over both) on the page-locked batch."""
+    pageable memory.  Against the link: the bytes that cross PCIe per topic each
+    way (in: the text + a u16 length; out: the u64 row offset + 4 B per match)
+    and the rates they reach beside this box's measured hipMemcpy peaks.
+    Returns (detail, the page-locked batch and its offsets for later calls)."""
     import numpy as np
-    from emqx_amd import Context
     d = {}
     ho = np.zeros(n_topics + 1, np.uint64)
     ctx.memcpy_d2h(ho, do, (n_topics + 1) * 8)
@@ -518,18 +557,98 @@ def host_io(ctx, idx, db, do, tbytes, n_topics, nnz, local, replicas=True, reps=
     del hb
     d["host_io_pageable_topics_per_s"] = n_topics / best_p
     d["host_io_nnz_matches_device"] = ok and ok_p
-    if replicas:
-        t0 = time.perf_counter()
-        with Context(devices=[local, local]) as c2:
-            i2 = c2.import_index(idx.export())  # one image, replicated to both entries
-            rep_ms = (time.perf_counter() - t0) * 1e3
-            best2, ok2 = timed(c2, i2, pb, "replicas")
-            i2.release()
-        d["host_io_replicas"] = {"devices": [local, local], "topics_per_s": n_topics / best2, "ms": best2 * 1e3,
-                                 "nnz_matches_device": ok2, "import_and_replicate_ms": rep_ms,
-                                 "note": "one-GPU rehearsal: two replicas share this GPU's PCIe link and CUs"}
     d["host_io_cpu_s_per_call"] = cpu
-    ctx.host_free(pb)
+    # the link: PCIe bytes per topic each way (gm_host.cpp: the text and a u16 length in, the
+    # u64 row offsets -- DMA'd into the caller's CSR -- and the 4-B ids out) and the rates
+    h2d = (tbytes + 2 * n_topics) / n_topics
+    d2h = (8 * n_topics + 4 * nnz) / n_topics
+    peaks = link_peaks(ctx)
+    link = {"h2d_bytes_per_topic": h2d, "d2h_bytes_per_topic": d2h,
+            "h2d_gbs": h2d * n_topics / best / 1e9, "d2h_gbs": d2h * n_topics / best / 1e9, **peaks}
+    link["h2d_frac_of_peak"] = link["h2d_gbs"] / peaks["h2d_peak_gbs"]
+    link["d2h_frac_of_peak"] = link["d2h_gbs"] / peaks["d2h_peak_gbs"]
+    link["bound"] = "h2d" if link["h2d_frac_of_peak"] >= link["d2h_frac_of_peak"] else "d2h"
+    link["note"] = ("the host-buffer call's ceiling is the PCIe link, not the kernel: "
+                    "topics/s <= h2d_peak_gbs / h2d_bytes_per_topic")
+    link["topics_per_s_link_ceiling"] = peaks["h2d_peak_gbs"] * 1e9 / h2d
+    d["host_io_link"] = link
+    return d, pb, ho
+
+
+def update_chain(ctx, idx, n_rounds=2, n_ops=200, seed=7):
+    """n_rounds in-place updates of n_ops (half deletes of present filters,
+    half inserts), each on the previous result; wall time and what the library
+    says each call did (emqx_gm_last_update_stats).  Returns (rounds, last)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    out, cur = [], idx
+    for rnd in range(n_rounds):
+        dels = [cur.filter(int(i)) for i in rng.choice(cur.n_filters, n_ops // 2, replace=False)]
+        ins = [b"upd%d/%d/+/#" % (rnd, i) for i in range(n_ops // 2)]
+        t0 = time.perf_counter()
+        new = ctx.update_index(cur, [(f, False) for f in dels] + [(f, True) for f in ins])
+        ms = (time.perf_counter() - t0) * 1e3
+        out.append({"ms": ms, **{k: v for k, v in ctx.update_stats().items()
+                                 if k in ("kind", "replica_mode", "replicas", "mirror_loaded", "mirror_bytes",
+                                          "mirror_ms", "device_ms", "blobs_reused", "blobs_fresh")}})
+        if cur is not idx:
+            cur.release()
+        cur = new
+    return out, cur
+
+
+def multi_device(ctx, idx, devices, pb, ho, n_topics, nnz, single):
+    """The drop-in path's multi-GPU form: ONE library context over ``devices``
+    (what the NIF opens on a node: emqx_gm_opts.n_devices), outside the timed
+    region.  The index goes in once (an import of this rank's snapshot) and is
+    replicated device to device in a tree; one host-buffer emqx_gm_match of
+    the whole page-locked batch is spread over every device (gm_host.cpp);
+    200-op updates are applied on every replica at once (O(delta), from each
+    replica's predecessor).  ``single``: this rank's single-device figures."""
+    from emqx_amd import Context
+    d = {"devices": list(devices)}
+    big = idx.info.device_bytes > (16 << 30)
+    img = idx.export(with_blob=big)
+    blob = None if big else idx.device_blob()[0]
+    if big:  # (C5's 53 GB: the replicas and an update's new tables fit only without this rank's copy)
+        idx.release()
+        ctx.pool_trim()
+    with Context(devices=list(devices)) as c:
+        t0 = time.perf_counter()
+        ix = c.import_index(img, d_blob=blob)
+        st = c.update_stats()
+        if not big:
+            idx.release()  # (the replicas are copies: this rank's snapshot is no longer needed)
+        d["import_and_replicate_ms"] = (time.perf_counter() - t0) * 1e3
+        d["replicate_ms"] = st["replicate_ms"]
+        d["replica_mode"] = st["replica_mode"]
+        d["replicated_bytes"] = int(ix.info.device_bytes) * (len(devices) - 1)
+        d["import_mirror_loaded"] = st["mirror_loaded"]
+        del img
+        c.match_host(ix, (pb, ho), exact=True).free()  # (warm: pinned staging, pools, workers on every device)
+        best, ok = None, True
+        for _ in range(2):
+            t0 = time.perf_counter()
+            h = c.match_host(ix, (pb, ho), exact=True)
+            dt = time.perf_counter() - t0
+            ok = ok and h.nnz == nnz
+            h.free()
+            best = dt if best is None else min(best, dt)
+        d["host_io_multi_topics_per_s"] = n_topics / best
+        d["host_io_multi_ms"] = best * 1e3
+        d["host_io_multi_nnz_matches_device"] = ok
+        if single.get("host_io_topics_per_s"):
+            d["host_io_multi_vs_single_device"] = d["host_io_multi_topics_per_s"] / single["host_io_topics_per_s"]
+        rounds, last = update_chain(c, ix)
+        d["index_update_replicas"] = {"ops": 200, "update_ms": rounds[-1]["ms"], "rounds": rounds}
+        if single.get("update_ms"):
+            d["index_update_replicas"]["vs_single_device"] = rounds[-1]["ms"] / single["update_ms"]
+        if len(set(devices)) == 1:
+            d["note"] = (f"one-GPU rehearsal: {len(devices)} replicas share this GPU's HBM, CUs and PCIe link "
+                         "(an update's device passes run side by side on one GPU)")
+        last.release()
+        if last is not ix:
+            ix.release()
     return d
 
 
@@ -682,34 +801,29 @@ def main():
                    "device_ms_per_call": st["total_device_ms"],
                    "calls_in_flight": 1 if a.no_pipeline else 2},
     }
+    pb = ho = None
     if not a.no_host_io and rank == 0:
         # PCIe-inclusive, outside the timed region: the same batch handed over in host
         # memory and its CSR returned in host memory (the NIF's call, gm_host.cpp)
-        out["detail"].update(host_io(ctx, idx, db, do, tbytes, n_topics, nnz, local,
-                                     replicas=not a.no_host_replicas and cfg in ("c1", "c2", "c3")))
+        hd, pb, ho = host_io(ctx, idx, db, do, tbytes, n_topics, nnz)
+        out["detail"].update(hd)
     if rank == 0 and world == 1 and not a.no_update:
         # incremental maintenance, outside the timed region: 100 deletes +
         # 100 inserts patched into this index, twice in a row, and a match of the same batch on
-        # the result.  The first update of a large index (C5: 38 GB of tables, whose host mirror
-        # is lazy) downloads the mirror; the second is the steady state.
-        rng = np.random.default_rng(7)
-        upd, cur = [], idx
-        for rnd in range(2):
-            dels = [cur.filter(int(i)) for i in rng.choice(cur.n_filters, 100, replace=False)]
-            ins = [b"upd%d/%d/+/#" % (rnd, i) for i in range(100)]
-            t0 = time.perf_counter()
-            new = ctx.update_index(cur, [(f, False) for f in dels] + [(f, True) for f in ins])
-            upd.append((time.perf_counter() - t0) * 1e3)
-            if cur is not idx:
-                cur.release()
-            cur = new
+        # the result.  The first update of an index whose host mirror is lazy (C5: 53 GB of
+        # tables) downloads the mirror -- the library reports whether it did
+        # (emqx_gm_last_update_stats); the second is the steady state.
+        rounds, cur = update_chain(ctx, idx)
         ks = []
         for _ in range(3):
             r = ctx.match_device(cur, db, do, n_topics, exact=True)
             ks.append(ctx.stats()["match_kernel_ms"])
             r.free()
-        out["detail"]["index_update"] = {"ops": 200, "update_ms": upd[-1], "first_update_ms": upd[0],
-                                         "first_includes_mirror_download": idx.info.device_bytes > 8 << 30,
+        f0 = rounds[0]
+        out["detail"]["index_update"] = {"ops": 200, "update_ms": rounds[-1]["ms"], "first_update_ms": f0["ms"],
+                                         "first_includes_mirror_download": f0["mirror_loaded"],
+                                         "first_mirror_bytes": f0["mirror_bytes"], "first_mirror_ms": f0["mirror_ms"],
+                                         "index_source": source, "rounds": rounds,
                                          "match_kernel_ms_after": min(ks), "vs_flat": min(ks) / min(kern_ms)}
         cur.release()
     if rank == 0 and world == 1 and not a.no_update and (cfg != "c5" or a.subs_update):
@@ -739,7 +853,22 @@ def main():
     last.free()
     ctx.dev_free(db)
     ctx.dev_free(do)
-    idx.release()
+    # the drop-in path's multi-GPU form (one context over the GPUs), rank 0, while the
+    # other ranks wait on the host
+    multi = not a.no_multi and pb is not None and (world > 1 or a.replicas > 1)
+    host_barrier(pg)
+    if multi and rank == 0:
+        devices = ([local] * world if "GM_BENCH_DEVICE" in os.environ else list(range(world))) if world > 1 \
+            else [local] * a.replicas
+        single = {"host_io_topics_per_s": out["detail"].get("host_io_topics_per_s"),
+                  "update_ms": out["detail"].get("index_update", {}).get("update_ms")}
+        out["detail"]["multi_device"] = multi_device(ctx, idx, devices, pb, ho, n_topics, nnz, single)
+        idx = None
+    host_barrier(pg)
+    if pb is not None:
+        ctx.host_free(pb)
+    if idx is not None:
+        idx.release()
     ctx.close()
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -57,6 +57,17 @@ class MatchStats(C.Structure):
                 ("total_device_ms", C.c_double), ("algo_bytes", C.c_uint64), ("probes", C.c_uint64)]
 
 
+class UpdateStats(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("replica_mode", C.c_uint32), ("replicas", C.c_uint32),
+                ("mirror_loaded", C.c_int32), ("mirror_bytes", C.c_uint64), ("mirror_ms", C.c_double),
+                ("device_ms", C.c_double), ("replicate_ms", C.c_double), ("total_ms", C.c_double),
+                ("blobs_reused", C.c_uint32), ("blobs_fresh", C.c_uint32)]
+
+
+UPD_KINDS = {0: "none", 1: "patch", 2: "overlay", 3: "rebuild", 4: "subs_only", 5: "build", 6: "import"}
+REP_MODES = {0: "none", 1: "patched", 2: "copied", 3: "shared"}
+
+
 # Every symbol declared in include/emqx_gpu_match.h and include/emqx_gm_ext.h.
 _vp, _u64, _i32, _u32 = C.c_void_p, C.c_uint64, C.c_int, C.c_uint32
 SIGNATURES = {
@@ -112,6 +123,8 @@ SIGNATURES = {
     "emqx_gm_matched_filter_bytes": (_i32, [_vp, _vp, C.POINTER(Csr), C.POINTER(_u64)]),
     "emqx_gm_fanout_part": (_i32, [_vp, _vp, C.POINTER(Csr), _u32, _u32, _u32, C.POINTER(Csr), C.POINTER(_u64)]),
     "emqx_gm_select_filters": (_i32, [_vp, _vp, _u64, _vp, _u32, _vp, _vp, C.POINTER(_u64), C.POINTER(_u64)]),
+    "emqx_gm_last_update_stats": (_i32, [_vp, C.POINTER(UpdateStats)]),
+    "emqx_gm_index_replica_digest": (_i32, [_vp, _vp, _u32, C.POINTER(_u64), C.POINTER(_u64)]),
 }
 
 _LIB = None

@@ -293,18 +293,20 @@ int emqx_gm_open(const emqx_gm_opts* opts, emqx_gm_ctx** out) {
       emqx_gm_close(ctx);
       return rc;
     }
+    m->parent = ctx;
     ctx->members.push_back(m);
-    // replicas are copied GPU to GPU: peer access lets the copy engines go over
-    // xGMI directly (already enabled, or unsupported: the runtime stages it)
-    if (devs[k] != devs[0]) {
-      int can = 0;
-      if (hipDeviceCanAccessPeer(&can, devs[k], devs[0]) == hipSuccess && can) {
-        hipSetDevice(devs[k]);
-        (void)hipDeviceEnablePeerAccess(devs[0], 0);
-        (void)hipGetLastError();  // (hipErrorPeerAccessAlreadyEnabled is fine)
-      }
-    }
   }
+  // replicas are copied GPU to GPU, in a tree (any listed device may be a
+  // copy's source): peer access between every pair lets the copy engines go
+  // over xGMI directly (already enabled, or unsupported: the runtime stages it)
+  for (int a : devs)
+    for (int b : devs) {
+      int can = 0;
+      if (a == b || hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+      hipSetDevice(a);
+      (void)hipDeviceEnablePeerAccess(b, 0);
+      (void)hipGetLastError();  // (hipErrorPeerAccessAlreadyEnabled is fine)
+    }
   hipSetDevice(devs[0]);
   *out = ctx;
   return EMQX_GM_OK;
@@ -415,12 +417,17 @@ int emqx_gm_synchronize(emqx_gm_ctx* ctx) {
   return EMQX_GM_OK;
 }
 
-// A snapshot made on a multi-device context gets its replicas (gm_multi.cpp);
-// `redo` repeats the call on a member for a result that cannot be copied.
-static int replicated(emqx_gm_ctx* ctx, int rc, emqx_gm_index* prev, emqx_gm_index** out,
-                      const std::function<int(emqx_gm_ctx*, emqx_gm_index*, emqx_gm_index**)>& redo = nullptr) {
-  if (rc || ctx->members.empty() || !out || !*out) return rc;
-  return gm::replicate_result(ctx, prev, out, redo);
+// A snapshot made on a multi-device context gets its replicas (gm_multi.cpp)
+// unless the update made them itself; the call's update stats are closed.
+static int replicated(emqx_gm_ctx* ctx, int rc, emqx_gm_index* prev, emqx_gm_index** out, double t0) {
+  if (!rc && !ctx->members.empty() && out && *out) rc = gm::replicate_result(ctx, prev, out);
+  gm::tl_ustats.total_ms = gm::now_ms() - t0;
+  return rc;
+}
+static double begin_index_call(uint32_t kind) {
+  gm::tl_ustats = emqx_gm_update_stats{};
+  gm::tl_ustats.kind = kind;
+  return gm::now_ms();
 }
 
 int emqx_gm_index_build(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_t n,
@@ -429,8 +436,9 @@ int emqx_gm_index_build(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo,
   if (!ctx) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   GM_GUARD_BEGIN
+  const double t0 = begin_index_call(EMQX_GM_UPD_BUILD);
   hipSetDevice(ctx->device);
-  return replicated(ctx, gm::build_index(ctx, fb, fo, n, sub_off, sub_ids, perm_out, out), nullptr, out);
+  return replicated(ctx, gm::build_index(ctx, fb, fo, n, sub_off, sub_ids, perm_out, out), nullptr, out, t0);
   GM_GUARD_END(ctx)
 }
 
@@ -441,12 +449,9 @@ int emqx_gm_index_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* f
   if (prev && prev->device != ctx->device)
     return gm::set_err(ctx, EMQX_GM_EINVAL, "index_update: index lives on another device");
   GM_GUARD_BEGIN
+  const double t0 = begin_index_call(EMQX_GM_UPD_NONE);
   hipSetDevice(ctx->device);
-  return replicated(ctx, gm::update_index(ctx, prev, fb, fo, ops, n_ops, out), prev, out,
-                    [&](emqx_gm_ctx* m, emqx_gm_index* p, emqx_gm_index** o) {
-                      hipSetDevice(m->device);
-                      return gm::update_index(m, p, fb, fo, ops, n_ops, o);
-                    });
+  return replicated(ctx, gm::update_index(ctx, prev, fb, fo, ops, n_ops, out), prev, out, t0);
   GM_GUARD_END(ctx)
 }
 
@@ -457,12 +462,9 @@ int emqx_gm_index_update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8
   if (prev && prev->device != ctx->device)
     return gm::set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: index lives on another device");
   GM_GUARD_BEGIN
+  const double t0 = begin_index_call(EMQX_GM_UPD_NONE);
   hipSetDevice(ctx->device);
-  return replicated(ctx, gm::update_subs(ctx, prev, fb, fo, subs, ops, n_ops, out), prev, out,
-                    [&](emqx_gm_ctx* m, emqx_gm_index* p, emqx_gm_index** o) {
-                      hipSetDevice(m->device);
-                      return gm::update_subs(m, p, fb, fo, subs, ops, n_ops, o);
-                    });
+  return replicated(ctx, gm::update_subs(ctx, prev, fb, fo, subs, ops, n_ops, out), prev, out, t0);
   GM_GUARD_END(ctx)
 }
 
@@ -487,8 +489,9 @@ int emqx_gm_index_import(emqx_gm_ctx* ctx, const uint8_t* image, uint64_t size, 
   if (!ctx) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   GM_GUARD_BEGIN
+  const double t0 = begin_index_call(EMQX_GM_UPD_IMPORT);
   hipSetDevice(ctx->device);
-  return replicated(ctx, gm::index_import(ctx, image, size, d_blob, out), nullptr, out);
+  return replicated(ctx, gm::index_import(ctx, image, size, d_blob, out), nullptr, out, t0);
   GM_GUARD_END(ctx)
 }
 
@@ -530,10 +533,53 @@ int emqx_gm_index_subscriber_count(const emqx_gm_index* idx, uint32_t id, uint64
   return EMQX_GM_OK;
 }
 
+// The stats of the calling thread's last match / fan-out call and the
+// context it ran on (emqx_gm_last_stats): concurrent callers of one context
+// each read their own call's.
+static thread_local emqx_gm_match_stats tl_stats;
+static thread_local const emqx_gm_ctx* tl_stats_ctx = nullptr;
+static int noted(const emqx_gm_ctx* api_ctx, const emqx_gm_ctx* ran, int rc) {
+  if (rc == EMQX_GM_OK) {
+    tl_stats = ran->stats;
+    tl_stats_ctx = api_ctx;
+  }
+  return rc;
+}
+
+// A host-buffer call of at most one chunk on a multi-device context: ONE
+// device serves it whole -- the first whose lock is free from a round-robin
+// start -- under that device's lock only, so concurrent callers (a NIF's dirty
+// schedulers, each with a publish window) run on different GPUs at once, as
+// the reference's publishers match in their own processes at once
+// (apps/emqx/src/emqx_trie.erl:66-70, emqx_router.erl:128-145).  Larger calls
+// are cut into chunks spread over every device (gm_host.cpp).
+static int match_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                       uint32_t flags, emqx_gm_csr* out) {
+  const size_t K = 1 + ctx->members.size();
+  auto mem = [&](size_t k) { return k ? ctx->members[k - 1] : ctx; };
+  const size_t s = ctx->rr.fetch_add(1, std::memory_order_relaxed) % K;
+  std::unique_lock<std::recursive_mutex> lk;
+  size_t pick = s;
+  for (size_t j = 0; j < K && !lk.owns_lock(); ++j) {
+    std::unique_lock<std::recursive_mutex> l(mem((s + j) % K)->mu, std::try_to_lock);
+    if (l.owns_lock()) {
+      lk = std::move(l);
+      pick = (s + j) % K;
+    }
+  }
+  if (!lk.owns_lock()) lk = std::unique_lock<std::recursive_mutex>(mem(s)->mu);
+  emqx_gm_ctx* mc = mem(pick);
+  const emqx_gm_index* rix = pick ? idx->reps[pick - 1] : idx;
+  hipSetDevice(mc->device);
+  const int rc = gm::run_match_host(mc, rix, tb, to, n, flags, out);  // (mc has no members: one device)
+  noted(ctx, mc, rc);
+  hipSetDevice(ctx->device);
+  return rc;
+}
+
 int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to,
                   uint64_t n, uint32_t flags, emqx_gm_csr* out) {
   if (!ctx) return EMQX_GM_EINVAL;
-  std::unique_lock<std::recursive_mutex> lk(ctx->mu);
   if (!idx || !out || (n && (!tb || !to))) return gm::set_err(ctx, EMQX_GM_EINVAL, "match: NULL argument");
   if (flags & ~(EMQX_GM_WITH_EXACT | EMQX_GM_DEVICE_IO | EMQX_GM_NO_TIMING))
     return gm::set_err(ctx, EMQX_GM_EINVAL, "match: flags");
@@ -543,18 +589,22 @@ int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb,
   if (idx->device != ctx->device) return gm::set_err(ctx, EMQX_GM_EINVAL, "match: index lives on another device");
   std::memset(out, 0, sizeof(*out));
   GM_GUARD_BEGIN
+  if (!(flags & EMQX_GM_DEVICE_IO) && !ctx->members.empty() && !idx->ov &&
+      idx->reps.size() == ctx->members.size() && n <= gm::host_chunk_topics() && !gm::knob("GM_HOST_SIMPLE"))
+    return match_small(ctx, idx, tb, to, n, flags, out);
+  std::unique_lock<std::recursive_mutex> lk(ctx->mu);
   hipSetDevice(ctx->device);
-  if (idx->ov) return gm::run_match_overlay(ctx, idx, tb, to, n, flags, out);
-  if (!(flags & EMQX_GM_DEVICE_IO) && !getenv("GM_HOST_SIMPLE"))  // host buffers: chunked, pipelined
-    return gm::run_match_host(ctx, idx, tb, to, n, flags, out);
-  if (!(flags & EMQX_GM_DEVICE_IO)) return gm::run_match(ctx, idx, tb, to, n, flags, out);
+  if (idx->ov) return noted(ctx, ctx, gm::run_match_overlay(ctx, idx, tb, to, n, flags, out));
+  if (!(flags & EMQX_GM_DEVICE_IO) && !gm::knob("GM_HOST_SIMPLE"))  // host buffers: chunked, pipelined
+    return noted(ctx, ctx, gm::run_match_host(ctx, idx, tb, to, n, flags, out));
+  if (!(flags & EMQX_GM_DEVICE_IO)) return noted(ctx, ctx, gm::run_match(ctx, idx, tb, to, n, flags, out));
   // device buffers: the call is queued under the lock and waited for outside
   // it, so concurrent callers' batches queue behind this one meanwhile
   void* t = nullptr;
   const int rc = gm::match_submit(ctx, idx, tb, to, n, flags, &t);
   if (rc) return rc;
   lk.unlock();
-  return gm::match_wait(ctx, t, out);
+  return noted(ctx, ctx, gm::match_wait(ctx, t, out));
   GM_GUARD_END(ctx)
 }
 
@@ -587,7 +637,7 @@ int emqx_gm_match_wait(emqx_gm_ctx* ctx, emqx_gm_call* call, emqx_gm_csr* out) {
   std::memset(out, 0, sizeof(*out));
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
-  return gm::match_wait(ctx, call, out);
+  return noted(ctx, ctx, gm::match_wait(ctx, call, out));
   GM_GUARD_END(ctx)
 }
 
@@ -604,8 +654,8 @@ int emqx_gm_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
   if (!ctx->members.empty() && !(flags & EMQX_GM_DEVICE_IO) && !m->on_device)
-    return gm::run_fanout_multi(ctx, idx, m, flags, out);
-  return gm::run_fanout(ctx, idx, m, flags, out);
+    return noted(ctx, ctx, gm::run_fanout_multi(ctx, idx, m, flags, out));
+  return noted(ctx, ctx, gm::run_fanout(ctx, idx, m, flags, out));
   GM_GUARD_END(ctx)
 }
 
@@ -623,17 +673,23 @@ int emqx_gm_fanout_part(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_g
   std::memset(out, 0, sizeof(*out));
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
-  return gm::run_fanout(ctx, idx, m, flags, out, part, n_parts, first);
+  return noted(ctx, ctx, gm::run_fanout(ctx, idx, m, flags, out, part, n_parts, first));
   GM_GUARD_END(ctx)
 }
 
 int emqx_gm_csr_free(emqx_gm_ctx* ctx, emqx_gm_csr* csr) {
   if (!ctx || !csr) return EMQX_GM_EINVAL;
-  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   // a result CSR records its context (priv): its buffers belong to that
-  // context's pools, and handing them to another one would corrupt both
-  if (csr->priv && csr->priv != static_cast<void*>(ctx))
-    return gm::set_err(ctx, EMQX_GM_EINVAL, "csr_free: the CSR belongs to another context");
+  // context's pools, and handing them to another one would corrupt both; a
+  // small call's rows belong to the member device that served it
+  if (csr->priv && csr->priv != static_cast<void*>(ctx)) {
+    emqx_gm_ctx* owner = nullptr;
+    for (emqx_gm_ctx* m : ctx->members)
+      if (csr->priv == static_cast<void*>(m)) owner = m;
+    if (!owner) return gm::set_err(ctx, EMQX_GM_EINVAL, "csr_free: the CSR belongs to another context");
+    ctx = owner;
+  }
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   if (csr->on_device) {
     // back to the pool once the work queued so far (which may still read the
     // rows: a fan-out, a later call's inputs) is done -- no wait here, so a
@@ -651,8 +707,45 @@ int emqx_gm_csr_free(emqx_gm_ctx* ctx, emqx_gm_csr* csr) {
 
 int emqx_gm_last_stats(const emqx_gm_ctx* ctx, emqx_gm_match_stats* stats) {
   if (!ctx || !stats) return EMQX_GM_EINVAL;
-  *stats = ctx->stats;
+  *stats = tl_stats_ctx == ctx ? tl_stats : ctx->stats;
   return EMQX_GM_OK;
+}
+
+int emqx_gm_last_update_stats(const emqx_gm_ctx* ctx, emqx_gm_update_stats* stats) {
+  if (!ctx || !stats) return EMQX_GM_EINVAL;
+  *stats = gm::tl_ustats;
+  return EMQX_GM_OK;
+}
+
+int emqx_gm_index_replica_digest(emqx_gm_ctx* ctx, const emqx_gm_index* idx, uint32_t k, uint64_t* tables,
+                                 uint64_t* subs) {
+  if (!ctx || !idx || !tables || !subs) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (k > idx->reps.size()) return gm::set_err(ctx, EMQX_GM_EINVAL, "replica_digest: no such replica");
+  const emqx_gm_index* r = k ? idx->reps[k - 1] : idx;
+  GM_GUARD_BEGIN
+  auto fnv = [](uint64_t h, const std::vector<uint8_t>& b) {
+    for (uint8_t x : b) h = (h ^ x) * 0x100000001B3ull;
+    return h;
+  };
+  hipSetDevice(r->device);
+  std::vector<uint8_t> b(r->dev_bytes);
+  if (!b.empty()) GM_HIP(ctx, hipMemcpy(b.data(), r->dev_base, b.size(), hipMemcpyDeviceToHost));
+  *tables = fnv(0xCBF29CE484222325ull, b);
+  *subs = 0;
+  if (r->view.sub_off) {
+    const uint64_t nf = r->info.n_filters;
+    std::vector<uint8_t> o((nf + 1) * 8);
+    GM_HIP(ctx, hipMemcpy(o.data(), r->view.sub_off, o.size(), hipMemcpyDeviceToHost));
+    uint64_t total = 0;
+    std::memcpy(&total, o.data() + nf * 8, 8);
+    std::vector<uint8_t> ids(total * 4);
+    if (total) GM_HIP(ctx, hipMemcpy(ids.data(), r->view.sub_ids, ids.size(), hipMemcpyDeviceToHost));
+    *subs = fnv(fnv(0xCBF29CE484222325ull, o), ids);
+  }
+  hipSetDevice(ctx->device);
+  return EMQX_GM_OK;
+  GM_GUARD_END(ctx)
 }
 
 // ---- extensions used by the bench / Python host layer (emqx_gm_ext.h) ----
@@ -731,9 +824,10 @@ int emqx_gm_index_build_shard(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   if (n && !global_ids) return gm::set_err(ctx, EMQX_GM_EINVAL, "index_build_shard: global_ids is NULL");
   GM_GUARD_BEGIN
+  const double t0 = begin_index_call(EMQX_GM_UPD_BUILD);
   hipSetDevice(ctx->device);
   return replicated(ctx, gm::build_index(ctx, fb, fo, n, sub_off, sub_ids, perm_out, out, nullptr, global_ids),
-                    nullptr, out);
+                    nullptr, out, t0);
   GM_GUARD_END(ctx)
 }
 

@@ -7,12 +7,14 @@
 // through four slots so that PCIe in, the match kernels and PCIe out of
 // consecutive chunks overlap:
 //
-//   worker threads   stage chunk i+2: validate offsets, copy text, offsets as
-//                    u32 chunk-relative (4 B/topic over PCIe instead of 8)
-//                    into pinned memory
+//   worker threads   stage chunk i+2: validate offsets, copy text, each
+//                    topic's length as u16 (2 B/topic over PCIe instead of 8:
+//                    MQTT topics are at most 65,535 bytes, emqx_topic.erl:45;
+//                    a chunk holding a longer one goes as u32 offsets) into
+//                    pinned memory
 //   h2d stream       pinned -> device                       (chunk i+1)
-//   ctx stream       u32 -> u64 offsets, the device match (run_match), row
-//                    offsets back to u32                     (chunk i)
+//   ctx stream       u16 lengths -> u64 offsets (a scan), the device match
+//                    (run_match), row offsets back to u32    (chunk i)
 //   d2h stream       rows -> pinned                          (chunk i)
 //   worker threads   unpack rows into the caller-visible CSR: u64 offsets
 //                    rebased by the rows of earlier chunks, ids copied
@@ -124,8 +126,10 @@ struct Device {
 constexpr int SLOTS = 4;
 
 struct Slot {
-  Pinned in_b, in_o, out_o, out_i;  // text, u32 offsets in; u32 row offsets, ids out
-  Device d_b, d_o32, d_o64, d_r32;  // text, offsets u32 -> u64 in; row offsets u32 out
+  Pinned in_b, in_l, in_o, out_o, out_i;  // text, u16 lengths (u32 offsets: fallback) in; u32 row offsets, ids out
+  Device d_b, d_l16, d_o32, d_o64, d_r32;  // text, lengths u16 (offsets u32) -> offsets u64 in; row offsets u32 out
+  std::atomic<int> long_topic{0};          // staging met a topic of more than 65,535 bytes
+  bool use32 = false;                      // this chunk goes up as u32 offsets
   hipEvent_t h2d = nullptr, comp = nullptr, d2h = nullptr;
   std::vector<std::future<void>> stage_f;  // this slot's staging (run_host_pipe)
   std::vector<std::future<void>> out_f;    // this slot's last unpack
@@ -136,7 +140,7 @@ struct Slot {
 };
 
 uint64_t env_u64(const char* name, uint64_t dflt) {
-  const char* e = getenv(name);
+  const char* e = knob(name);
   return e ? strtoull(e, nullptr, 10) : dflt;
 }
 
@@ -146,7 +150,70 @@ void join(std::vector<std::future<void>>& fs) {
   fs.clear();
 }
 
+// Worker-side staging of topics [a, e) of the chunk [c0, c0 + nc): offsets
+// validated (monotone, inside the chunk's text), each topic's length as u16
+// into l -- MQTT caps a topic at 65,535 bytes (apps/emqx/src/emqx_topic.erl:
+// 45, MAX_TOPIC_LEN); a longer one (the ABI takes any) sets long_topic and the
+// chunk goes up as u32 offsets (stage_off32) -- and the text copied into b
+// (nullptr: sent from where it lies), with the chunk's 64 B of padding zeroed.
+void stage_part(const uint8_t* tb, const uint64_t* to, uint64_t c0, uint64_t nc, uint64_t a, uint64_t e, uint16_t* l,
+                uint8_t* b, std::atomic<int>& bad, std::atomic<int>& long_topic) {
+  const uint64_t b0 = to[c0], b1 = to[c0 + nc];
+  uint64_t lng = 0;
+  for (uint64_t j = a; j < e; ++j) {
+    if (to[j + 1] < to[j]) {
+      bad.store(1);
+      return;
+    }
+    const uint64_t len = to[j + 1] - to[j];
+    lng |= len >> 16;
+    l[j - c0] = uint16_t(len);
+  }
+  if (lng) long_topic.store(1);
+  if (to[a] < b0 || to[e] > b1) {  // inside the chunk's text (the chunk plan checked b0 <= b1)
+    bad.store(1);
+    return;
+  }
+  if (b && e > a) std::memcpy(b + (to[a] - b0), tb + to[a], to[e] - to[a]);
+  if (b && e == c0 + nc) std::memset(b + (to[e] - b0), 0, 64);
+}
+// the fallback: the chunk's offsets as u32, chunk-relative (validated by stage_part)
+void stage_off32(const uint64_t* to, uint64_t c0, uint64_t nc, uint32_t* o) {
+  const uint64_t b0 = to[c0];
+  for (uint64_t j = 0; j <= nc; ++j) o[j] = uint32_t(to[c0 + j] - b0);
+}
+
 }  // namespace
+
+// A staged chunk to its device on stream h: the text (from the pinned staging,
+// which holds the 64 B of padding, or -- text != nullptr -- straight from the
+// caller's page-locked buffer, the padding zeroed on the device) and its u16
+// lengths, or its u32 offsets when a topic was longer than 65,535 bytes.
+hipError_t send_in(Slot& s, const uint64_t* to, const uint8_t* text, hipStream_t h) {
+  hipError_t e;
+  if (!text) {
+    e = hipMemcpyAsync(s.d_b.p, s.in_b.p, s.nbytes + 64, hipMemcpyHostToDevice, h);
+  } else {
+    e = s.nbytes ? hipMemcpyAsync(s.d_b.p, text, s.nbytes, hipMemcpyHostToDevice, h) : hipSuccess;
+    if (e == hipSuccess) e = hipMemsetAsync(s.d_b.as<uint8_t>() + s.nbytes, 0, 64, h);
+  }
+  s.use32 = s.long_topic.load() != 0 || env_u64("GM_HOST_OFF32", 0) != 0;
+  if (e == hipSuccess && s.use32) {
+    if (!s.in_o.reserve((s.nc + 1) * 4) || !s.d_o32.reserve((s.nc + 1) * 4)) return hipErrorOutOfMemory;
+    hipEventSynchronize(s.h2d);  // (the slot's previous send has read in_o)
+    stage_off32(to, s.c0, s.nc, s.in_o.as<uint32_t>());
+    e = hipMemcpyAsync(s.d_o32.p, s.in_o.p, (s.nc + 1) * 4, hipMemcpyHostToDevice, h);
+  } else if (e == hipSuccess) {
+    e = hipMemcpyAsync(s.d_l16.p, s.in_l.p, s.nc * 2, hipMemcpyHostToDevice, h);
+  }
+  if (e == hipSuccess) e = hipEventRecord(s.h2d, h);
+  return e;
+}
+// the chunk's u64 offsets on the device (stream st: the context's), from what send_in sent
+int offsets_in(emqx_gm_ctx* c, hipStream_t st, Slot& s) {
+  if (s.use32) return launch_off32_to_64(st, s.d_o32.as<uint32_t>(), s.nc + 1, s.d_o64.as<uint64_t>());
+  return scan_len16(c, st, s.d_l16.as<uint16_t>(), s.nc, s.d_o64.as<uint64_t>());
+}
 
 struct HostPipe {
   int device = 0;
@@ -258,34 +325,18 @@ static int run_host_serial(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uin
     return to[hi] >= to[c0] && to[hi] - to[c0] < (1ull << 32);
   };
 
-  // worker-side staging of chunk [c0, c1) into slot s: offsets checked and
-  // rebased to u32, text copied, 64 zero bytes of padding (the tokenizer's slack)
+  // worker-side staging of chunk [c0, c1) into slot s: offsets checked, u16
+  // lengths, text copied, 64 zero bytes of padding (the tokenizer's slack)
   auto stage = [&](Slot& s) {
-    const uint64_t c0 = s.c0, nc = s.nc, b0 = to[c0];
-    uint32_t* o = s.in_o.as<uint32_t>();
+    const uint64_t c0 = s.c0, nc = s.nc;
+    uint16_t* l = s.in_l.as<uint16_t>();
     uint8_t* b = s.in_b.as<uint8_t>();
+    s.long_topic.store(0);
+    std::atomic<int>* lt = &s.long_topic;
     const uint64_t parts = nc < 65536 ? 1 : T;
     for (uint64_t p = 0; p < parts; ++p) {
       const uint64_t a = c0 + nc * p / parts, e = c0 + nc * (p + 1) / parts;
-      const uint64_t b1 = to[c0 + nc];
-      auto job = [=, &bad] {
-        for (uint64_t j = a; j < e; ++j) {
-          if (to[j + 1] < to[j]) {
-            bad.store(1);
-            return;
-          }
-          o[j - c0] = uint32_t(to[j] - b0);
-        }
-        if (to[a] < b0 || to[e] > b1) {  // inside the chunk's text (plan() checked b0 <= b1)
-          bad.store(1);
-          return;
-        }
-        if (e > a) std::memcpy(b + (to[a] - b0), tb + to[a], to[e] - to[a]);
-        if (e == c0 + nc) {
-          o[nc] = uint32_t(to[e] - b0);
-          std::memset(b + (to[e] - b0), 0, 64);
-        }
-      };
+      auto job = [=, &bad] { stage_part(tb, to, c0, nc, a, e, l, b, bad, *lt); };
       if (parts == 1) job();
       else stage_f.push_back(W.submit(job));
     }
@@ -310,8 +361,8 @@ static int run_host_serial(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uin
     s.c0 = cb[i];
     s.nc = cb[i + 1] - cb[i];
     s.nbytes = to[cb[i + 1]] - to[cb[i]];
-    if (!s.in_b.reserve(s.nbytes + 64) || !s.in_o.reserve((s.nc + 1) * 4) || !s.d_b.reserve(s.nbytes + 64) ||
-        !s.d_o32.reserve((s.nc + 1) * 4) || !s.d_o64.reserve((s.nc + 1) * 8) || !s.d_r32.reserve((s.nc + 1) * 4) ||
+    if (!s.in_b.reserve(s.nbytes + 64) || !s.in_l.reserve(s.nc * 2 + 2) || !s.d_b.reserve(s.nbytes + 64) ||
+        !s.d_l16.reserve(s.nc * 2 + 2) || !s.d_o64.reserve((s.nc + 1) * 8) || !s.d_r32.reserve((s.nc + 1) * 4) ||
         !s.out_o.reserve((s.nc + 1) * 4))
       return EMQX_GM_ENOMEM;
     stage(s);
@@ -321,11 +372,8 @@ static int run_host_serial(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uin
     Slot& s = hp->slot[i % SLOTS];
     join(stage_f);
     if (bad.load()) return EMQX_GM_EINVAL;
-    if (hipMemcpyAsync(s.d_b.p, s.in_b.p, s.nbytes + 64, hipMemcpyHostToDevice, hp->h2d) != hipSuccess ||
-        hipMemcpyAsync(s.d_o32.p, s.in_o.p, (s.nc + 1) * 4, hipMemcpyHostToDevice, hp->h2d) != hipSuccess ||
-        hipEventRecord(s.h2d, hp->h2d) != hipSuccess)
-      return EMQX_GM_EDEVICE;
-    return 0;
+    const hipError_t e = send_in(s, to, nullptr, hp->h2d);
+    return e == hipSuccess ? 0 : e == hipErrorOutOfMemory ? EMQX_GM_ENOMEM : EMQX_GM_EDEVICE;
   };
   auto pipe_err = [](int code) {
     return code == EMQX_GM_EINVAL ? "match: topic offsets not monotone"
@@ -338,8 +386,7 @@ static int run_host_serial(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uin
     if (i + 1 < m && (rc = send_chunk(i + 1))) return fail(rc, pipe_err(rc));  // queued behind chunk i's send
     if (i + 2 < m && (rc = begin_chunk(i + 2))) return fail(rc, pipe_err(rc));  // staged on the workers meanwhile
     // match chunk i on the context's stream once its text is on the device
-    if (hipStreamWaitEvent(ctx->stream, s.h2d, 0) != hipSuccess ||
-        launch_off32_to_64(ctx->stream, s.d_o32.as<uint32_t>(), s.nc + 1, s.d_o64.as<uint64_t>()))
+    if (hipStreamWaitEvent(ctx->stream, s.h2d, 0) != hipSuccess || offsets_in(ctx, ctx->stream, s))
       return fail(EMQX_GM_EDEVICE, "match: offsets to device");
     s.csr = emqx_gm_csr{};
     // a one-chunk call queues the rows' copy-out behind the speculative assembly,
@@ -560,37 +607,22 @@ static int run_host_pipe(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8
     s.c0 = cb[i];
     s.nc = cb[i + 1] - cb[i];
     s.nbytes = to[cb[i + 1]] - to[cb[i]];
-    if ((!direct_in && !s.in_b.reserve(s.nbytes + 64)) || !s.in_o.reserve((s.nc + 1) * 4) ||
-        !s.d_b.reserve(s.nbytes + 64) || !s.d_o32.reserve((s.nc + 1) * 4) || !s.d_o64.reserve((s.nc + 1) * 8) ||
+    if ((!direct_in && !s.in_b.reserve(s.nbytes + 64)) || !s.in_l.reserve(s.nc * 2 + 2) ||
+        !s.d_b.reserve(s.nbytes + 64) || !s.d_l16.reserve(s.nc * 2 + 2) || !s.d_o64.reserve((s.nc + 1) * 8) ||
         (!direct_out && (!s.d_r32.reserve((s.nc + 1) * 4) || !s.out_o.reserve((s.nc + 1) * 4)))) {
       hipSetDevice(ctx->device);
       return EMQX_GM_ENOMEM;
     }
     hipSetDevice(ctx->device);
-    const uint64_t c0 = s.c0, nc = s.nc, b0 = to[c0], b1 = to[c0 + nc];
-    uint32_t* o = s.in_o.as<uint32_t>();
+    const uint64_t c0 = s.c0, nc = s.nc;
+    uint16_t* l = s.in_l.as<uint16_t>();
     uint8_t* b = direct_in ? nullptr : s.in_b.as<uint8_t>();
+    s.long_topic.store(0);
+    std::atomic<int>* lt = &s.long_topic;
     const uint64_t parts = nc < 65536 ? 1 : T;
     for (uint64_t p = 0; p < parts; ++p) {
       const uint64_t a = c0 + nc * p / parts, e = c0 + nc * (p + 1) / parts;
-      s.stage_f.push_back(W.submit([=, &bad] {
-        for (uint64_t j = a; j < e; ++j) {
-          if (to[j + 1] < to[j]) {
-            bad.store(1);
-            return;
-          }
-          o[j - c0] = uint32_t(to[j] - b0);
-        }
-        if (to[a] < b0 || to[e] > b1) {  // inside the chunk's text (plan() checked b0 <= b1)
-          bad.store(1);
-          return;
-        }
-        if (b && e > a) std::memcpy(b + (to[a] - b0), tb + to[a], to[e] - to[a]);
-        if (e == c0 + nc) {
-          o[nc] = uint32_t(to[e] - b0);
-          if (b) std::memset(b + (to[e] - b0), 0, 64);
-        }
-      }));
+      s.stage_f.push_back(W.submit([=, &bad] { stage_part(tb, to, c0, nc, a, e, l, b, bad, *lt); }));
     }
     return 0;
   };
@@ -600,19 +632,10 @@ static int run_host_pipe(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8
     Slot& s = slot_of(i);
     join(s.stage_f);
     if (bad.load()) return EMQX_GM_EINVAL;
-    hipStream_t h = hps[k]->h2d;
     hipSetDevice(mem[k]->device);
-    hipError_t e;
-    if (direct_in) {
-      e = s.nbytes ? hipMemcpyAsync(s.d_b.p, tb + to[s.c0], s.nbytes, hipMemcpyHostToDevice, h) : hipSuccess;
-      if (e == hipSuccess) e = hipMemsetAsync(s.d_b.as<uint8_t>() + s.nbytes, 0, 64, h);
-    } else {
-      e = hipMemcpyAsync(s.d_b.p, s.in_b.p, s.nbytes + 64, hipMemcpyHostToDevice, h);
-    }
-    if (e == hipSuccess) e = hipMemcpyAsync(s.d_o32.p, s.in_o.p, (s.nc + 1) * 4, hipMemcpyHostToDevice, h);
-    if (e == hipSuccess) e = hipEventRecord(s.h2d, h);
+    const hipError_t e = send_in(s, to, direct_in ? tb + to[s.c0] : nullptr, hps[k]->h2d);
     hipSetDevice(ctx->device);
-    return e == hipSuccess ? 0 : EMQX_GM_EDEVICE;
+    return e == hipSuccess ? 0 : e == hipErrorOutOfMemory ? EMQX_GM_ENOMEM : EMQX_GM_EDEVICE;
   };
   // chunk i's match queued on its device
   auto submit = [&](int i) -> int {
@@ -623,8 +646,7 @@ static int run_host_pipe(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8
     int rc = 0;
     {
       std::lock_guard<std::recursive_mutex> lk(mc->mu);
-      if (hipStreamWaitEvent(mc->stream, s.h2d, 0) != hipSuccess ||
-          launch_off32_to_64(mc->stream, s.d_o32.as<uint32_t>(), s.nc + 1, s.d_o64.as<uint64_t>()))
+      if (hipStreamWaitEvent(mc->stream, s.h2d, 0) != hipSuccess || offsets_in(mc, mc->stream, s))
         rc = set_err(ctx, EMQX_GM_EDEVICE, "match: offsets to device");
       else
         rc = match_submit(mc, rix[k], s.d_b.as<uint8_t>(), s.d_o64.as<uint64_t>(), s.nc, flags | EMQX_GM_DEVICE_IO,
@@ -753,6 +775,8 @@ static int run_host_pipe(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8
   return 0;
 }
 
+uint64_t host_chunk_topics() { return std::max<uint64_t>(1024, env_u64("GM_HOST_CHUNK", 256u << 10)); }
+
 int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                    uint32_t flags, emqx_gm_csr* out) {
   // the devices: this context, then the members the index has replicas on
@@ -786,7 +810,7 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
       return set_err(ctx, EMQX_GM_EINVAL, "match: topic offsets not monotone");
     cb.push_back(hi);
   }
-  const char* pe = getenv("GM_HOST_PIPE");  // A/B: "serial" = the one-device serial path for every batch
+  const char* pe = knob("GM_HOST_PIPE");  // A/B: "serial" = the one-device serial path for every batch
   const bool serial = pe && !std::strcmp(pe, "serial") && K == 1;
   if (cb.size() <= 2 || serial) return run_host_serial(ctx, idx, tb, to, n, flags, out);
   return run_host_pipe(ctx, idx, tb, to, n, flags, mem, rix, cb, out);

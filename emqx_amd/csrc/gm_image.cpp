@@ -429,6 +429,37 @@ int index_import(emqx_gm_ctx* ctx, const uint8_t* img, uint64_t size, const void
   for (int i = 0; i < kPtrs; ++i)
     if (*pf[i]) *pf[i] = B + (reinterpret_cast<uintptr_t>(*pf[i]) - 1);
   if (idx->dev_flen) idx->dev_flen = reinterpret_cast<uint16_t*>(B + (reinterpret_cast<uintptr_t>(idx->dev_flen) - 1));
+  // The updatable line's host mirror, by the build's policy (gm_index.cpp): kept
+  // for tables up to kEagerMirrorBytes unless EMQX_GM_OPEN_MIRROR_* says
+  // otherwise, so a joining node's first update does not pay a silent download.
+  // An image that carries the tables gives the mirror its bytes directly (the
+  // device tables ARE those bytes); a device-blob import downloads them.
+  if (Mirror* M = idx->mirror) {
+    bool eager = M->blob_size <= kEagerMirrorBytes;
+    if (const char* pol = knob("GM_MIRROR")) eager = !std::strcmp(pol, "eager");
+    if (ctx->open_flags & EMQX_GM_OPEN_MIRROR_EAGER) eager = true;
+    if (ctx->open_flags & EMQX_GM_OPEN_MIRROR_LAZY) eager = false;
+    if (eager && M->blob_size <= h.dev_bytes) {
+      if (!d_blob) {
+        const double t0 = now_ms();
+        M->blob.resize(M->blob_size);
+        const uint8_t* src = img + h.sec_off[5];
+        const size_t nb = M->blob_size;
+        const unsigned T = nb < (size_t(1) << 24) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (unsigned r = 1; r < T; ++r)
+          th.emplace_back([&, r] { std::memcpy(M->blob.data() + nb * r / T, src + nb * r / T, nb * (r + 1) / T - nb * r / T); });
+        std::memcpy(M->blob.data(), src, nb / T);
+        for (auto& t : th) t.join();
+        tl_ustats.mirror_loaded = 1;
+        tl_ustats.mirror_bytes = nb;
+        tl_ustats.mirror_ms = now_ms() - t0;
+      } else if (const int rc = load_mirror_blob(ctx, idx.get())) {
+        free_index(idx.release());
+        return rc;
+      }
+    }
+  }
   *out = idx.release();
   return EMQX_GM_OK;
 }
@@ -497,6 +528,7 @@ hipError_t download_blob(uint8_t* host, const uint8_t* dev, size_t bytes) {
 int load_mirror_blob(emqx_gm_ctx* ctx, emqx_gm_index* idx) {
   Mirror& M = *idx->mirror;
   if (!M.blob.empty() || !idx->dev_base) return EMQX_GM_OK;
+  const double t0 = now_ms();
   hipSetDevice(idx->device);
   if (ctx) GM_HIP(ctx, hipStreamSynchronize(ctx->stream));
   M.blob.resize(M.blob_size);  // (left unwritten: the download below fills every byte)
@@ -505,6 +537,9 @@ int load_mirror_blob(emqx_gm_ctx* ctx, emqx_gm_index* idx) {
     HostBytes().swap(M.blob);
     return set_err(ctx, EMQX_GM_EDEVICE, std::string("index_update: mirror download: ") + hipGetErrorString(e));
   }
+  tl_ustats.mirror_loaded = 1;  // (emqx_gm_last_update_stats: what this call did)
+  tl_ustats.mirror_bytes = M.blob_size;
+  tl_ustats.mirror_ms = now_ms() - t0;
   return EMQX_GM_OK;
 }
 

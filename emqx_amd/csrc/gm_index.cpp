@@ -301,7 +301,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   auto* idx = new emqx_gm_index;
   idx->device = ctx ? ctx->device : -1;
   // GM_INDEX_STATS: phase times on stderr (diagnostics)
-  const bool stats = getenv("GM_INDEX_STATS") != nullptr;
+  const bool stats = knob("GM_INDEX_STATS") != nullptr;
   auto t_last = std::chrono::steady_clock::now();
   auto phase = [&](const char* what) {
     if (!stats) return;
@@ -516,7 +516,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   std::vector<TrieRun> runs;
   {
     // GM_TRIE_RUNS: the number of runs asked for (1: the serial build; tests)
-    const char* rk = getenv("GM_TRIE_RUNS");
+    const char* rk = knob("GM_TRIE_RUNS");
     const uint32_t want = rk ? std::max(1u, uint32_t(strtoul(rk, nullptr, 10)))
                              : (nf < 200000 || T == 1) ? 1u : 4u * T;
     uint32_t f0 = 0;
@@ -805,7 +805,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     });
   }
   phase("v1: buckets");
-  const bool verify_tables = getenv("GM_INDEX_VERIFY") != nullptr;
+  const bool verify_tables = knob("GM_INDEX_VERIFY") != nullptr;
   std::vector<EdgeMap> tabs;
   tabs.reserve(EDGE_DEPTHS);
   for (int d = 0; d < EDGE_DEPTHS; ++d) tabs.emplace_back(by_tab[d].empty() ? 1 : 0);  // (sized on its thread)
@@ -890,23 +890,23 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
     if ((nodes[i].flags & NF_HAS_EXACT) && nodes[i].kind != 2) x_parents[hot_table(nodes[i].depth + 1)]++;
   {
     uint64_t lo = 4096, hi = 131072;
-    if (const char* e = getenv("GM_MPH_MIN_KEYS")) lo = strtoull(e, nullptr, 10);
-    if (const char* e = getenv("GM_MPH_MAX_KEYS")) hi = strtoull(e, nullptr, 10);
+    if (const char* e = knob("GM_MPH_MIN_KEYS")) lo = strtoull(e, nullptr, 10);
+    if (const char* e = knob("GM_MPH_MAX_KEYS")) hi = strtoull(e, nullptr, 10);
     // GM_MPH_TABLES: A/B knob, a bit mask of the tables to place this way (overrides the bounds)
-    const char* mt = getenv("GM_MPH_TABLES");
+    const char* mt = knob("GM_MPH_TABLES");
     const uint32_t mask = mt ? uint32_t(strtoul(mt, nullptr, 0)) : 0u;
     for (int t = 1; t < HOT_TABLES - 1; ++t) {  // (the shared last table mixes depths: open addressing)
-      if (getenv("GM_NO_MPH") || !hot_n[t]) continue;
+      if (knob("GM_NO_MPH") || !hot_n[t]) continue;
       const bool small = hot_n[t] >= lo && hot_n[t] <= hi;
-      const bool filtered = x_keys[t] >= 4 * x_parents[t] && hot_n[t] <= (1u << 20) && !getenv("GM_MPH_NO_FILTERED");
+      const bool filtered = x_keys[t] >= 4 * x_parents[t] && hot_n[t] <= (1u << 20) && !knob("GM_MPH_NO_FILTERED");
       if (mt ? !((mask >> t) & 1u) : !(small || filtered)) continue;
       uint64_t slack = 16;  // GM_MPH_SLACK (A/B knob): spare slots = keys / slack (6 keys per bucket need 1/16 to place without overflow)
-      if (const char* e = getenv("GM_MPH_SLACK")) slack = std::max<uint64_t>(4, strtoull(e, nullptr, 10));
+      if (const char* e = knob("GM_MPH_SLACK")) slack = std::max<uint64_t>(4, strtoull(e, nullptr, 10));
       mph_cap[t] = uint32_t(hot_n[t] + hot_n[t] / slack + 16);
       // GM_MPH_LAMBDA (A/B knob): keys per bucket -- fewer bucket words (an L2-resident
       // table) against a fuller 48-bit Bloom filter and harder displacement searches
       uint32_t lam = MPH_LAMBDA;
-      if (const char* e = getenv("GM_MPH_LAMBDA")) lam = std::max<uint32_t>(1, std::min<uint32_t>(16, uint32_t(atoi(e))));
+      if (const char* e = knob("GM_MPH_LAMBDA")) lam = std::max<uint32_t>(1, std::min<uint32_t>(16, uint32_t(atoi(e))));
       mph_nb[t] = uint32_t((hot_n[t] + lam - 1) / lam);
       mph_off[t] = mph_total;
       mph_total += mph_nb[t];
@@ -916,16 +916,21 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   uint64_t mph_ovf_n[HOT_TABLES] = {0};
   std::vector<uint64_t> mph_word(mph_total + 1, 0);
   uint64_t hot_sparse = 0;
-  if (const char* e = getenv("GM_HOT_SPARSE")) hot_sparse = std::min<uint64_t>(1u << 22, strtoull(e, nullptr, 10));
-  uint64_t hot_load_pct = 25;  // load factor (%); GM_HOT_LOAD_PCT: A/B knob (10..90)
-  if (const char* e = getenv("GM_HOT_LOAD_PCT")) hot_load_pct = std::min<uint64_t>(90, std::max<uint64_t>(10, strtoull(e, nullptr, 10)));
+  if (const char* e = knob("GM_HOT_SPARSE")) hot_sparse = std::min<uint64_t>(1u << 22, strtoull(e, nullptr, 10));
+  // load factor (%) of the hash-placed hot tables; GM_HOT_LOAD_PCT: A/B knob (10..90).
+  // 0.15 (round 6): the walk's found probes end at their home slot more often
+  // and its failed ones stop sooner -- the kernel against 0.25, same box: C2
+  // -0.5 %, C3 -1.0 % (profiles/r05_r, r05_q), C5 -3.0 % (17.24 -> 16.72 ms,
+  // profiles/r06_a/ab.txt) for 1.38x the table bytes (C5: 38.4 -> 53.0 GB of 288)
+  uint64_t hot_load_pct = 15;
+  if (const char* e = knob("GM_HOT_LOAD_PCT")) hot_load_pct = std::min<uint64_t>(90, std::max<uint64_t>(10, strtoull(e, nullptr, 10)));
   for (int t = 0; t < HOT_TABLES; ++t) {
-    // load <= 0.25: shorter probe chains beat a smaller footprint (C2, fused
-    // kernel, 4-8 bit/key edge filter: load 0.40 / 0.35 / 0.30 / 0.25 / 0.20 /
-    // 0.15 / 0.10 -> 9.73 / 9.51 / 9.39 / 9.20 / 9.22 / 9.24 / 9.35 ms);
-    // at least 8 slots so the probe loop always finds an empty one
+    // a low load: shorter probe chains beat a smaller footprint (C2, round 2's
+    // fused kernel, 4-8 bit/key edge filter: load 0.40 / 0.35 / 0.30 / 0.25 /
+    // 0.20 / 0.15 / 0.10 -> 9.73 / 9.51 / 9.39 / 9.20 / 9.22 / 9.24 / 9.35 ms;
+    // round 6 above); at least 8 slots so the probe loop always finds an empty one
     uint64_t pct = hot_load_pct;
-    if (const char* e = getenv("GM_HOT_LOAD_PCT_UPPER"))  // A/B knob: load of the depth 1-2 tables
+    if (const char* e = knob("GM_HOT_LOAD_PCT_UPPER"))  // A/B knob: load of the depth 1-2 tables
       if (t <= 2) pct = std::min<uint64_t>(90, std::max<uint64_t>(10, strtoull(e, nullptr, 10)));
     hot_cap[t] = hot_n[t] ? std::max<uint64_t>(8, hot_n[t] * 100 / pct + 1) : 0;
     // GM_HOT_SPARSE=65536 (A/B knob, off by default until measured): a small
@@ -968,8 +973,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // is in (the next depth's keys hold them).  The shared last table keeps
   // plain linear probing (its earlier depths' ids are already referenced).
   std::vector<uint32_t> occ;  // old node index per slot of the table being placed
-  const bool rh_insert = getenv("GM_HOT_RH_INSERT") != nullptr;  // A/B: RH insertion key by key
-  const bool verify = getenv("GM_INDEX_VERIFY") != nullptr;
+  const bool rh_insert = knob("GM_HOT_RH_INSERT") != nullptr;  // A/B: RH insertion key by key
+  const bool verify = knob("GM_INDEX_VERIFY") != nullptr;
   auto fill_slot = [&](HotSlot& o, const HNode& h) {
     o.sig = h.sig;
     o.hf = hf_of(h);
@@ -1218,8 +1223,8 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // built for larger tables only; GM_CHAIN=0/1 forces (A/B knob).
   uint64_t n_chain = 0;
   bool chains = hot_total * sizeof(HotSlot) > (256ull << 20);
-  if (const char* e = getenv("GM_CHAIN")) chains = atoi(e) != 0;
-  if (getenv("GM_NO_CHAIN")) chains = false;
+  if (const char* e = knob("GM_CHAIN")) chains = atoi(e) != 0;
+  if (knob("GM_NO_CHAIN")) chains = false;
   if (chains) {
     std::vector<uint32_t> nex(NN, 0), exch(NN, NONE);
     for (uint64_t i = 1; i < NN; ++i)
@@ -1249,7 +1254,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
       ++n_chain;
     }
   }
-  if (getenv("GM_INDEX_STATS")) {  // diagnostics: the hot tables' sizes (stderr)
+  if (knob("GM_INDEX_STATS")) {  // diagnostics: the hot tables' sizes (stderr)
     fprintf(stderr, "[gm_index] chain nodes %llu\n", (unsigned long long)n_chain);
     uint64_t inl_n = 0;
     for (uint64_t i = 1; i < NN; ++i) inl_n += inl[i];
@@ -1275,19 +1280,19 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   uint64_t efilt_off[HOT_TABLES] = {0}, efilt_total = 0;
   uint32_t efilt_mask[HOT_TABLES] = {0};
   for (int t = 0; t < HOT_TABLES; ++t) {
-    if (getenv("GM_NO_EDGE_FILTER")) break;  // A/B knob
-    if (!ex_edges[t] || (ex_edges[t] < 4 * ex_parents[t] && !getenv("GM_EFILT_ALL"))) continue;  // A/B knob
+    if (knob("GM_NO_EDGE_FILTER")) break;  // A/B knob
+    if (!ex_edges[t] || (ex_edges[t] < 4 * ex_parents[t] && !knob("GM_EFILT_ALL"))) continue;  // A/B knob
     if (mph_cap[t]) continue;  // an MPH table's bucket words carry its filter
     // 4-8 bits per key: the filter is a dependent read in front of every exact
     // probe and pays only while it stays in L2 (C2 A/B, bits per key -> kernel ms:
     // 16-32 10.04, 8-16 9.54, 4-8 9.37, 2-4 9.40, 1-2 9.60, no filter 9.50)
     uint64_t div = 8;  // GM_EFILT_DIV: A/B knob (words = keys / div)
-    if (const char* e = getenv("GM_EFILT_DIV")) div = std::min<uint64_t>(64, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
+    if (const char* e = knob("GM_EFILT_DIV")) div = std::min<uint64_t>(64, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
     const uint64_t words = std::max<uint64_t>(32, next_pow2(ex_edges[t] / div + 1));
     // an L2 budget (a filter that does not stay in L2 costs more than it saves:
     // C3's 4 MB one took its kernel from 14.1 to 14.9 ms); GM_EFILT_MAX_KB: A/B knob
     uint64_t max_kb = 1024;
-    if (const char* e = getenv("GM_EFILT_MAX_KB")) max_kb = strtoull(e, nullptr, 10);
+    if (const char* e = knob("GM_EFILT_MAX_KB")) max_kb = strtoull(e, nullptr, 10);
     if (words * 4 > max_kb * 1024) continue;
     efilt_off[t] = efilt_total;
     efilt_mask[t] = uint32_t(words - 1);
@@ -1314,7 +1319,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // the slots holding words are ever read, so the sparse table's cache
   // footprint stays ~one line per word.  GM_DICT_MUL (A/B knob): slots per word.
   uint64_t dslots = std::max<uint64_t>(nw * 4 + 4, std::min<uint64_t>(nw * 32, 1ull << 17));
-  if (const char* e = getenv("GM_DICT_MUL"))
+  if (const char* e = knob("GM_DICT_MUL"))
     dslots = nw * std::min<uint64_t>(64, std::max<uint64_t>(1, strtoull(e, nullptr, 10))) + 4;
   uint64_t dcap = next_pow2(dslots);
   std::vector<DictSlot> dict(dcap, DictSlot{0, DICT_EMPTY_LEN, 0});
@@ -1365,7 +1370,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   // keep_mirror: the layout reserves update headroom and the index carries a
   // Mirror; its host copy of the blob is kept from here (eager) or downloaded
   // on the line's first update (load_mirror_blob), see EMQX_GM_OPEN_MIRROR_*
-  const bool keep_mirror = host_mirror || (ctx && !gids && !getenv("GM_NO_MIRROR"));
+  const bool keep_mirror = host_mirror || (ctx && !gids && !knob("GM_NO_MIRROR"));
   const uint64_t nodes_cap = keep_mirror ? NN + NN / 4 + 1024 : NN;
   const uint64_t arena_cap = keep_mirror ? arena.size() + arena.size() / 4 + 65536 : arena.size();
   const uint64_t flen_cap = keep_mirror ? uint64_t(nf) + nf / 4 + 1024 : nf;
@@ -1412,7 +1417,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   idx->dev_bytes = total;
   bool eager = host_mirror || o_soff <= kEagerMirrorBytes;  // (keep_mirror: the mirror's policy)
   if (keep_mirror && !host_mirror) {
-    if (const char* pol = getenv("GM_MIRROR")) eager = !strcmp(pol, "eager");  // A/B and test knob
+    if (const char* pol = knob("GM_MIRROR")) eager = !strcmp(pol, "eager");  // A/B and test knob
     if (ctx->open_flags & EMQX_GM_OPEN_MIRROR_EAGER) eager = true;
     if (ctx->open_flags & EMQX_GM_OPEN_MIRROR_LAZY) eager = false;
   }
@@ -1509,7 +1514,7 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.mph_ovf = mph_ovf;
   v.l1_bypass = 0;
   v.hot_policy = 1;  // (sc1, for the tables GM_L1_BYPASS selects; both A/B knobs, read per call too)
-  if (const char* e = getenv("GM_L1_BYPASS")) v.l1_bypass = uint32_t(strtoul(e, nullptr, 0));
+  if (const char* e = knob("GM_L1_BYPASS")) v.l1_bypass = uint32_t(strtoul(e, nullptr, 0));
   for (int t = 0; t < HOT_TABLES; ++t) {
     v.mph_off[t] = mph_off[t];
     v.mph_nb[t] = mph_nb[t];
@@ -1521,9 +1526,9 @@ int build_index(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_
   v.flags = 0;
   for (int t = 0; t < HOT_TABLES; ++t)
     if (hot_cap[t] * sizeof(HotSlot) >= (1ull << 31)) v.flags |= IX_HOT_FLAT;
-  if (getenv("GM_HOT_FLAT")) v.flags |= IX_HOT_FLAT;  // test knob: exercise the flat-load path
+  if (knob("GM_HOT_FLAT")) v.flags |= IX_HOT_FLAT;  // test knob: exercise the flat-load path
   // every per-depth table is Robin Hood ordered; the shared last one is not (GM_NO_RH_EXIT: A/B knob)
-  v.rh_mask = getenv("GM_NO_RH_EXIT") ? 0u : (1u << (HOT_TABLES - 1)) - 1u;
+  v.rh_mask = knob("GM_NO_RH_EXIT") ? 0u : (1u << (HOT_TABLES - 1)) - 1u;
   v.n_nodes = uint32_t(NN);
   v.n_filters = nf;
   v.plus_word = plus_word;
@@ -1566,11 +1571,14 @@ struct SpareBlob {
 };
 constexpr int kSpareDevices = 64;
 std::mutex g_spare_mu;
-SpareBlob g_spare[kSpareDevices];
+// per device, oldest first: at most one per context open there (a
+// multi-device context listing a device twice opens two: each replica line
+// frees and reuses its own size)
+std::vector<SpareBlob> g_spare[kSpareDevices];
 int g_ctx_open[kSpareDevices] = {};  // (under g_spare_mu)
 // blobs below this size allocate quickly anyway (GM_SPARE_BLOB_MIN, bytes; 0: off)
 size_t spare_min() {
-  const char* e = getenv("GM_SPARE_BLOB_MIN");
+  const char* e = knob("GM_SPARE_BLOB_MIN");
   return e ? size_t(strtoull(e, nullptr, 10)) : size_t(256) << 20;
 }
 }  // namespace
@@ -1579,17 +1587,21 @@ void* take_spare_blob(int device, size_t bytes) {
   const size_t lo = spare_min();
   if (device < 0 || device >= kSpareDevices || !lo || bytes < lo) return nullptr;
   std::lock_guard<std::mutex> lk(g_spare_mu);
-  SpareBlob& s = g_spare[device];
-  if (!s.p || s.bytes < bytes || s.bytes - bytes > bytes / 4) return nullptr;
-  void* p = s.p;
-  s = SpareBlob{};
+  auto& v = g_spare[device];
+  size_t best = v.size();
+  for (size_t i = 0; i < v.size(); ++i)
+    if (v[i].bytes >= bytes && v[i].bytes - bytes <= bytes / 4 && (best == v.size() || v[i].bytes < v[best].bytes))
+      best = i;
+  if (best == v.size()) return nullptr;
+  void* p = v[best].p;
+  v.erase(v.begin() + best);
   return p;
 }
 
 void give_spare_blob(int device, void* p, size_t bytes) {
   if (!p) return;
   const size_t lo = spare_min();
-  void* drop = p;
+  std::vector<void*> drop{p};
   bool keep = device >= 0 && device < kSpareDevices && lo && bytes >= lo;
   if (keep) {
     std::lock_guard<std::mutex> lk(g_spare_mu);
@@ -1599,10 +1611,15 @@ void give_spare_blob(int device, void* p, size_t bytes) {
     // hipFree waits for the device's work; so does keeping the blob for reuse
     (void)hipDeviceSynchronize();
     std::lock_guard<std::mutex> lk(g_spare_mu);
-    std::swap(drop, g_spare[device].p);  // the newest blob stays (a line of updates frees its own size)
-    g_spare[device].bytes = bytes;
+    auto& v = g_spare[device];
+    drop.clear();
+    v.push_back(SpareBlob{p, bytes});  // the newest stays (a line of updates frees its own size)
+    while (v.size() > size_t(std::max(1, g_ctx_open[device]))) {
+      drop.push_back(v.front().p);
+      v.erase(v.begin());
+    }
   }
-  if (drop) (void)hipFree(drop);
+  for (void* q : drop) (void)hipFree(q);
 }
 
 void note_ctx_open(int device) {
@@ -1619,16 +1636,13 @@ void note_ctx_close(int device) {
 
 void trim_spare_blob(int device) {
   if (device < 0 || device >= kSpareDevices) return;
-  void* p;
+  std::vector<SpareBlob> v;
   {
     std::lock_guard<std::mutex> lk(g_spare_mu);
-    p = g_spare[device].p;
-    g_spare[device] = SpareBlob{};
+    v.swap(g_spare[device]);
   }
-  if (p) {
-    (void)hipSetDevice(device);
-    (void)hipFree(p);
-  }
+  if (!v.empty()) (void)hipSetDevice(device);
+  for (const SpareBlob& b : v) (void)hipFree(b.p);
 }
 
 void free_index(emqx_gm_index* idx) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <cstdint>
 #include <map>
 #include <mutex>
@@ -13,6 +14,7 @@
 #include <vector>
 
 #include "../../include/emqx_gpu_match.h"
+#include "../../include/emqx_gm_ext.h"
 #include "gm_common.h"
 #include "gm_filters.h"
 
@@ -172,10 +174,29 @@ struct emqx_gm_ctx {
   // index made through this context carries a replica per member
   // (emqx_gm_index::reps).
   std::vector<emqx_gm_ctx*> members;
+  emqx_gm_ctx* parent = nullptr;    // a member: its multi-device context
+  std::atomic<uint32_t> rr{0};      // round-robin start of the next small host-buffer call (gm_api.cpp)
 };
 
 namespace gm {
 struct OverlayState;
+
+// The library's A/B and diagnostic knobs (GM_* environment variables: table
+// layout, load factor, walk form, staging, update path, host pipeline) are
+// read only when EMQX_GM_AB is set (non-empty, not "0"), so a library loaded
+// into a BEAM runs its one default layout and walk whatever else the host's
+// environment holds (the list: emqx_gpu_match.h).  Read per call, so a test
+// or an A/B script sets it beside the knob.
+inline const char* knob(const char* name) {
+  const char* ab = getenv("EMQX_GM_AB");
+  if (!ab || !*ab || (ab[0] == '0' && !ab[1])) return nullptr;
+  return getenv(name);
+}
+
+// What the calling thread's last index call did (emqx_gm_last_update_stats):
+// the entry points reset it, the update paths fill it in.
+extern thread_local emqx_gm_update_stats tl_ustats;
+double now_ms();
 
 // The id change of an in-place update, from O(delta) lists: prev ids `dels`
 // deleted (ascending), new filter k (byte order) inserted with addpos[k] prev
@@ -262,6 +283,7 @@ struct emqx_gm_index {
   // of an older replica it shares as this snapshot shares its owner's).  Owned:
   // released with this snapshot.
   std::vector<emqx_gm_index*> reps;
+  bool reused_blob = false;  // (replicate_index: dev_base was a released snapshot's blob)
 };
 
 namespace gm {
@@ -321,6 +343,16 @@ int unpermute_rows(emqx_gm_ctx* ctx, uint64_t n, const uint32_t* d_perm, const u
                    uint32_t flags, emqx_gm_csr* out);
 int scan_lengths(emqx_gm_ctx* ctx, const uint64_t* len, uint64_t n, uint64_t* out);
 
+// A replica an update makes on member context m from prev's replica `prev`
+// (gm_overlay.cpp patch_update, gm_subs.cpp update_subs): each member applies
+// the same O(delta) plan to its own device copy at the same time as the first
+// device -- the reference's every-node-applies-the-delta replication
+// (apps/emqx/src/emqx_router_utils.erl:33-38, emqx_trie.erl:114-136).
+struct RepTarget {
+  emqx_gm_ctx* m = nullptr;
+  emqx_gm_index* prev = nullptr;
+  emqx_gm_index* out = nullptr;  // made by the update (owned by the caller until attached)
+};
 // gm_overlay.cpp — incremental index maintenance.  An
 // overlay snapshot = an immutable base snapshot (shared, retained) minus
 // tombstoned base filters plus a small delta index over the inserted filters.
@@ -349,9 +381,10 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
 // new ids of dset's filters in byte order.
 // trie_only: the new blob holds the tables up to the subscriber CSR only (the
 // caller gives the snapshot a CSR of its own).
+// reps (optional): the member replicas to patch alongside (RepTarget::out set on success).
 int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>& tomb,
                  const std::set<std::string>& dset, emqx_gm_index** out, std::vector<uint32_t>* rmap_out = nullptr,
-                 bool trie_only = false);
+                 bool trie_only = false, std::vector<RepTarget>* reps = nullptr);
 bool well_formed_filter(const uint8_t* p, uint64_t len);
 // gm_image.cpp: index images (emqx_gm_index_export / _import) and the lazy host mirror
 int index_export(emqx_gm_ctx* ctx, const emqx_gm_index* idx, uint32_t flags, uint8_t* buf, uint64_t* size);
@@ -426,10 +459,14 @@ int set_err(emqx_gm_ctx* ctx, int code, const std::string& msg);
 int launch_off32_to_64(hipStream_t st, const uint32_t* in, uint64_t n1, uint64_t* out);
 int launch_off64_to_32(hipStream_t st, const uint64_t* in, uint64_t n1, uint32_t* out);
 int launch_add_u64(hipStream_t st, uint64_t* p, uint64_t n1, uint64_t add);
+// the host path's u16 topic lengths -> u64 offsets (n + 1 entries, an exclusive scan) on stream st
+int scan_len16(emqx_gm_ctx* ctx, hipStream_t st, const uint16_t* len, uint64_t n, uint64_t* out);
 // gm_host.cpp: emqx_gm_match on host buffers, chunked and pipelined (H2D / match / D2H overlap)
 int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                    uint32_t flags, emqx_gm_csr* out);
 void free_host_pipe(emqx_gm_ctx* ctx);
+// the topics of one host-pipeline chunk at most (a call this small runs whole on one device)
+uint64_t host_chunk_topics();
 // gm_multi.cpp: multi-device contexts (emqx_gm_opts.n_devices).
 // A copy of flat snapshot `src` (any device) on member context m's device:
 // the host tables shared or copied, the device tables copied device to device
@@ -438,13 +475,24 @@ void free_host_pipe(emqx_gm_ctx* ctx);
 // share is that owner's replica), those tables shared.  No host mirror (the
 // primary snapshot's line owns it).
 int replicate_index(emqx_gm_ctx* m, const emqx_gm_index* src, emqx_gm_index* share, emqx_gm_index** out);
+// f(k) for k = 0..K-1 at once, one thread each (k = 0 on the calling thread);
+// the first failure's code, its message set on the calling thread
+int run_all(int K, const std::function<int(int)>& f);
+// the targets of an update of `prev` through ctx: one per member when prev has
+// its replicas there, else none (the result is copied by replicate_result)
+std::vector<RepTarget> rep_targets(emqx_gm_ctx* ctx, emqx_gm_index* prev);
+// a new replica on m carrying src's host fields (filter table, subscriber
+// table, info; shared bases) and no device tables yet
+emqx_gm_index* replica_shell(emqx_gm_ctx* m, const emqx_gm_index* src);
+// attach the targets' replicas to out (all made), or free them (rc != 0)
+int attach_replicas(emqx_gm_index* out, std::vector<RepTarget>& t, int rc);
 // After an index call on a multi-device context made `out` from `prev` (NULL
-// for a build / import): give `out` its replicas.  A flat result is copied
-// (sharing prev's replica's tables when out shares prev's); an overlay result
-// repeats the call on each member (`redo(member, prev's replica, &rep)`).  On
-// failure `out` is released and *out_p cleared.
-int replicate_result(emqx_gm_ctx* ctx, emqx_gm_index* prev, emqx_gm_index** out_p,
-                     const std::function<int(emqx_gm_ctx*, emqx_gm_index*, emqx_gm_index**)>& redo);
+// for a build / import): give `out` its replicas unless the update already
+// made them (an in-place patch or update_subs applies its delta on every
+// device, RepTarget).  A flat result is copied device to device in a tree
+// (sharing prev's replica's tables when out shares prev's); an overlay stays
+// on the first device.  On failure `out` is released and *out_p cleared.
+int replicate_result(emqx_gm_ctx* ctx, emqx_gm_index* prev, emqx_gm_index** out_p);
 // emqx_gm_fanout of host rows over a multi-device context's replicas (one
 // slice per device, one page-locked result); small batches: run_fanout
 int run_fanout_multi(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,

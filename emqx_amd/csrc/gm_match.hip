@@ -2680,7 +2680,7 @@ int apply_patch_device(emqx_gm_ctx* ctx, void* dst, const void* src, size_t byte
   for (int t = 0; t < HOT_TABLES; ++t) n_hot = std::max<uint64_t>(n_hot, v.hot_off[t] + v.hot_cap[t]);
   const uint64_t hot_end = o_hot + n_hot * sizeof(HotSlot), nodes_end = o_nodes + n_nodes * sizeof(Node);
   if (hot_end > bytes || nodes_end > bytes) return set_err(ctx, EMQX_GM_EINVAL, "index_update: tables outside the blob");
-  const bool unfused = getenv("GM_UPDATE_UNFUSED") != nullptr;
+  const bool unfused = knob("GM_UPDATE_UNFUSED") != nullptr;
   // fused (one pass): the two id-bearing tables must not overlap
   const bool fused = !unfused && (hot_end <= o_nodes || nodes_end <= o_hot);
   // coalesce overlapping / adjacent ranges only (the bytes between two written
@@ -3043,7 +3043,7 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
 // split2 (k_walk expanding frontier entries in pairs).
 enum MainKind { MAIN_SPLIT, MAIN_SPLITW8, MAIN_SPLIT2, MAIN_COOP, MAIN_FUSED };
 MainKind main_kind() {
-  const char* e = getenv("GM_MATCH_MAIN");
+  const char* e = knob("GM_MATCH_MAIN");
   static const struct { const char* name; MainKind kind; } names[] = {
       {"split", MAIN_SPLIT}, {"splitw8", MAIN_SPLITW8}, {"split2", MAIN_SPLIT2}, {"coop", MAIN_COOP},
       {"fused", MAIN_FUSED}};
@@ -3060,7 +3060,7 @@ constexpr int LISTED_FC = 16;  // frontier capacity of the listed pass
 // slots loaded G at a time.  Measured at C2: 3.54 / 3.42 / 3.90 ms (G = 5
 // needs 80 VGPRs, 6 waves per SIMD).  Read per call, so tests cover all three.
 int tok_group() {
-  const char* e = getenv("GM_TOK_GROUP");
+  const char* e = knob("GM_TOK_GROUP");
   const int v = e ? atoi(e) : 3;
   return (v == 1 || v == 5) ? v : 3;
 }
@@ -3069,7 +3069,7 @@ int tok_group() {
 // text, word ids, headers, staging and counts as nt loads / stores (default;
 // C2: 12.15 -> 12.03 ms for the split pair, 10.45 -> 10.24 ms fused), 0 = plain.
 bool nt_streams() {
-  const char* e = getenv("GM_NT");
+  const char* e = knob("GM_NT");
   return !e || atoi(e) != 0;
 }
 
@@ -3085,17 +3085,17 @@ bool nt_streams() {
 // most 64 blocks (calls up to ~4M topics: C1) ends after its first launch and
 // k_assemble_c sums the block prefixes itself.
 bool sums_mode() {
-  const char* e = getenv("GM_SCAN_SUMS");
+  const char* e = knob("GM_SCAN_SUMS");
   return !e || atoi(e) != 0;
 }
 
 uint64_t asm_stream_min() {
-  const char* e = getenv("GM_ASM_STREAM");
+  const char* e = knob("GM_ASM_STREAM");
   return e ? strtoull(e, nullptr, 10) : 0;
 }
 
 bool stage_compact() {
-  const char* e = getenv("GM_STAGE_COMPACT");
+  const char* e = knob("GM_STAGE_COMPACT");
   return !e || atoi(e) != 0;
 }
 struct CmpBufs {
@@ -3148,7 +3148,7 @@ void launch_tokenize(hipStream_t st, uint64_t nblk, const uint8_t* tb, const uin
 // the CUs).  Kernels index by t_base + their own grid, so the layouts are
 // those of one launch.
 int overlap_chunks() {
-  const char* e = getenv("GM_OVERLAP");
+  const char* e = knob("GM_OVERLAP");
   const int v = e ? atoi(e) : 1;
   return v < 1 ? 1 : (v > 8 ? 8 : v);
 }
@@ -3205,7 +3205,7 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
   }
 #endif
   if (main_kind() == MAIN_FUSED) {
-    const char* pe = getenv("GM_FUSED_PRIO");  // A/B knob (read per call): 0 = every phase at priority 0
+    const char* pe = knob("GM_FUSED_PRIO");  // A/B knob (read per call): 0 = every phase at priority 0
     const bool tp = !pe || atoi(pe) != 0;
     uint32_t* const tl = cb ? cb->tlen : nullptr;
     uint8_t* const c8 = cb ? cb->cnt8 : nullptr;
@@ -3298,7 +3298,7 @@ void launch_match(emqx_gm_ctx* ctx, const IndexView& v, const uint8_t* tb, const
   // pass queued rows, instead of an (almost always idle) launch per call.
   // GM_LISTED_DEFER=0: launch it here (A/B knob).
   if (cb && main_kind() == MAIN_FUSED) {
-    const char* le = getenv("GM_LISTED_DEFER");
+    const char* le = knob("GM_LISTED_DEFER");
     if (!le || atoi(le) != 0) {
       *listed_deferred = true;
       return;
@@ -3504,7 +3504,7 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
 
   cmp = main_kind() == MAIN_FUSED && stage_compact() && uint64_t(idx->view.n_filters) < (1ull << CMP_SHIFT);
   if (cmp) {
-    const char* le = getenv("GM_LISTED_CAP");  // (tests: listed rows past it go to the slow path)
+    const char* le = knob("GM_LISTED_CAP");  // (tests: listed rows past it go to the slow path)
     cmpb.lcap = std::min<uint64_t>(n, le ? strtoull(le, nullptr, 10) : (1u << 20));
     c_tlen = PoolBuf(ctx->pool, n_tiles * 4 + 16);
     c_cnt8 = PoolBuf(ctx->pool, n + 64);
@@ -3523,12 +3523,12 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   if (!timed) main_ev0 = main_ev1 = nullptr;
   // GM_D0=0 (A/B knob, read per call): level 0 probed like any other level
   IndexView vcall = idx->view;
-  if (const char* de = getenv("GM_D0"))
+  if (const char* de = knob("GM_D0"))
     if (!atoi(de)) vcall.flags &= ~IX_D0;
-  if (const char* se = getenv("GM_STAGE_SC1"))  // A/B knobs (read per call)
+  if (const char* se = knob("GM_STAGE_SC1"))  // A/B knobs (read per call)
     if (atoi(se)) vcall.flags |= IX_STAGE_SC1;
-  if (const char* be = getenv("GM_L1_BYPASS")) vcall.l1_bypass = uint32_t(strtoul(be, nullptr, 0));
-  if (const char* pe = getenv("GM_HOT_POLICY")) vcall.hot_policy = uint32_t(strtoul(pe, nullptr, 0));
+  if (const char* be = knob("GM_L1_BYPASS")) vcall.l1_bypass = uint32_t(strtoul(be, nullptr, 0));
+  if (const char* pe = knob("GM_HOT_POLICY")) vcall.hot_policy = uint32_t(strtoul(pe, nullptr, 0));
   if (exact)
     launch_match<true>(ctx, vcall, tb, to, n, cnt.as<uint32_t>(), stage.as<uint32_t>(), list1.as<uint32_t>(), n1,
                        list2.as<uint32_t>(), n2, probe_ctr, wild_ctr, hdr.as<uint32_t>(), wids.as<uint32_t>(),
@@ -3564,7 +3564,7 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   // (tsum: per-tile match counts, written by the main pass and topped up by the listed and slow passes)
   // (compact staging: a two-level scan is left split, k_assemble_c adds the
   // block offsets -- one launch fewer; GM_SCAN_SPLIT=0 turns it off)
-  const char* se = getenv("GM_SCAN_SPLIT");
+  const char* se = knob("GM_SCAN_SPLIT");
   split = cmp && (!se || atoi(se) != 0);
   // Speculative assembly: the rows are written before the host has read the
   // match total, into an ids buffer sized from this context's recent matches
@@ -3576,7 +3576,7 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   cap_spec = 1024 + uint64_t(double(n) * std::min(ctx->ids_per_topic, double(FAST_MC)));
   // (no room for the speculative buffer: skip speculation, the rows are
   // assembled at their exact size once the total is known)
-  if (!getenv("GM_NO_SPEC_IDS")) ids = PoolBuf(ctx->pool, cap_spec * 4 + 16);  // (test knob: as if it failed)
+  if (!knob("GM_NO_SPEC_IDS")) ids = PoolBuf(ctx->pool, cap_spec * 4 + 16);  // (test knob: as if it failed)
   spec = ids.p != nullptr;
   // The scan may hand back block SUMS (split_sums) only when the speculative
   // assembly runs: that kernel sums them and writes the grand total to
@@ -3825,7 +3825,7 @@ __global__ void k_d0_refresh(IndexView v, uint4* __restrict__ d0) {
 }
 
 int refresh_d0(emqx_gm_ctx* ctx, const IndexView& v, void* d0) {
-  if (const char* e = getenv("GM_D0"))  // A/B knob: 0 = the walk probes level 0 like any other
+  if (const char* e = knob("GM_D0"))  // A/B knob: 0 = the walk probes level 0 like any other
     if (!atoi(e)) return 1;
   hipLaunchKernelGGL(k_d0_refresh, dim3(1), dim3(1), 0, ctx->stream, v, static_cast<uint4*>(d0));
   GM_HIP(ctx, hipGetLastError());
@@ -3835,6 +3835,16 @@ int refresh_d0(emqx_gm_ctx* ctx, const IndexView& v, void* d0) {
 
 int scan_lengths(emqx_gm_ctx* ctx, const uint64_t* len, uint64_t n, uint64_t* out) {
   return scan_excl(ctx, LoadU64{len}, n, out);
+}
+
+namespace {
+struct LoadU16 {
+  const uint16_t* p;
+  __device__ uint64_t operator()(uint64_t i) const { return p[i]; }
+};
+}  // namespace
+int scan_len16(emqx_gm_ctx* ctx, hipStream_t st, const uint16_t* len, uint64_t n, uint64_t* out) {
+  return scan_excl(ctx, LoadU16{len}, n, out, SideSum{}, nullptr, st);
 }
 
 int sum_filter_lengths(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint32_t* d_ids, uint64_t nnz,

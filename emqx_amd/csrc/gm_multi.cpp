@@ -19,6 +19,7 @@
 //   * a host-buffer emqx_gm_match runs its chunks on every device at once
 //     (gm_host.cpp) and returns ONE CSR in batch order.
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <thread>
@@ -56,9 +57,79 @@ int copy_device(emqx_gm_ctx* m, void* dst, const void* src, int src_dev, size_t 
 
 }  // namespace
 
+extern thread_local std::string tl_err;  // gm_api.cpp
+thread_local emqx_gm_update_stats tl_ustats{};
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int run_all(int K, const std::function<int(int)>& f) {
+  if (K <= 0) return 0;
+  if (K == 1) return f(0);
+  std::vector<int> rc(K, 0);
+  std::vector<std::string> msg(K);
+  auto one = [&](int k) {
+    rc[k] = f(k);
+    if (rc[k]) msg[k] = tl_err;
+  };
+  std::vector<std::thread> th;
+  th.reserve(K - 1);
+  for (int k = 1; k < K; ++k) th.emplace_back(one, k);
+  one(0);
+  for (auto& t : th) t.join();
+  for (int k = 0; k < K; ++k)
+    if (rc[k]) return set_err(nullptr, rc[k], msg[k]);
+  return 0;
+}
+
+std::vector<RepTarget> rep_targets(emqx_gm_ctx* ctx, emqx_gm_index* prev) {
+  std::vector<RepTarget> t;
+  const size_t K = ctx->members.size();
+  if (!K || !prev || prev->ov || prev->reps.size() != K) return t;
+  for (size_t k = 0; k < K; ++k)
+    if (!prev->reps[k] || prev->reps[k]->device != ctx->members[k]->device) return {};  // (another context's)
+  for (size_t k = 0; k < K; ++k) t.push_back(RepTarget{ctx->members[k], prev->reps[k], nullptr});
+  return t;
+}
+
+emqx_gm_index* replica_shell(emqx_gm_ctx* m, const emqx_gm_index* src) {
+  auto* r = new emqx_gm_index;
+  r->device = m->device;
+  r->dev_bytes = src->dev_bytes;
+  r->view = src->view;
+  r->ft = src->ft;  // (a shared base + a small delta: cheap)
+  r->gmap = src->gmap;
+  r->subs = src->subs;  // (a shared base + a small delta: cheap)
+  r->level_nodes = src->level_nodes;
+  r->flen_stale = src->flen_stale.load();
+  r->info = src->info;
+  return r;
+}
+
+int attach_replicas(emqx_gm_index* out, std::vector<RepTarget>& t, int rc) {
+  for (auto& x : t)
+    if (!x.out) rc = rc ? rc : EMQX_GM_EDEVICE;
+  if (rc) {
+    for (auto& x : t) {
+      if (x.out) free_index(x.out);
+      x.out = nullptr;
+    }
+    return rc;
+  }
+  for (auto& x : t) {
+    out->reps.push_back(x.out);
+    x.out = nullptr;
+  }
+  return EMQX_GM_OK;
+}
+
 int replicate_index(emqx_gm_ctx* m, const emqx_gm_index* src, emqx_gm_index* share, emqx_gm_index** out) {
   if (src->ov) return set_err(m, EMQX_GM_EUNSUPPORTED, "replicate: overlay snapshot");
-  std::unique_ptr<emqx_gm_index> r(new emqx_gm_index);
+  // (a member's stream and pools are also used by small calls that hold only its lock)
+  std::unique_lock<std::recursive_mutex> lk(m->mu, std::defer_lock);
+  if (m->parent) lk.lock();
+  std::unique_ptr<emqx_gm_index> r(replica_shell(m, src));
   struct Undo {  // a half-made replica's device memory and owner reference
     emqx_gm_index* r;
     ~Undo() {
@@ -69,16 +140,6 @@ int replicate_index(emqx_gm_ctx* m, const emqx_gm_index* src, emqx_gm_index* sha
       if (r->blob_owner && r->blob_owner->refs.fetch_sub(1) == 1) free_index(r->blob_owner);
     }
   } undo{r.get()};
-  r->device = m->device;
-  r->dev_bytes = src->dev_bytes;
-  r->view = src->view;
-  r->ft = src->ft;  // (a shared base + a small delta: cheap)
-  r->gmap = src->gmap;
-  r->subs = src->subs;  // (a shared base + a small delta: cheap)
-  r->ov = nullptr;
-  r->level_nodes = src->level_nodes;
-  r->flen_stale = src->flen_stale.load();
-  r->info = src->info;
   if (src->dev_base) {
     if (share) {
       emqx_gm_index* owner = share->blob_owner ? share->blob_owner : share;
@@ -87,9 +148,17 @@ int replicate_index(emqx_gm_ctx* m, const emqx_gm_index* src, emqx_gm_index* sha
       r->dev_base = share->dev_base;
     } else {
       GM_HIP(m, hipSetDevice(m->device));
-      const hipError_t e = hipMalloc(&r->dev_base, src->dev_bytes);
-      if (e != hipSuccess)
-        return set_err(m, EMQX_GM_ENOMEM, std::string("replicate: hipMalloc: ") + hipGetErrorString(e));
+      // the blob of a released snapshot of this size, when the device keeps one
+      // (a fresh multi-GB hipMalloc after a few update cycles stalls)
+      if ((r->dev_base = take_spare_blob(m->device, src->dev_bytes))) {
+        r->reused_blob = true;
+      } else {
+        const hipError_t e = hipMalloc(&r->dev_base, src->dev_bytes);
+        if (e != hipSuccess) {
+          r->dev_base = nullptr;
+          return set_err(m, EMQX_GM_ENOMEM, std::string("replicate: hipMalloc: ") + hipGetErrorString(e));
+        }
+      }
       if (const int rc = copy_device(m, r->dev_base, src->dev_base, src->device, src->dev_bytes)) return rc;
     }
   }
@@ -121,40 +190,60 @@ int replicate_index(emqx_gm_ctx* m, const emqx_gm_index* src, emqx_gm_index* sha
   return EMQX_GM_OK;
 }
 
-int replicate_result(emqx_gm_ctx* ctx, emqx_gm_index* prev, emqx_gm_index** out_p,
-                     const std::function<int(emqx_gm_ctx*, emqx_gm_index*, emqx_gm_index**)>& redo) {
+int replicate_result(emqx_gm_ctx* ctx, emqx_gm_index* prev, emqx_gm_index** out_p) {
   emqx_gm_index* out = *out_p;
   const size_t K = ctx->members.size();
-  if (!K || !out || out->reps.size() == K) return EMQX_GM_OK;  // single device, or a snapshot already replicated
+  if (!K || !out || out->reps.size() == K) return EMQX_GM_OK;  // single device, or replicated by the update itself
   auto fail = [&](int rc) {
     if (out->refs.fetch_sub(1) == 1) free_index(out);
     *out_p = nullptr;
     return rc;
   };
   if (out->reps.size()) return fail(set_err(ctx, EMQX_GM_EINVAL, "replicate: a snapshot of another context"));
-  // an overlay made from a snapshot without replicas (one made through another
-  // context) stays on the first device: it is matched there, as its base is
-  if (out->ov && (!prev || prev->reps.size() != K)) return EMQX_GM_OK;
+  // an overlay (a filter with '#' inside, or an update of a superseded
+  // snapshot) stays on the first device: it is matched there, as its base is
+  if (out->ov) return EMQX_GM_OK;
   // the snapshot whose device tables `out` shares (update_subs without a route
   // change) and, when prev is that one or shares it too, prev's replica of it
   const emqx_gm_index* own = out->blob_owner;
   const bool share = own && prev && prev->reps.size() == K && (prev == own || prev->blob_owner == own);
-  for (size_t k = 0; k < K; ++k) {
-    emqx_gm_ctx* m = ctx->members[k];
-    emqx_gm_index* rep = nullptr;
-    int rc;
-    if (out->ov) {
-      rc = redo(m, prev->reps[k], &rep);
-    } else {
-      rc = replicate_index(m, out, share ? prev->reps[k] : nullptr, &rep);
+  const double t0 = now_ms();
+  std::vector<emqx_gm_index*> reps(K, nullptr);
+  int rc = 0;
+  if (share) {
+    rc = run_all(int(K), [&](int k) { return replicate_index(ctx->members[k], out, prev->reps[k], &reps[k]); });
+  } else {
+    // a tree of device-to-device copies: every replica made is the source of
+    // one more in the next round (rounds: 1, 2, 4, ... copies at once), so the
+    // first device's links are not the only ones that carry the tables
+    std::vector<const emqx_gm_index*> src{out};
+    size_t next = 0;
+    while (!rc && next < K) {
+      std::vector<std::pair<size_t, const emqx_gm_index*>> jobs;
+      for (const emqx_gm_index* s : src)
+        if (next < K) jobs.emplace_back(next++, s);
+      rc = run_all(int(jobs.size()), [&](int j) {
+        return replicate_index(ctx->members[jobs[j].first], jobs[j].second, nullptr, &reps[jobs[j].first]);
+      });
+      for (const auto& j : jobs)
+        if (reps[j.first]) src.push_back(reps[j.first]);
     }
-    if (rc) {
-      hipSetDevice(ctx->device);
-      return fail(rc);
-    }
-    out->reps.push_back(rep);
   }
   hipSetDevice(ctx->device);
+  if (rc) {
+    for (emqx_gm_index* r : reps)
+      if (r) free_index(r);
+    return fail(rc);
+  }
+  for (const emqx_gm_index* r : reps) {
+    if (r->blob_owner) continue;
+    if (r->reused_blob) ++tl_ustats.blobs_reused;
+    else ++tl_ustats.blobs_fresh;
+  }
+  out->reps = std::move(reps);
+  tl_ustats.replicas = uint32_t(K);
+  tl_ustats.replica_mode = share ? EMQX_GM_REP_SHARED : EMQX_GM_REP_COPIED;
+  tl_ustats.replicate_ms = now_ms() - t0;
   return EMQX_GM_OK;
 }
 
@@ -180,7 +269,7 @@ int run_fanout_multi(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_c
     rix.push_back(idx->reps[k]);
   }
   const uint64_t n = m->n_rows, nnz = m->nnz;
-  const char* me = getenv("GM_FANOUT_MULTI_MIN");
+  const char* me = knob("GM_FANOUT_MULTI_MIN");
   const uint64_t min_rows = me ? strtoull(me, nullptr, 10) : 65536;
   if (mem.size() < 2 || n < min_rows) return run_fanout(ctx, idx, m, flags, out);
   for (uint64_t i = 0; i < nnz; ++i)

@@ -497,7 +497,7 @@ uint64_t filter_rank(const emqx_gm_index* idx, const uint8_t* f, uint64_t len, b
 // Returns 1 (nothing changed) when the snapshot's tables lack room: the caller rebuilds.
 int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>& tomb,
                  const std::set<std::string>& dset, emqx_gm_index** out, std::vector<uint32_t>* rmap_out,
-                 bool trie_only) {
+                 bool trie_only, std::vector<RepTarget>* reps) {
   if (const int rc = load_mirror_blob(ctx, prev)) return rc;  // (a lazy mirror: the first update loads it)
   Mirror& M = *prev->mirror;
   const uint64_t nb = prev->info.n_filters, K = dset.size();
@@ -505,7 +505,7 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
   const uint64_t nf_new = nb - tomb.size() + K;
   if (nf_new > M.flen_cap) return 1;  // the other tables are checked per insert (NoRoom)
   // GM_UPDATE_TIMING: phase times on stderr (diagnostics)
-  const bool timing = getenv("GM_UPDATE_TIMING") != nullptr;
+  const bool timing = knob("GM_UPDATE_TIMING") != nullptr;
   auto t_last = std::chrono::steady_clock::now();
   auto phase = [&](const char* what) {
     if (!timing) return;
@@ -515,9 +515,8 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
   };
   auto* idx = new emqx_gm_index;
   idx->device = prev->device;
-  idx->view = prev->view;
   idx->info = prev->info;
-  IndexView& v = idx->view;
+  IndexView v = prev->view;  // the new view: patched here, rebased per device below
   Patcher P{M, v};
   // final ids (IdShift: prev id -> new id, temporaries nb + k -> new id) from
   // O(delta) lists, and the new snapshot's host filter table derived from
@@ -566,64 +565,92 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
   // filter lengths (stats only, emqx_gm_matched_filter_bytes): rewritten in
   // final ids when first asked for (sum_filter_lengths), not per update
   idx->flen_stale = true;
-  // device: copy the previous blob, apply the patched ranges (still in temporary
-  // ids), renumber every filter-id field; then the mirror the same way
-  phase("flen");
   const size_t blob_bytes = trie_only ? M.blob.size() : prev->dev_bytes;  // the mirror ends at the CSR
-  if (!host) {
-    hipError_t e = hipSetDevice(prev->device);
-    if (e == hipSuccess && !(idx->dev_base = take_spare_blob(prev->device, blob_bytes)))
-      e = hipMalloc(&idx->dev_base, blob_bytes);
-    if (e != hipSuccess) {
-      P.rollback();
-      delete idx;
-      return set_err(ctx, EMQX_GM_ENOMEM, std::string("index_update: hipMalloc: ") + hipGetErrorString(e));
-    }
-    phase("alloc");
-    const int rc = apply_patch_device(ctx, idx->dev_base, prev->dev_base, blob_bytes, P.dirty, M.blob.data(), v,
-                                      M.o_hot, M.o_nodes, M.nodes_n, shift, P.orops);
-    if (rc) {  // the mirror no longer matches any snapshot: later updates take the overlay path
-      (void)hipFree(idx->dev_base);
-      delete idx;
-      delete prev->mirror;
-      prev->mirror = nullptr;
-      return rc;
-    }
-    phase("device");
-  }
   idx->dev_bytes = blob_bytes;
-  // A host-only index (CPU tests) IS its mirror: renumber it.  A device index's
-  // mirror keeps its filter-id fields stale: the patcher never reads them and
-  // uploads only the fields it writes (Patcher::dirty / orops), so the host
-  // side of an update stays O(delta) instead of a pass over the whole blob.
-  if (host) renumber_host(M, v, rmap);
-  phase("renumber");
-  // the view's pointers follow the new blob (a host-only index keeps the mirror's)
-  uint8_t* NB = host ? M.blob.data() : static_cast<uint8_t*>(idx->dev_base);
+  // device: copy the previous blob, apply the patched ranges (still in temporary
+  // ids), renumber every filter-id field -- on the first device and, at the
+  // same time, on every member replica (the same plan applied to its own copy
+  // of prev's tables, which are byte-identical to prev's)
   const uint8_t* OB = host ? M.blob.data() : static_cast<const uint8_t*>(prev->dev_base);
-  auto rebase = [&](auto p) {
-    return p ? reinterpret_cast<decltype(p)>(NB + (reinterpret_cast<const uint8_t*>(p) - OB)) : p;
+  std::atomic<uint32_t> reused{0}, fresh{0};
+  auto device_half = [&](emqx_gm_ctx* c, const emqx_gm_index* src, emqx_gm_index* dst) -> int {
+    std::unique_lock<std::recursive_mutex> lk(c->mu, std::defer_lock);
+    if (c->parent) lk.lock();  // (a member: small calls hold only its lock)
+    GM_HIP(c, hipSetDevice(src->device));
+    if ((dst->dev_base = take_spare_blob(src->device, blob_bytes))) {
+      reused.fetch_add(1);
+    } else {
+      fresh.fetch_add(1);
+      const hipError_t e = hipMalloc(&dst->dev_base, blob_bytes);
+      if (e != hipSuccess) {
+        dst->dev_base = nullptr;
+        return set_err(c, EMQX_GM_ENOMEM, std::string("index_update: hipMalloc: ") + hipGetErrorString(e));
+      }
+    }
+    dst->dev_bytes = blob_bytes;
+    if (const int rc = apply_patch_device(c, dst->dev_base, src->dev_base, blob_bytes, P.dirty, M.blob.data(), v,
+                                          M.o_hot, M.o_nodes, M.nodes_n, shift, P.orops))
+      return rc;
+    // the view's pointers follow the new blob
+    IndexView w = v;
+    uint8_t* NB = static_cast<uint8_t*>(dst->dev_base);
+    auto rebase = [&](auto p) {
+      return p ? reinterpret_cast<decltype(p)>(NB + (reinterpret_cast<const uint8_t*>(p) - OB)) : p;
+    };
+    w.nodes = rebase(w.nodes);
+    w.dict = rebase(w.dict);
+    w.d0_root = rebase(w.d0_root);
+    w.edges = rebase(w.edges);
+    w.hot = rebase(w.hot);
+    w.arena = rebase(w.arena);
+    w.sub_off = trie_only ? nullptr : rebase(w.sub_off);  // trie_only: set by the caller
+    w.sub_ids = trie_only ? nullptr : rebase(w.sub_ids);
+    w.efilt = rebase(w.efilt);
+    w.mph_word = rebase(w.mph_word);
+    dst->dev_flen = reinterpret_cast<uint16_t*>(NB + M.o_flen);
+    if (w.flags & IX_D0) {  // the root's '+' record again, from the patched and renumbered tables
+      const int rc = refresh_d0(c, w, const_cast<uint32_t*>(w.d0_root));
+      if (rc < 0) return rc;
+      if (rc) w.flags &= ~IX_D0;
+    }
+    dst->view = w;
+    return 0;
   };
-  v.nodes = rebase(v.nodes);
-  v.dict = rebase(v.dict);
-  v.d0_root = rebase(v.d0_root);
-  v.edges = rebase(v.edges);
-  v.hot = rebase(v.hot);
-  v.arena = rebase(v.arena);
-  v.sub_off = trie_only ? nullptr : rebase(v.sub_off);  // trie_only: set by the caller
-  v.sub_ids = trie_only ? nullptr : rebase(v.sub_ids);
-  v.efilt = rebase(v.efilt);
-  v.mph_word = rebase(v.mph_word);
-  idx->dev_flen = host ? nullptr : reinterpret_cast<uint16_t*>(NB + M.o_flen);
-  if (!host && (v.flags & IX_D0)) {  // the root's '+' record again, from the patched and renumbered tables
-    const int rc = refresh_d0(ctx, v, const_cast<uint32_t*>(v.d0_root));
-    if (rc < 0) {  // (the mirror is past prev's tables now: later updates of this line rebuild)
+  if (!host) {
+    std::vector<RepTarget> none;
+    std::vector<RepTarget>& R = reps ? *reps : none;
+    for (auto& t : R) t.out = replica_shell(t.m, prev);
+    const double t0 = now_ms();
+    int rc = run_all(int(1 + R.size()), [&](int k) {
+      return k == 0 ? device_half(ctx, prev, idx) : device_half(R[k - 1].m, R[k - 1].prev, R[k - 1].out);
+    });
+    hipSetDevice(prev->device);
+    tl_ustats.device_ms = now_ms() - t0;
+    tl_ustats.blobs_reused += reused.load();
+    tl_ustats.blobs_fresh += fresh.load();
+    phase("device");
+    if (rc) {  // the mirror no longer matches any snapshot: later updates take the overlay path / rebuild
+      for (auto& t : R) {
+        free_index(t.out);
+        t.out = nullptr;
+      }
       free_index(idx);
       delete prev->mirror;
       prev->mirror = nullptr;
       return rc;
     }
-    if (rc) v.flags &= ~IX_D0;
+    if (!R.empty()) {
+      tl_ustats.replicas = uint32_t(R.size());
+      tl_ustats.replica_mode = EMQX_GM_REP_PATCHED;
+    }
+  } else {
+    // A host-only index (CPU tests) IS its mirror: renumber it.  A device index's
+    // mirror keeps its filter-id fields stale: the patcher never reads them and
+    // uploads only the fields it writes (Patcher::dirty / orops), so the host
+    // side of an update stays O(delta) instead of a pass over the whole blob.
+    renumber_host(M, v, rmap);
+    idx->view = v;  // (a host-only index keeps the mirror's pointers)
+    phase("renumber");
   }
   emqx_gm_index_info_t& in = idx->info;
   in.n_filters = nf_new;
@@ -638,6 +665,14 @@ int patch_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const std::set<uint32_t>
   if (rmap_out) *rmap_out = std::move(rmap);
   idx->mirror = prev->mirror;  // the mirror follows the newest snapshot
   prev->mirror = nullptr;
+  if (reps && !host)
+    for (auto& t : *reps) {  // the replicas' host side: the new snapshot's (shared bases)
+      t.out->ft = idx->ft;
+      t.out->info = idx->info;
+      t.out->level_nodes = idx->level_nodes;
+      t.out->flen_stale = true;
+    }
+  tl_ustats.kind = EMQX_GM_UPD_PATCH;
   *out = idx;
   return EMQX_GM_OK;
 }
@@ -676,6 +711,7 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
   if (tomb.empty() && dset.empty()) {
     base->refs.fetch_add(1);
     *out = base;
+    tl_ustats.kind = EMQX_GM_UPD_NONE;
     return EMQX_GM_OK;
   }
   // a plain snapshot with its mirror: patched in place into a new flat snapshot
@@ -684,13 +720,23 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
   // the snapshot's tables: a rebuild, which restores the headroom)
   bool no_room = false;
   std::unique_lock<std::mutex> mirror_lock(prev->mirror_mu);  // updates of one snapshot from several contexts
-  if (!prev->ov && prev->mirror && !getenv("GM_UPDATE_OVERLAY") &&
+  if (!prev->ov && prev->mirror && !knob("GM_UPDATE_OVERLAY") &&
       tomb.size() + dset.size() <= std::max<uint64_t>(4096, nb / 8)) {
     bool wf = true;
     for (const std::string& d : dset) wf = wf && well_formed(reinterpret_cast<const uint8_t*>(d.data()), d.size());
     if (wf) {
-      const int rc = patch_update(ctx, prev, tomb, dset, out);
-      if (rc <= 0) return rc;
+      // a multi-device context: every member patches its replica at once
+      std::vector<RepTarget> reps = rep_targets(ctx, prev);
+      const int rc = patch_update(ctx, prev, tomb, dset, out, nullptr, false, &reps);
+      if (rc < 0) return rc;
+      if (rc == 0) {
+        const int ra = attach_replicas(*out, reps, 0);
+        if (ra) {
+          free_index(*out);
+          *out = nullptr;
+        }
+        return ra;
+      }
       no_room = true;
     }
   }
@@ -719,7 +765,9 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
       offs.push_back(bytes.size());
     }
     bytes.resize(bytes.size() + 64, 0);
-    return build_index(ctx, bytes.data(), offs.data(), offs.size() - 1, nullptr, nullptr, nullptr, out);
+    const int rc = build_index(ctx, bytes.data(), offs.data(), offs.size() - 1, nullptr, nullptr, nullptr, out);
+    tl_ustats.kind = EMQX_GM_UPD_REBUILD;
+    return rc;
   }
   auto* idx = new emqx_gm_index;
   idx->device = base->device;
@@ -783,6 +831,7 @@ int update_index(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const
   in.n_wildcard = base->info.n_wildcard - twild + dwild;
   in.trie_empty = in.n_wildcard == 0;
   in.device_bytes = base->info.device_bytes + bytes;
+  tl_ustats.kind = EMQX_GM_UPD_OVERLAY;
   if (ov->delta) {
     in.n_nodes += ov->delta->info.n_nodes;
     in.n_edges += ov->delta->info.n_edges;

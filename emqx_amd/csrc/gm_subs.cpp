@@ -22,6 +22,7 @@
 // lists.
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <string>
 #include <unordered_map>
@@ -200,6 +201,22 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
   std::vector<uint32_t> rmap;
   int rc = 1;
   bool same_routes = false;
+  // a multi-device context: every member applies the same batch to its replica
+  // of prev, on its own device, at the same time as the first device
+  std::vector<RepTarget> reps = rep_targets(ctx, prev);
+  auto locked = [](emqx_gm_ctx* c, const std::function<int()>& f) {
+    std::unique_lock<std::recursive_mutex> lk(c->mu, std::defer_lock);
+    if (c->parent) lk.lock();  // (a member: small calls hold only its lock)
+    hipSetDevice(c->device);
+    return f();
+  };
+  auto drop_reps = [&]() {
+    for (auto& t : reps)
+      if (t.out) {
+        free_index(t.out);
+        t.out = nullptr;
+      }
+  };
   {
     std::unique_lock<std::mutex> lk(prev->mirror_mu);
     if (tomb.empty() && dset.empty()) {
@@ -223,14 +240,29 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
       idx->level_nodes = prev->level_nodes;
       idx->mirror = prev->mirror;
       prev->mirror = nullptr;
+      for (auto& t : reps) {  // each replica shares its predecessor replica's tables the same way
+        emqx_gm_index* r = replica_shell(t.m, idx);
+        emqx_gm_index* rown = t.prev->blob_owner ? t.prev->blob_owner : t.prev;
+        rown->refs.fetch_add(1);
+        r->blob_owner = rown;
+        r->dev_base = t.prev->dev_base;
+        r->dev_bytes = t.prev->dev_bytes;
+        r->view = t.prev->view;
+        r->dev_flen = t.prev->dev_flen;
+        t.out = r;
+      }
       same_routes = true;
       rc = 0;
     } else if (prev->mirror && wf && tomb.size() + dset.size() <= std::max<uint64_t>(4096, nb / 8)) {
-      rc = patch_update(ctx, prev, tomb, dset, &idx, &rmap, /*trie_only=*/true);
+      rc = patch_update(ctx, prev, tomb, dset, &idx, &rmap, /*trie_only=*/true, &reps);
     }
   }
   if (rc < 0) return rc;
-  if (rc == 1) return rebuild(ctx, prev, ed, out);
+  if (rc == 1) {
+    const int rb = rebuild(ctx, prev, ed, out);
+    tl_ustats.kind = EMQX_GM_UPD_REBUILD;
+    return rb;
+  }
   if (same_routes) {
     // the touched filters' counts and marks (ids ascending = byte order: ed's order)
     std::vector<std::pair<uint32_t, uint64_t>> cnt;
@@ -247,12 +279,31 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
       aff_off.push_back(aff_buf.size());
     }
     idx->subs = prev->subs.apply(cnt, pin);
-    rc = shift_subs_device(ctx, prev, idx, aff_ids, aff_off, aff_buf);
+    rc = run_all(int(1 + reps.size()), [&](int k) {
+      if (k == 0) return shift_subs_device(ctx, prev, idx, aff_ids, aff_off, aff_buf);
+      RepTarget& t = reps[k - 1];
+      return locked(t.m, [&] { return shift_subs_device(t.m, t.prev, t.out, aff_ids, aff_off, aff_buf); });
+    });
+    hipSetDevice(ctx->device);
     if (rc) {
+      drop_reps();
       free_index(idx);
       return rc;
     }
     idx->info.n_subs = idx->subs.total();
+    for (auto& t : reps) {
+      t.out->subs = idx->subs;
+      t.out->info.n_subs = idx->info.n_subs;
+    }
+    if (!reps.empty()) {
+      tl_ustats.replicas = uint32_t(reps.size());
+      tl_ustats.replica_mode = EMQX_GM_REP_SHARED;
+    }
+    tl_ustats.kind = EMQX_GM_UPD_SUBS_ONLY;
+    if (const int ra = attach_replicas(idx, reps, 0)) {
+      free_index(idx);
+      return ra;
+    }
     *out = idx;
     return EMQX_GM_OK;
   }
@@ -285,8 +336,14 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
   }
   std::vector<uint64_t> new_soff(nf + 1, 0);
   for (uint64_t f = 0; f < nf; ++f) new_soff[f + 1] = new_soff[f] + cnt[f];
-  rc = rebuild_subs_device(ctx, prev, idx, new_soff, inv, aff_ids, aff_off, aff_buf);
+  rc = run_all(int(1 + reps.size()), [&](int k) {
+    if (k == 0) return rebuild_subs_device(ctx, prev, idx, new_soff, inv, aff_ids, aff_off, aff_buf);
+    RepTarget& t = reps[k - 1];
+    return locked(t.m, [&] { return rebuild_subs_device(t.m, t.prev, t.out, new_soff, inv, aff_ids, aff_off, aff_buf); });
+  });
+  hipSetDevice(ctx->device);
   if (rc) {
+    drop_reps();
     free_index(idx);  // (its mirror goes too: later updates of this line rebuild)
     return rc;
   }
@@ -305,6 +362,14 @@ int update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const 
     }
   }
   idx->subs = SubTable(std::move(new_soff), std::move(marks));
+  for (auto& t : reps) {
+    t.out->subs = idx->subs;
+    t.out->info.n_subs = idx->info.n_subs;
+  }
+  if (const int ra = attach_replicas(idx, reps, 0)) {
+    free_index(idx);
+    return ra;
+  }
   *out = idx;
   return EMQX_GM_OK;
 }

@@ -190,6 +190,14 @@ class Index:
         check(lib().emqx_gm_index_device_blob(self.h, C.byref(p), C.byref(n)), None, "index_device_blob")
         return p.value, int(n.value)
 
+    def replica_digest(self, k: int) -> Tuple[int, int]:
+        """(tables, subscriber CSR) FNV digests of replica k of this snapshot
+        (0: the snapshot itself; k: its replica on the context's k-th member)."""
+        t, u = C.c_uint64(), C.c_uint64()
+        check(lib().emqx_gm_index_replica_digest(self.ctx.h, self.h, k, C.byref(t), C.byref(u)), self.ctx.h,
+              "index_replica_digest")
+        return int(t.value), int(u.value)
+
     def release(self):
         if self.h:
             lib().emqx_gm_index_release(self.h)
@@ -486,6 +494,17 @@ class Context:
         s = MatchStats()
         check(lib().emqx_gm_last_stats(self.h, C.byref(s)), self.h, "last_stats")
         return {k: getattr(s, k) for k, _ in MatchStats._fields_}
+
+    def update_stats(self) -> dict:
+        """What this thread's last index call (build, import, update, update_subs) did
+        (emqx_gm_last_update_stats): path, replica mode, mirror download, times."""
+        s = _lib.UpdateStats()
+        check(lib().emqx_gm_last_update_stats(self.h, C.byref(s)), self.h, "last_update_stats")
+        d = {k: getattr(s, k) for k, _ in _lib.UpdateStats._fields_}
+        d["kind"] = _lib.UPD_KINDS.get(d["kind"], d["kind"])
+        d["replica_mode"] = _lib.REP_MODES.get(d["replica_mode"], d["replica_mode"])
+        d["mirror_loaded"] = bool(d["mirror_loaded"])
+        return d
 
     def last_kernel_ms(self) -> float:
         """stats()["match_kernel_ms"] without building the dict (a serving loop's per-call read)."""

@@ -64,6 +64,44 @@ int emqx_gm_matched_filter_bytes(emqx_gm_ctx *ctx, const emqx_gm_index *idx, con
 int emqx_gm_fanout_part(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const emqx_gm_csr *matches, uint32_t part,
                         uint32_t n_parts, uint32_t flags, emqx_gm_csr *out, uint64_t *first);
 
+/* What the calling thread's last index call (build, import, update,
+ * update_subs) did -- observed, not inferred from sizes: the path it took,
+ * whether it had to download the snapshot line's host mirror first (a lazy
+ * mirror's first update: its bytes and time), and how the replicas of a
+ * multi-device context were made. */
+#define EMQX_GM_UPD_NONE 0      /* no change (the same snapshot retained)              */
+#define EMQX_GM_UPD_PATCH 1     /* in-place patch of a device copy, O(delta)           */
+#define EMQX_GM_UPD_OVERLAY 2   /* base + tombstones + delta index                     */
+#define EMQX_GM_UPD_REBUILD 3   /* the updated set recompiled                          */
+#define EMQX_GM_UPD_SUBS_ONLY 4 /* update_subs without a route change: tables shared   */
+#define EMQX_GM_UPD_BUILD 5
+#define EMQX_GM_UPD_IMPORT 6
+#define EMQX_GM_REP_NONE 0      /* no replicas (single device, or left on the first)   */
+#define EMQX_GM_REP_PATCHED 1   /* every member applied the same delta to its replica  */
+#define EMQX_GM_REP_COPIED 2    /* device tables copied device to device (tree order)  */
+#define EMQX_GM_REP_SHARED 3    /* members share their replica's tables + own new CSR  */
+typedef struct {
+  uint32_t kind;          /* EMQX_GM_UPD_*                                        */
+  uint32_t replica_mode;  /* EMQX_GM_REP_*                                        */
+  uint32_t replicas;      /* member replicas made                                 */
+  int32_t mirror_loaded;  /* 1: the host mirror was loaded by this call           */
+  uint64_t mirror_bytes;  /* ... its bytes                                        */
+  double mirror_ms;       /* ... its time                                         */
+  double device_ms;       /* the device part (every device at once), wall         */
+  double replicate_ms;    /* replica copies after the first device's result, wall */
+  double total_ms;        /* the whole call, wall                                 */
+  uint32_t blobs_reused;  /* device tables placed in a released snapshot's blob   */
+  uint32_t blobs_fresh;   /* ... in a fresh allocation (every device counted)     */
+} emqx_gm_update_stats;
+int emqx_gm_last_update_stats(const emqx_gm_ctx *ctx, emqx_gm_update_stats *stats);
+
+/* Test support: FNV-1a digests of replica k's device tables (k = 0: the
+ * snapshot itself, k >= 1: its replica on the context's k-th member) and of
+ * its subscriber CSR (offsets + ids; 0 without one).  Replicas of one snapshot
+ * hold byte-identical tables. */
+int emqx_gm_index_replica_digest(emqx_gm_ctx *ctx, const emqx_gm_index *idx, uint32_t k, uint64_t *tables,
+                                 uint64_t *subs);
+
 #ifdef __cplusplus
 }
 #endif

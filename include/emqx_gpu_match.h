@@ -46,6 +46,27 @@
  * Device topic buffers (EMQX_GM_DEVICE_IO): the tokenizer reads whole aligned
  * 8-byte words, so at least 64 readable bytes must follow topic_bytes[toff[n]]
  * (the library pads its own copies of host buffers the same way).
+ *
+ * Environment: the default library reads ONE variable, EMQX_GM_AB.  Unless it
+ * is set (non-empty, not "0"), every GM_* knob below is ignored, so a library
+ * loaded into a BEAM runs one table layout and one walk whatever else the
+ * host's environment holds.  With EMQX_GM_AB set (A/B scripts, the test
+ * suite) the library reads, per call:
+ *   layout (at build):  GM_HOT_LOAD_PCT, GM_HOT_LOAD_PCT_UPPER, GM_HOT_FLAT,
+ *     GM_HOT_SPARSE, GM_HOT_RH_INSERT, GM_NO_RH_EXIT, GM_NO_MPH, GM_MPH_TABLES,
+ *     GM_MPH_SLACK, GM_MPH_LAMBDA, GM_MPH_MIN_KEYS, GM_MPH_MAX_KEYS,
+ *     GM_MPH_NO_FILTERED, GM_CHAIN, GM_NO_CHAIN, GM_NO_EDGE_FILTER,
+ *     GM_EFILT_ALL, GM_EFILT_DIV, GM_EFILT_MAX_KB, GM_DICT_MUL, GM_L1_BYPASS,
+ *     GM_TRIE_RUNS, GM_MIRROR, GM_NO_MIRROR;
+ *   walk and staging:   GM_MATCH_MAIN (the superseded split / coop / lds
+ *     forms), GM_TOK_GROUP, GM_OVERLAP, GM_FUSED_PRIO, GM_HOT_POLICY, GM_NT,
+ *     GM_D0, GM_STAGE_COMPACT, GM_STAGE_SC1, GM_LISTED_CAP, GM_LISTED_DEFER,
+ *     GM_SCAN_SPLIT, GM_SCAN_SUMS, GM_NO_SPEC_IDS, GM_ASM_STREAM;
+ *   host path:          GM_HOST_SIMPLE, GM_HOST_PIPE, GM_HOST_CHUNK,
+ *     GM_HOST_THREADS, GM_HOST_BOUNCE, GM_HOST_WIDE_ROWS, GM_HOST_OFF32,
+ *     GM_FANOUT_MULTI_MIN;
+ *   updates:            GM_UPDATE_OVERLAY, GM_UPDATE_UNFUSED, GM_SPARE_BLOB_MIN;
+ *   diagnostics:        GM_UPDATE_TIMING, GM_INDEX_STATS, GM_INDEX_VERIFY.
  */
 #ifndef EMQX_GPU_MATCH_H
 #define EMQX_GPU_MATCH_H
@@ -90,11 +111,23 @@ typedef struct emqx_gm_call emqx_gm_call;
  * one replica of every index per listed device (a device may be listed more
  * than once: several replicas, e.g. a one-GPU rehearsal):
  *   - an index is compiled ONCE on the host and its device tables are copied
- *     to the other devices (device to device / peer copy over xGMI); every
- *     emqx_gm_index_update / _update_subs / _import result is replicated too;
- *   - emqx_gm_match on host buffers cuts the batch into chunks that run on
- *     all the devices at once (one host pipeline per device); the rows come
- *     back in the caller's ONE CSR, in batch order;
+ *     to the other devices device to device (peer copies over xGMI, in a tree:
+ *     every replica made is the source of another, so 8 devices take 3 rounds
+ *     of copies and every device's links carry them);
+ *   - an update is applied on every device at once, each from its own replica
+ *     of the predecessor, as every EMQX node applies the same route delta to
+ *     its own tables (emqx_router_utils.erl:33-38, emqx_trie.erl:114-136): the
+ *     in-place patch's host plan is made once and each device runs its own
+ *     one-pass patch; a subscriber-only emqx_gm_index_update_subs shares each
+ *     replica's tables and writes each device's new subscriber CSR there;
+ *     rebuilds and imports are copied as at a build; an overlay result (a
+ *     filter with '#' inside) stays on the first device and is matched there;
+ *   - emqx_gm_match on host buffers: a batch of more than one chunk (256K
+ *     topics) is cut into chunks that run on all the devices at once (one host
+ *     pipeline per device), the rows back in the caller's ONE CSR in batch
+ *     order; a smaller batch runs whole on ONE device -- the first whose lock is
+ *     free from a round-robin start -- so concurrent callers (dirty
+ *     schedulers) run on different GPUs at once;
  *   - emqx_gm_fanout on host rows (65,536 rows or more) cuts them into one
  *     slice per device, balanced by matches, into the caller's ONE result;
  *   - device-buffer calls (EMQX_GM_DEVICE_IO, emqx_gm_match_submit, a

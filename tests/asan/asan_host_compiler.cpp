@@ -27,6 +27,17 @@ int apply_patch_device(emqx_gm_ctx*, void*, const void*, size_t, const std::vect
                        const std::vector<std::pair<uint64_t, uint32_t>>&) {
   return EMQX_GM_EDEVICE;
 }
+// gm_multi.cpp's replica helpers: a host-only index has no replicas
+thread_local emqx_gm_update_stats tl_ustats{};
+double now_ms() { return 0.0; }
+int run_all(int K, const std::function<int(int)>& f) {
+  for (int k = 0; k < K; ++k)
+    if (const int rc = f(k)) return rc;
+  return 0;
+}
+std::vector<RepTarget> rep_targets(emqx_gm_ctx*, emqx_gm_index*) { return {}; }
+emqx_gm_index* replica_shell(emqx_gm_ctx*, const emqx_gm_index*) { return nullptr; }
+int attach_replicas(emqx_gm_index*, std::vector<RepTarget>&, int rc) { return rc; }
 }
 
 static int compile(const std::vector<std::string>& fs) {

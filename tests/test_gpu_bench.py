@@ -43,6 +43,21 @@ def test_bench_two_ranks_c2():
     assert two["value"] > 0 and two["roofline"]["frac"] > 0
     # the two slices are different windows of the same stream: same matches/topic within noise
     assert abs(two["detail"]["matches_per_topic"] - one["detail"]["matches_per_topic"]) < 0.1
+    # the drop-in path's multi-GPU form: rank 0 opens ONE context over the ranks' devices (here
+    # device 0 twice), replicates the index in a tree, spreads one host-buffer call over both
+    # and applies 200-op updates on both replicas at once
+    for out, devs in ((one, [0, 0]), (two, [0, 0])):
+        m = out["detail"]["multi_device"]
+        assert m["devices"] == devs and m["replica_mode"] == "copied", m
+        assert m["host_io_multi_topics_per_s"] > 0 and m["host_io_multi_nnz_matches_device"] is True, m
+        u = m["index_update_replicas"]
+        assert all(r["replica_mode"] == "patched" and r["replicas"] == 1 for r in u["rounds"]), u
+    assert one["detail"]["multi_device"]["index_update_replicas"]["vs_single_device"] > 0
+    # the host path against its link: bytes per topic each way and the measured peaks
+    link = one["detail"]["host_io_link"]
+    assert link["h2d_bytes_per_topic"] > 2 and link["h2d_peak_gbs"] > 0 and 0 < link["h2d_frac_of_peak"] < 1.5
+    # the first update says what it did (an index built here keeps its mirror: no download)
+    assert one["detail"]["index_update"]["first_includes_mirror_download"] is False
 
 
 @pytest.mark.gpu

@@ -112,12 +112,22 @@ def test_c2_fixture_and_4m_batch_two_replicas(ctx1, ctx2, orc, monkeypatch):
     i2.release()
 
 
+def _same_tables(ix, k_max):
+    """Every replica of a snapshot holds the first device's bytes (tables and
+    subscriber CSR)."""
+    d0 = ix.replica_digest(0)
+    for k in range(1, k_max + 1):
+        assert ix.replica_digest(k) == d0, k
+
+
 def test_updates_replicated(ctx1, ctx2, orc, monkeypatch):
     """Every kind of new snapshot reaches every replica: an in-place patch
-    (copied), an overlay update (a filter with '#' inside: repeated on each
-    replica), an import; each snapshot's rows through the multi-device host
-    path (forced into 1,024-topic chunks, so both replicas serve the batch)
-    equal the oracle's."""
+    (applied on each device from its own predecessor replica, O(delta): the
+    replica's tables byte-equal to the first device's), an overlay update (a
+    filter with '#' inside: stays on the first device, where it is matched),
+    an import (copied); each snapshot's rows through the multi-device host path
+    (forced into 1,024-topic chunks, so both replicas serve the batch) equal
+    the oracle's."""
     import random
     rng = random.Random(11)
     words = ["a", "b", "c", "d", "+"]
@@ -142,21 +152,39 @@ def test_updates_replicated(ctx1, ctx2, orc, monkeypatch):
         assert np.array_equal(ro, oro) and np.array_equal(ids, oids)
 
     check(idx)
+    st = ctx2.update_stats()
+    assert st["kind"] == "build" and st["replica_mode"] == "copied" and st["replicas"] == 1, st
+    _same_tables(idx, 1)
     # an in-place patch: deletes and inserts of ordinary filters
     dels = rng.sample(sorted(live), 20)
     adds = sorted({rand_filter() for _ in range(30)} - live)
     ops = [(f, False) for f in dels] + [(f, True) for f in adds]
     nidx = ctx2.update_index(idx, ops)
+    st = ctx2.update_stats()
+    assert st["kind"] == "patch" and st["replica_mode"] == "patched" and st["replicas"] == 1, st
     live -= set(dels)
     live |= set(adds)
     check(nidx)
+    _same_tables(nidx, 1)
+    # a second patch continues the line on every device
+    ops2 = [(sorted(live)[3], False), (b"q/+/z", True)]
+    n2 = ctx2.update_index(nidx, ops2)
+    live.discard(sorted(live)[3])
+    live.add(b"q/+/z")
+    assert ctx2.update_stats()["replica_mode"] == "patched"
+    check(n2)
+    _same_tables(n2, 1)
+    nidx.release()
+    nidx = n2
     check_old = sorted(set(filters))  # the old snapshot is untouched (RCU)
     ro, ids = ctx2.match(idx, topics, exact=True)
     oro, oids = _oracle_rows(orc, check_old, topics)
     assert np.array_equal(ro, oro) and np.array_equal(ids, oids)
     idx.release()
-    # an overlay: a filter with '#' inside
+    # an overlay: a filter with '#' inside (matched on the first device only)
     ov = ctx2.update_index(nidx, [(b"a/#/b", True), (sorted(live)[0], False)])
+    st = ctx2.update_stats()
+    assert st["kind"] == "overlay" and st["replica_mode"] == "none", st
     live.add(b"a/#/b")
     live.discard(sorted(live - {b"a/#/b"})[0])
     check(ov)
@@ -164,20 +192,58 @@ def test_updates_replicated(ctx1, ctx2, orc, monkeypatch):
     # import: the image replicated to both
     flat = ctx1.build_index(sorted(live - {b"a/#/b"}))
     imp = ctx2.import_index(flat.export())
+    st = ctx2.update_stats()
+    assert st["kind"] == "import" and st["replica_mode"] == "copied", st
     live.discard(b"a/#/b")
     check(imp)
+    _same_tables(imp, 1)
     flat.release()
     ov.release()
     imp.release()
 
 
+def test_update_cycle_reuses_blobs_on_every_replica(ctx2, orc, monkeypatch):
+    """An update chain on a two-replica context: once the previous snapshot
+    is released, its blob and its replica's blob are the spares the next
+    update's two device passes take (gm_index.cpp take/give_spare_blob, one
+    spare per open context on a device; GM_SPARE_BLOB_MIN=1: any size), with
+    rows equal to the oracle after each update."""
+    import random
+    monkeypatch.setenv("GM_SPARE_BLOB_MIN", "1")
+    monkeypatch.setenv("GM_HOST_CHUNK", "1024")
+    rng = random.Random(5)
+    live = {("/".join(rng.choice(["a", "b", "c", "+"]) for _ in range(rng.randint(1, 5)))).encode()
+            for _ in range(2000)}
+    topics = ["/".join(rng.choice("abc") for _ in range(rng.randint(1, 6))).encode() for _ in range(3000)]
+    idx = ctx2.build_index(sorted(live))
+    reused = []
+    for it in range(4):
+        adds = {b"cyc/%d/%d/+" % (it, i) for i in range(30)}
+        ops = [(f, True) for f in sorted(adds)] + [(f, False) for f in sorted(live)[:10]]
+        nidx = ctx2.update_index(idx, ops)
+        st = ctx2.update_stats()
+        assert st["replica_mode"] == "patched", st
+        reused.append(st["blobs_reused"])
+        live = (live - set(sorted(live)[:10])) | adds
+        idx.release()  # (its blob and its replica's become the device's spares)
+        idx = nidx
+        ro, ids = ctx2.match(idx, topics, exact=True)
+        oro, oids = _oracle_rows(orc, sorted(live), topics)
+        assert np.array_equal(ro, oro) and np.array_equal(ids, oids), it
+        _same_tables(idx, 1)
+    assert reused[1:] == [2, 2, 2], reused
+    idx.release()
+
+
 def test_update_subs_replicated(ctx2, monkeypatch):
     """Subscriber maintenance on a two-replica context: a subscriber-only batch
     (the new snapshot shares its predecessor's tables; each replica shares its
-    predecessor replica's and copies only the new subscriber CSR) and a batch
-    with route changes (patched, then copied): the fan-out rows (match through
-    the multi-device host path) equal the broker bookkeeping's deliveries --
-    each matching filter's subscribers/1 (emqx_broker.erl:296-322, 506-530)."""
+    predecessor replica's and writes its own new subscriber CSR on its device)
+    and a batch with route changes (patched on every device at once, each
+    device's new CSR written there): the fan-out rows (match through the
+    multi-device host path) equal the broker bookkeeping's deliveries -- each
+    matching filter's subscribers/1 (emqx_broker.erl:296-322, 506-530) -- and
+    every replica's tables and CSR equal the first device's, byte for byte."""
     from emqx_amd import topic
     from emqx_amd.routing import Broker
     monkeypatch.setenv("GM_HOST_CHUNK", "1024")
@@ -200,23 +266,33 @@ def test_update_subs_replicated(ctx2, monkeypatch):
         b.unsubscribe(fl[k], 1000 + k)
         b.subscribe(fl[k], 5000 + k)
     check()
+    st = ctx2.update_stats()
+    assert st["kind"] == "subs_only" and st["replica_mode"] == "shared", st
+    _same_tables(b.snapshot().index, 1)
     for k in range(40, 60):  # routes change: the last subscribers leave, a new filter comes
         b.unsubscribe(fl[k], k)
         b.unsubscribe(fl[k], 1000 + k)
     b.subscribe(b"s/+/x", 7)
     check()
+    st = ctx2.update_stats()
+    assert st["kind"] == "patch" and st["replica_mode"] == "patched", st
+    _same_tables(b.snapshot().index, 1)
 
 
 def test_concurrent_callers_three_replicas(orc, monkeypatch):
     """NIF-style use: one context over three replicas (device 0 listed three
     times) shared by four threads (dirty schedulers), each matching its own
-    host batches -- some small (the one-chunk serial path), some spread over
-    the replicas in 1,024-topic chunks -- while a fifth thread swaps in
-    updated snapshots (RCU): every result equals the oracle's rows for the
-    snapshot that call used."""
+    host batches -- small ones run whole on one replica picked round-robin
+    under that replica's lock only, larger ones spread over the replicas in
+    1,024-topic chunks -- while a fifth thread swaps in updated snapshots (RCU:
+    each update is applied on all three replicas; the old snapshot is released
+    as soon as it is swapped out, the callers' retained references keep it
+    alive): every result equals the oracle's rows for the snapshot that call
+    used."""
     import random
     import threading
     from emqx_amd import Context
+    from emqx_amd._lib import lib
     monkeypatch.setenv("GM_HOST_CHUNK", "1024")
     rng = random.Random(3)
     words = ["a", "b", "c", "+"]
@@ -228,31 +304,99 @@ def test_concurrent_callers_three_replicas(orc, monkeypatch):
     for fs_key, fs in (("base", base), ("more", sorted(base + extra))):
         for k, ts in enumerate(topics):
             want[(fs_key, k)] = _oracle_rows(orc, fs, ts)
+
+    class _Held:  # a retained snapshot handle (emqx_gm_index_retain), released after the call
+        def __init__(self, ix):
+            lib().emqx_gm_index_retain(ix.h)
+            self.h = ix.h
+
+        def release(self):
+            lib().emqx_gm_index_release(self.h)
+
     with Context(devices=[0, 0, 0]) as c:
-        snaps = {"base": c.build_index(base)}
-        snaps["more"] = c.update_index(snaps["base"], [(f, True) for f in extra])
-        errors = []
+        lock = threading.Lock()
+        cur = {"key": "base", "ix": c.build_index(base)}
+        errors, swaps = [], [0]
+        stop = threading.Event()
 
         def caller(tid):
             try:
-                for it in range(6):
-                    key = "base" if (tid + it) % 2 else "more"
-                    k = (tid + it) % len(topics)
-                    ro, ids = c.match(snaps[key], topics[k], exact=True)
+                for it in range(8):
+                    with lock:
+                        key, held = cur["key"], _Held(cur["ix"])
+                    try:
+                        k = (tid + it) % len(topics)
+                        ro, ids = c.match(held, topics[k], exact=True)
+                    finally:
+                        held.release()
                     wro, wids = want[(key, k)]
                     if not (np.array_equal(ro, wro) and np.array_equal(ids, wids)):
                         errors.append((tid, it, key, k))
             except Exception as e:  # noqa: BLE001
                 errors.append((tid, repr(e)))
 
+        def updater():
+            try:
+                while not stop.is_set() and swaps[0] < 12:
+                    with lock:
+                        key, old = cur["key"], cur["ix"]
+                    ops = [(f, key == "base") for f in extra]  # base -> more (insert), more -> base (delete)
+                    nix = c.update_index(old, ops)
+                    st = c.update_stats()
+                    if st["replica_mode"] != "patched" or st["replicas"] != 2:
+                        errors.append(("update", st))
+                    with lock:
+                        cur["key"], cur["ix"] = ("more" if key == "base" else "base"), nix
+                    old.release()  # (callers holding it retained it)
+                    swaps[0] += 1
+            except Exception as e:  # noqa: BLE001
+                errors.append(("updater", repr(e)))
+
         th = [threading.Thread(target=caller, args=(t,)) for t in range(4)]
+        up = threading.Thread(target=updater)
+        up.start()
         for t in th:
             t.start()
         for t in th:
             t.join()
+        stop.set()
+        up.join()
         assert not errors, errors
-        for s in snaps.values():
-            s.release()
+        assert swaps[0] >= 1
+        cur["ix"].release()
+
+
+@pytest.mark.skipif("not __import__('torch').cuda.device_count() >= 2", reason="needs two GPUs")
+def test_two_gpus_replicas_and_small_calls(ctx1, orc, monkeypatch):
+    """Devices [0, 1] (the driver's multi-GPU node): the tree copy crosses xGMI
+    (hipMemcpyPeerAsync between two devices, peer access enabled at open), an
+    in-place update is applied on both GPUs, a small call runs whole on either
+    GPU (round-robin) and a large one is spread over both: every row equals
+    the single-device context's, every replica's tables the first GPU's."""
+    from emqx_amd import Context
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    codes = gen_filter_codes(7, 200_000)
+    fpack = render_codes(codes)
+    tb, to = orc.render_codes(orc.gen_topic_codes(7, 0, 600_000, codes))
+    i1 = ctx1.build_index(fpack)
+    want = ctx1.match(i1, (tb, to), exact=True)
+    with Context(devices=[0, 1]) as c:
+        ix = c.build_index(fpack)
+        _same_tables(ix, 1)
+        _eq(c.match(ix, (tb, to), exact=True), want, "spread over two GPUs")
+        small = (tb, to[:2001].copy())
+        ws = ctx1.match(i1, small, exact=True)
+        for _ in range(4):  # round-robin: both GPUs serve small calls
+            _eq(c.match(ix, small, exact=True), ws, "small call")
+        ops = [(b"two/+/gpus/%d" % i, True) for i in range(100)]
+        nx = c.update_index(ix, ops)
+        assert c.update_stats()["replica_mode"] == "patched"
+        _same_tables(nx, 1)
+        n1 = ctx1.update_index(i1, ops)
+        _eq(c.match(nx, (tb, to), exact=True), ctx1.match(n1, (tb, to), exact=True), "after the update")
+        for x in (ix, nx, n1):
+            x.release()
+    i1.release()
 
 
 @pytest.mark.parametrize("replicas", [2, 3])

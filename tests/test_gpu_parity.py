@@ -565,8 +565,8 @@ def test_fanout_split_two_ranks():
 @pytest.mark.parametrize("chunk,wide", [("1024", "0"), ("5000", "0"), ("4194304", "0"), ("5000", "1")])
 def test_host_path_chunks_equal_device_path(ctx, orc, monkeypatch, chunk, wide):
     """emqx_gm_match on host buffers -- chunked (GM_HOST_CHUNK topics), staged
-    through pinned memory with u32 chunk-relative offsets, three chunks in
-    flight -- gives the rows of one DEVICE_IO call over the same batch, which
+    through pinned memory with u16 topic lengths (the device scans them into
+    offsets), three chunks in flight -- gives the rows of one DEVICE_IO call over the same batch, which
     a strided sample ties to the oracle.  Small chunks put many chunk
     boundaries (and partial last chunks) in one call.  wide: the row offsets
     return as u64 (the form a chunk of 2^32 ids or more takes)."""
@@ -595,6 +595,32 @@ def test_host_path_chunks_equal_device_path(ctx, orc, monkeypatch, chunk, wide):
     res.free()
     ctx.dev_free(d_tb)
     ctx.dev_free(d_to)
+    idx.release()
+
+
+@pytest.mark.parametrize("chunk", ["1024", "default"])
+def test_host_path_long_topics_take_u32_offsets(ctx, orc, monkeypatch, chunk):
+    """The host path sends topic lengths as u16 (MQTT caps a topic at 65,535
+    bytes, emqx_topic.erl:45), but the ABI takes any length: a chunk holding a
+    longer topic goes up as u32 offsets instead.  Topics of 65,535, 65,536,
+    70,000 and 200,000 bytes (one deep, one one long word) among 50k ordinary
+    ones: rows equal the device path's and the oracle's, with the default
+    staging and with every chunk forced to u32 offsets (GM_HOST_OFF32)."""
+    if chunk != "default":
+        monkeypatch.setenv("GM_HOST_CHUNK", chunk)
+    filters = [b"l0w1/+/#", b"#", b"x/+", b"+/+/+", b"deep/#", b"long"]
+    idx = ctx.build_index(filters)
+    topics = [b"l0w1/a/b", b"x/y", b"a/b/c"] * 16_000
+    for n_bytes, at in ((65_535, 100), (65_536, 2_000), (70_000, 30_000), (200_000, 47_999)):
+        deep = b"deep/" + b"/".join([b"w"] * ((n_bytes - 5) // 2))
+        topics.insert(at, (deep + b"q" * (n_bytes - len(deep)))[:n_bytes])
+        topics.insert(at + 1, b"x/" + b"z" * (n_bytes - 2))
+    assert max(len(t) for t in topics) == 200_000 and len(topics) == 48_008
+    want_ro, want_ids = _oracle_rows(orc, sorted(filters), topics, 1)
+    for off32 in ("0", "1"):
+        monkeypatch.setenv("GM_HOST_OFF32", off32)
+        ro, ids = ctx.match(idx, topics, exact=True)
+        assert np.array_equal(ro, want_ro) and np.array_equal(ids, want_ids), off32
     idx.release()
 
 

@@ -142,6 +142,38 @@ def _compile(filters, subs=None):
     return info, perm[:n]
 
 
+def test_knobs_need_the_ab_opt_in(monkeypatch):
+    """The shipped library ignores its GM_* A/B knobs unless EMQX_GM_AB opts in
+    (gm_internal.h knob(); the default build reads EMQX_GM_AB alone, as
+    include/emqx_gpu_match.h lists): a stray GM_NO_MPH on an EMQX host
+    must not change a production node's table layout."""
+    fs = [f"a/{i}/+/x{i % 7}".encode() for i in range(20000)]
+    monkeypatch.delenv("EMQX_GM_AB", raising=False)
+    base, _ = _compile(fs)
+    monkeypatch.setenv("GM_NO_MPH", "1")  # (with the opt-in: no perfect-hash placement, larger tables)
+    assert _compile(fs)[0].device_bytes == base.device_bytes
+    monkeypatch.setenv("EMQX_GM_AB", "0")
+    assert _compile(fs)[0].device_bytes == base.device_bytes
+    monkeypatch.setenv("EMQX_GM_AB", "1")
+    assert _compile(fs)[0].device_bytes > base.device_bytes
+    # the library's sources read no other variable (the header's list)
+    import glob
+    names = set()
+    for f in glob.glob(os.path.join(ROOT, "emqx_amd", "csrc", "*.*")):
+        if f.endswith((".cpp", ".hip", ".h")):
+            src = open(f).read()
+            names |= set(re.findall(r'getenv\("([A-Z0-9_]+)"', src))
+    assert names == {"EMQX_GM_AB"}, names
+    # ... and the header lists exactly the knobs the sources read behind it
+    knobs = set()
+    for f in glob.glob(os.path.join(ROOT, "emqx_amd", "csrc", "*.*")):
+        if f.endswith((".cpp", ".hip", ".h")):
+            knobs |= set(re.findall(r'(?:knob|env_u64)\("(GM_[A-Z0-9_]+)"', open(f).read()))
+    h = open(os.path.join(ROOT, "include", "emqx_gpu_match.h")).read()
+    env = h[h.index(" * Environment:"):h.index("*/", h.index(" * Environment:"))]
+    assert knobs == set(re.findall(r"\bGM_[A-Z0-9_]+", env))
+
+
 @pytest.mark.timeout(60)
 def test_index_compiler_host_small(golden):
     """The host index compiler (the part of emqx_gm_index_build that runs on
