@@ -597,7 +597,7 @@ def update_chain(ctx, idx, n_rounds=2, n_ops=200, seed=7):
     return out, cur
 
 
-def multi_device(ctx, idx, devices, pb, ho, n_topics, nnz, single):
+def multi_device(ctx, idx, img, big, devices, pb, ho, n_topics, nnz, single):
     """The drop-in path's multi-GPU form: ONE library context over ``devices``
     (what the NIF opens on a node: emqx_gm_opts.n_devices), outside the timed
     region.  The index goes in once (an import of this rank's snapshot) and is
@@ -607,8 +607,6 @@ def multi_device(ctx, idx, devices, pb, ho, n_topics, nnz, single):
     replica's predecessor).  ``single``: this rank's single-device figures."""
     from emqx_amd import Context
     d = {"devices": list(devices)}
-    big = idx.info.device_bytes > (16 << 30)
-    img = idx.export(with_blob=big)
     blob = None if big else idx.device_blob()[0]
     if big:  # (C5's 53 GB: the replicas and an update's new tables fit only without this rank's copy)
         idx.release()
@@ -802,6 +800,15 @@ def main():
                    "calls_in_flight": 1 if a.no_pipeline else 2},
     }
     pb = ho = None
+    multi = not a.no_multi and not a.no_host_io and (world > 1 or a.replicas > 1)
+    mimg = big_img = None
+    if multi and rank == 0:
+        # the image the multi-device context imports, taken before this rank's own updates
+        # move the snapshot line's host mirror on (an image carries the line's mirror
+        # metadata).  C5's tables go in the image itself (53 GB: the replicas and an
+        # update's new tables fit the GPU only once this rank's copy is released)
+        big_img = idx.info.device_bytes > (16 << 30)
+        mimg = idx.export(with_blob=big_img)
     if not a.no_host_io and rank == 0:
         # PCIe-inclusive, outside the timed region: the same batch handed over in host
         # memory and its CSR returned in host memory (the NIF's call, gm_host.cpp)
@@ -855,15 +862,14 @@ def main():
     ctx.dev_free(do)
     # the drop-in path's multi-GPU form (one context over the GPUs), rank 0, while the
     # other ranks wait on the host
-    multi = not a.no_multi and pb is not None and (world > 1 or a.replicas > 1)
     host_barrier(pg)
     if multi and rank == 0:
         devices = ([local] * world if "GM_BENCH_DEVICE" in os.environ else list(range(world))) if world > 1 \
             else [local] * a.replicas
         single = {"host_io_topics_per_s": out["detail"].get("host_io_topics_per_s"),
                   "update_ms": out["detail"].get("index_update", {}).get("update_ms")}
-        out["detail"]["multi_device"] = multi_device(ctx, idx, devices, pb, ho, n_topics, nnz, single)
-        idx = None
+        out["detail"]["multi_device"] = multi_device(ctx, idx, mimg, big_img, devices, pb, ho, n_topics, nnz, single)
+        idx = mimg = None
     host_barrier(pg)
     if pb is not None:
         ctx.host_free(pb)

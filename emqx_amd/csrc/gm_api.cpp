@@ -408,6 +408,7 @@ int emqx_gm_synchronize(emqx_gm_ctx* ctx) {
   if (!ctx) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   for (emqx_gm_ctx* m : ctx->members) {
+    std::lock_guard<std::recursive_mutex> ml(m->mu);
     hipSetDevice(m->device);
     GM_HIP(ctx, hipStreamSynchronize(m->stream));
   }
@@ -941,6 +942,7 @@ int emqx_gm_pool_trim(emqx_gm_ctx* ctx) {
   ctx->pool->trim();
   gm::trim_spare_blob(ctx->device);
   for (emqx_gm_ctx* m : ctx->members) {
+    std::lock_guard<std::recursive_mutex> ml(m->mu);  // (small calls hold only a member's lock)
     m->pool->trim();
     gm::trim_spare_blob(m->device);
   }

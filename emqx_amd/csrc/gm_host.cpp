@@ -520,6 +520,12 @@ static int run_host_pipe(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8
                          emqx_gm_csr* out) {
   const int K = int(mem.size());
   const int m = int(cb.size()) - 1;
+  // every member device for the whole call: its host pipeline, pools and
+  // stream are also what a small call on that device alone uses (gm_api.cpp
+  // match_small holds only the member's lock).  Order: the first device's lock
+  // (the caller's), then the members' in order; a small call takes one member's.
+  std::vector<std::unique_lock<std::recursive_mutex>> held;
+  for (int k = 1; k < K; ++k) held.emplace_back(mem[k]->mu);
   std::vector<HostPipe*> hps(K);
   for (int k = 0; k < K; ++k)
     if (int rc = host_pipe(mem[k], &hps[k], k == 0)) return rc;

@@ -332,6 +332,10 @@ int run_fanout_multi(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_c
     work(0);
     for (auto& t : th) t.join();
   }
+  // the rows' copy-out and the slices' buffers use every member's stream and
+  // pools: their locks from here on (small calls hold only a member's lock)
+  std::vector<std::unique_lock<std::recursive_mutex>> held;
+  for (int k = 1; k < K; ++k) held.emplace_back(mem[k]->mu);
   auto drop = [&]() {
     for (int k = 0; k < K; ++k) {
       hipSetDevice(mem[k]->device);

@@ -604,7 +604,7 @@ def test_host_path_long_topics_take_u32_offsets(ctx, orc, monkeypatch, chunk):
     bytes, emqx_topic.erl:45), but the ABI takes any length: a chunk holding a
     longer topic goes up as u32 offsets instead.  Topics of 65,535, 65,536,
     70,000 and 200,000 bytes (one deep, one one long word) among 50k ordinary
-    ones: rows equal the device path's and the oracle's, with the default
+    ones: rows equal the oracle's, with the default
     staging and with every chunk forced to u32 offsets (GM_HOST_OFF32)."""
     if chunk != "default":
         monkeypatch.setenv("GM_HOST_CHUNK", chunk)
@@ -612,8 +612,10 @@ def test_host_path_long_topics_take_u32_offsets(ctx, orc, monkeypatch, chunk):
     idx = ctx.build_index(filters)
     topics = [b"l0w1/a/b", b"x/y", b"a/b/c"] * 16_000
     for n_bytes, at in ((65_535, 100), (65_536, 2_000), (70_000, 30_000), (200_000, 47_999)):
-        deep = b"deep/" + b"/".join([b"w"] * ((n_bytes - 5) // 2))
-        topics.insert(at, (deep + b"q" * (n_bytes - len(deep)))[:n_bytes])
+        # (hundreds of 299-byte levels: the oracle restates the reference's recursion, so
+        # its stack bounds the depth a CPU check can take)
+        deep = b"deep/" + b"/".join([b"w" * 299] * (n_bytes // 300 + 1))
+        topics.insert(at, deep[:n_bytes])
         topics.insert(at + 1, b"x/" + b"z" * (n_bytes - 2))
     assert max(len(t) for t in topics) == 200_000 and len(topics) == 48_008
     want_ro, want_ids = _oracle_rows(orc, sorted(filters), topics, 1)
