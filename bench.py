@@ -575,10 +575,11 @@ def host_io(ctx, idx, db, do, tbytes, n_topics, nnz, reps=2):
     return d, pb, ho
 
 
-def update_chain(ctx, idx, n_rounds=2, n_ops=200, seed=7):
+def update_chain(ctx, idx, n_rounds=2, n_ops=200, seed=7, own=False):
     """n_rounds in-place updates of n_ops (half deletes of present filters,
     half inserts), each on the previous result; wall time and what the library
-    says each call did (emqx_gm_last_update_stats).  Returns (rounds, last)."""
+    says each call did (emqx_gm_last_update_stats).  Returns (rounds, last).
+    own: idx is released once the first update has replaced it."""
     import numpy as np
     rng = np.random.default_rng(seed)
     out, cur = [], idx
@@ -591,13 +592,45 @@ def update_chain(ctx, idx, n_rounds=2, n_ops=200, seed=7):
         out.append({"ms": ms, **{k: v for k, v in ctx.update_stats().items()
                                  if k in ("kind", "replica_mode", "replicas", "mirror_loaded", "mirror_bytes",
                                           "mirror_ms", "device_ms", "blobs_reused", "blobs_fresh")}})
-        if cur is not idx:
+        if cur is not idx or own:
             cur.release()
         cur = new
     return out, cur
 
 
-def multi_device(ctx, idx, img, big, devices, pb, ho, n_topics, nnz, single):
+def small_calls(c, ix, pb, ho, threads=8, calls=32, batch=16_384):
+    """A NIF-sized workload: `threads` callers (dirty schedulers), each issuing
+    `calls` host-buffer calls of `batch` topics (publish windows) from the
+    page-locked batch, all at once on one context.  Topics/s over the wall time
+    of the whole set (a multi-device context runs each small call whole on one
+    of its GPUs, round-robin; a single-device context queues them on one)."""
+    import threading
+    n = len(ho) - 1
+    errs = []
+
+    def run(t):
+        try:
+            for k in range(calls):
+                s0 = ((t * calls + k) * batch) % max(1, n - batch)
+                c.match_host(ix, (pb, ho[s0:s0 + batch + 1]), exact=True).free()
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    run(0)  # (warm: every device's pinned slots and pools)
+    th = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    dt = time.perf_counter() - t0
+    if errs:
+        raise RuntimeError(errs[0])
+    return {"threads": threads, "calls_per_thread": calls, "topics_per_call": batch,
+            "topics_per_s": threads * calls * batch / dt, "ms_per_call_avg": dt * 1e3 / calls}
+
+
+def multi_device(ctx, idx, img, devices, pb, ho, n_topics, nnz, single):
     """The drop-in path's multi-GPU form: ONE library context over ``devices``
     (what the NIF opens on a node: emqx_gm_opts.n_devices), outside the timed
     region.  The index goes in once (an import of this rank's snapshot) and is
@@ -607,16 +640,13 @@ def multi_device(ctx, idx, img, big, devices, pb, ho, n_topics, nnz, single):
     replica's predecessor).  ``single``: this rank's single-device figures."""
     from emqx_amd import Context
     d = {"devices": list(devices)}
-    blob = None if big else idx.device_blob()[0]
-    if big:  # (C5's 53 GB: the replicas and an update's new tables fit only without this rank's copy)
-        idx.release()
-        ctx.pool_trim()
+    d["small_calls_single_device"] = small_calls(ctx, idx, pb, ho)
+    ctx.pool_trim()  # (this rank's cached buffers and spare tables: C5's replicas need the room)
     with Context(devices=list(devices)) as c:
         t0 = time.perf_counter()
-        ix = c.import_index(img, d_blob=blob)
+        ix = c.import_index(img, d_blob=idx.device_blob()[0])
         st = c.update_stats()
-        if not big:
-            idx.release()  # (the replicas are copies: this rank's snapshot is no longer needed)
+        idx.release()  # (the replicas are copies: this rank's snapshot is no longer needed)
         d["import_and_replicate_ms"] = (time.perf_counter() - t0) * 1e3
         d["replicate_ms"] = st["replicate_ms"]
         d["replica_mode"] = st["replica_mode"]
@@ -637,7 +667,10 @@ def multi_device(ctx, idx, img, big, devices, pb, ho, n_topics, nnz, single):
         d["host_io_multi_nnz_matches_device"] = ok
         if single.get("host_io_topics_per_s"):
             d["host_io_multi_vs_single_device"] = d["host_io_multi_topics_per_s"] / single["host_io_topics_per_s"]
-        rounds, last = update_chain(c, ix)
+        d["small_calls"] = small_calls(c, ix, pb, ho)
+        d["small_calls"]["vs_single_device"] = (d["small_calls"]["topics_per_s"] /
+                                                d["small_calls_single_device"]["topics_per_s"])
+        rounds, last = update_chain(c, ix, own=True)
         d["index_update_replicas"] = {"ops": 200, "update_ms": rounds[-1]["ms"], "rounds": rounds}
         if single.get("update_ms"):
             d["index_update_replicas"]["vs_single_device"] = rounds[-1]["ms"] / single["update_ms"]
@@ -645,8 +678,6 @@ def multi_device(ctx, idx, img, big, devices, pb, ho, n_topics, nnz, single):
             d["note"] = (f"one-GPU rehearsal: {len(devices)} replicas share this GPU's HBM, CUs and PCIe link "
                          "(an update's device passes run side by side on one GPU)")
         last.release()
-        if last is not ix:
-            ix.release()
     return d
 
 
@@ -684,6 +715,12 @@ def main():
     # library's part alone (emqx_gm_index_build, or the image broadcast and import)
     build_info = {"index_source": source, "index_build_s": t_build, "filters_gen_s": t_gen,
                   "index_compile_s": t_build - t_gen}
+    if source.startswith("imported"):
+        # the mirror policy at an import (gm_image.cpp): the build's -- kept up to 8 GiB of
+        # tables (from the image's own bytes), lazy above -- as the library observed it
+        ust = ctx.update_stats()
+        build_info.update(index_import_mirror_loaded=ust["mirror_loaded"],
+                          index_import_mirror_bytes=ust["mirror_bytes"], index_import_mirror_ms=ust["mirror_ms"])
     if pg is not None:  # how many ranks compiled, the slowest rank's build, the largest host RSS
         n_built = _reduce_tensor(local, float(source == "built"))
         pg.all_reduce(n_built)
@@ -801,14 +838,12 @@ def main():
     }
     pb = ho = None
     multi = not a.no_multi and not a.no_host_io and (world > 1 or a.replicas > 1)
-    mimg = big_img = None
+    mimg = None
     if multi and rank == 0:
-        # the image the multi-device context imports, taken before this rank's own updates
-        # move the snapshot line's host mirror on (an image carries the line's mirror
-        # metadata).  C5's tables go in the image itself (53 GB: the replicas and an
-        # update's new tables fit the GPU only once this rank's copy is released)
-        big_img = idx.info.device_bytes > (16 << 30)
-        mimg = idx.export(with_blob=big_img)
+        # the image (host part; the tables are copied from this rank's device blob) that
+        # the multi-device context imports, taken before this rank's own updates move the
+        # snapshot line's host mirror on (an image carries the line's mirror metadata)
+        mimg = idx.export(with_blob=False)
     if not a.no_host_io and rank == 0:
         # PCIe-inclusive, outside the timed region: the same batch handed over in host
         # memory and its CSR returned in host memory (the NIF's call, gm_host.cpp)
@@ -868,7 +903,7 @@ def main():
             else [local] * a.replicas
         single = {"host_io_topics_per_s": out["detail"].get("host_io_topics_per_s"),
                   "update_ms": out["detail"].get("index_update", {}).get("update_ms")}
-        out["detail"]["multi_device"] = multi_device(ctx, idx, mimg, big_img, devices, pb, ho, n_topics, nnz, single)
+        out["detail"]["multi_device"] = multi_device(ctx, idx, mimg, devices, pb, ho, n_topics, nnz, single)
         idx = mimg = None
     host_barrier(pg)
     if pb is not None:

@@ -150,7 +150,8 @@ typedef struct {
  * in-place emqx_gm_index_update patches (host RAM ~ the tables' size).  By
  * default it is kept from the build for tables up to 8 GiB and downloaded from
  * the device on a snapshot line's first update above that (a 100M-filter index
- * holds no 38 GB host copy unless it is updated). */
+ * holds no 53 GB host copy unless it is updated; an import follows the same
+ * policy, its copy made from the image when it carries the tables). */
 #define EMQX_GM_OPEN_MIRROR_EAGER 0x1u /* always keep it from the build            */
 #define EMQX_GM_OPEN_MIRROR_LAZY  0x2u /* never at build: on the first update      */
 
