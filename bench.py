@@ -76,6 +76,8 @@ def parse():
     p.add_argument("--replicas", type=int, default=2,
                    help="N=1: the multi-device context's rehearsal lists this GPU this many times (0: skip); "
                         "N>1: rank 0 opens one context over all N GPUs instead (the drop-in NIF's form)")
+    p.add_argument("--multi-child", default=None, help=argparse.SUPPRESS)  # (internal: run_multi_child)
+    p.add_argument("--multi-single", default=None, help=argparse.SUPPRESS)
     p.add_argument("--no-multi", action="store_true",
                    help="skip the multi-device context (one library context over the GPUs: replication, "
                         "host-buffer match spread over the devices, replicated updates)")
@@ -630,17 +632,48 @@ def small_calls(c, ix, pb, ho, threads=8, calls=32, batch=16_384):
             "topics_per_s": threads * calls * batch / dt, "ms_per_call_avg": dt * 1e3 / calls}
 
 
+def multi_measure(c, ix, devices, pb, ho, n_topics, nnz, single, d):
+    """On a multi-device context c holding snapshot ix (replicated on every
+    device): one host-buffer emqx_gm_match of the whole page-locked batch spread
+    over every device (gm_host.cpp), the NIF-sized concurrent small calls, and
+    200-op updates applied on every replica at once (O(delta), each from its own
+    predecessor replica).  ix is released."""
+    c.match_host(ix, (pb, ho), exact=True).free()  # (warm: pinned staging, pools, workers on every device)
+    best, ok = None, True
+    for _ in range(2):
+        t0 = time.perf_counter()
+        h = c.match_host(ix, (pb, ho), exact=True)
+        dt = time.perf_counter() - t0
+        ok = ok and h.nnz == nnz
+        h.free()
+        best = dt if best is None else min(best, dt)
+    d["host_io_multi_topics_per_s"] = n_topics / best
+    d["host_io_multi_ms"] = best * 1e3
+    d["host_io_multi_nnz_matches_device"] = ok
+    if single.get("host_io_topics_per_s"):
+        d["host_io_multi_vs_single_device"] = d["host_io_multi_topics_per_s"] / single["host_io_topics_per_s"]
+    d["small_calls"] = small_calls(c, ix, pb, ho)
+    if single.get("small_calls"):
+        d["small_calls"]["vs_single_device"] = d["small_calls"]["topics_per_s"] / single["small_calls"]["topics_per_s"]
+    rounds, last = update_chain(c, ix, own=True)
+    d["index_update_replicas"] = {"ops": 200, "update_ms": rounds[-1]["ms"], "rounds": rounds}
+    if single.get("update_ms"):
+        d["index_update_replicas"]["vs_single_device"] = rounds[-1]["ms"] / single["update_ms"]
+    if len(set(devices)) == 1:
+        d["note"] = (f"one-GPU rehearsal: {len(devices)} replicas share this GPU's HBM, CUs and PCIe link "
+                     "(an update's device passes run side by side on one GPU)")
+    last.release()
+    return d
+
+
 def multi_device(ctx, idx, img, devices, pb, ho, n_topics, nnz, single):
-    """The drop-in path's multi-GPU form: ONE library context over ``devices``
-    (what the NIF opens on a node: emqx_gm_opts.n_devices), outside the timed
-    region.  The index goes in once (an import of this rank's snapshot) and is
-    replicated device to device in a tree; one host-buffer emqx_gm_match of
-    the whole page-locked batch is spread over every device (gm_host.cpp);
-    200-op updates are applied on every replica at once (O(delta), from each
-    replica's predecessor).  ``single``: this rank's single-device figures."""
+    """The drop-in path's multi-GPU form, rehearsed in this process (N=1):
+    ONE library context over ``devices`` (what the NIF opens on a node:
+    emqx_gm_opts.n_devices), outside the timed region.  The index goes in once
+    (an import of this rank's snapshot) and is replicated device to device in a
+    tree; then multi_measure.  ``single``: this rank's single-device figures."""
     from emqx_amd import Context
-    d = {"devices": list(devices)}
-    d["small_calls_single_device"] = small_calls(ctx, idx, pb, ho)
+    d = {"devices": list(devices), "process": "in-process"}
     ctx.pool_trim()  # (this rank's cached buffers and spare tables: C5's replicas need the room)
     with Context(devices=list(devices)) as c:
         t0 = time.perf_counter()
@@ -653,37 +686,78 @@ def multi_device(ctx, idx, img, devices, pb, ho, n_topics, nnz, single):
         d["replicated_bytes"] = int(ix.info.device_bytes) * (len(devices) - 1)
         d["import_mirror_loaded"] = st["mirror_loaded"]
         del img
-        c.match_host(ix, (pb, ho), exact=True).free()  # (warm: pinned staging, pools, workers on every device)
-        best, ok = None, True
-        for _ in range(2):
-            t0 = time.perf_counter()
-            h = c.match_host(ix, (pb, ho), exact=True)
-            dt = time.perf_counter() - t0
-            ok = ok and h.nnz == nnz
-            h.free()
-            best = dt if best is None else min(best, dt)
-        d["host_io_multi_topics_per_s"] = n_topics / best
-        d["host_io_multi_ms"] = best * 1e3
-        d["host_io_multi_nnz_matches_device"] = ok
-        if single.get("host_io_topics_per_s"):
-            d["host_io_multi_vs_single_device"] = d["host_io_multi_topics_per_s"] / single["host_io_topics_per_s"]
-        d["small_calls"] = small_calls(c, ix, pb, ho)
-        d["small_calls"]["vs_single_device"] = (d["small_calls"]["topics_per_s"] /
-                                                d["small_calls_single_device"]["topics_per_s"])
-        rounds, last = update_chain(c, ix, own=True)
-        d["index_update_replicas"] = {"ops": 200, "update_ms": rounds[-1]["ms"], "rounds": rounds}
-        if single.get("update_ms"):
-            d["index_update_replicas"]["vs_single_device"] = rounds[-1]["ms"] / single["update_ms"]
-        if len(set(devices)) == 1:
-            d["note"] = (f"one-GPU rehearsal: {len(devices)} replicas share this GPU's HBM, CUs and PCIe link "
-                         "(an update's device passes run side by side on one GPU)")
-        last.release()
+        multi_measure(c, ix, devices, pb, ho, n_topics, nnz, single, d)
     return d
+
+
+def multi_device_child(a):
+    """`--multi-child DEVICES`: the multi-device measurement in a process of its
+    own (rank 0 at N>1 starts it while the other ranks wait on the host): a
+    fault on the 8-GPU node then costs this detail, not the bench line.  Builds
+    the config's index through ONE context over the devices (compiled once,
+    replicated in a tree), generates the same topic stream and prints one JSON
+    line."""
+    import numpy as np
+    from emqx_amd import Context
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    devices = [int(x) for x in a.multi_child.split(",")]
+    single = json.loads(a.multi_single) if a.multi_single else {}
+    n_filters = a.filters or {"c1": 10_000, "c2": 1_000_000, "c3": 10_000_000, "c5": 100_000_000}[a.config]
+    n_topics = a.topics or {"c1": 1_000_000, "c2": 100_000_000, "c3": 100_000_000, "c5": 100_000_000}[a.config]
+    codes = gen_filter_codes(a.seed, n_filters, wildcard_only=a.config == "c2")
+    fpack = render_codes(codes)
+    d = {"devices": devices, "process": "child"}
+    with Context(devices=devices) as c:
+        t0 = time.perf_counter()
+        ix = c.build_index(fpack)
+        st = c.update_stats()
+        d["build_and_replicate_ms"] = (time.perf_counter() - t0) * 1e3
+        d["replicate_ms"] = st["replicate_ms"]
+        d["replica_mode"] = st["replica_mode"]
+        d["replicated_bytes"] = int(ix.info.device_bytes) * (len(devices) - 1)
+        del fpack
+        db, do, tbytes = c.gen_topics_device(codes, a.seed, 0, n_topics)
+        r = c.match_device(ix, db, do, n_topics, exact=True)
+        nnz = r.nnz
+        r.free()
+        ho = np.zeros(n_topics + 1, np.uint64)
+        c.memcpy_d2h(ho, do, (n_topics + 1) * 8)
+        pb = c.host_alloc(tbytes + 64)
+        c.memcpy_d2h(pb, db, tbytes)
+        pb[tbytes:] = 0
+        c.dev_free(db)
+        c.dev_free(do)
+        multi_measure(c, ix, devices, pb, ho, n_topics, nnz, single, d)
+        c.host_free(pb)
+    print(json.dumps(d), flush=True)
+
+
+def run_multi_child(a, devices, single):
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "GM_BENCH_DEVICE", "GM_BENCH_BACKEND")}
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--multi-child", ",".join(map(str, devices)),
+           "--config", a.config, "--seed", str(a.seed), "--multi-single", json.dumps(single)]
+    if a.filters:
+        cmd += ["--filters", str(a.filters)]
+    if a.topics:
+        cmd += ["--topics", str(a.topics)]
+    try:
+        p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    except subprocess.TimeoutExpired:
+        return {"devices": devices, "error": "timed out (900 s)"}
+    lines = [l for l in p.stdout.splitlines() if l.startswith('{"devices"')]
+    if p.returncode != 0 or not lines:
+        return {"devices": devices, "error": f"exit {p.returncode}", "stderr_tail": p.stderr[-2000:]}
+    return json.loads(lines[-1])
 
 
 def main():
     a = parse()
     heartbeat()
+    if a.multi_child:
+        return multi_device_child(a)
     world, rank, local, pg = dist_setup(a.gpus)
     import numpy as np
     from emqx_amd import Context
@@ -839,7 +913,7 @@ def main():
     pb = ho = None
     multi = not a.no_multi and not a.no_host_io and (world > 1 or a.replicas > 1)
     mimg = None
-    if multi and rank == 0:
+    if multi and rank == 0 and world == 1:
         # the image (host part; the tables are copied from this rank's device blob) that
         # the multi-device context imports, taken before this rank's own updates move the
         # snapshot line's host mirror on (an image carries the line's mirror metadata)
@@ -899,12 +973,18 @@ def main():
     # other ranks wait on the host
     host_barrier(pg)
     if multi and rank == 0:
-        devices = ([local] * world if "GM_BENCH_DEVICE" in os.environ else list(range(world))) if world > 1 \
-            else [local] * a.replicas
         single = {"host_io_topics_per_s": out["detail"].get("host_io_topics_per_s"),
-                  "update_ms": out["detail"].get("index_update", {}).get("update_ms")}
-        out["detail"]["multi_device"] = multi_device(ctx, idx, mimg, devices, pb, ho, n_topics, nnz, single)
-        idx = mimg = None
+                  "update_ms": out["detail"].get("index_update", {}).get("update_ms"),
+                  "small_calls": small_calls(ctx, idx, pb, ho)}
+        out["detail"]["small_calls_single_device"] = single["small_calls"]
+        if world == 1:
+            out["detail"]["multi_device"] = multi_device(ctx, idx, mimg, [local] * a.replicas, pb, ho, n_topics,
+                                                         nnz, single)
+            idx = mimg = None
+        else:
+            # N>1: one context over all the node's GPUs, in a process of its own
+            devices = [local] * world if "GM_BENCH_DEVICE" in os.environ else list(range(world))
+            out["detail"]["multi_device"] = run_multi_child(a, devices, single)
     host_barrier(pg)
     if pb is not None:
         ctx.host_free(pb)

@@ -101,6 +101,7 @@ SIGNATURES = {
     "emqx_gm_filter_ranks": (_i32, [_vp, _vp, _u64, _vp, C.POINTER(_u64)]),
     "emqx_gm_shard_of": (_i32, [_vp, _vp, _u64, _u32, _vp]),
     "emqx_gm_index_build_shard": (_i32, [_vp, _vp, _vp, _u64, _vp, _vp, _vp, _vp, C.POINTER(_vp)]),
+    "emqx_gm_index_build_sharded": (_i32, [_vp, _vp, _vp, _u64, _vp, _vp, _vp, C.POINTER(_vp)]),
     "emqx_gm_csr_row_lengths": (_i32, [_vp, C.POINTER(Csr), _vp]),
     "emqx_gm_merge_rows": (_i32, [_vp, _u64, _u64, _u32, _vp, _vp, _u32, C.POINTER(Csr)]),
     "emqx_gm_prefix_plan": (_i32, [_vp, _vp, _u64, _u32, _vp, C.POINTER(_vp)]),

@@ -443,12 +443,28 @@ int emqx_gm_index_build(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo,
   GM_GUARD_END(ctx)
 }
 
+int emqx_gm_index_build_sharded(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_t n,
+                                const uint64_t* sub_off, const uint32_t* sub_ids, uint32_t* perm_out,
+                                emqx_gm_index** out) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  GM_GUARD_BEGIN
+  const double t0 = begin_index_call(EMQX_GM_UPD_BUILD);
+  hipSetDevice(ctx->device);
+  const int rc = gm::build_sharded(ctx, fb, fo, n, sub_off, sub_ids, perm_out, out);
+  gm::tl_ustats.total_ms = gm::now_ms() - t0;
+  return rc;
+  GM_GUARD_END(ctx)
+}
+
 int emqx_gm_index_update(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8_t* fb, const uint64_t* fo,
                          const uint8_t* ops, uint64_t n_ops, emqx_gm_index** out) {
   if (!ctx) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   if (prev && prev->device != ctx->device)
     return gm::set_err(ctx, EMQX_GM_EINVAL, "index_update: index lives on another device");
+  if (prev && prev->route)
+    return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "index_update: sharded index (rebuild it)");
   GM_GUARD_BEGIN
   const double t0 = begin_index_call(EMQX_GM_UPD_NONE);
   hipSetDevice(ctx->device);
@@ -462,6 +478,8 @@ int emqx_gm_index_update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   if (prev && prev->device != ctx->device)
     return gm::set_err(ctx, EMQX_GM_EINVAL, "index_update_subs: index lives on another device");
+  if (prev && prev->route)
+    return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "index_update_subs: sharded index (rebuild it)");
   GM_GUARD_BEGIN
   const double t0 = begin_index_call(EMQX_GM_UPD_NONE);
   hipSetDevice(ctx->device);
@@ -472,6 +490,7 @@ int emqx_gm_index_update_subs(emqx_gm_ctx* ctx, emqx_gm_index* prev, const uint8
 int emqx_gm_index_export(emqx_gm_ctx* ctx, const emqx_gm_index* idx, uint32_t flags, uint8_t* buf, uint64_t* size) {
   if (!ctx) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (idx && idx->route) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "index_export: sharded index");
   GM_GUARD_BEGIN
   return gm::index_export(ctx, idx, flags, buf, size);
   GM_GUARD_END(ctx)
@@ -590,6 +609,13 @@ int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb,
   if (idx->device != ctx->device) return gm::set_err(ctx, EMQX_GM_EINVAL, "match: index lives on another device");
   std::memset(out, 0, sizeof(*out));
   GM_GUARD_BEGIN
+  if (idx->route) {  // a sharded index: each topic to its one device's shard (gm_shard.cpp)
+    if (flags & EMQX_GM_DEVICE_IO)
+      return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "match: sharded index takes host buffers");
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    hipSetDevice(ctx->device);
+    return noted(ctx, ctx, gm::run_match_sharded(ctx, idx, tb, to, n, flags, out));
+  }
   if (!(flags & EMQX_GM_DEVICE_IO) && !ctx->members.empty() && !idx->ov &&
       idx->reps.size() == ctx->members.size() && n <= gm::host_chunk_topics() && !gm::knob("GM_HOST_SIMPLE"))
     return match_small(ctx, idx, tb, to, n, flags, out);
@@ -623,6 +649,7 @@ int emqx_gm_match_submit(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8
   if (n >= 0xFFFFFFF0ull) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: batch too large (>= 2^32 topics)");
   if (idx->device != ctx->device) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_submit: index lives on another device");
   if (idx->ov) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "match_submit: overlay snapshot (use emqx_gm_match)");
+  if (idx->route) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "match_submit: sharded index (use emqx_gm_match)");
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
   void* t = nullptr;
@@ -654,6 +681,12 @@ int emqx_gm_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr
   std::memset(out, 0, sizeof(*out));
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
+  if (idx->route) {  // a sharded index: each row on the shard of its filters (gm_shard.cpp)
+    if ((flags & EMQX_GM_DEVICE_IO) || m->on_device)
+      return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "fanout: sharded index takes host rows");
+    if (idx->subs.empty()) return gm::set_err(ctx, EMQX_GM_EINVAL, "fanout: index without subscriber lists");
+    return noted(ctx, ctx, gm::run_fanout_sharded(ctx, idx, m, flags, out));
+  }
   if (!ctx->members.empty() && !(flags & EMQX_GM_DEVICE_IO) && !m->on_device)
     return noted(ctx, ctx, gm::run_fanout_multi(ctx, idx, m, flags, out));
   return noted(ctx, ctx, gm::run_fanout(ctx, idx, m, flags, out));
@@ -671,6 +704,7 @@ int emqx_gm_fanout_part(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_g
     return gm::set_err(ctx, EMQX_GM_EINVAL, "fanout_part: flags");
   if (idx->view.gmap) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "fanout_part: shard index");
   if (idx->ov) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "fanout_part: overlay snapshot");
+  if (idx->route) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "fanout_part: sharded index");
   std::memset(out, 0, sizeof(*out));
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
@@ -754,7 +788,7 @@ int emqx_gm_matched_filter_bytes(emqx_gm_ctx* ctx, const emqx_gm_index* idx, con
                                  uint64_t* out) {
   if (!ctx || !idx || !csr || !out || !csr->on_device) return EMQX_GM_EINVAL;
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
-  if (idx->ov) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "matched_filter_bytes: overlay snapshot");
+  if (idx->ov || idx->route) return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED, "matched_filter_bytes: overlay or sharded");
   GM_GUARD_BEGIN
   hipSetDevice(ctx->device);
   return gm::sum_filter_lengths(ctx, idx, csr->ids, csr->nnz, out);

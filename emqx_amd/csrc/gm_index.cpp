@@ -1650,6 +1650,10 @@ void free_index(emqx_gm_index* idx) {
   for (emqx_gm_index* r : idx->reps)
     if (r && r->refs.fetch_sub(1) == 1) free_index(r);
   idx->reps.clear();
+  for (emqx_gm_index* s : idx->shards)
+    if (s && s->refs.fetch_sub(1) == 1) free_index(s);
+  idx->shards.clear();
+  if (idx->route) free_route(idx->route);
   if (idx->ov) free_overlay(idx);
   delete idx->mirror;
   if (idx->dev_base || idx->dev_subs) {

@@ -284,6 +284,13 @@ struct emqx_gm_index {
   // released with this snapshot.
   std::vector<emqx_gm_index*> reps;
   bool reused_blob = false;  // (replicate_index: dev_base was a released snapshot's blob)
+  // a prefix-sharded index (emqx_gm_index_build_sharded, gm_shard.cpp): shards[k]
+  // on the context's k-th device (a shard index with global ids), route sends a
+  // topic to its one shard, fshard[global id] = a filter's shard (or
+  // EMQX_GM_ALL_SHARDS).  This object holds only the host side (ft, subs, info).
+  std::vector<emqx_gm_index*> shards;
+  emqx_gm_route* route = nullptr;
+  std::vector<uint32_t> fshard;
 };
 
 namespace gm {
@@ -493,6 +500,13 @@ int attach_replicas(emqx_gm_index* out, std::vector<RepTarget>& t, int rc);
 // (sharing prev's replica's tables when out shares prev's); an overlay stays
 // on the first device.  On failure `out` is released and *out_p cleared.
 int replicate_result(emqx_gm_ctx* ctx, emqx_gm_index* prev, emqx_gm_index** out_p);
+// gm_shard.cpp: the prefix-sharded index of a multi-device context
+int build_sharded(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint64_t n, const uint64_t* sub_off,
+                  const uint32_t* sub_ids, uint32_t* perm_out, emqx_gm_index** out);
+int run_match_sharded(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                      uint32_t flags, emqx_gm_csr* out);
+int run_fanout_sharded(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
+                       emqx_gm_csr* out);
 // emqx_gm_fanout of host rows over a multi-device context's replicas (one
 // slice per device, one page-locked result); small batches: run_fanout
 int run_fanout_multi(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,

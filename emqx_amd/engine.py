@@ -289,7 +289,7 @@ class Context:
         self.close()
 
     # ------------------------------------------------------------------ index
-    def build_index(self, filters, subs=None) -> Index:
+    def build_index(self, filters, subs=None, _entry: str = "emqx_gm_index_build") -> Index:
         """filters: sequence of bytes/str, or a packed (bytes, offsets) pair.
         subs: optional per-filter subscriber lists, or a packed (offsets, ids) pair."""
         fb, fo = filters if isinstance(filters, tuple) else pack(filters)
@@ -307,9 +307,14 @@ class Context:
                 si = np.zeros(1, np.uint32)
         perm = np.zeros(max(n, 1), np.uint32)
         h = C.c_void_p()
-        check(lib().emqx_gm_index_build(self.h, _ptr(fb), _ptr(fo), n, _ptr(so), _ptr(si), _ptr(perm),
-                                        C.byref(h)), self.h, "index_build")
+        check(getattr(lib(), _entry)(self.h, _ptr(fb), _ptr(fo), n, _ptr(so), _ptr(si), _ptr(perm), C.byref(h)),
+              self.h, _entry[8:])
         return Index(self, h, perm[:n])
+
+    def build_index_sharded(self, filters, subs=None) -> Index:
+        """A prefix-sharded index over this context's devices (emqx_gm_index_build_sharded):
+        one shard per listed device, each topic matched on its one shard."""
+        return self.build_index(filters, subs, _entry="emqx_gm_index_build_sharded")
 
     def import_index(self, image: np.ndarray, d_blob: Optional[int] = None) -> Index:
         """A snapshot from an image (emqx_gm_index_import); its device tables from

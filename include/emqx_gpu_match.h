@@ -367,6 +367,21 @@ int emqx_gm_merge_rows(emqx_gm_ctx *ctx, uint64_t n_rows, uint64_t stride, uint3
 typedef struct emqx_gm_route emqx_gm_route;
 int emqx_gm_prefix_plan(const uint8_t *filter_bytes, const uint64_t *filter_off, uint64_t n_filters,
                         uint32_t n_shards, uint32_t *shard_out, emqx_gm_route **route);
+/* The prefix-sharded index behind ONE multi-device context (the NIF's form of
+ * this plan, for a filter set that does not fit one GPU): the filters are
+ * partitioned as emqx_gm_prefix_plan does over the context's devices (one
+ * shard per listed device; '+' / '#'-first filters on every one), each shard
+ * compiled and placed on its device at once.  The returned index is used like
+ * any other: emqx_gm_match on host buffers routes each topic to its one shard,
+ * matches every device's topics there at the same time and returns the rows in
+ * batch order (global ids, bit-exact with an unsharded index); emqx_gm_fanout
+ * on host rows fans each row out on its shard; emqx_gm_index_info / _filter /
+ * _subscriber_count answer for the whole set.  Device-buffer calls, updates and
+ * images of a sharded index: EMQX_GM_EUNSUPPORTED (a global id shifts on every
+ * shard when one filter is added: rebuild it).  Arguments as emqx_gm_index_build. */
+int emqx_gm_index_build_sharded(emqx_gm_ctx *ctx, const uint8_t *filter_bytes, const uint64_t *filter_off,
+                                uint64_t n_filters, const uint64_t *sub_off, const uint32_t *sub_ids,
+                                uint32_t *perm_out, emqx_gm_index **out);
 /* dest[i] = the shard of topic i (host buffers / device buffers, n_topics entries) */
 int emqx_gm_route_topics_host(const emqx_gm_route *route, const uint8_t *topic_bytes, const uint64_t *topic_off,
                               uint64_t n_topics, uint32_t *dest);

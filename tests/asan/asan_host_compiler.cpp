@@ -38,6 +38,7 @@ int run_all(int K, const std::function<int(int)>& f) {
 std::vector<RepTarget> rep_targets(emqx_gm_ctx*, emqx_gm_index*) { return {}; }
 emqx_gm_index* replica_shell(emqx_gm_ctx*, const emqx_gm_index*) { return nullptr; }
 int attach_replicas(emqx_gm_index*, std::vector<RepTarget>&, int rc) { return rc; }
+void free_route(emqx_gm_route*) {}  // (gm_route.hip's: no host-only index has a route)
 }
 
 static int compile(const std::vector<std::string>& fs) {

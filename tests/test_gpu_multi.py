@@ -399,6 +399,56 @@ def test_two_gpus_replicas_and_small_calls(ctx1, orc, monkeypatch):
     i1.release()
 
 
+@pytest.mark.parametrize("devices,chunk", [([0, 0], None), ([0, 0, 0], "4096")])
+def test_sharded_index_behind_the_c_abi(ctx1, orc, monkeypatch, devices, chunk):
+    """emqx_gm_index_build_sharded: the prefix plan behind ONE multi-device
+    context (SURVEY §8e C5's sharded form, reachable from the NIF): filters
+    partitioned by first word over the devices ('+' / '#'-first ones on every
+    device), each topic matched on its one shard -- rows equal the unsharded
+    single-device index's and the oracle's (global ids, batch order), with
+    '$SYS', empty, wildcard and unknown-first-word topics, an empty batch and
+    chunked shard batches; the fan-out of those rows equals the unsharded
+    fan-out; the set-wide lookups answer for every filter; updates, images
+    and device-buffer calls are refused."""
+    from emqx_amd import Context, GpuMatchError
+    from emqx_amd.engine import gen_filter_codes, render_codes
+    if chunk:
+        monkeypatch.setenv("GM_HOST_CHUNK", chunk)
+    codes = gen_filter_codes(5, 60_000)
+    fb, fo = render_codes(codes)
+    extra = [b"#", b"+/x", b"$SYS/#", b"solo/word", b"solo/+/#"]
+    filters = sorted(set(orc.unpack(fb, fo)) | set(extra))
+    rng = np.random.default_rng(8)
+    subs = [rng.integers(0, 10**6, size=int(rng.integers(0, 4))).tolist() for _ in filters]
+    tb, to = orc.render_codes(orc.gen_topic_codes(5, 0, 200_000, codes))
+    topics = orc.unpack(tb, to) + [b"$SYS/broker", b"", b"/", b"a/+", b"solo/word", b"solo/x/y", b"nosuch/1",
+                                   b"+/x", b"l0w1"]
+    i1 = ctx1.build_index(filters, subs=subs)
+    want = ctx1.match(i1, topics, exact=True)
+    wf = ctx1.fanout(i1, *want)
+    oro, oids = _oracle_rows(orc, filters, topics[::97])
+    with Context(devices=devices) as c:
+        ix = c.build_index_sharded(filters, subs=subs)
+        assert ix.n_filters == len(filters) and ix.info.n_subs == sum(len(x) for x in subs)
+        assert ix.info.n_wildcard == i1.info.n_wildcard
+        for f in (0, 7, len(filters) // 2, len(filters) - 1):
+            assert ix.filter(f) == filters[f] and ix.subscriber_count(f) == len(subs[f])
+        got = c.match(ix, topics, exact=True)
+        _eq(got, want, "sharded rows")
+        sub = [got[1][got[0][i]:got[0][i + 1]].tolist() for i in range(0, len(topics), 97)]
+        assert sub == [oids[oro[j]:oro[j + 1]].tolist() for j in range(len(oro) - 1)]
+        _eq(c.match(ix, topics, exact=False), ctx1.match(i1, topics, exact=False), "trie mode")
+        _eq(c.fanout(ix, *got), wf, "sharded fan-out")
+        e = c.match(ix, [], exact=True)
+        assert e[0].tolist() == [0] and len(e[1]) == 0
+        for bad in (lambda: c.update_index(ix, [(b"q/+", True)]), lambda: ix.export(),
+                    lambda: c.match_device(ix, 0, 0, 0)):
+            with pytest.raises(GpuMatchError):
+                bad()
+        ix.release()
+    i1.release()
+
+
 @pytest.mark.parametrize("replicas", [2, 3])
 def test_fanout_spread_over_replicas(ctx1, orc, monkeypatch, replicas):
     """emqx_gm_fanout of host rows through a multi-device context: one slice of
