@@ -93,8 +93,7 @@ int build_sharded(emqx_gm_ctx* ctx, const uint8_t* fb, const uint64_t* fo, uint6
   std::iota(ord.begin(), ord.end(), 0u);
   sort_filters(ord, fb, fo);
   std::vector<uint32_t> gid(n);
-  auto sf = std::make_shared<SortedFilters>();
-  sf->off.push_back(0);
+  auto sf = std::make_shared<SortedFilters>();  // (off starts as {0})
   for (uint64_t k = 0; k < n; ++k) {
     const uint32_t i = ord[k];
     const uint64_t li = fo[i + 1] - fo[i];
