@@ -144,6 +144,42 @@ void HostPool::release(void* p) {
   cached_ += r;
 }
 
+PinPool::~PinPool() {
+  for (auto& kv : size_) (void)hipHostFree(kv.first);
+}
+void* PinPool::get(size_t bytes) {
+  size_t r = 64 << 10;  // powers of two from 64 KiB
+  while (r < bytes) r <<= 1;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = free_.find(r);
+    if (it != free_.end()) {
+      void* p = it->second;
+      free_.erase(it);
+      cached_ -= r;
+      return p;
+    }
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, r, hipHostMallocPortable) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu_);
+  size_[p] = r;
+  return p;
+}
+void PinPool::put(void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = size_.find(p);
+  if (it == size_.end()) return;
+  if (cached_ + it->second > kCap) {  // (over the cap: freed)
+    (void)hipHostFree(p);
+    size_.erase(it);
+    return;
+  }
+  free_.emplace(it->second, p);
+  cached_ += it->second;
+}
+
 namespace {
 std::mutex g_pin_mu;
 std::map<uintptr_t, size_t> g_pinned;  // emqx_gm_host_alloc buffers: start -> bytes
@@ -256,6 +292,7 @@ static int open_one(int dev, uint32_t flags, emqx_gm_ctx** out) {
   gm::note_ctx_open(dev);
   ctx->pool = new gm::DevPool(dev);
   ctx->hpool = new gm::HostPool;
+  ctx->pins = new gm::PinPool;
   for (auto& e : ctx->ev) {
     if (hipEventCreate(&e) != hipSuccess) {
       emqx_gm_close(ctx);
@@ -360,6 +397,7 @@ int emqx_gm_close(emqx_gm_ctx* ctx) {
     gm::free_host_pipe(ctx);
     delete ctx->pool;
     delete ctx->hpool;
+    delete ctx->pins;
     for (auto& e : ctx->ev)
       if (e) hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) hipStreamDestroy(ctx->stream);
@@ -566,33 +604,27 @@ static int noted(const emqx_gm_ctx* api_ctx, const emqx_gm_ctx* ran, int rc) {
   return rc;
 }
 
-// A host-buffer call of at most one chunk on a multi-device context: ONE
-// device serves it whole -- the first whose lock is free from a round-robin
-// start -- under that device's lock only, so concurrent callers (a NIF's dirty
-// schedulers, each with a publish window) run on different GPUs at once, as
-// the reference's publishers match in their own processes at once
+// A host-buffer call of at most one chunk (a publish window): ONE device serves
+// it whole -- on a multi-device context the next one round-robin -- and the
+// call holds that device's lock only while it queues its work and collects
+// its rows (gm_host.cpp run_host_small), so concurrent callers (a NIF's dirty
+// schedulers) overlap on one device and run on different GPUs at once, as the
+// reference's publishers match in their own processes at once
 // (apps/emqx/src/emqx_trie.erl:66-70, emqx_router.erl:128-145).  Larger calls
-// are cut into chunks spread over every device (gm_host.cpp).
+// are cut into chunks spread over every device (gm_host.cpp run_host_pipe).
 static int match_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                        uint32_t flags, emqx_gm_csr* out) {
-  const size_t K = 1 + ctx->members.size();
-  auto mem = [&](size_t k) { return k ? ctx->members[k - 1] : ctx; };
-  const size_t s = ctx->rr.fetch_add(1, std::memory_order_relaxed) % K;
-  std::unique_lock<std::recursive_mutex> lk;
-  size_t pick = s;
-  for (size_t j = 0; j < K && !lk.owns_lock(); ++j) {
-    std::unique_lock<std::recursive_mutex> l(mem((s + j) % K)->mu, std::try_to_lock);
-    if (l.owns_lock()) {
-      lk = std::move(l);
-      pick = (s + j) % K;
-    }
-  }
-  if (!lk.owns_lock()) lk = std::unique_lock<std::recursive_mutex>(mem(s)->mu);
-  emqx_gm_ctx* mc = mem(pick);
+  const size_t K = 1 + (idx->reps.size() == ctx->members.size() ? ctx->members.size() : 0);
+  const size_t pick = K > 1 ? ctx->rr.fetch_add(1, std::memory_order_relaxed) % K : 0;
+  emqx_gm_ctx* mc = pick ? ctx->members[pick - 1] : ctx;
   const emqx_gm_index* rix = pick ? idx->reps[pick - 1] : idx;
   hipSetDevice(mc->device);
-  const int rc = gm::run_match_host(mc, rix, tb, to, n, flags, out);  // (mc has no members: one device)
-  noted(ctx, mc, rc);
+  emqx_gm_match_stats st{};
+  const int rc = gm::run_host_small(mc, rix, tb, to, n, flags, out, &st);
+  if (rc == EMQX_GM_OK) {
+    tl_stats = st;
+    tl_stats_ctx = ctx;
+  }
   hipSetDevice(ctx->device);
   return rc;
 }
@@ -616,8 +648,8 @@ int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb,
     hipSetDevice(ctx->device);
     return noted(ctx, ctx, gm::run_match_sharded(ctx, idx, tb, to, n, flags, out));
   }
-  if (!(flags & EMQX_GM_DEVICE_IO) && !ctx->members.empty() && !idx->ov &&
-      idx->reps.size() == ctx->members.size() && n <= gm::host_chunk_topics() && !gm::knob("GM_HOST_SIMPLE"))
+  if (!(flags & EMQX_GM_DEVICE_IO) && !idx->ov && n <= gm::host_chunk_topics() &&
+      (n == 0 || to[n] - to[0] <= (uint64_t(64) << 20)) && !gm::knob("GM_HOST_SIMPLE") && !gm::knob("GM_HOST_PIPE"))
     return match_small(ctx, idx, tb, to, n, flags, out);
   std::unique_lock<std::recursive_mutex> lk(ctx->mu);
   hipSetDevice(ctx->device);

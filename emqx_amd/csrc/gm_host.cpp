@@ -783,6 +783,132 @@ static int run_host_pipe(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8
 
 uint64_t host_chunk_topics() { return std::max<uint64_t>(1024, env_u64("GM_HOST_CHUNK", 256u << 10)); }
 
+int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                   uint32_t flags, emqx_gm_csr* out, emqx_gm_match_stats* st_out) {
+  // ---- outside the lock: the offsets checked, the call's inputs staged in
+  // page-locked buffers of its own (u16 lengths; u32 offsets past 65,535 B)
+  uint64_t lng = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (to[i + 1] < to[i]) return set_err(ctx, EMQX_GM_EINVAL, "match: topic offsets not monotone");
+    lng |= (to[i + 1] - to[i]) >> 16;
+  }
+  const bool use32 = lng != 0 || env_u64("GM_HOST_OFF32", 0) != 0;
+  const bool wide = env_u64("GM_HOST_WIDE_ROWS", 0) != 0;  // (tests: u64 row offsets over PCIe)
+  const uint64_t b0 = n ? to[0] : 0, nbytes = n ? to[n] - b0 : 0;
+  const bool direct = nbytes && host_pinned_range(tb + b0, nbytes);
+  struct Pins {
+    PinPool* pool;
+    void* p[4] = {};
+    ~Pins() {
+      for (void* q : p)
+        if (q) pool->put(q);
+    }
+  } pins{ctx->pins};
+  const size_t lbytes = use32 ? (n + 1) * 4 : n * 2 + 2, obytes = (n + 1) * (wide ? 8 : 4);
+  if ((!direct && !(pins.p[0] = ctx->pins->get(nbytes + 64))) || !(pins.p[1] = ctx->pins->get(lbytes)) ||
+      !(pins.p[2] = ctx->pins->get(obytes)))
+    return set_err(ctx, EMQX_GM_ENOMEM, "match: pinned staging");
+  if (!direct) {
+    uint8_t* tx = static_cast<uint8_t*>(pins.p[0]);
+    if (nbytes) std::memcpy(tx, tb + b0, nbytes);
+    std::memset(tx + nbytes, 0, 64);
+  }
+  if (use32) {
+    stage_off32(to, 0, n, static_cast<uint32_t*>(pins.p[1]));
+  } else {
+    uint16_t* l = static_cast<uint16_t*>(pins.p[1]);
+    for (uint64_t i = 0; i < n; ++i) l[i] = uint16_t(to[i + 1] - to[i]);
+  }
+  // ---- under the lock: the inputs up, the call queued, its rows' copy-out
+  // behind its speculative assembly (one device round trip for the call)
+  std::unique_lock<std::recursive_mutex> lk(ctx->mu);
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  void* dv[4] = {ctx->pool->alloc(nbytes + 64), ctx->pool->alloc(lbytes), ctx->pool->alloc((n + 1) * 8),
+                 ctx->pool->alloc(wide ? 16 : (n + 1) * 4)};
+  auto drop_dev = [&]() {  // (under the lock; the call's work is done or was never queued)
+    for (void*& q : dv)
+      if (q) ctx->pool->release(q);
+  };
+  if (!dv[0] || !dv[1] || !dv[2] || !dv[3]) {
+    drop_dev();
+    return set_err(ctx, EMQX_GM_ENOMEM, "match: input workspace");
+  }
+  uint8_t* d_b = static_cast<uint8_t*>(dv[0]);
+  uint64_t* d_o = static_cast<uint64_t*>(dv[2]);
+  hipError_t e = direct ? hipMemcpyAsync(d_b, tb + b0, nbytes, hipMemcpyHostToDevice, st)
+                        : hipMemcpyAsync(d_b, pins.p[0], nbytes + 64, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && direct) e = hipMemsetAsync(d_b + nbytes, 0, 64, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dv[1], pins.p[1], lbytes, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess || (use32 ? launch_off32_to_64(st, static_cast<const uint32_t*>(dv[1]), n + 1, d_o)
+                                : scan_len16(ctx, st, static_cast<const uint16_t*>(dv[1]), n, d_o))) {
+    hipStreamSynchronize(st);
+    drop_dev();
+    return set_err(ctx, EMQX_GM_EDEVICE, "match: inputs to device");
+  }
+  MatchTail tail;
+  tail.enqueue = [&](const uint64_t* d_ro, const uint32_t* d_ids, uint64_t cap) -> int {
+    if (!(pins.p[3] = ctx->pins->get(cap * 4 + 4))) return set_err(ctx, EMQX_GM_ENOMEM, "match: pinned rows");
+    hipError_t x = hipSuccess;
+    if (wide) {
+      x = hipMemcpyAsync(pins.p[2], d_ro, (n + 1) * 8, hipMemcpyDeviceToHost, st);
+    } else if (launch_off64_to_32(st, d_ro, n + 1, static_cast<uint32_t*>(dv[3]))) {
+      x = hipErrorLaunchFailure;
+    } else {
+      x = hipMemcpyAsync(pins.p[2], dv[3], (n + 1) * 4, hipMemcpyDeviceToHost, st);
+    }
+    if (x == hipSuccess && cap) x = hipMemcpyAsync(pins.p[3], d_ids, cap * 4, hipMemcpyDeviceToHost, st);
+    return x == hipSuccess ? 0 : set_err(ctx, EMQX_GM_EDEVICE, "match: rows to host");
+  };
+  void* ticket = nullptr;
+  int rc = match_submit(ctx, idx, d_b, d_o, n, flags | EMQX_GM_DEVICE_IO, &ticket, &tail);
+  if (rc) {
+    hipStreamSynchronize(st);
+    drop_dev();
+    return rc;
+  }
+  lk.unlock();
+  // ---- outside the lock: the device round trip (other callers queue theirs meanwhile)
+  emqx_gm_csr dc{};
+  rc = match_wait(ctx, ticket, &dc, &tail, st_out);
+  lk.lock();
+  drop_dev();  // (match_wait returned: this call's work on them is done)
+  if (rc) return rc;
+  const uint64_t nnz = dc.nnz;
+  const bool fast = tail.used;  // the rows came back with the call
+  uint64_t* r_off = static_cast<uint64_t*>(ctx->hpool->alloc((n + 1) * 8));
+  uint32_t* r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(nnz * 4 + 4));
+  if (!r_off || !r_ids || (!fast && (e = hipMemcpyAsync(r_off, dc.row_off, (n + 1) * 8, hipMemcpyDeviceToHost, st),
+                                     e == hipSuccess && nnz &&
+                                         (e = hipMemcpyAsync(r_ids, dc.ids, nnz * 4, hipMemcpyDeviceToHost, st)),
+                                     e == hipSuccess && (e = hipStreamSynchronize(st)), e != hipSuccess))) {
+    ctx->hpool->release(r_off);
+    ctx->hpool->release(r_ids);
+    ctx->pool->release(dc.row_off);
+    ctx->pool->release(dc.ids);
+    return set_err(ctx, r_off && r_ids ? EMQX_GM_EDEVICE : EMQX_GM_ENOMEM, "match: host result");
+  }
+  ctx->pool->release(dc.row_off);
+  ctx->pool->release(dc.ids);
+  lk.unlock();
+  if (fast) {  // the rows out of the call's page-locked buffers (outside the lock)
+    if (wide) {
+      std::memcpy(r_off, pins.p[2], (n + 1) * 8);
+    } else {
+      const uint32_t* ro = static_cast<const uint32_t*>(pins.p[2]);
+      for (uint64_t i = 0; i <= n; ++i) r_off[i] = ro[i];
+    }
+    if (nnz) std::memcpy(r_ids, pins.p[3], nnz * 4);
+  }
+  out->n_rows = n;
+  out->nnz = nnz;
+  out->row_off = r_off;
+  out->ids = r_ids;
+  out->on_device = 0;
+  out->priv = ctx;  // the owning context (emqx_gm_csr_free checks it)
+  return 0;
+}
+
 int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                    uint32_t flags, emqx_gm_csr* out) {
   // the devices: this context, then the members the index has replicas on

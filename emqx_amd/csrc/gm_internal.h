@@ -88,6 +88,22 @@ class HostPool {
   void drop(void* p, bool pinned);
 };
 
+// Page-locked staging buffers of the small host-buffer calls (gm_host.cpp
+// run_host_small): each call in flight owns its own, so concurrent calls on
+// one context overlap; a thread-safe size-keyed free list (at most kCap cached).
+class PinPool {
+ public:
+  ~PinPool();
+  void* get(size_t bytes);  // nullptr on failure
+  void put(void* p);
+ private:
+  static constexpr size_t kCap = 512ull << 20;
+  std::mutex mu_;
+  std::multimap<size_t, void*> free_;
+  std::map<void*, size_t> size_;
+  size_t cached_ = 0;
+};
+
 // Page-locked host buffers handed out by emqx_gm_host_alloc: the host-buffer
 // match sends topic text that lies in one of them by DMA, without staging it
 // (gm_host.cpp).  Process-wide, so a buffer is found from any context.
@@ -152,6 +168,7 @@ struct emqx_gm_ctx {
   std::recursive_mutex mu;
   gm::DevPool* pool = nullptr;
   gm::HostPool* hpool = nullptr;
+  gm::PinPool* pins = nullptr;  // (thread safe: small host calls stage outside mu)
   emqx_gm_match_stats stats{};
   hipEvent_t ev[6]{};
   // per match call (gm_match.hip MatchCall, under mu): reusable events and
@@ -327,9 +344,12 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, con
               uint32_t flags, emqx_gm_csr* out, MatchTail* tail = nullptr);
 // the two halves of run_match (emqx_gm_match_submit / _wait): submit under
 // ctx->mu; wait without it (it takes the lock after the device wait)
+// tail (optional): as run_match's, kept by the caller until match_wait;
+// st_out (optional): the call's own stats (ctx->stats may belong to a later call by then)
 int match_submit(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
-                 uint32_t flags, void** ticket);
-int match_wait(emqx_gm_ctx* ctx, void* ticket, emqx_gm_csr* out);
+                 uint32_t flags, void** ticket, MatchTail* tail = nullptr);
+int match_wait(emqx_gm_ctx* ctx, void* ticket, emqx_gm_csr* out, MatchTail* tail = nullptr,
+               emqx_gm_match_stats* st_out = nullptr);
 int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
                emqx_gm_csr* out, uint32_t part = 0, uint32_t n_parts = 1, uint64_t* first_out = nullptr);
 int run_merge_rows(emqx_gm_ctx* ctx, uint64_t n_rows, uint64_t stride, uint32_t n_pieces, const uint32_t* d_lens,
@@ -474,6 +494,13 @@ int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
 void free_host_pipe(emqx_gm_ctx* ctx);
 // the topics of one host-pipeline chunk at most (a call this small runs whole on one device)
 uint64_t host_chunk_topics();
+// A host-buffer call of at most one chunk, entered WITHOUT ctx->mu: staged into
+// the call's own page-locked buffers outside the lock, queued under it (inputs
+// up, the match, the rows' copy-out behind its speculative assembly), waited
+// for outside it -- so concurrent small calls on one device overlap one
+// another's host work and device round trips
+int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                   uint32_t flags, emqx_gm_csr* out, emqx_gm_match_stats* st_out);
 // gm_multi.cpp: multi-device contexts (emqx_gm_opts.n_devices).
 // A copy of flat snapshot `src` (any device) on member context m's device:
 // the host tables shared or copied, the device tables copied device to device

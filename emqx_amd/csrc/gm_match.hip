@@ -3355,6 +3355,7 @@ struct MatchCall {
   uint8_t* ctrs_p = nullptr;
   uint64_t* pin = nullptr;  // [0] match total, [1..4] the pass counters
   hipEvent_t ev[3] = {};    // start, after the main pass, done
+  emqx_gm_match_stats st_copy{};  // the stats finish() wrote for this call
   explicit MatchCall(emqx_gm_ctx* c) : ctx(c) {}
   MatchCall(const MatchCall&) = delete;
   MatchCall& operator=(const MatchCall&) = delete;
@@ -3631,6 +3632,10 @@ int MatchCall::finish(emqx_gm_csr* out, MatchTail* tail, bool locked) {
   }
   std::unique_lock<std::recursive_mutex> lk(ctx->mu, std::defer_lock);
   if (!locked) lk.lock();
+  struct StatsCopy {  // this call's stats, kept with it (destroyed before lk: still under the lock)
+    MatchCall* c;
+    ~StatsCopy() { c->st_copy = c->ctx->stats; }
+  } stats_copy{this};
   hipStream_t st = ctx->stream;
   emqx_gm_match_stats& S = ctx->stats;
   S = emqx_gm_match_stats{};
@@ -3770,9 +3775,9 @@ int run_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb_in, 
 }
 
 int match_submit(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
-                 uint32_t flags, void** ticket) {
+                 uint32_t flags, void** ticket, MatchTail* tail) {
   auto* c = new MatchCall(ctx);
-  if (int rc = c->submit(idx, tb, to, n, flags, nullptr)) {
+  if (int rc = c->submit(idx, tb, to, n, flags, tail)) {
     delete c;
     return rc;
   }
@@ -3781,10 +3786,11 @@ int match_submit(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, 
 }
 
 // (called without ctx->mu; takes it after the wait)
-int match_wait(emqx_gm_ctx* ctx, void* ticket, emqx_gm_csr* out) {
+int match_wait(emqx_gm_ctx* ctx, void* ticket, emqx_gm_csr* out, MatchTail* tail, emqx_gm_match_stats* st_out) {
   auto* c = static_cast<MatchCall*>(ticket);
-  const int rc = c->finish(out, nullptr, false);
+  const int rc = c->finish(out, tail, false);
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  if (st_out) *st_out = c->st_copy;
   delete c;
   return rc;
 }
