@@ -618,7 +618,11 @@ def small_calls(c, ix, pb, ho, threads=8, calls=32, batch=16_384):
         except Exception as e:  # noqa: BLE001
             errs.append(repr(e))
 
-    run(0)  # (warm: every device's pinned slots and pools)
+    warm = [threading.Thread(target=run, args=(t,)) for t in range(threads)]  # (every caller's pinned staging)
+    for x in warm:
+        x.start()
+    for x in warm:
+        x.join()
     th = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
     t0 = time.perf_counter()
     for x in th:
