@@ -10,8 +10,8 @@
 %% On {error, _} the wrapper falls back to emqx_trie:match/1 (SURVEY.md §8b).
 -module(emqx_gpu_match).
 
--export([load_index/1, load_index/2, update_index/2, update_subs/2, match_batch/2, match_routes_batch/2, fanout_batch/2,
-         empty/1, export_index/1, import_index/1]).
+-export([load_index/1, load_index/2, load_index_sharded/1, load_index_sharded/2, update_index/2, update_subs/2,
+         match_batch/2, match_routes_batch/2, fanout_batch/2, empty/1, export_index/1, import_index/1]).
 -export([match/2]).
 
 -on_load(init/0).
@@ -35,6 +35,16 @@ load_index(_Filters) -> erlang:nif_error(nif_not_loaded).
 %% index fanout_batch/2 needs.
 -spec load_index([binary()], [[non_neg_integer()]]) -> {ok, reference()} | {error, term()}.
 load_index(_Filters, _SubIds) -> erlang:nif_error(nif_not_loaded).
+
+%% A route table too large for one GPU: the filters partitioned by first word
+%% over the node's GPUs (the NIF context's device list), each topic matched on
+%% its one GPU (emqx_gm_index_build_sharded).  Used like any index by the match
+%% and fan-out calls; updates and exports of it return {error, _}: rebuild it.
+-spec load_index_sharded([binary()]) -> {ok, reference()} | {error, term()}.
+load_index_sharded(_Filters) -> erlang:nif_error(nif_not_loaded).
+
+-spec load_index_sharded([binary()], [[non_neg_integer()]]) -> {ok, reference()} | {error, term()}.
+load_index_sharded(_Filters, _SubIds) -> erlang:nif_error(nif_not_loaded).
 
 %% Route changes (do_add_route/do_delete_route) as one batch -> a new snapshot;
 %% the old one stays valid for readers holding it (emqx_gm_index_update).

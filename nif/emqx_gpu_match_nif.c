@@ -209,7 +209,7 @@ static int pack_subs(ErlNifEnv *env, ERL_NIF_TERM lists, uint64_t n, uint64_t **
  *   with each filter's subscriber ids (the emqx_subscriber bag of
  *   emqx_broker.erl:147-165 with its {shard, I} buckets flattened), which
  *   fanout_batch/2 returns per topic. */
-static ERL_NIF_TERM load_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+static ERL_NIF_TERM do_load(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[], int sharded) {
   uint8_t *fb;
   uint64_t *fo, n, *so = NULL;
   uint32_t *si = NULL;
@@ -221,13 +221,28 @@ static ERL_NIF_TERM load_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
     enif_free(fo);
     return enif_make_badarg(env);
   }
-  rc = emqx_gm_index_build(CTX, fb, fo, n, so, si, NULL, &idx);
+  rc = sharded ? emqx_gm_index_build_sharded(CTX, fb, fo, n, so, si, NULL, &idx)
+               : emqx_gm_index_build(CTX, fb, fo, n, so, si, NULL, &idx);
   enif_free(fb);
   enif_free(fo);
   if (so) enif_free(so);
   if (si) enif_free(si);
   if (rc != EMQX_GM_OK) return error_tuple(env, rc);
   return make_index_term(env, idx);
+}
+
+static ERL_NIF_TERM load_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+  return do_load(env, argc, argv, 0);
+}
+
+/* load_index_sharded/1,2: as load_index/1,2, for a route table too large for
+ * one GPU: the filters partitioned by first word over the context's devices
+ * (emqx_gm_index_build_sharded), each topic matched on its one device.
+ * match_batch/2, match_routes_batch/2 and fanout_batch/2 take the result like
+ * any index; update_index/2, update_subs/2 and export_index/1 return
+ * {error, Reason} for it (EMQX_GM_EUNSUPPORTED: rebuild it). */
+static ERL_NIF_TERM load_index_sharded(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+  return do_load(env, argc, argv, 1);
 }
 
 /* update_index(Index, [{Filter :: binary(), insert | delete}]) -> {ok, NewIndex} | {error, Reason}
@@ -474,6 +489,8 @@ static ERL_NIF_TERM import_index(ErlNifEnv *env, int argc, const ERL_NIF_TERM ar
 static ErlNifFunc funcs[] = {
     {"load_index", 1, load_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"load_index", 2, load_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"load_index_sharded", 1, load_index_sharded, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"load_index_sharded", 2, load_index_sharded, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"update_index", 2, update_index, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"update_subs", 2, update_subs, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"match_batch", 2, match_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
