@@ -125,9 +125,11 @@ typedef struct emqx_gm_call emqx_gm_call;
  *   - emqx_gm_match on host buffers: a batch of more than one chunk (256K
  *     topics) is cut into chunks that run on all the devices at once (one host
  *     pipeline per device), the rows back in the caller's ONE CSR in batch
- *     order; a smaller batch runs whole on ONE device -- the first whose lock is
- *     free from a round-robin start -- so concurrent callers (dirty
- *     schedulers) run on different GPUs at once;
+ *     order; a smaller batch runs whole on ONE device, the next one
+ *     round-robin, so concurrent callers (dirty schedulers) run on different
+ *     GPUs at once (on any context, such a call stages its topics into
+ *     page-locked buffers of its own and waits for the device without the
+ *     context lock: concurrent small calls overlap on one GPU too);
  *   - emqx_gm_fanout on host rows (65,536 rows or more) cuts them into one
  *     slice per device, balanced by matches, into the caller's ONE result;
  *   - device-buffer calls (EMQX_GM_DEVICE_IO, emqx_gm_match_submit, a
