@@ -781,90 +781,123 @@ static int run_host_pipe(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8
   return 0;
 }
 
+// Small host-buffer calls: copies up to this many bytes run as kernels over
+// mapped page-locked memory; larger ones on the copy engine (gm_host.cpp A/B,
+// profiles/r06_p: at 262,144 C2 topics the mapped copies ran at 0.56x)
+constexpr size_t kMappedMax = size_t(1) << 20;
+
 uint64_t host_chunk_topics() { return std::max<uint64_t>(1024, env_u64("GM_HOST_CHUNK", 256u << 10)); }
 
 int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                    uint32_t flags, emqx_gm_csr* out, emqx_gm_match_stats* st_out) {
-  // ---- outside the lock: the offsets checked, the call's inputs staged in
-  // page-locked buffers of its own (u16 lengths; u32 offsets past 65,535 B)
+  // ---- outside the lock: the offsets checked, the call's inputs staged in a
+  // page-locked buffer of its own: [text | 64 B of padding | u16 lengths (u32
+  // offsets past 65,535 B)] -- past kMappedMax of text already page-locked, the
+  // lengths alone (the text goes up from the caller's buffer on the copy engine)
   uint64_t lng = 0;
   for (uint64_t i = 0; i < n; ++i) {
     if (to[i + 1] < to[i]) return set_err(ctx, EMQX_GM_EINVAL, "match: topic offsets not monotone");
     lng |= (to[i + 1] - to[i]) >> 16;
   }
   const bool use32 = lng != 0 || env_u64("GM_HOST_OFF32", 0) != 0;
-  const bool wide = env_u64("GM_HOST_WIDE_ROWS", 0) != 0;  // (tests: u64 row offsets over PCIe)
   const uint64_t b0 = n ? to[0] : 0, nbytes = n ? to[n] - b0 : 0;
-  const bool direct = nbytes && host_pinned_range(tb + b0, nbytes);
-  struct Pins {
+  const bool direct = nbytes > kMappedMax && host_pinned_range(tb + b0, nbytes);
+  struct Pin {
     PinPool* pool;
-    void* p[4] = {};
-    ~Pins() {
-      for (void* q : p)
-        if (q) pool->put(q);
+    void* p = nullptr;
+    ~Pin() {
+      if (p) pool->put(p);
     }
-  } pins{ctx->pins};
-  const size_t lbytes = use32 ? (n + 1) * 4 : n * 2 + 2, obytes = (n + 1) * (wide ? 8 : 4);
-  if ((!direct && !(pins.p[0] = ctx->pins->get(nbytes + 64))) || !(pins.p[1] = ctx->pins->get(lbytes)) ||
-      !(pins.p[2] = ctx->pins->get(obytes)))
-    return set_err(ctx, EMQX_GM_ENOMEM, "match: pinned staging");
+  } pin{ctx->pins};
+  const size_t lbytes = use32 ? (n + 1) * 4 : n * 2 + 2;
+  const size_t o_len = direct ? 0 : (nbytes + 64 + 255) & ~size_t(255);  // the lengths' offset in the input
+  const size_t in_bytes = (o_len + lbytes + 15) & ~size_t(15), obytes = (n + 1) * 8;
+  if (!(pin.p = ctx->pins->get(in_bytes))) return set_err(ctx, EMQX_GM_ENOMEM, "match: pinned staging");
+  uint8_t* in = static_cast<uint8_t*>(pin.p);
   if (!direct) {
-    uint8_t* tx = static_cast<uint8_t*>(pins.p[0]);
-    if (nbytes) std::memcpy(tx, tb + b0, nbytes);
-    std::memset(tx + nbytes, 0, 64);
+    if (nbytes) std::memcpy(in, tb + b0, nbytes);
+    std::memset(in + nbytes, 0, 64);
   }
   if (use32) {
-    stage_off32(to, 0, n, static_cast<uint32_t*>(pins.p[1]));
+    stage_off32(to, 0, n, reinterpret_cast<uint32_t*>(in + o_len));
   } else {
-    uint16_t* l = static_cast<uint16_t*>(pins.p[1]);
+    uint16_t* l = reinterpret_cast<uint16_t*>(in + o_len);
     for (uint64_t i = 0; i < n; ++i) l[i] = uint16_t(to[i + 1] - to[i]);
   }
-  // ---- under the lock: the inputs up, the call queued, its rows' copy-out
-  // behind its speculative assembly (one device round trip for the call)
+  // the page-locked buffers as the device addresses them: up to kMappedMax a copy
+  // runs as a kernel on the call's own queue (k_copy_u32x2: no hand-over between
+  // the copy engine and the call's kernels, ~10 us each) -- past it, or if a
+  // buffer is not mapped, on the copy engine
+  auto mapped = [](void* h, size_t bytes) -> uint32_t* {
+    void* d = nullptr;
+    return bytes <= kMappedMax && hipHostGetDevicePointer(&d, h, 0) == hipSuccess ? static_cast<uint32_t*>(d) : nullptr;
+  };
+  const uint32_t* in_dev = mapped(pin.p, in_bytes);
+  // ---- under the lock: the inputs up, the call queued (untimed: no timestamps
+  // on the stream), its rows' copy-out behind its speculative assembly -- one
+  // device round trip for the call
   std::unique_lock<std::recursive_mutex> lk(ctx->mu);
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
-  void* dv[4] = {ctx->pool->alloc(nbytes + 64), ctx->pool->alloc(lbytes), ctx->pool->alloc((n + 1) * 8),
-                 ctx->pool->alloc(wide ? 16 : (n + 1) * 4)};
+  void* dv[3] = {ctx->pool->alloc(in_bytes), ctx->pool->alloc((n + 1) * 8),
+                 direct ? ctx->pool->alloc(nbytes + 64) : nullptr};
   auto drop_dev = [&]() {  // (under the lock; the call's work is done or was never queued)
     for (void*& q : dv)
       if (q) ctx->pool->release(q);
   };
-  if (!dv[0] || !dv[1] || !dv[2] || !dv[3]) {
+  if (!dv[0] || !dv[1] || (direct && !dv[2])) {
     drop_dev();
     return set_err(ctx, EMQX_GM_ENOMEM, "match: input workspace");
   }
-  uint8_t* d_b = static_cast<uint8_t*>(dv[0]);
-  uint64_t* d_o = static_cast<uint64_t*>(dv[2]);
-  hipError_t e = direct ? hipMemcpyAsync(d_b, tb + b0, nbytes, hipMemcpyHostToDevice, st)
-                        : hipMemcpyAsync(d_b, pins.p[0], nbytes + 64, hipMemcpyHostToDevice, st);
+  uint8_t* d_b = static_cast<uint8_t*>(direct ? dv[2] : dv[0]);
+  const void* d_l = static_cast<uint8_t*>(dv[0]) + o_len;
+  uint64_t* d_o = static_cast<uint64_t*>(dv[1]);
+  hipError_t e = in_dev ? (launch_copy_u32x2(st, in_dev, static_cast<uint32_t*>(dv[0]), in_bytes / 4, nullptr,
+                                             nullptr, 0) ? hipErrorLaunchFailure : hipSuccess)
+                        : hipMemcpyAsync(dv[0], in, in_bytes, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && direct) e = hipMemcpyAsync(d_b, tb + b0, nbytes, hipMemcpyHostToDevice, st);
   if (e == hipSuccess && direct) e = hipMemsetAsync(d_b + nbytes, 0, 64, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(dv[1], pins.p[1], lbytes, hipMemcpyHostToDevice, st);
-  if (e != hipSuccess || (use32 ? launch_off32_to_64(st, static_cast<const uint32_t*>(dv[1]), n + 1, d_o)
-                                : scan_len16(ctx, st, static_cast<const uint16_t*>(dv[1]), n, d_o))) {
+  if (e != hipSuccess || (use32 ? launch_off32_to_64(st, static_cast<const uint32_t*>(d_l), n + 1, d_o)
+                                : scan_len16(ctx, st, static_cast<const uint16_t*>(d_l), n, d_o))) {
     hipStreamSynchronize(st);
     drop_dev();
     return set_err(ctx, EMQX_GM_EDEVICE, "match: inputs to device");
   }
+  // the caller-visible result, page-locked from the context's host pool
+  // (emqx_gm_csr_free hands it back): the rows land there straight from the
+  // device, behind the call's speculative assembly (the row offsets as they
+  // are, u64: one launch fewer)
+  uint64_t* r_off = nullptr;
+  uint32_t* r_ids = nullptr;
+  auto drop_res = [&]() {  // (under the lock)
+    ctx->hpool->release(r_off);
+    ctx->hpool->release(r_ids);
+    r_off = nullptr;
+    r_ids = nullptr;
+  };
   MatchTail tail;
   tail.enqueue = [&](const uint64_t* d_ro, const uint32_t* d_ids, uint64_t cap) -> int {
-    if (!(pins.p[3] = ctx->pins->get(cap * 4 + 4))) return set_err(ctx, EMQX_GM_ENOMEM, "match: pinned rows");
+    r_off = static_cast<uint64_t*>(ctx->hpool->alloc(obytes, true));
+    r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(cap * 4 + 16, true));
+    if (!r_off || !r_ids) return set_err(ctx, EMQX_GM_ENOMEM, "match: host result");
+    uint32_t* off_dev = mapped(r_off, obytes + cap * 4);
+    uint32_t* ids_dev = mapped(r_ids, obytes + cap * 4);
     hipError_t x = hipSuccess;
-    if (wide) {
-      x = hipMemcpyAsync(pins.p[2], d_ro, (n + 1) * 8, hipMemcpyDeviceToHost, st);
-    } else if (launch_off64_to_32(st, d_ro, n + 1, static_cast<uint32_t*>(dv[3]))) {
-      x = hipErrorLaunchFailure;
+    if (off_dev && ids_dev) {
+      if (launch_copy_u32x2(st, reinterpret_cast<const uint32_t*>(d_ro), off_dev, obytes / 4, d_ids, ids_dev, cap))
+        x = hipErrorLaunchFailure;
     } else {
-      x = hipMemcpyAsync(pins.p[2], dv[3], (n + 1) * 4, hipMemcpyDeviceToHost, st);
+      x = hipMemcpyAsync(r_off, d_ro, obytes, hipMemcpyDeviceToHost, st);
+      if (x == hipSuccess && cap) x = hipMemcpyAsync(r_ids, d_ids, cap * 4, hipMemcpyDeviceToHost, st);
     }
-    if (x == hipSuccess && cap) x = hipMemcpyAsync(pins.p[3], d_ids, cap * 4, hipMemcpyDeviceToHost, st);
     return x == hipSuccess ? 0 : set_err(ctx, EMQX_GM_EDEVICE, "match: rows to host");
   };
   void* ticket = nullptr;
-  int rc = match_submit(ctx, idx, d_b, d_o, n, flags | EMQX_GM_DEVICE_IO, &ticket, &tail);
+  int rc = match_submit(ctx, idx, d_b, d_o, n, flags | EMQX_GM_DEVICE_IO | EMQX_GM_NO_TIMING, &ticket, &tail);
   if (rc) {
     hipStreamSynchronize(st);
     drop_dev();
+    drop_res();
     return rc;
   }
   lk.unlock();
@@ -873,33 +906,29 @@ int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
   rc = match_wait(ctx, ticket, &dc, &tail, st_out);
   lk.lock();
   drop_dev();  // (match_wait returned: this call's work on them is done)
-  if (rc) return rc;
+  if (rc) {
+    drop_res();
+    return rc;
+  }
   const uint64_t nnz = dc.nnz;
-  const bool fast = tail.used;  // the rows came back with the call
-  uint64_t* r_off = static_cast<uint64_t*>(ctx->hpool->alloc((n + 1) * 8));
-  uint32_t* r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(nnz * 4 + 4));
-  if (!r_off || !r_ids || (!fast && (e = hipMemcpyAsync(r_off, dc.row_off, (n + 1) * 8, hipMemcpyDeviceToHost, st),
-                                     e == hipSuccess && nnz &&
-                                         (e = hipMemcpyAsync(r_ids, dc.ids, nnz * 4, hipMemcpyDeviceToHost, st)),
-                                     e == hipSuccess && (e = hipStreamSynchronize(st)), e != hipSuccess))) {
-    ctx->hpool->release(r_off);
+  if (!tail.used) {  // past the speculative capacity: the rows copied out now, into a result of their size
     ctx->hpool->release(r_ids);
-    ctx->pool->release(dc.row_off);
-    ctx->pool->release(dc.ids);
-    return set_err(ctx, r_off && r_ids ? EMQX_GM_EDEVICE : EMQX_GM_ENOMEM, "match: host result");
+    if (!r_off) r_off = static_cast<uint64_t*>(ctx->hpool->alloc(obytes));
+    r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(nnz * 4 + 4));
+    hipError_t x = r_off && r_ids ? hipMemcpyAsync(r_off, dc.row_off, obytes, hipMemcpyDeviceToHost, st)
+                                  : hipErrorOutOfMemory;
+    if (x == hipSuccess && nnz) x = hipMemcpyAsync(r_ids, dc.ids, nnz * 4, hipMemcpyDeviceToHost, st);
+    if (x == hipSuccess) x = hipStreamSynchronize(st);
+    if (x != hipSuccess) {
+      drop_res();
+      ctx->pool->release(dc.row_off);
+      ctx->pool->release(dc.ids);
+      return set_err(ctx, x == hipErrorOutOfMemory ? EMQX_GM_ENOMEM : EMQX_GM_EDEVICE, "match: host result");
+    }
   }
   ctx->pool->release(dc.row_off);
   ctx->pool->release(dc.ids);
   lk.unlock();
-  if (fast) {  // the rows out of the call's page-locked buffers (outside the lock)
-    if (wide) {
-      std::memcpy(r_off, pins.p[2], (n + 1) * 8);
-    } else {
-      const uint32_t* ro = static_cast<const uint32_t*>(pins.p[2]);
-      for (uint64_t i = 0; i <= n; ++i) r_off[i] = ro[i];
-    }
-    if (nnz) std::memcpy(r_ids, pins.p[3], nnz * 4);
-  }
   out->n_rows = n;
   out->nnz = nnz;
   out->row_off = r_off;
@@ -908,6 +937,7 @@ int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
   out->priv = ctx;  // the owning context (emqx_gm_csr_free checks it)
   return 0;
 }
+
 
 int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                    uint32_t flags, emqx_gm_csr* out) {

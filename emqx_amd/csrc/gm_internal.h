@@ -485,6 +485,8 @@ int set_err(emqx_gm_ctx* ctx, int code, const std::string& msg);
 // gm_match.hip: offset conversions of the host-buffer path (n1 = entries)
 int launch_off32_to_64(hipStream_t st, const uint32_t* in, uint64_t n1, uint64_t* out);
 int launch_off64_to_32(hipStream_t st, const uint64_t* in, uint64_t n1, uint32_t* out);
+int launch_copy_u32x2(hipStream_t st, const uint32_t* s0, uint32_t* d0, uint64_t n0, const uint32_t* s1, uint32_t* d1,
+                      uint64_t n1);
 int launch_add_u64(hipStream_t st, uint64_t* p, uint64_t n1, uint64_t add);
 // the host path's u16 topic lengths -> u64 offsets (n + 1 entries, an exclusive scan) on stream st
 int scan_len16(emqx_gm_ctx* ctx, hipStream_t st, const uint16_t* len, uint64_t n, uint64_t* out);

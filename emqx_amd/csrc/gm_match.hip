@@ -2531,6 +2531,30 @@ int launch_off64_to_32(hipStream_t st, const uint64_t* in, uint64_t n1, uint32_t
   hipLaunchKernelGGL(k_off64_to_32, dim3(g ? g : 1), dim3(256), 0, st, in, n1, out);
   return hipGetLastError() == hipSuccess ? 0 : EMQX_GM_EDEVICE;
 }
+// Small host-buffer calls (gm_host.cpp run_host_small): inputs in and rows out
+// through page-locked host memory the device addresses directly -- two copies
+// in one launch on the call's own queue, so no copy engine has to hand over to
+// the compute queue between the call's kernels (~10 us a hand-over)
+__global__ __launch_bounds__(256) void k_copy_u32x2(const uint32_t* __restrict__ s0, uint32_t* __restrict__ d0,
+                                                    uint64_t n0, const uint32_t* __restrict__ s1,
+                                                    uint32_t* __restrict__ d1, uint64_t n1) {
+  const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x, stride = uint64_t(gridDim.x) * 256u;
+  const uint64_t q0 = n0 / 4, q1 = n1 / 4;  // (16-B units; every buffer here is 16-B aligned)
+  for (uint64_t i = t; i < q0; i += stride)
+    reinterpret_cast<uint4*>(d0)[i] = reinterpret_cast<const uint4*>(s0)[i];
+  for (uint64_t i = t; i < q1; i += stride)
+    reinterpret_cast<uint4*>(d1)[i] = reinterpret_cast<const uint4*>(s1)[i];
+  if (t < (n0 & 3)) d0[q0 * 4 + t] = s0[q0 * 4 + t];
+  if (t < (n1 & 3)) d1[q1 * 4 + t] = s1[q1 * 4 + t];
+  __threadfence_system();  // (host-bound stores visible before the call's end event)
+}
+int launch_copy_u32x2(hipStream_t st, const uint32_t* s0, uint32_t* d0, uint64_t n0, const uint32_t* s1, uint32_t* d1,
+                      uint64_t n1) {
+  const uint64_t q = (std::max(n0, n1) + 3) / 4;
+  const uint64_t g = std::min<uint64_t>(1024, (q + 255) / 256);
+  hipLaunchKernelGGL(k_copy_u32x2, dim3(g ? g : 1), dim3(256), 0, st, s0, d0, n0, s1, d1, n1);
+  return hipGetLastError() == hipSuccess ? 0 : EMQX_GM_EDEVICE;
+}
 // p[0..n1) += add, in place (a chunk's row offsets rebased to the whole call's rows)
 __global__ __launch_bounds__(256) void k_add_u64(uint64_t* __restrict__ p, uint64_t n1, uint64_t add) {
   for (uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x; i < n1; i += uint64_t(gridDim.x) * 256u) p[i] += add;
@@ -3591,9 +3615,12 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
   // (compact staging with no host copy-out queued behind: the assembly kernel
   // writes the read-back words itself and its stop event is the call's end --
   // a copy and an event record fewer, ~10 us of idle stream per call at C1)
+  // (a host copy-out queued behind -- the small host-buffer call's tail -- goes
+  // between the assembly and the call's end event, recorded after it)
   uint32_t* pin_dev = nullptr;  // the pinned words as the device addresses them
-  const bool rb_kernel = spec && cmp && !(tail && tail->enqueue) &&
-                         hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_dev), pin, 0) == hipSuccess && pin_dev;
+  const bool tail_q = tail && tail->enqueue;
+  const bool rb_kernel =
+      spec && cmp && hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_dev), pin, 0) == hipSuccess && pin_dev;
   // (compact staging: the assembly also zeroes the ring's next block for the next call, if it is dirty)
   uint32_t* zero_next = nullptr;
   if (spec && cmp && ctr_slot >= 0 && !on_asm) {
@@ -3607,11 +3634,12 @@ int MatchCall::submit(const emqx_gm_index* index, const uint8_t* tb_in, const ui
     launch_assemble(sa, nblk, cmp ? &cmpb : nullptr, cnt.as<uint32_t>(), n, toff_p, stage.as<uint32_t>(),
                     row_off.as<uint64_t>(), ids.as<uint32_t>(), idx->view.gmap, cap_spec, scan_blk.as<uint64_t>(),
                     rb_kernel ? pin_dev : nullptr, reinterpret_cast<const uint32_t*>(ctrs_p),
-                    rb_kernel ? ev[2] : nullptr, zero_next, split_sums);
+                    rb_kernel && !tail_q ? ev[2] : nullptr, zero_next, split_sums);
     GM_HIP(ctx, hipGetLastError());
-    if (tail && tail->enqueue) {
+    if (tail_q) {
       rc = tail->enqueue(row_off.as<uint64_t>(), ids.as<uint32_t>(), cap_spec);
       if (rc) return rc;
+      if (rb_kernel) GM_HIP(ctx, hipEventRecord(ev[2], sa));
     }
   }
   if (!rb_kernel) {

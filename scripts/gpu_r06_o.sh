@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round 6, GPU call o: leaner small host calls (one input copy, untimed, u64 rows
+# back, the assembly's read-back words) -- parity, then the A/B and the probe.
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+O=gpurun_out/${OUT:-r06_o}
+mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+  tests/test_gpu_parity.py tests/test_gpu_multi.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 300 python3 -u scripts/small_call_probe.py 200 1024 > $O/probe.log 2>&1 || { tail -5 $O/probe.log; exit 1; }
+tail -2 $O/probe.log
+timeout -k 10 400 python3 -u scripts/small_calls_ab.py --reps 2 > $O/ab.log 2>&1 || { tail -5 $O/ab.log; exit 1; }
+cat $O/ab.log

@@ -63,7 +63,7 @@ def main():
     pb = c.host_alloc(tot + 64)
     c.memcpy_d2h(pb, db, tot)
     os.environ["EMQX_GM_AB"] = "1"
-    for batch, calls in ((1024, 256), (16384, 32)):
+    for batch, calls in ((1024, 256), (16384, 32), (65536, 8), (262144, 4)):
         for threads in (1, 2, 4, 8):
             res = {"serial": [], "concurrent": []}
             for _ in range(a.reps):

@@ -626,6 +626,38 @@ def test_host_path_long_topics_take_u32_offsets(ctx, orc, monkeypatch, chunk):
     idx.release()
 
 
+@pytest.mark.parametrize("spec", ["on", "off"])
+def test_small_host_calls_every_staging_branch(ctx, orc, monkeypatch, spec):
+    """Small host-buffer calls (gm_host.cpp run_host_small): copies of up to
+    1 MiB run as kernels over mapped page-locked memory, larger ones on the copy
+    engine (and page-locked caller text goes up from the caller's buffer); the
+    rows land in the caller's result straight from the device when the call's
+    speculative ids buffer held them, and are copied out at their exact size
+    when it did not (a context primed on rowless topics, then heavy rows; or no
+    speculative buffer at all: GM_NO_SPEC_IDS).  Every form gives the oracle's
+    rows, the empty call included."""
+    from emqx_amd.engine import pack
+    if spec == "off":
+        monkeypatch.setenv("GM_NO_SPEC_IDS", "1")
+    filters = sorted({b"#", b"a/#", b"a/+", b"a/+/#", b"+/+", b"+/+/+", b"+/b/#", b"a/b", b"a/b/c", b"q/#"})
+    idx = ctx.build_index(filters)
+    rowless = [b"$SYS/x/%d" % i for i in range(3_000)]  # ('#' does not match '$' topics)
+    heavy = [b"a/b/c", b"a/b", b"a/x/y", b"q/b/z", b"zz/b"] * 600
+    big = heavy * 12  # 48k topics with the long ones below: 1.2 MB of text, past the mapped-copy limit
+    big += [b"a/" + b"w" * 80 + b"/%d" % i for i in range(12_000)]
+    for topics in ([], rowless, heavy, rowless, big, heavy[:7]):
+        want_ro, want_ids = _oracle_rows(orc, filters, topics, 1)
+        tb, to = pack(topics)
+        ro, ids = ctx.match(idx, (tb, to), exact=True)
+        assert np.array_equal(ro, want_ro) and np.array_equal(ids, want_ids), len(topics)
+        pb = ctx.host_alloc(len(tb) + 64)  # the caller's text page-locked
+        pb[:len(tb)] = tb
+        ro, ids = ctx.match(idx, (pb, to), exact=True)
+        ctx.host_free(pb)
+        assert np.array_equal(ro, want_ro) and np.array_equal(ids, want_ids), ("pinned", len(topics))
+    idx.release()
+
+
 def test_host_path_rejects_bad_offsets_and_survives(ctx):
     """Non-monotone host offsets -> EINVAL with a message (no GPU fault, no
     partial result), and the context keeps working afterwards."""
