@@ -497,10 +497,11 @@ void free_host_pipe(emqx_gm_ctx* ctx);
 // the topics of one host-pipeline chunk at most (a call this small runs whole on one device)
 uint64_t host_chunk_topics();
 // A host-buffer call of at most one chunk, entered WITHOUT ctx->mu: staged into
-// the call's own page-locked buffers outside the lock, queued under it (inputs
-// up, the match, the rows' copy-out behind its speculative assembly), waited
-// for outside it -- so concurrent small calls on one device overlap one
-// another's host work and device round trips
+// the call's own page-locked buffer outside the lock, queued under it (inputs
+// up, the match, the rows' copy-out behind its speculative assembly straight
+// into the page-locked result; copies up to 1 MiB as kernels over mapped
+// memory), waited for outside it -- so concurrent small calls on one device
+// overlap one another's host work and device round trips
 int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                    uint32_t flags, emqx_gm_csr* out, emqx_gm_match_stats* st_out);
 // gm_multi.cpp: multi-device contexts (emqx_gm_opts.n_devices).
