@@ -701,9 +701,38 @@ int emqx_gm_match_wait(emqx_gm_ctx* ctx, emqx_gm_call* call, emqx_gm_csr* out) {
   GM_GUARD_END(ctx)
 }
 
+// A host-row fan-out of a publish window (fewer than 65,536 rows, at most 16M
+// deliveries): like match_small, ONE device serves it whole, round-robin over a
+// multi-device context's replicas, holding that device's lock only to queue
+// its work (gm_host.cpp run_fanout_small).  1: not small, take the ordinary path.
+static int fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, emqx_gm_csr* out) {
+  const size_t K = 1 + (idx->reps.size() == ctx->members.size() ? ctx->members.size() : 0);
+  const size_t pick = K > 1 ? ctx->rr.fetch_add(1, std::memory_order_relaxed) % K : 0;
+  emqx_gm_ctx* mc = pick ? ctx->members[pick - 1] : ctx;
+  const emqx_gm_index* rix = pick ? idx->reps[pick - 1] : idx;
+  hipSetDevice(mc->device);
+  emqx_gm_match_stats st{};
+  const int rc = gm::run_fanout_small(mc, rix, idx, m, out, &st);
+  if (rc == EMQX_GM_OK) {
+    tl_stats = st;
+    tl_stats_ctx = ctx;
+  }
+  hipSetDevice(ctx->device);
+  return rc;
+}
+
 int emqx_gm_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t flags,
                    emqx_gm_csr* out) {
   if (!ctx) return EMQX_GM_EINVAL;
+  if (idx && m && out && flags == (flags & EMQX_GM_WITH_EXACT) && !m->on_device && m->row_off && (!m->nnz || m->ids) &&
+      m->n_rows < 65536 && !idx->view.gmap && !idx->ov && !idx->route && !idx->subs.empty() &&
+      idx->device == ctx->device && !gm::knob("GM_FANOUT_SIMPLE")) {
+    std::memset(out, 0, sizeof(*out));
+    GM_GUARD_BEGIN
+    const int rc = fanout_small(ctx, idx, m, out);
+    if (rc != 1) return rc;
+    GM_GUARD_END(ctx)
+  }
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   if (!idx || !m || !out || (m->nnz && !m->ids) || !m->row_off)
     return gm::set_err(ctx, EMQX_GM_EINVAL, "fanout: NULL argument");

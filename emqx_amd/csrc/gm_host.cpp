@@ -785,6 +785,22 @@ static int run_host_pipe(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8
 // mapped page-locked memory; larger ones on the copy engine (gm_host.cpp A/B,
 // profiles/r06_p: at 262,144 C2 topics the mapped copies ran at 0.56x)
 constexpr size_t kMappedMax = size_t(1) << 20;
+// a page-locked buffer as the device addresses it, for a copy of `bytes` as a kernel (nullptr: the copy engine)
+static uint32_t* mapped(void* h, size_t bytes) {
+  void* d = nullptr;
+  return bytes <= kMappedMax && hipHostGetDevicePointer(&d, h, 0) == hipSuccess ? static_cast<uint32_t*>(d) : nullptr;
+}
+// one host <-> device copy of a small call: a kernel over mapped memory up to kMappedMax, else the copy engine
+static hipError_t small_copy(hipStream_t st, void* dst, const void* src, size_t bytes, bool to_dev) {
+  if (!bytes) return hipSuccess;
+  uint32_t* hm = mapped(const_cast<void*>(to_dev ? src : dst), bytes);
+  if (hm && !(bytes & 3))
+    return launch_copy_u32x2(st, to_dev ? hm : static_cast<const uint32_t*>(src),
+                             to_dev ? static_cast<uint32_t*>(dst) : hm, bytes / 4, nullptr, nullptr, 0)
+               ? hipErrorLaunchFailure
+               : hipSuccess;
+  return hipMemcpyAsync(dst, src, bytes, to_dev ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, st);
+}
 
 uint64_t host_chunk_topics() { return std::max<uint64_t>(1024, env_u64("GM_HOST_CHUNK", 256u << 10)); }
 
@@ -828,10 +844,6 @@ int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
   // runs as a kernel on the call's own queue (k_copy_u32x2: no hand-over between
   // the copy engine and the call's kernels, ~10 us each) -- past it, or if a
   // buffer is not mapped, on the copy engine
-  auto mapped = [](void* h, size_t bytes) -> uint32_t* {
-    void* d = nullptr;
-    return bytes <= kMappedMax && hipHostGetDevicePointer(&d, h, 0) == hipSuccess ? static_cast<uint32_t*>(d) : nullptr;
-  };
   const uint32_t* in_dev = mapped(pin.p, in_bytes);
   // ---- under the lock: the inputs up, the call queued (untimed: no timestamps
   // on the stream), its rows' copy-out behind its speculative assembly -- one
@@ -938,6 +950,119 @@ int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
   return 0;
 }
 
+
+// a small host fan-out: at most this many deliveries (its page-locked result is sized to them)
+constexpr uint64_t kFanSmallDeliveries = uint64_t(16) << 20;
+
+int run_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_index* host, const emqx_gm_csr* m,
+                     emqx_gm_csr* out, emqx_gm_match_stats* st_out) {
+  // ---- outside the lock: the rows checked, their deliveries counted from the
+  // host's subscriber table (the device's agrees: checked after the call), the
+  // rows staged in a page-locked buffer of the call's own: [row offsets | ids]
+  // (rows that are not a plain CSR over [0, nnz) take the ordinary path, as they always have)
+  const uint64_t n = m->n_rows, nnz = m->nnz, nf = host->view.n_filters;
+  if (m->row_off[0] != 0 || m->row_off[n] != nnz) return 1;
+  for (uint64_t i = 0; i < n; ++i)
+    if (m->row_off[i + 1] < m->row_off[i]) return 1;
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < nnz; ++i) {
+    if (m->ids[i] >= nf) return set_err(ctx, EMQX_GM_EINVAL, "fanout: filter id out of range");
+    total += host->subs.count(m->ids[i]);
+  }
+  if (total > kFanSmallDeliveries) return 1;
+  const size_t obytes = (n + 1) * 8, o_ids = (obytes + 15) & ~size_t(15);
+  const size_t in_bytes = (o_ids + nnz * 4 + 15) & ~size_t(15);
+  struct Pin {
+    PinPool* pool;
+    void* p = nullptr;
+    ~Pin() {
+      if (p) pool->put(p);
+    }
+  } pin{ctx->pins};
+  if (!(pin.p = ctx->pins->get(in_bytes))) return set_err(ctx, EMQX_GM_ENOMEM, "fanout: pinned staging");
+  uint8_t* in = static_cast<uint8_t*>(pin.p);
+  std::memcpy(in, m->row_off, obytes);
+  if (nnz) std::memcpy(in + o_ids, m->ids, nnz * 4);
+  // ---- under the lock: rows up, the deliveries, the result's copy-out straight
+  // into the page-locked result, the call's end event; the device workspace
+  // handed back behind it
+  std::unique_lock<std::recursive_mutex> lk(ctx->mu);
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  void* dv[4] = {ctx->pool->alloc(in_bytes), ctx->pool->alloc((nnz + 1) * 8), ctx->pool->alloc(obytes),
+                 ctx->pool->alloc(total * 4 + 16)};
+  uint64_t* r_off = static_cast<uint64_t*>(ctx->hpool->alloc(obytes, true));
+  uint32_t* r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(total * 4 + 16, true));
+  hipEvent_t done = nullptr;
+  if (!ctx->ev_free.empty()) {
+    done = ctx->ev_free.back();
+    ctx->ev_free.pop_back();
+  } else if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
+    done = nullptr;
+  }
+  auto fail = [&](int code, const char* msg) {  // (under the lock)
+    hipStreamSynchronize(st);
+    for (void* q : dv)
+      if (q) ctx->pool->release(q);
+    ctx->hpool->release(r_off);
+    ctx->hpool->release(r_ids);
+    if (done) ctx->ev_free.push_back(done);
+    return set_err(ctx, code, msg);
+  };
+  if (!dv[0] || !dv[1] || !dv[2] || !dv[3] || !r_off || !r_ids) return fail(EMQX_GM_ENOMEM, "fanout: workspace");
+  if (!done) return fail(EMQX_GM_EDEVICE, "fanout: event");
+  uint8_t* d_in = static_cast<uint8_t*>(dv[0]);
+  hipError_t e = small_copy(st, d_in, in, in_bytes, true);
+  if (e != hipSuccess) return fail(EMQX_GM_EDEVICE, "fanout: rows to device");
+  if (int rc = queue_fanout_small(ctx, idx, reinterpret_cast<const uint64_t*>(d_in),
+                                  reinterpret_cast<const uint32_t*>(d_in + o_ids), n, nnz, total,
+                                  static_cast<uint64_t*>(dv[1]), static_cast<uint64_t*>(dv[2]),
+                                  static_cast<uint32_t*>(dv[3]))) {
+    hipStreamSynchronize(st);
+    for (void* q : dv) ctx->pool->release(q);
+    ctx->hpool->release(r_off);
+    ctx->hpool->release(r_ids);
+    ctx->ev_free.push_back(done);
+    return rc;
+  }
+  uint32_t* off_dev = mapped(r_off, obytes + total * 4);
+  uint32_t* ids_dev = mapped(r_ids, obytes + total * 4);
+  if (off_dev && ids_dev) {
+    e = launch_copy_u32x2(st, static_cast<const uint32_t*>(dv[2]), off_dev, obytes / 4,
+                          static_cast<const uint32_t*>(dv[3]), ids_dev, total)
+            ? hipErrorLaunchFailure
+            : hipSuccess;
+  } else {
+    e = hipMemcpyAsync(r_off, dv[2], obytes, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && total) e = hipMemcpyAsync(r_ids, dv[3], total * 4, hipMemcpyDeviceToHost, st);
+  }
+  if (e == hipSuccess) e = hipEventRecord(done, st);
+  if (e != hipSuccess) return fail(EMQX_GM_EDEVICE, "fanout: rows to host");
+  ctx->pool->release_after(dv, 4, st);
+  lk.unlock();
+  // ---- outside the lock: the device round trip
+  e = hipEventSynchronize(done);
+  lk.lock();
+  ctx->ev_free.push_back(done);
+  if (e != hipSuccess || r_off[n] != total) {  // (a device fault, or the device's table disagreed with the host's)
+    ctx->hpool->release(r_off);
+    ctx->hpool->release(r_ids);
+    return set_err(ctx, EMQX_GM_EDEVICE, e != hipSuccess ? "fanout: device" : "fanout: subscriber tables disagree");
+  }
+  lk.unlock();
+  if (st_out) {
+    *st_out = emqx_gm_match_stats{};
+    st_out->n_topics = n;
+    st_out->nnz = total;
+  }
+  out->n_rows = n;
+  out->nnz = total;
+  out->row_off = r_off;
+  out->ids = r_ids;
+  out->on_device = 0;
+  out->priv = ctx;  // the owning context (emqx_gm_csr_free checks it)
+  return 0;
+}
 
 int run_match_host(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                    uint32_t flags, emqx_gm_csr* out) {

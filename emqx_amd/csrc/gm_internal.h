@@ -504,6 +504,15 @@ uint64_t host_chunk_topics();
 // overlap one another's host work and device round trips
 int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                    uint32_t flags, emqx_gm_csr* out, emqx_gm_match_stats* st_out);
+// A host-row fan-out of a publish window, the same way (entered WITHOUT
+// ctx->mu): the deliveries counted from the host's subscriber table, the rows
+// staged outside the lock, one device round trip.  idx: the snapshot on this
+// device (a replica), host: the one whose host tables count (the primary).
+// Returns 1 -- nothing done -- for a fan-out past kFanSmallDeliveries.
+int run_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_index* host, const emqx_gm_csr* m,
+                     emqx_gm_csr* out, emqx_gm_match_stats* st_out);
+int queue_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint64_t* d_off, const uint32_t* d_ids,
+                       uint64_t n, uint64_t nnz, uint64_t total, uint64_t* seg_dst, uint64_t* row_off, uint32_t* ids);
 // gm_multi.cpp: multi-device contexts (emqx_gm_opts.n_devices).
 // A copy of flat snapshot `src` (any device) on member context m's device:
 // the host tables shared or copied, the device tables copied device to device

@@ -2288,12 +2288,13 @@ __global__ __launch_bounds__(256) void k_fanout_rowoff(const uint64_t* __restric
   if (i <= n) out_off[i] = seg_dst[m_off[i]];
 }
 
-// Output elements per workgroup: from 4,096 (small fan-outs still spread over
-// every CU) up to 65,536 for large ones (C4: 0.94 -> 0.81 ms against 4,096,
-// fewer per-block segment searches), a multiple of 1,024 (4 per thread step).
+// Output elements per workgroup: from 1,024 (a publish window's ~100k
+// deliveries in ~100 workgroups, not 30: 63 -> ~20 us) up to 65,536 for large
+// fan-outs (C4: 0.94 -> 0.81 ms against 4,096, fewer per-block segment
+// searches), a multiple of 1,024 (4 per thread step).
 inline uint64_t fan_per_block(uint64_t total) {
   uint64_t per = total / 2048;  // ~8 workgroups per CU
-  per = per < 4096 ? 4096 : per > 65536 ? 65536 : per;
+  per = per < 1024 ? 1024 : per > 65536 ? 65536 : per;
   return (per + 1023) & ~uint64_t(1023);
 }
 
@@ -2321,6 +2322,9 @@ __global__ __launch_bounds__(256) void k_fanout_copy(const uint64_t* __restrict_
                                                      const uint32_t* __restrict__ sub_ids, uint64_t glo,
                                                      uint64_t total, uint64_t per_block, uint32_t* __restrict__ out0) {
   // this launch produces the global delivery range [glo, total); out0[0] is delivery glo
+  // (never past the device's own total: a small host fan-out sizes the launch
+  // from the host's subscriber table, gm_host.cpp run_fanout_small)
+  total = min(total, seg_dst[nseg]);
   const uint64_t lo = glo + uint64_t(blockIdx.x) * per_block;
   if (lo >= total) return;
   const uint64_t hi = min(total, lo + per_block);
@@ -3963,6 +3967,24 @@ int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m,
   ctx->stats.match_kernel_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
   ctx->stats.total_device_ms = ev_ms(ctx->ev[0], ctx->ev[2]);
   return finish_csr(ctx, n, cnt, row_off, ids, dev_out, out);
+}
+
+// A small host fan-out's device work (gm_host.cpp run_fanout_small), queued
+// without a wait: the deliveries' offsets, the rows' offsets and the delivery
+// lists of [0, total) -- total counted by the host from its subscriber table.
+int queue_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint64_t* d_off, const uint32_t* d_ids,
+                       uint64_t n, uint64_t nnz, uint64_t total, uint64_t* seg_dst, uint64_t* row_off, uint32_t* ids) {
+  hipStream_t st = ctx->stream;
+  if (int rc = scan_excl(ctx, LoadSegLen{d_ids, idx->view.sub_off}, nnz, seg_dst)) return rc;
+  hipLaunchKernelGGL(k_fanout_rowoff, dim3((n + 1 + 255) / 256), dim3(256), 0, st, d_off, n, seg_dst, row_off);
+  GM_HIP(ctx, hipGetLastError());
+  if (total) {
+    const uint64_t per = fan_per_block(total);
+    hipLaunchKernelGGL(k_fanout_copy, dim3((total + per - 1) / per), dim3(256), 0, st, seg_dst, nnz, d_ids,
+                       idx->view.sub_off, idx->view.sub_ids, uint64_t(0), total, per, ids);
+    GM_HIP(ctx, hipGetLastError());
+  }
+  return 0;
 }
 
 // Rows back in their batch order after a prefix-routed exchange (sharded.py,

@@ -64,7 +64,7 @@
  *     GM_SCAN_SPLIT, GM_SCAN_SUMS, GM_NO_SPEC_IDS, GM_ASM_STREAM;
  *   host path:          GM_HOST_SIMPLE, GM_HOST_PIPE, GM_HOST_CHUNK,
  *     GM_HOST_THREADS, GM_HOST_BOUNCE, GM_HOST_WIDE_ROWS, GM_HOST_OFF32,
- *     GM_FANOUT_MULTI_MIN;
+ *     GM_FANOUT_MULTI_MIN, GM_FANOUT_SIMPLE;
  *   updates:            GM_UPDATE_OVERLAY, GM_UPDATE_UNFUSED, GM_SPARE_BLOB_MIN;
  *   diagnostics:        GM_UPDATE_TIMING, GM_INDEX_STATS, GM_INDEX_VERIFY.
  */
@@ -132,6 +132,9 @@ typedef struct emqx_gm_call emqx_gm_call;
  *     context lock: concurrent small calls overlap on one GPU too);
  *   - emqx_gm_fanout on host rows (65,536 rows or more) cuts them into one
  *     slice per device, balanced by matches, into the caller's ONE result;
+ *     fewer rows (a publish window's, at most 16M deliveries) run whole on
+ *     ONE device, round-robin like a small match, and -- on any context --
+ *     hold its lock only to queue their work, so concurrent fan-outs overlap;
  *   - device-buffer calls (EMQX_GM_DEVICE_IO, emqx_gm_match_submit, a
  *     device-row fan-out), the sharding helpers, emqx_gm_set_stream and
  *     emqx_gm_index_device_blob / _export use the first listed device; so

@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-O=gpurun_out/r06_n
+O=gpurun_out/${OUT:-r06_n}
 mkdir -p $O
 timeout -k 10 300 python3 -u scripts/small_call_probe.py 200 1024 > $O/plain.log 2>&1 || { tail -5 $O/plain.log; exit 1; }
 tail -1 $O/plain.log

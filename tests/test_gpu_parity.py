@@ -387,6 +387,81 @@ def test_hot_fanout_c4_small(ctx, orc):
     idx.release()
 
 
+def test_small_fanout_equals_locked_path(ctx, orc, monkeypatch):
+    """Host-row fan-outs of publish windows (gm_host.cpp run_fanout_small: the
+    deliveries counted from the host's subscriber table, one device round trip,
+    the context lock held only to queue) give the rows of the one-at-a-time
+    path (GM_FANOUT_SIMPLE) and the oracle's: on a built index and after
+    update_subs deltas (the host table's overrides), with empty rows, filters
+    without subscribers, a window past 1 MiB of deliveries (copy-engine rows),
+    from four threads at once; rows that are not a plain CSR over [0, nnz) take
+    the ordinary path, and a filter id out of range is EINVAL."""
+    import threading
+    from emqx_amd._lib import GpuMatchError
+    rng = np.random.default_rng(5)
+    filters = sorted({b"a/#", b"a/+", b"a/b", b"+/b", b"#", b"c/d", b"a/+/c", b"none/+"})
+    subs = [rng.integers(0, 1 << 20, size=int(rng.integers(1, 400))).astype(np.uint32).tolist() for _ in filters]
+    subs[filters.index(b"none/+")] = []
+    idx = ctx.build_index(filters, subs=subs)
+    idx2 = ctx.update_subs(idx, [(b"a/b", 7, True), (b"#", int(subs[filters.index(b"#")][0]), False),
+                                 (b"zz/+", 9, True), (b"c/d", 11, True)])
+    topics = [b"a/b", b"a/x", b"c/d", b"q", b"a/b/c", b"$SYS/a", b"none/x", b"zz/q"] * 40
+    for ix in (idx, idx2):
+        ro, ids = ctx.match(ix, topics, exact=True)
+        one_row = np.array([0, len(ids)], np.uint64)  # every match in one row
+        monkeypatch.setenv("GM_FANOUT_SIMPLE", "1")
+        want = ctx.fanout(ix, ro, ids)
+        want_one = ctx.fanout(ix, one_row, ids)
+        monkeypatch.delenv("GM_FANOUT_SIMPLE")
+        got = ctx.fanout(ix, ro, ids)
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+        got_one = ctx.fanout(ix, one_row, ids)
+        assert np.array_equal(got_one[0], want_one[0]) and np.array_equal(got_one[1], want_one[1])
+        assert ctx.fanout(ix, np.zeros(1, np.uint64), np.zeros(0, np.uint32))[0].tolist() == [0]
+        # (a slice whose offsets start past 0: the ordinary path, same rows as that path gives)
+        sl = ro[3:10].copy()
+        monkeypatch.setenv("GM_FANOUT_SIMPLE", "1")
+        want_sl = ctx.fanout(ix, sl - sl[0], ids[int(sl[0]):int(sl[-1])])
+        monkeypatch.delenv("GM_FANOUT_SIMPLE")
+        got_sl = ctx.fanout(ix, sl - sl[0], ids[int(sl[0]):int(sl[-1])])
+        assert np.array_equal(got_sl[1], want_sl[1])
+        errs, outs = [], [None] * 4
+
+        def one(k):
+            try:
+                for _ in range(25):
+                    outs[k] = ctx.fanout(ix, ro, ids)
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+        th = [threading.Thread(target=one, args=(k,)) for k in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs[0]
+        for o in outs:
+            assert np.array_equal(o[0], want[0]) and np.array_equal(o[1], want[1])
+    # the built index against the oracle
+    ro, ids = ctx.match(idx, topics, exact=True)
+    fro, fids = ctx.fanout(idx, ro, ids)
+    so = np.zeros(len(filters) + 1, np.uint64)
+    so[1:] = np.cumsum([len(s) for s in subs])
+    si = np.array([x for s in subs for x in s], np.uint32)
+    ero, eids = orc.fanout(ro, ids, so, si)
+    assert np.array_equal(fro, ero) and np.array_equal(fids, eids)
+    # past 1 MiB of deliveries: rows back on the copy engine
+    big = ctx.build_index([b"x/#"], subs=[list(range(300_000))])
+    fro, fids = ctx.fanout(big, np.array([0, 1, 1, 2], np.uint64), np.zeros(2, np.uint32))
+    assert fro.tolist() == [0, 300_000, 300_000, 600_000]
+    assert np.array_equal(fids[:300_000], np.arange(300_000)) and np.array_equal(fids[300_000:], np.arange(300_000))
+    with pytest.raises(GpuMatchError) as e:
+        ctx.fanout(big, np.array([0, 1], np.uint64), np.array([5], np.uint32))
+    assert "out of range" in str(e.value)
+    big.release()
+    idx2.release()
+    idx.release()
+
+
 def test_tokenizer_alignments_and_bytes(ctx, orc):
     """Words of every length 0..19 at every byte alignment, with bytes next to
     '/' in value ('.', '0', 0x2E, 0x30, NUL, 0xFF) right after separators: the
