@@ -890,13 +890,16 @@ int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
   MatchTail tail;
   tail.enqueue = [&](const uint64_t* d_ro, const uint32_t* d_ids, uint64_t cap) -> int {
     r_off = static_cast<uint64_t*>(ctx->hpool->alloc(obytes, true));
-    r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(cap * 4 + 16, true));
+    size_t ib = 4096;  // (a power of two: the result buffers come back from the host pool's cache)
+    while (ib < cap * 4 + 16) ib <<= 1;
+    r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(ib, true));
     if (!r_off || !r_ids) return set_err(ctx, EMQX_GM_ENOMEM, "match: host result");
     uint32_t* off_dev = mapped(r_off, obytes + cap * 4);
     uint32_t* ids_dev = mapped(r_ids, obytes + cap * 4);
     hipError_t x = hipSuccess;
     if (off_dev && ids_dev) {
-      if (launch_copy_u32x2(st, reinterpret_cast<const uint32_t*>(d_ro), off_dev, obytes / 4, d_ids, ids_dev, cap))
+      if (launch_copy_u32x2(st, reinterpret_cast<const uint32_t*>(d_ro), off_dev, obytes / 4, d_ids, ids_dev, cap,
+                            d_ro + n))
         x = hipErrorLaunchFailure;
     } else {
       x = hipMemcpyAsync(r_off, d_ro, obytes, hipMemcpyDeviceToHost, st);
@@ -951,25 +954,20 @@ int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
 }
 
 
-// a small host fan-out: at most this many deliveries (its page-locked result is sized to them)
+// a small host fan-out: at most this many deliveries (its speculative page-locked result)
 constexpr uint64_t kFanSmallDeliveries = uint64_t(16) << 20;
 
 int run_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_index* host, const emqx_gm_csr* m,
                      emqx_gm_csr* out, emqx_gm_match_stats* st_out) {
-  // ---- outside the lock: the rows checked, their deliveries counted from the
-  // host's subscriber table (the device's agrees: checked after the call), the
-  // rows staged in a page-locked buffer of the call's own: [row offsets | ids]
+  // ---- outside the lock: the rows checked and staged in a page-locked buffer
+  // of the call's own: [row offsets | ids]
   // (rows that are not a plain CSR over [0, nnz) take the ordinary path, as they always have)
   const uint64_t n = m->n_rows, nnz = m->nnz, nf = host->view.n_filters;
   if (m->row_off[0] != 0 || m->row_off[n] != nnz) return 1;
   for (uint64_t i = 0; i < n; ++i)
     if (m->row_off[i + 1] < m->row_off[i]) return 1;
-  uint64_t total = 0;
-  for (uint64_t i = 0; i < nnz; ++i) {
+  for (uint64_t i = 0; i < nnz; ++i)
     if (m->ids[i] >= nf) return set_err(ctx, EMQX_GM_EINVAL, "fanout: filter id out of range");
-    total += host->subs.count(m->ids[i]);
-  }
-  if (total > kFanSmallDeliveries) return 1;
   const size_t obytes = (n + 1) * 8, o_ids = (obytes + 15) & ~size_t(15);
   const size_t in_bytes = (o_ids + nnz * 4 + 15) & ~size_t(15);
   struct Pin {
@@ -979,20 +977,28 @@ int run_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_i
       if (p) pool->put(p);
     }
   } pin{ctx->pins};
+  // ---- under the lock: rows up, the deliveries into a speculative capacity
+  // (this context's recent deliveries per match x1.25, a power of two: the
+  // result buffers come back from the host pool's cache), the result's
+  // copy-out straight into the page-locked result (as long as the device's
+  // total), the call's end event; the device workspace handed back behind it
+  std::unique_lock<std::recursive_mutex> lk(ctx->mu);
+  const double want = 1024.0 + double(nnz) * ctx->subs_per_match * 1.25;
+  if (want > double(kFanSmallDeliveries)) return 1;  // (a wide fan-out: the ordinary path counts first)
+  uint64_t cap = 1024;
+  while (double(cap) < want) cap <<= 1;
+  lk.unlock();
   if (!(pin.p = ctx->pins->get(in_bytes))) return set_err(ctx, EMQX_GM_ENOMEM, "fanout: pinned staging");
   uint8_t* in = static_cast<uint8_t*>(pin.p);
   std::memcpy(in, m->row_off, obytes);
   if (nnz) std::memcpy(in + o_ids, m->ids, nnz * 4);
-  // ---- under the lock: rows up, the deliveries, the result's copy-out straight
-  // into the page-locked result, the call's end event; the device workspace
-  // handed back behind it
-  std::unique_lock<std::recursive_mutex> lk(ctx->mu);
+  lk.lock();
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   void* dv[4] = {ctx->pool->alloc(in_bytes), ctx->pool->alloc((nnz + 1) * 8), ctx->pool->alloc(obytes),
-                 ctx->pool->alloc(total * 4 + 16)};
+                 ctx->pool->alloc(cap * 4 + 16)};
   uint64_t* r_off = static_cast<uint64_t*>(ctx->hpool->alloc(obytes, true));
-  uint32_t* r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(total * 4 + 16, true));
+  uint32_t* r_ids = static_cast<uint32_t*>(ctx->hpool->alloc(cap * 4 + 16, true));
   hipEvent_t done = nullptr;
   if (!ctx->ev_free.empty()) {
     done = ctx->ev_free.back();
@@ -1015,7 +1021,7 @@ int run_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_i
   hipError_t e = small_copy(st, d_in, in, in_bytes, true);
   if (e != hipSuccess) return fail(EMQX_GM_EDEVICE, "fanout: rows to device");
   if (int rc = queue_fanout_small(ctx, idx, reinterpret_cast<const uint64_t*>(d_in),
-                                  reinterpret_cast<const uint32_t*>(d_in + o_ids), n, nnz, total,
+                                  reinterpret_cast<const uint32_t*>(d_in + o_ids), n, nnz, cap,
                                   static_cast<uint64_t*>(dv[1]), static_cast<uint64_t*>(dv[2]),
                                   static_cast<uint32_t*>(dv[3]))) {
     hipStreamSynchronize(st);
@@ -1025,16 +1031,17 @@ int run_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_i
     ctx->ev_free.push_back(done);
     return rc;
   }
-  uint32_t* off_dev = mapped(r_off, obytes + total * 4);
-  uint32_t* ids_dev = mapped(r_ids, obytes + total * 4);
+  const uint64_t* d_total = static_cast<const uint64_t*>(dv[2]) + n;  // the rows' row_off[n]
+  uint32_t* off_dev = mapped(r_off, obytes + cap * 4);
+  uint32_t* ids_dev = mapped(r_ids, obytes + cap * 4);
   if (off_dev && ids_dev) {
     e = launch_copy_u32x2(st, static_cast<const uint32_t*>(dv[2]), off_dev, obytes / 4,
-                          static_cast<const uint32_t*>(dv[3]), ids_dev, total)
+                          static_cast<const uint32_t*>(dv[3]), ids_dev, cap, d_total)
             ? hipErrorLaunchFailure
             : hipSuccess;
   } else {
     e = hipMemcpyAsync(r_off, dv[2], obytes, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess && total) e = hipMemcpyAsync(r_ids, dv[3], total * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(r_ids, dv[3], cap * 4, hipMemcpyDeviceToHost, st);
   }
   if (e == hipSuccess) e = hipEventRecord(done, st);
   if (e != hipSuccess) return fail(EMQX_GM_EDEVICE, "fanout: rows to host");
@@ -1044,10 +1051,12 @@ int run_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_i
   e = hipEventSynchronize(done);
   lk.lock();
   ctx->ev_free.push_back(done);
-  if (e != hipSuccess || r_off[n] != total) {  // (a device fault, or the device's table disagreed with the host's)
+  const uint64_t total = e == hipSuccess ? r_off[n] : 0;
+  if (e == hipSuccess && nnz) ctx->subs_per_match = std::max(1.0, double(total) / double(nnz));
+  if (e != hipSuccess || total > cap) {  // (a device fault; or past the capacity: the ordinary path, which counts first)
     ctx->hpool->release(r_off);
     ctx->hpool->release(r_ids);
-    return set_err(ctx, EMQX_GM_EDEVICE, e != hipSuccess ? "fanout: device" : "fanout: subscriber tables disagree");
+    return e != hipSuccess ? set_err(ctx, EMQX_GM_EDEVICE, "fanout: device") : 1;
   }
   lk.unlock();
   if (st_out) {

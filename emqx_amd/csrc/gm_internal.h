@@ -176,6 +176,7 @@ struct emqx_gm_ctx {
   std::vector<hipEvent_t> ev_free;
   std::vector<void*> pin_free, pin_all;
   double ids_per_topic = 4.0;  // speculative ids capacity of a match call (run_match), from recent calls
+  double subs_per_match = 16.0;  // speculative deliveries capacity of a small host fan-out, from recent calls
   // A ring of 64-B pass-counter blocks (gm_match.hip MatchCall): a call takes
   // the next block, already zeroed -- the previous call's assembly kernel zeroes
   // it -- so a call needs no zeroing launch of its own.  State per block: 0 ready
@@ -486,7 +487,7 @@ int set_err(emqx_gm_ctx* ctx, int code, const std::string& msg);
 int launch_off32_to_64(hipStream_t st, const uint32_t* in, uint64_t n1, uint64_t* out);
 int launch_off64_to_32(hipStream_t st, const uint64_t* in, uint64_t n1, uint32_t* out);
 int launch_copy_u32x2(hipStream_t st, const uint32_t* s0, uint32_t* d0, uint64_t n0, const uint32_t* s1, uint32_t* d1,
-                      uint64_t n1);
+                      uint64_t n1, const uint64_t* n1_max = nullptr);
 int launch_add_u64(hipStream_t st, uint64_t* p, uint64_t n1, uint64_t add);
 // the host path's u16 topic lengths -> u64 offsets (n + 1 entries, an exclusive scan) on stream st
 int scan_len16(emqx_gm_ctx* ctx, hipStream_t st, const uint16_t* len, uint64_t n, uint64_t* out);
@@ -505,10 +506,12 @@ uint64_t host_chunk_topics();
 int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
                    uint32_t flags, emqx_gm_csr* out, emqx_gm_match_stats* st_out);
 // A host-row fan-out of a publish window, the same way (entered WITHOUT
-// ctx->mu): the deliveries counted from the host's subscriber table, the rows
-// staged outside the lock, one device round trip.  idx: the snapshot on this
-// device (a replica), host: the one whose host tables count (the primary).
-// Returns 1 -- nothing done -- for a fan-out past kFanSmallDeliveries.
+// ctx->mu): the rows staged outside the lock, the deliveries written into a
+// speculative capacity, one device round trip.  idx: the snapshot on this
+// device (a replica), host: the primary (its filter count).  Returns 1 --
+// nothing delivered -- for rows that are not a plain CSR, a fan-out whose
+// expected size is past kFanSmallDeliveries, or one past its capacity: the
+// caller takes the ordinary path.
 int run_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_index* host, const emqx_gm_csr* m,
                      emqx_gm_csr* out, emqx_gm_match_stats* st_out);
 int queue_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint64_t* d_off, const uint32_t* d_ids,

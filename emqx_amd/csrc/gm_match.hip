@@ -2538,10 +2538,14 @@ int launch_off64_to_32(hipStream_t st, const uint64_t* in, uint64_t n1, uint32_t
 // Small host-buffer calls (gm_host.cpp run_host_small): inputs in and rows out
 // through page-locked host memory the device addresses directly -- two copies
 // in one launch on the call's own queue, so no copy engine has to hand over to
-// the compute queue between the call's kernels (~10 us a hand-over)
+// the compute queue between the call's kernels (~10 us a hand-over).  n1_max
+// (optional): the second copy stops at the count the device wrote there (a
+// result's row_off[n]: the rows' true length inside a speculative capacity)
 __global__ __launch_bounds__(256) void k_copy_u32x2(const uint32_t* __restrict__ s0, uint32_t* __restrict__ d0,
                                                     uint64_t n0, const uint32_t* __restrict__ s1,
-                                                    uint32_t* __restrict__ d1, uint64_t n1) {
+                                                    uint32_t* __restrict__ d1, uint64_t n1,
+                                                    const uint64_t* __restrict__ n1_max) {
+  if (n1_max) n1 = min(n1, *n1_max);
   const uint64_t t = uint64_t(blockIdx.x) * 256u + threadIdx.x, stride = uint64_t(gridDim.x) * 256u;
   const uint64_t q0 = n0 / 4, q1 = n1 / 4;  // (16-B units; every buffer here is 16-B aligned)
   for (uint64_t i = t; i < q0; i += stride)
@@ -2553,10 +2557,10 @@ __global__ __launch_bounds__(256) void k_copy_u32x2(const uint32_t* __restrict__
   __threadfence_system();  // (host-bound stores visible before the call's end event)
 }
 int launch_copy_u32x2(hipStream_t st, const uint32_t* s0, uint32_t* d0, uint64_t n0, const uint32_t* s1, uint32_t* d1,
-                      uint64_t n1) {
+                      uint64_t n1, const uint64_t* n1_max) {
   const uint64_t q = (std::max(n0, n1) + 3) / 4;
   const uint64_t g = std::min<uint64_t>(1024, (q + 255) / 256);
-  hipLaunchKernelGGL(k_copy_u32x2, dim3(g ? g : 1), dim3(256), 0, st, s0, d0, n0, s1, d1, n1);
+  hipLaunchKernelGGL(k_copy_u32x2, dim3(g ? g : 1), dim3(256), 0, st, s0, d0, n0, s1, d1, n1, n1_max);
   return hipGetLastError() == hipSuccess ? 0 : EMQX_GM_EDEVICE;
 }
 // p[0..n1) += add, in place (a chunk's row offsets rebased to the whole call's rows)
