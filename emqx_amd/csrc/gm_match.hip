@@ -2320,11 +2320,12 @@ __global__ __launch_bounds__(256) void k_fanout_copy(const uint64_t* __restrict_
                                                      const uint32_t* __restrict__ m_ids,
                                                      const uint64_t* __restrict__ sub_off,
                                                      const uint32_t* __restrict__ sub_ids, uint64_t glo,
-                                                     uint64_t total, uint64_t per_block, uint32_t* __restrict__ out0) {
+                                                     uint64_t total, uint64_t per_block, uint32_t* __restrict__ out0,
+                                                     bool clamp) {
   // this launch produces the global delivery range [glo, total); out0[0] is delivery glo
-  // (never past the device's own total: a small host fan-out sizes the launch
-  // from the host's subscriber table, gm_host.cpp run_fanout_small)
-  total = min(total, seg_dst[nseg]);
+  // (clamp: never past the device's own total -- a small host fan-out sizes
+  // the launch by a speculative capacity, gm_host.cpp run_fanout_small)
+  if (clamp) total = min(total, seg_dst[nseg]);
   const uint64_t lo = glo + uint64_t(blockIdx.x) * per_block;
   if (lo >= total) return;
   const uint64_t hi = min(total, lo + per_block);
@@ -3962,7 +3963,7 @@ int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m,
     const uint64_t per = fan_per_block(cnt);
     const uint64_t blocks = (cnt + per - 1) / per;
     hipLaunchKernelGGL(k_fanout_copy, dim3(blocks), dim3(256), 0, st, seg_dst.as<uint64_t>(), nnz, m_ids,
-                       idx->view.sub_off, idx->view.sub_ids, glo, ghi, per, ids.as<uint32_t>());
+                       idx->view.sub_off, idx->view.sub_ids, glo, ghi, per, ids.as<uint32_t>(), false);
     GM_HIP(ctx, hipGetLastError());
   }
   GM_HIP(ctx, hipEventRecord(ctx->ev[2], st));
@@ -3975,7 +3976,7 @@ int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m,
 
 // A small host fan-out's device work (gm_host.cpp run_fanout_small), queued
 // without a wait: the deliveries' offsets, the rows' offsets and the delivery
-// lists of [0, total) -- total counted by the host from its subscriber table.
+// lists of [0, min(total, the device's count)) -- total: the call's capacity.
 int queue_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint64_t* d_off, const uint32_t* d_ids,
                        uint64_t n, uint64_t nnz, uint64_t total, uint64_t* seg_dst, uint64_t* row_off, uint32_t* ids) {
   hipStream_t st = ctx->stream;
@@ -3985,7 +3986,7 @@ int queue_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint64_
   if (total) {
     const uint64_t per = fan_per_block(total);
     hipLaunchKernelGGL(k_fanout_copy, dim3((total + per - 1) / per), dim3(256), 0, st, seg_dst, nnz, d_ids,
-                       idx->view.sub_off, idx->view.sub_ids, uint64_t(0), total, per, ids);
+                       idx->view.sub_off, idx->view.sub_ids, uint64_t(0), total, per, ids, true);
     GM_HIP(ctx, hipGetLastError());
   }
   return 0;
