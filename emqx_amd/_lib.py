@@ -96,6 +96,7 @@ SIGNATURES = {
     "emqx_gm_host_free": (_i32, [_vp, _vp]),
     "emqx_gm_devices": (_i32, [_vp, _vp, C.POINTER(_u32)]),
     "emqx_gm_fanout": (_i32, [_vp, _vp, C.POINTER(Csr), _u32, C.POINTER(Csr)]),
+    "emqx_gm_match_fanout": (_i32, [_vp, _vp, _vp, _vp, _u64, _u32, C.POINTER(Csr), C.POINTER(Csr)]),
     "emqx_gm_csr_free": (_i32, [_vp, C.POINTER(Csr)]),
     "emqx_gm_last_stats": (_i32, [_vp, C.POINTER(MatchStats)]),
     "emqx_gm_filter_ranks": (_i32, [_vp, _vp, _u64, _vp, C.POINTER(_u64)]),

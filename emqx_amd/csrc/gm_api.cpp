@@ -613,20 +613,26 @@ static int noted(const emqx_gm_ctx* api_ctx, const emqx_gm_ctx* ran, int rc) {
 // (apps/emqx/src/emqx_trie.erl:66-70, emqx_router.erl:128-145).  Larger calls
 // are cut into chunks spread over every device (gm_host.cpp run_host_pipe).
 static int match_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
-                       uint32_t flags, emqx_gm_csr* out) {
+                       uint32_t flags, emqx_gm_csr* out, gm::SmallFan* fan = nullptr) {
   const size_t K = 1 + (idx->reps.size() == ctx->members.size() ? ctx->members.size() : 0);
   const size_t pick = K > 1 ? ctx->rr.fetch_add(1, std::memory_order_relaxed) % K : 0;
   emqx_gm_ctx* mc = pick ? ctx->members[pick - 1] : ctx;
   const emqx_gm_index* rix = pick ? idx->reps[pick - 1] : idx;
   hipSetDevice(mc->device);
   emqx_gm_match_stats st{};
-  const int rc = gm::run_host_small(mc, rix, tb, to, n, flags, out, &st);
+  const int rc = gm::run_host_small(mc, rix, tb, to, n, flags, out, &st, fan);
   if (rc == EMQX_GM_OK) {
     tl_stats = st;
     tl_stats_ctx = ctx;
   }
   hipSetDevice(ctx->device);
   return rc;
+}
+
+// a host-buffer call that runs whole on one device (run_host_small)
+static bool small_call(const emqx_gm_index* idx, const uint64_t* to, uint64_t n, uint32_t flags) {
+  return !(flags & EMQX_GM_DEVICE_IO) && !idx->ov && !idx->route && n <= gm::host_chunk_topics() &&
+         (n == 0 || to[n] - to[0] <= (uint64_t(64) << 20)) && !gm::knob("GM_HOST_SIMPLE") && !gm::knob("GM_HOST_PIPE");
 }
 
 int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to,
@@ -648,9 +654,7 @@ int emqx_gm_match(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb,
     hipSetDevice(ctx->device);
     return noted(ctx, ctx, gm::run_match_sharded(ctx, idx, tb, to, n, flags, out));
   }
-  if (!(flags & EMQX_GM_DEVICE_IO) && !idx->ov && n <= gm::host_chunk_topics() &&
-      (n == 0 || to[n] - to[0] <= (uint64_t(64) << 20)) && !gm::knob("GM_HOST_SIMPLE") && !gm::knob("GM_HOST_PIPE"))
-    return match_small(ctx, idx, tb, to, n, flags, out);
+  if (small_call(idx, to, n, flags)) return match_small(ctx, idx, tb, to, n, flags, out);
   std::unique_lock<std::recursive_mutex> lk(ctx->mu);
   hipSetDevice(ctx->device);
   if (idx->ov) return noted(ctx, ctx, gm::run_match_overlay(ctx, idx, tb, to, n, flags, out));
@@ -752,6 +756,48 @@ int emqx_gm_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr
     return noted(ctx, ctx, gm::run_fanout_multi(ctx, idx, m, flags, out));
   return noted(ctx, ctx, gm::run_fanout(ctx, idx, m, flags, out));
   GM_GUARD_END(ctx)
+}
+
+int emqx_gm_match_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
+                         uint32_t flags, emqx_gm_csr* matches, emqx_gm_csr* deliveries) {
+  if (!ctx) return EMQX_GM_EINVAL;
+  if (!idx || !matches || !deliveries || (n && (!tb || !to)))
+    return gm::set_err(ctx, EMQX_GM_EINVAL, "match_fanout: NULL argument");
+  if (flags & ~EMQX_GM_WITH_EXACT) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_fanout: flags (host buffers only)");
+  if (n >= 0xFFFFFFF0ull) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_fanout: batch too large (>= 2^32 topics)");
+  if (idx->device != ctx->device) return gm::set_err(ctx, EMQX_GM_EINVAL, "match_fanout: index lives on another device");
+  std::memset(matches, 0, sizeof(*matches));
+  std::memset(deliveries, 0, sizeof(*deliveries));
+  int rc = EMQX_GM_OK;
+  bool fused = false;
+  gm::SmallFan fan;
+  GM_GUARD_BEGIN
+  // a publish window: the fan-out rides the match's one device round trip
+  // (gm_host.cpp run_host_small); otherwise, or when its speculation did not
+  // hold, the two calls one after the other
+  if (small_call(idx, to, n, flags) && !idx->view.gmap && !idx->subs.empty() && !gm::knob("GM_FANOUT_SIMPLE")) {
+    rc = match_small(ctx, idx, tb, to, n, flags, matches, &fan);
+    if (rc != EMQX_GM_OK) return rc;
+    if (fan.ok) {
+      *deliveries = fan.out;
+      fused = true;
+    }
+  } else {
+    rc = emqx_gm_match(ctx, idx, tb, to, n, flags, matches);
+    if (rc != EMQX_GM_OK) return rc;
+  }
+  GM_GUARD_END(ctx)
+  if (fused) return EMQX_GM_OK;
+  if (gm::knob("GM_FANOUT_FUSED_ONLY")) {  // (tests: the fused form must have held)
+    emqx_gm_csr_free(ctx, matches);
+    return gm::set_err(ctx, EMQX_GM_EUNSUPPORTED,
+                       "match_fanout: not fused (queued " + std::to_string(fan.queued) + ", speculative rows " +
+                           std::to_string(fan.rows_spec) + ", deliveries " + std::to_string(fan.total) + " of " +
+                           std::to_string(fan.cap) + ")");
+  }
+  rc = emqx_gm_fanout(ctx, idx, matches, 0, deliveries);
+  if (rc != EMQX_GM_OK) emqx_gm_csr_free(ctx, matches);  // (the error message stays the fan-out's)
+  return rc;
 }
 
 int emqx_gm_fanout_part(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m, uint32_t part,

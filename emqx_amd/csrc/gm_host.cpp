@@ -802,10 +802,13 @@ static hipError_t small_copy(hipStream_t st, void* dst, const void* src, size_t 
   return hipMemcpyAsync(dst, src, bytes, to_dev ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, st);
 }
 
+// a small host fan-out: at most this many deliveries (its speculative page-locked result)
+constexpr uint64_t kFanSmallDeliveries = uint64_t(16) << 20;
+
 uint64_t host_chunk_topics() { return std::max<uint64_t>(1024, env_u64("GM_HOST_CHUNK", 256u << 10)); }
 
 int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
-                   uint32_t flags, emqx_gm_csr* out, emqx_gm_match_stats* st_out) {
+                   uint32_t flags, emqx_gm_csr* out, emqx_gm_match_stats* st_out, SmallFan* fan) {
   // ---- outside the lock: the offsets checked, the call's inputs staged in a
   // page-locked buffer of its own: [text | 64 B of padding | u16 lengths (u32
   // offsets past 65,535 B)] -- past kMappedMax of text already page-locked, the
@@ -881,11 +884,24 @@ int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
   // are, u64: one launch fewer)
   uint64_t* r_off = nullptr;
   uint32_t* r_ids = nullptr;
+  // fan: the deliveries of the speculative rows, queued behind them into a
+  // capacity of their own (this context's recent deliveries per match), their
+  // page-locked result filled the same way
+  uint64_t* f_off = nullptr;
+  uint32_t* f_ids = nullptr;
+  uint64_t cap_f = 0;
+  auto drop_fan = [&]() {  // (under the lock)
+    ctx->hpool->release(f_off);
+    ctx->hpool->release(f_ids);
+    f_off = nullptr;
+    f_ids = nullptr;
+  };
   auto drop_res = [&]() {  // (under the lock)
     ctx->hpool->release(r_off);
     ctx->hpool->release(r_ids);
     r_off = nullptr;
     r_ids = nullptr;
+    drop_fan();
   };
   MatchTail tail;
   tail.enqueue = [&](const uint64_t* d_ro, const uint32_t* d_ids, uint64_t cap) -> int {
@@ -905,7 +921,41 @@ int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
       x = hipMemcpyAsync(r_off, d_ro, obytes, hipMemcpyDeviceToHost, st);
       if (x == hipSuccess && cap) x = hipMemcpyAsync(r_ids, d_ids, cap * 4, hipMemcpyDeviceToHost, st);
     }
-    return x == hipSuccess ? 0 : set_err(ctx, EMQX_GM_EDEVICE, "match: rows to host");
+    if (x != hipSuccess) return set_err(ctx, EMQX_GM_EDEVICE, "match: rows to host");
+    // (cap = 1024 + the topics x recent ids per topic x1.25: the expected rows past the slack)
+    const double want = 1024.0 + double(cap > 1024 ? cap - 1024 : 1) * ctx->subs_per_match;
+    if (fan) fan->cap = uint64_t(want);
+    if (!fan || want > double(kFanSmallDeliveries)) return 0;  // (no fan-out here: the caller runs its own)
+    for (cap_f = 1024; double(cap_f) < want;) cap_f <<= 1;
+    void* fd[3] = {ctx->pool->alloc((cap + 1) * 8), ctx->pool->alloc(obytes), ctx->pool->alloc(cap_f * 4 + 16)};
+    f_off = static_cast<uint64_t*>(ctx->hpool->alloc(obytes, true));
+    f_ids = static_cast<uint32_t*>(ctx->hpool->alloc(cap_f * 4 + 16, true));
+    if (!fd[0] || !fd[1] || !fd[2] || !f_off || !f_ids) {  // (no room: the caller runs its own fan-out)
+      for (void* q : fd)
+        if (q) ctx->pool->release(q);
+      drop_fan();
+      return 0;
+    }
+    int frc = queue_fanout_spec(ctx, idx, d_ro, d_ids, n, cap, cap_f, static_cast<uint64_t*>(fd[0]),
+                                static_cast<uint64_t*>(fd[1]), static_cast<uint32_t*>(fd[2]));
+    uint32_t* fo_dev = mapped(f_off, obytes + cap_f * 4);
+    uint32_t* fi_dev = mapped(f_ids, obytes + cap_f * 4);
+    if (!frc && fo_dev && fi_dev) {
+      if (launch_copy_u32x2(st, static_cast<const uint32_t*>(fd[1]), fo_dev, obytes / 4,
+                            static_cast<const uint32_t*>(fd[2]), fi_dev, cap_f, static_cast<const uint64_t*>(fd[1]) + n))
+        frc = set_err(ctx, EMQX_GM_EDEVICE, "match_fanout: deliveries to host");
+    } else if (!frc) {
+      if (hipMemcpyAsync(f_off, fd[1], obytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipMemcpyAsync(f_ids, fd[2], cap_f * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+        frc = set_err(ctx, EMQX_GM_EDEVICE, "match_fanout: deliveries to host");
+    }
+    if (frc) {
+      hipStreamSynchronize(st);
+      for (void* q : fd) ctx->pool->release(q);
+      return frc;
+    }
+    ctx->pool->release_after(fd, 3, st);
+    return 0;
   };
   void* ticket = nullptr;
   int rc = match_submit(ctx, idx, d_b, d_o, n, flags | EMQX_GM_DEVICE_IO | EMQX_GM_NO_TIMING, &ticket, &tail);
@@ -941,6 +991,26 @@ int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
       return set_err(ctx, x == hipErrorOutOfMemory ? EMQX_GM_ENOMEM : EMQX_GM_EDEVICE, "match: host result");
     }
   }
+  if (fan) fan->rows_spec = tail.used;
+  if (f_off) {  // the fused fan-out holds if the rows were the speculative ones and its deliveries fit
+    const uint64_t tot = f_off[n];
+    fan->queued = true;
+    fan->total = tot;
+    fan->cap = cap_f;
+    if (tail.used && nnz) ctx->subs_per_match = std::max(1.0, double(tot) / double(nnz));
+    if (tail.used && tot <= cap_f) {
+      fan->ok = true;
+      fan->out = emqx_gm_csr{};
+      fan->out.n_rows = n;
+      fan->out.nnz = tot;
+      fan->out.row_off = f_off;
+      fan->out.ids = f_ids;
+      fan->out.on_device = 0;
+      fan->out.priv = ctx;
+    } else {
+      drop_fan();
+    }
+  }
   ctx->pool->release(dc.row_off);
   ctx->pool->release(dc.ids);
   lk.unlock();
@@ -953,9 +1023,6 @@ int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb
   return 0;
 }
 
-
-// a small host fan-out: at most this many deliveries (its speculative page-locked result)
-constexpr uint64_t kFanSmallDeliveries = uint64_t(16) << 20;
 
 int run_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_index* host, const emqx_gm_csr* m,
                      emqx_gm_csr* out, emqx_gm_match_stats* st_out) {

@@ -503,8 +503,20 @@ uint64_t host_chunk_topics();
 // into the page-locked result; copies up to 1 MiB as kernels over mapped
 // memory), waited for outside it -- so concurrent small calls on one device
 // overlap one another's host work and device round trips
+// fan (optional, emqx_gm_match_fanout): the call's fan-out queued behind its
+// speculative rows in the same round trip; fan->ok says whether it held (the
+// match's rows and the deliveries both within their capacities)
+struct SmallFan {
+  emqx_gm_csr out{};
+  bool ok = false;
+  // (why not, for the tests' message: queued, the rows were the speculative ones, deliveries vs capacity)
+  bool queued = false, rows_spec = false;
+  uint64_t total = 0, cap = 0;
+};
 int run_host_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint8_t* tb, const uint64_t* to, uint64_t n,
-                   uint32_t flags, emqx_gm_csr* out, emqx_gm_match_stats* st_out);
+                   uint32_t flags, emqx_gm_csr* out, emqx_gm_match_stats* st_out, SmallFan* fan = nullptr);
+int queue_fanout_spec(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint64_t* d_ro, const uint32_t* d_ids,
+                      uint64_t n, uint64_t cap_m, uint64_t cap_f, uint64_t* seg_dst, uint64_t* row_off, uint32_t* ids);
 // A host-row fan-out of a publish window, the same way (entered WITHOUT
 // ctx->mu): the rows staged outside the lock, the deliveries written into a
 // speculative capacity, one device round trip.  idx: the snapshot on this

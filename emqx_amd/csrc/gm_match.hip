@@ -1788,6 +1788,23 @@ struct LoadSegLen {  // subscriber count of the filter of match entry i
   }
 };
 
+// LoadSegLen over a small call's SPECULATIVE rows (emqx_gm_match_fanout): the
+// fan-out is queued before the host knows the match count, so entries past the
+// device's own count (*nnz, the rows' row_off[n]) and ids out of range (an
+// overflowed speculative buffer holds stale words) count 0 -- such a fan-out
+// is discarded, but it reads nothing out of bounds
+struct LoadSegLenSpec {
+  const uint32_t* ids;
+  const uint64_t* sub_off;
+  const uint64_t* nnz;
+  uint32_t nf;
+  __device__ uint64_t operator()(uint64_t i) const {
+    if (i >= *nnz) return 0;
+    const uint32_t f = ids[i];
+    return f < nf ? sub_off[f + 1] - sub_off[f] : 0;
+  }
+};
+
 // Exclusive scan of n_in loaded values into out[0..n_in] (out[n_in] = total).
 // split (optional): for a two-level scan, leave out[0..n_in) block-local and
 // hand back the blocks' offsets in *split (out[i] + (*split)[i / SCAN_B] is the
@@ -2281,11 +2298,12 @@ __global__ __launch_bounds__(256) void k_copy_slow(const uint32_t* __restrict__ 
 // ---------------------------------------------------------------------------
 // fan-out
 // ---------------------------------------------------------------------------
+// (nseg: the segments seg_dst holds -- a speculative call's row offsets may point past them)
 __global__ __launch_bounds__(256) void k_fanout_rowoff(const uint64_t* __restrict__ m_off, uint64_t n,
                                                        const uint64_t* __restrict__ seg_dst,
-                                                       uint64_t* __restrict__ out_off) {
+                                                       uint64_t* __restrict__ out_off, uint64_t nseg) {
   const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
-  if (i <= n) out_off[i] = seg_dst[m_off[i]];
+  if (i <= n) out_off[i] = seg_dst[min(m_off[i], nseg)];
 }
 
 // Output elements per workgroup: from 1,024 (a publish window's ~100k
@@ -3945,13 +3963,15 @@ int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m,
   int rc = scan_excl(ctx, LoadSegLen{m_ids, idx->view.sub_off}, nnz, seg_dst.as<uint64_t>());
   if (rc) return rc;
   hipLaunchKernelGGL(k_fanout_rowoff, dim3((n + 1 + 255) / 256), dim3(256), 0, st, m_off, n, seg_dst.as<uint64_t>(),
-                     row_off.as<uint64_t>());
+                     row_off.as<uint64_t>(), nnz);
   GM_HIP(ctx, hipGetLastError());
   uint64_t total = 0;
   GM_HIP(ctx, hipMemcpyAsync(&total, seg_dst.as<uint64_t>() + nnz, 8, hipMemcpyDeviceToHost, st));
   GM_HIP(ctx, hipStreamSynchronize(st));
   // part `part` of n_parts: the contiguous delivery range [glo, ghi) of the
   // whole fan-out (rows and wide rows alike are cut wherever the range ends)
+  // (the deliveries per match a small host fan-out sizes its speculative capacity by)
+  if (nnz) ctx->subs_per_match = std::max(1.0, double(total) / double(nnz));
   const uint64_t glo = uint64_t((unsigned __int128)total * part / n_parts);
   const uint64_t ghi = uint64_t((unsigned __int128)total * (part + 1) / n_parts);
   const uint64_t cnt = ghi - glo;
@@ -3981,7 +4001,7 @@ int queue_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint64_
                        uint64_t n, uint64_t nnz, uint64_t total, uint64_t* seg_dst, uint64_t* row_off, uint32_t* ids) {
   hipStream_t st = ctx->stream;
   if (int rc = scan_excl(ctx, LoadSegLen{d_ids, idx->view.sub_off}, nnz, seg_dst)) return rc;
-  hipLaunchKernelGGL(k_fanout_rowoff, dim3((n + 1 + 255) / 256), dim3(256), 0, st, d_off, n, seg_dst, row_off);
+  hipLaunchKernelGGL(k_fanout_rowoff, dim3((n + 1 + 255) / 256), dim3(256), 0, st, d_off, n, seg_dst, row_off, nnz);
   GM_HIP(ctx, hipGetLastError());
   if (total) {
     const uint64_t per = fan_per_block(total);
@@ -3989,6 +4009,24 @@ int queue_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint64_
                        idx->view.sub_off, idx->view.sub_ids, uint64_t(0), total, per, ids, true);
     GM_HIP(ctx, hipGetLastError());
   }
+  return 0;
+}
+
+// The fan-out of a small host call's speculative rows, queued right behind its
+// assembly (emqx_gm_match_fanout, gm_host.cpp run_host_small): d_ro/d_ids the
+// speculative CSR (cap_m ids), the deliveries into cap_f -- both counts checked
+// by the host after the call's one wait.
+int queue_fanout_spec(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint64_t* d_ro, const uint32_t* d_ids,
+                      uint64_t n, uint64_t cap_m, uint64_t cap_f, uint64_t* seg_dst, uint64_t* row_off, uint32_t* ids) {
+  hipStream_t st = ctx->stream;
+  const LoadSegLenSpec ld{d_ids, idx->view.sub_off, d_ro + n, uint32_t(idx->view.n_filters)};
+  if (int rc = scan_excl(ctx, ld, cap_m, seg_dst)) return rc;
+  hipLaunchKernelGGL(k_fanout_rowoff, dim3((n + 1 + 255) / 256), dim3(256), 0, st, d_ro, n, seg_dst, row_off, cap_m);
+  GM_HIP(ctx, hipGetLastError());
+  const uint64_t per = fan_per_block(cap_f);
+  hipLaunchKernelGGL(k_fanout_copy, dim3((cap_f + per - 1) / per), dim3(256), 0, st, seg_dst, cap_m, d_ids,
+                     idx->view.sub_off, idx->view.sub_ids, uint64_t(0), cap_f, per, ids, true);
+  GM_HIP(ctx, hipGetLastError());
   return 0;
 }
 

@@ -430,6 +430,22 @@ class Context:
         finally:
             lib().emqx_gm_csr_free(self.h, C.byref(out))
 
+    def match_fanout(self, index: Index, topics, exact: bool = True):
+        """emqx_broker:publish/1's route + dispatch of a batch in one call
+        (emqx_gm_match_fanout): ((row_off, filter ids), (row_off, subscriber ids)),
+        equal to match() followed by fanout() -- one device round trip for a
+        publish window."""
+        tb, to = topics if isinstance(topics, tuple) else pack(topics)
+        m, d = Csr(), Csr()
+        flags = _lib.WITH_EXACT if exact else 0
+        check(lib().emqx_gm_match_fanout(self.h, index.h, _ptr(tb), _ptr(to), len(to) - 1, flags, C.byref(m),
+                                         C.byref(d)), self.h, "match_fanout")
+        try:
+            return _csr_to_numpy(m), _csr_to_numpy(d)
+        finally:
+            lib().emqx_gm_csr_free(self.h, C.byref(m))
+            lib().emqx_gm_csr_free(self.h, C.byref(d))
+
     def fanout_part(self, index: Index, matches: DeviceCsr, part: int, n_parts: int) -> Tuple[DeviceCsr, int]:
         """Part ``part`` of ``n_parts`` of the fan-out of ``matches`` (emqx_gm_fanout_part):
         a device CSR whose row_off are the global delivery offsets and whose ids are the

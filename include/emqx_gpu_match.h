@@ -19,6 +19,8 @@
  *                            EMQX_GM_WITH_EXACT; batched over many topics
  *   emqx_gm_fanout        <- emqx_broker:dispatch/2 + do_dispatch/2,3 +
  *                            subscribers/1 (emqx_broker.erl:296-322, 506-530)
+ *   emqx_gm_match_fanout  <- emqx_broker:publish/1's route/2 + dispatch/2 of a
+ *                            batch (emqx_broker.erl:204-215, 245-322)
  *
  * Result semantics (bit-exact with the reference, compared as sets):
  *   - filter ids are the lexicographic rank of the filter bytes (Erlang binary
@@ -64,7 +66,7 @@
  *     GM_SCAN_SPLIT, GM_SCAN_SUMS, GM_NO_SPEC_IDS, GM_ASM_STREAM;
  *   host path:          GM_HOST_SIMPLE, GM_HOST_PIPE, GM_HOST_CHUNK,
  *     GM_HOST_THREADS, GM_HOST_BOUNCE, GM_HOST_WIDE_ROWS, GM_HOST_OFF32,
- *     GM_FANOUT_MULTI_MIN, GM_FANOUT_SIMPLE;
+ *     GM_FANOUT_MULTI_MIN, GM_FANOUT_SIMPLE, GM_FANOUT_FUSED_ONLY;
  *   updates:            GM_UPDATE_OVERLAY, GM_UPDATE_UNFUSED, GM_SPARE_BLOB_MIN;
  *   diagnostics:        GM_UPDATE_TIMING, GM_INDEX_STATS, GM_INDEX_VERIFY.
  */
@@ -324,6 +326,19 @@ int emqx_gm_host_free(emqx_gm_ctx *ctx, void *p);
 int emqx_gm_devices(const emqx_gm_ctx *ctx, int32_t *devices, uint32_t *n);
 int emqx_gm_fanout(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const emqx_gm_csr *matches,
                    uint32_t flags, emqx_gm_csr *out_subs);
+/* emqx_broker:publish/1's route + dispatch of a batch in one call
+ * (emqx_broker.erl:204-215, 245-322): the rows of emqx_gm_match(flags) into
+ * *matches and their fan-out, as emqx_gm_fanout gives it, into *deliveries
+ * (host buffers only; flags: EMQX_GM_WITH_EXACT or 0).  A publish window (a
+ * batch of at most one chunk, 256K topics) makes ONE device round trip for
+ * both: the fan-out is queued right behind the match's speculative rows and
+ * kept when the rows and the deliveries fit their capacities (else the
+ * fan-out runs after the match, as the two calls would).  On error nothing is
+ * returned; both results are freed with emqx_gm_csr_free.  The NIF's
+ * fanout_batch/2. */
+int emqx_gm_match_fanout(emqx_gm_ctx *ctx, const emqx_gm_index *idx, const uint8_t *topic_bytes,
+                         const uint64_t *topic_off, uint64_t n_topics, uint32_t flags, emqx_gm_csr *matches,
+                         emqx_gm_csr *deliveries);
 int emqx_gm_csr_free(emqx_gm_ctx *ctx, emqx_gm_csr *csr);
 int emqx_gm_last_stats(const emqx_gm_ctx *ctx, emqx_gm_match_stats *stats);
 

@@ -401,15 +401,10 @@ static ERL_NIF_TERM fanout_batch(ErlNifEnv *env, int argc, const ERL_NIF_TERM ar
   (void)argc;
   if (!enif_get_resource(env, argv[0], INDEX_RT, (void **)&r)) return enif_make_badarg(env);
   if (!pack_topics(env, argv[1], &tb, &to, &n)) return enif_make_badarg(env);
-  rc = emqx_gm_match(CTX, r->idx, tb, to, n, EMQX_GM_WITH_EXACT, &m);
+  /* the match and its fan-out in one call: one device round trip per window */
+  rc = emqx_gm_match_fanout(CTX, r->idx, tb, to, n, EMQX_GM_WITH_EXACT, &m, &d);
   free_topics(tb, to);
   if (rc != EMQX_GM_OK) return error_tuple(env, rc);
-  rc = emqx_gm_fanout(CTX, r->idx, &m, 0, &d);
-  if (rc != EMQX_GM_OK) {
-    ERL_NIF_TERM e = error_tuple(env, rc);
-    emqx_gm_csr_free(CTX, &m);
-    return e;
-  }
   rows = enif_alloc(sizeof(ERL_NIF_TERM) * (n ? n : 1));
   for (i = 0; i < n; ++i) {
     ERL_NIF_TERM row = enif_make_list(env, 0);

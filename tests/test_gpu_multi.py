@@ -455,7 +455,8 @@ def test_fanout_spread_over_replicas(ctx1, orc, monkeypatch, replicas):
     the rows per replica (balanced by matches), each fanned out on its device,
     the slices' deliveries put back in order into one result -- equal to the
     single-device fan-out and the oracle's dispatch fold, including empty rows,
-    rows of one hot filter and slices that start and end anywhere."""
+    rows of one hot filter and slices that start and end anywhere; and
+    emqx_gm_match_fanout's publish windows served by every replica in turn."""
     from emqx_amd import Context
     from emqx_amd.engine import gen_filter_codes, render_codes
     monkeypatch.setenv("GM_FANOUT_MULTI_MIN", "1")
@@ -483,5 +484,14 @@ def test_fanout_spread_over_replicas(ctx1, orc, monkeypatch, replicas):
         e = np.zeros(1, np.uint64), np.zeros(0, np.uint32)  # no rows at all
         got0 = c.fanout(ix, *e)
         assert got0[0].tolist() == [0] and len(got0[1]) == 0
+        # publish windows (match + fan-out in one round trip) round-robin over the replicas:
+        # every device's replica gives the single-device rows and deliveries
+        win = (tb, to[:2049])
+        wro, wids = ctx1.match(i1, win, exact=True)
+        wd = ctx1.fanout(i1, wro, wids)
+        for _ in range(2 * replicas + 1):
+            (mro, mids), (dro, dids) = c.match_fanout(ix, win)
+            assert np.array_equal(mro, wro) and np.array_equal(mids, wids)
+            assert np.array_equal(dro, wd[0]) and np.array_equal(dids, wd[1])
         ix.release()
     i1.release()

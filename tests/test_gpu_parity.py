@@ -465,6 +465,100 @@ def test_small_fanout_equals_locked_path(ctx, orc, monkeypatch):
     idx.release()
 
 
+def test_match_fanout_one_round_trip(ctx, orc, monkeypatch):
+    """emqx_gm_match_fanout (the NIF's fanout_batch: route + dispatch of a
+    publish window) equals emqx_gm_match followed by emqx_gm_fanout, and the
+    oracle's rows and deliveries: with the fan-out fused into the match's round
+    trip (GM_FANOUT_FUSED_ONLY: an error unless it held), and when it cannot
+    hold -- the first wide fan-out past its capacity, no speculative match
+    buffer (GM_NO_SPEC_IDS), a batch of more than one chunk, an overlay
+    snapshot (EUNSUPPORTED, nothing leaked) -- in both match modes, from four
+    threads at once, the empty batch included."""
+    import threading
+    from emqx_amd._lib import GpuMatchError
+    from emqx_amd.engine import pack
+    rng = np.random.default_rng(9)
+    filters = sorted({b"a/#", b"a/+", b"a/b", b"+/b", b"#", b"c/d", b"a/+/c", b"none/+", b"x/y/z"})
+    subs = [rng.integers(0, 1 << 20, size=int(rng.integers(1, 300))).astype(np.uint32).tolist() for _ in filters]
+    subs[filters.index(b"none/+")] = []
+    idx = ctx.build_index(filters, subs=subs)
+    so = np.zeros(len(filters) + 1, np.uint64)
+    so[1:] = np.cumsum([len(s) for s in subs])
+    si = np.array([x for s in subs for x in s], np.uint32)
+    topics = [b"a/b", b"a/x", b"c/d", b"q", b"a/b/c", b"$SYS/a", b"none/x", b"x/y/z"] * 64
+
+    def want(ix, tps, exact=True):
+        ro, ids = ctx.match(ix, tps, exact=exact)
+        monkeypatch.setenv("GM_FANOUT_SIMPLE", "1")
+        d = ctx.fanout(ix, ro, ids)
+        monkeypatch.delenv("GM_FANOUT_SIMPLE")
+        return (ro, ids), d
+
+    def same(a, b):
+        return all(np.array_equal(x, y) for p, q in zip(a, b) for x, y in zip(p, q))
+
+    for exact in (True, False):
+        got = ctx.match_fanout(idx, topics, exact=exact)  # (warms the context's deliveries per match)
+        assert same(got, want(idx, topics, exact))
+        monkeypatch.setenv("GM_FANOUT_FUSED_ONLY", "1")
+        got = ctx.match_fanout(idx, topics, exact=exact)
+        monkeypatch.delenv("GM_FANOUT_FUSED_ONLY")
+        assert same(got, want(idx, topics, exact))
+    (ro, ids), (fro, fids) = ctx.match_fanout(idx, topics)
+    oro, oids = _oracle_rows(orc, filters, topics, 1)
+    ero, eids = orc.fanout(oro, oids, so, si)
+    assert np.array_equal(ro, oro) and np.array_equal(ids, oids)
+    assert np.array_equal(fro, ero) and np.array_equal(fids, eids)
+    assert same(ctx.match_fanout(idx, []), want(idx, []))
+    # after update_subs (the device subscriber CSR replaced)
+    idx2 = ctx.update_subs(idx, [(b"a/b", 7, True), (b"zz/+", 9, True), (b"c/d", 11, True)])
+    t2 = topics + [b"zz/q"] * 5
+    assert same(ctx.match_fanout(idx2, t2), want(idx2, t2))
+    # no speculative match buffer: the fan-out after the match
+    monkeypatch.setenv("GM_NO_SPEC_IDS", "1")
+    assert same(ctx.match_fanout(idx, topics), want(idx, topics))
+    monkeypatch.delenv("GM_NO_SPEC_IDS")
+    # a wide fan-out: past the capacity the first time, fused (copy-engine rows) after
+    big = ctx.build_index([b"x/#", b"y"], subs=[list(range(300_000)), [5]])
+    bt = [b"x/1", b"y", b"x/2/3", b"q"]
+    assert same(ctx.match_fanout(big, bt), want(big, bt))
+    monkeypatch.setenv("GM_FANOUT_FUSED_ONLY", "1")
+    assert same(ctx.match_fanout(big, bt), want(big, bt))
+    monkeypatch.delenv("GM_FANOUT_FUSED_ONLY")
+    # more than one chunk: the two calls in turn
+    monkeypatch.setenv("GM_HOST_CHUNK", "1024")
+    many = topics * 4
+    assert same(ctx.match_fanout(idx, many), want(idx, many))
+    monkeypatch.delenv("GM_HOST_CHUNK")
+    # concurrent callers
+    errs, outs = [], [None] * 4
+    ref = want(idx, topics)
+
+    def one(k):
+        try:
+            for _ in range(20):
+                outs[k] = ctx.match_fanout(idx, topics)
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+    th = [threading.Thread(target=one, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs[0]
+    assert all(same(o, ref) for o in outs)
+    # an overlay snapshot (a filter with '#' inside): the fan-out refuses it, nothing is returned
+    plain = ctx.build_index(filters)
+    ov = ctx.update_index(plain, [(b"a/#/b", True)])
+    with pytest.raises(GpuMatchError) as e:
+        ctx.match_fanout(ov, topics)
+    assert "overlay" in str(e.value)
+    tb, to = pack(topics)
+    assert same(ctx.match_fanout(idx, (tb, to)), ref)
+    for x in (ov, plain, big, idx2, idx):
+        x.release()
+
+
 def test_tokenizer_alignments_and_bytes(ctx, orc):
     """Words of every length 0..19 at every byte alignment, with bytes next to
     '/' in value ('.', '0', 0x2E, 0x30, NUL, 0xFF) right after separators: the
