@@ -1761,6 +1761,22 @@ __global__ __launch_bounds__(SCAN1_T) void k_scan_one(LOAD load, uint64_t n_in, 
   if (mirror && threadIdx.x == 0) *mirror = tot;  // the grand total, also at the caller's out[n]
 }
 
+// A small call's scan of up to 8 x SCAN1_B values in ONE launch: the workgroup
+// walks the chunks with a running carry (a publish window's fan-out: ~5-15k
+// matches, where the three-launch form idled the queue ~20 us between launches)
+template <class LOAD>
+__global__ __launch_bounds__(SCAN1_T) void k_scan_loop(LOAD load, uint64_t n_in, uint64_t n_out,
+                                                        uint64_t* __restrict__ out) {
+  __shared__ uint64_t s_w[2 * (SCAN1_T / 64)];
+  uint64_t pre = 0;
+  for (uint64_t b0 = 0; b0 < n_out; b0 += SCAN1_B) {
+    pre += block_scan<SCAN1_T, SCAN1_V>(load, b0 + uint64_t(threadIdx.x) * SCAN1_V, n_in, n_out, pre, out, s_w,
+                                        SideSum{});
+    __syncthreads();  // (s_w is rewritten by the next chunk)
+  }
+}
+constexpr uint64_t SCAN_LOOP_MAX = 8ull * SCAN1_B;
+
 __global__ __launch_bounds__(SCAN_T) void k_scan_add(uint64_t* __restrict__ out, uint64_t n_out,
                                                       const uint64_t* __restrict__ block_off) {
   const uint64_t base = uint64_t(blockIdx.x) * SCAN_B;
@@ -4000,7 +4016,13 @@ int run_fanout(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_csr* m,
 int queue_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint64_t* d_off, const uint32_t* d_ids,
                        uint64_t n, uint64_t nnz, uint64_t total, uint64_t* seg_dst, uint64_t* row_off, uint32_t* ids) {
   hipStream_t st = ctx->stream;
-  if (int rc = scan_excl(ctx, LoadSegLen{d_ids, idx->view.sub_off}, nnz, seg_dst)) return rc;
+  if (nnz + 1 <= SCAN_LOOP_MAX) {
+    hipLaunchKernelGGL(k_scan_loop<LoadSegLen>, dim3(1), dim3(SCAN1_T), 0, st, LoadSegLen{d_ids, idx->view.sub_off},
+                       nnz, nnz + 1, seg_dst);
+    GM_HIP(ctx, hipGetLastError());
+  } else if (int rc = scan_excl(ctx, LoadSegLen{d_ids, idx->view.sub_off}, nnz, seg_dst)) {
+    return rc;
+  }
   hipLaunchKernelGGL(k_fanout_rowoff, dim3((n + 1 + 255) / 256), dim3(256), 0, st, d_off, n, seg_dst, row_off, nnz);
   GM_HIP(ctx, hipGetLastError());
   if (total) {
@@ -4020,7 +4042,12 @@ int queue_fanout_spec(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const uint64_t
                       uint64_t n, uint64_t cap_m, uint64_t cap_f, uint64_t* seg_dst, uint64_t* row_off, uint32_t* ids) {
   hipStream_t st = ctx->stream;
   const LoadSegLenSpec ld{d_ids, idx->view.sub_off, d_ro + n, uint32_t(idx->view.n_filters)};
-  if (int rc = scan_excl(ctx, ld, cap_m, seg_dst)) return rc;
+  if (cap_m + 1 <= SCAN_LOOP_MAX) {
+    hipLaunchKernelGGL(k_scan_loop<LoadSegLenSpec>, dim3(1), dim3(SCAN1_T), 0, st, ld, cap_m, cap_m + 1, seg_dst);
+    GM_HIP(ctx, hipGetLastError());
+  } else if (int rc = scan_excl(ctx, ld, cap_m, seg_dst)) {
+    return rc;
+  }
   hipLaunchKernelGGL(k_fanout_rowoff, dim3((n + 1 + 255) / 256), dim3(256), 0, st, d_ro, n, seg_dst, row_off, cap_m);
   GM_HIP(ctx, hipGetLastError());
   const uint64_t per = fan_per_block(cap_f);
