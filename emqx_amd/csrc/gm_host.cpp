@@ -1070,7 +1070,7 @@ int run_fanout_small(emqx_gm_ctx* ctx, const emqx_gm_index* idx, const emqx_gm_i
   if (!ctx->ev_free.empty()) {
     done = ctx->ev_free.back();
     ctx->ev_free.pop_back();
-  } else if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
+  } else if (hipEventCreate(&done) != hipSuccess) {  // (a timing event: the list serves timed match calls too)
     done = nullptr;
   }
   auto fail = [&](int code, const char* msg) {  // (under the lock)
