@@ -152,8 +152,8 @@ class GpuRoutes:
         if self.stale:
             raise RuntimeError("stale_index")
         idx = self.index
-        ro, ids = self.ctx.match(idx, list(topics), exact=True)
-        fro, fids = self.ctx.fanout(idx, ro, ids)
+        # (the NIF's fanout_batch/2: emqx_gm_match_fanout, the match and its fan-out in one call)
+        (ro, ids), (fro, fids) = self.ctx.match_fanout(idx, list(topics), exact=True)
         out = []
         for k in range(len(ro) - 1):
             row, pos = [], int(fro[k])

@@ -319,8 +319,7 @@ class Broker:
         'messages.dropped.no_subscribers' (emqx_broker.erl:245-248)."""
         snap = self.snapshot()
         ctx = self._context()
-        ro, ids = ctx.match(snap.index, list(topics), exact=True)
-        fro, fids = ctx.fanout(snap.index, ro, ids)
+        (ro, ids), (fro, fids) = ctx.match_fanout(snap.index, list(topics), exact=True)
         return [fids[fro[k]:fro[k + 1]].astype(np.int64).tolist() for k in range(len(fro) - 1)]
 
     def publish(self, t) -> List[int]:

@@ -69,8 +69,7 @@ class TopicRuleIndex:
         for t in names:
             if T.wildcard(t):
                 raise ValueError(f"topic names only (got filter {t!r})")
-        ro, ids = self.ctx.match(self.index, names, exact=True)
-        fro, rids = self.ctx.fanout(self.index, ro, ids)
+        (ro, ids), (fro, rids) = self.ctx.match_fanout(self.index, names, exact=True)
         out = []
         for k in range(len(names)):
             out.append(np.unique(rids[fro[k]:fro[k + 1]]).astype(np.int64).tolist())

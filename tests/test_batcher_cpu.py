@@ -198,7 +198,7 @@ class _FakeIndex:
 
 
 class _FakeCtx:
-    """build_index / update_subs / match / fanout over Python dicts, ids = rank of
+    """build_index / update_subs / match / fanout / match_fanout over Python dicts, ids = rank of
     the filter bytes (the library's id rule), matching by emqx_amd.topic.match."""
 
     def build_index(self, filters, subs=None):
@@ -232,6 +232,10 @@ class _FakeCtx:
         for k in range(len(ro) - 1):
             out[k + 1] = out[k] + sum(len(segs[j]) for j in range(int(ro[k]), int(ro[k + 1])))
         return out, np.array([s for seg in segs for s in seg], np.uint32)
+
+    def match_fanout(self, idx, topics, exact=True):  # (emqx_gm_match_fanout: the two in one call)
+        m = self.match(idx, topics, exact)
+        return m, self.fanout(idx, *m)
 
 
 def test_subscriber_ids_are_never_reused_after_down():
