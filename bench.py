@@ -1216,6 +1216,23 @@ def bench_c4(a, world, rank, local, pg):
     algo = 4 * part + 8 * (K + 1) + 4 * S
     kavg = sum(kms) / len(kms)
     achieved = algo / (kavg / 1e3) / 1e9
+    # roofline.traffic: the PMC bytes of k_fanout_copy from a profile of this very build
+    # (scripts/profile.sh CONFIG=c4 -> scripts/traffic.py --kernel k_fanout_copy), else null
+    traffic, traffic_note, pmc = None, "no profile of this build", {}
+    try:
+        import hashlib
+        with open(a.traffic_json) as f:
+            tj = json.load(f)
+        with open(os.path.join(ROOT, "emqx_amd", "libemqx_gpu_match.so"), "rb") as f:
+            sha = hashlib.sha256(f.read()).hexdigest()[:16]
+        if tj.get("config") == "c4" and tj.get("kernel") == "k_fanout_copy" and tj.get("lib_sha16") == sha \
+                and world == 1:
+            traffic = tj.get("hbm_bytes_per_launch")
+            pmc = {k: tj[k] for k in ("l2_hit_rate", "occupancy_waves_per_cu", "occupancy_frac")
+                   if tj.get(k) is not None}
+            traffic_note = f"PMC of this build ({os.path.relpath(a.traffic_json, ROOT)}, lib {sha})"
+    except (OSError, ValueError):
+        pass
     out = {"metric": "hot-topic fan-out deliveries/sec (C4: 1k topics x 1M subscribers)",
            "value": pairs * a.steps / elapsed, "unit": "deliveries/s", "n_gpus": world, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps, "higher_is_better": True,
@@ -1223,8 +1240,8 @@ def bench_c4(a, world, rank, local, pg):
            "config": {"workload": "C4: 1k hot topics x 1M subscribers, CSR subscriber lists, delivery range "
                                   f"split over {world} GPU(s)", "pairs": pairs, "pairs_per_rank": parts},
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_fanout_copy",
-                        "kernel_ms": kavg, "algo_bytes_per_launch": algo}}
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
+                        "kernel": "k_fanout_copy", "kernel_ms": kavg, "algo_bytes_per_launch": algo, **pmc}}
     m.free()
     ctx.dev_free(d_tb)
     ctx.dev_free(d_to)
