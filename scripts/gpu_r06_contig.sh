@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 6 A/B: the C5 index blob from a contiguous allocation (GM_BLOB_CONTIG)
-# against plain hipMalloc, same box, kernel time of the bench line.
+# against plain hipMalloc, same box, kernel time of the bench line.  (The knob
+# lived in gm_index.cpp for this A/B only; no difference, so it was removed.)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp EMQX_GM_AB=1
